@@ -1,0 +1,302 @@
+"""Benchmark: device-resident Bloom probes/s on the C3 workload (BASELINE.json).
+
+One step = one batched multi-filter probe of 1M 16-byte lookup keys (already
+in HBM) against this GPU's 32 resident 8-MiB filters (m = 2^26), producing the
+[filter][n/64] hit bitmaps; for N > 1 GPUs each rank holds its own 32 filters
+(filters shard one subset per GPU, weak scaling) and the step also all-gathers
+the hit bitmaps over RCCL/xGMI. value = probes of all ranks / max-rank time.
+
+Also reported (same JSON line): C2 build keys/s (1M keys -> one 16 MiB filter),
+the dominant kernel's roofline (HIP events on its own stream), the CPU oracle
+baseline (rank 0, N = 1), and the PCIe-inclusive end-to-end probe rate.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Bloom probes/sec device-resident (1M keys × 32 filters); build keys/sec"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--n-keys", type=int, default=1 << 20)
+    p.add_argument("--filters", type=int, default=32, help="filters per GPU")
+    p.add_argument("--m-bits", type=int, default=1 << 26)
+    p.add_argument("--keys-per-filter", type=int, default=1 << 19)
+    p.add_argument("--build-keys", type=int, default=1 << 20)
+    p.add_argument("--build-m-bits", type=int, default=1 << 27)
+    p.add_argument("--path", type=int, default=0, help="0 auto, 1 direct, 2 tiled")
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
+    p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--check", action="store_true", help="verify hits against the oracle (slow)")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import lsmt_amd
+    from lsmt_amd import _lib, workload
+
+    L = _lib.load()
+    lsmt_amd.set_path(args.path)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    F, n, m, kpf = args.filters, args.n_keys, args.m_bits, args.keys_per_filter
+    nf_total = F * world
+    f_lo = rank * F
+
+    # ---- setup (untimed): build this rank's filters, stage the lookups in HBM
+    t_setup = time.time()
+    filters = []
+    for f in range(f_lo, f_lo + F):
+        keys = torch.from_numpy(workload.key_range(100 + f, kpf)).to(dev)
+        b = lsmt_amd.BloomFilter(m, device=local)
+        b.insert_batch(lsmt_amd.DeviceKeys(keys), stream=sh)
+        filters.append(b)
+    look_np = workload.probe_lookups(n, nf_total, kpf, seed_base=100, absent_seed=999)
+    look = torch.from_numpy(look_np).to(dev)
+    words = (n + 63) // 64
+    hits = torch.zeros((F, words), dtype=torch.int64, device=dev)
+    hits_all = torch.zeros((nf_total, words), dtype=torch.int64, device=dev) if world > 1 else hits
+    torch.cuda.synchronize(dev)
+    log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: {F} filters m={m} built, {n} lookups in HBM")
+    keys_batch = lsmt_amd.DeviceKeys(look)
+
+    def step():
+        lsmt_amd.probe(filters, keys_batch, out=hits, stream=sh)
+        if world > 1:
+            dist.all_gather_into_tensor(hits_all, hits)
+
+    def timed(fn, k):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    for _ in range(args.warmup):
+        step()
+    el = timed(step, args.steps)
+    ms_step = el / args.steps * 1e3
+    probes_per_step = n * nf_total
+    value = probes_per_step / (el / args.steps)
+    path_used = int(L.cb_last_path())
+
+    # ---- separate profiled pass: per-kernel durations from HIP events on `sh`
+    def kernel_ms(names, fn, k):
+        L.cb_profile_reset()
+        L.cb_profile_enable(1)
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        L.cb_profile_enable(0)
+        out = {}
+        for nm in names:
+            tot = __import__("ctypes").c_double()
+            cnt = __import__("ctypes").c_uint64()
+            L.cb_profile_read(nm.encode(), __import__("ctypes").byref(tot), __import__("ctypes").byref(cnt))
+            if cnt.value:
+                out[nm] = {"avg_us": tot.value * 1e3 / cnt.value, "launches": int(cnt.value)}
+        return out
+
+    probe_kernels = ["k_part_probe", "k_tile_probe", "k_masks_to_hits", "k_probe_direct"]
+    kprof = kernel_ms(probe_kernels, step, args.steps)
+    dominant = max(kprof, key=lambda k: kprof[k]["avg_us"]) if kprof else None
+
+    # algorithmic bytes per probe launch:
+    # F*m/8*tau (each filter streamed once) + 16*n (keys) + F*n/8 (hit bitmaps)
+    tau = 1.0 - np.exp(-n * 1.0155 / (m / 512.0))
+    alg_bytes = F * m / 8 * tau + 16 * n + F * n / 8
+    roof = None
+    if dominant:
+        dur_s = kprof[dominant]["avg_us"] * 1e-6
+        ach = alg_bytes / dur_s / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("k_tile_probe" if dominant == "k_tile_probe" else dominant),
+                "kernel": dominant, "kernel_avg_us": round(kprof[dominant]["avg_us"], 2),
+                "algorithmic_bytes": int(alg_bytes),
+                "step_effective_GBps": round(alg_bytes / (el / args.steps) / 1e9, 1)}
+
+    # ---- C2 build: 1M keys -> one fresh 16 MiB filter (zero-fill + batched insert)
+    bk = torch.from_numpy(workload.c2_build_keys(args.build_keys)).to(dev)
+    bf = lsmt_amd.BloomFilter(args.build_m_bits, device=local)
+    bkb = lsmt_amd.DeviceKeys(bk)
+
+    def build_step():
+        bf.clear(stream=sh)
+        bf.insert_batch(bkb, stream=sh)
+
+    for _ in range(args.warmup):
+        build_step()
+    bel = timed(build_step, args.steps)
+    bprof = kernel_ms(["k_part_build", "k_tile_build", "k_insert_direct"], build_step, args.steps)
+    b_alg = 16 * args.build_keys + args.build_m_bits / 8
+    build = {"metric": "build keys/s (C2: 1M 16-B keys -> one 16 MiB filter, m=2^27)",
+             "value": round(args.build_keys * world / (bel / args.steps), 1), "unit": "keys/s",
+             "ms_per_step": round(bel / args.steps * 1e3, 4), "path": int(L.cb_last_path()),
+             "kernels": {k: round(v["avg_us"], 2) for k, v in bprof.items()},
+             "algorithmic_bytes": int(b_alg),
+             "step_effective_GBps": round(b_alg / (bel / args.steps) / 1e9, 1)}
+
+    # ---- PCIe-inclusive end-to-end probe (pinned host keys -> host hits)
+    e2e = None
+    if not args.no_e2e and rank == 0:
+        look_pin = torch.from_numpy(look_np).pin_memory()
+        hits_host = torch.zeros((F, words), dtype=torch.int64).pin_memory()
+        hb = lsmt_amd.KeyBatch(n=n, key_len=16, keys=look_pin)
+
+        def e2e_step():
+            lsmt_amd.probe(filters, hb, out=hits_host, stream=sh)
+
+        e2e_step()
+        t0 = time.perf_counter()
+        k_e2e = max(3, args.steps // 2)
+        for _ in range(k_e2e):
+            e2e_step()
+        t_e2e = (time.perf_counter() - t0) / k_e2e
+        e2e = {"probes_per_s": round(n * F / t_e2e, 1), "ms_per_step": round(t_e2e * 1e3, 3),
+               "h2d_bytes": 16 * n, "d2h_bytes": F * words * 8, "host_buffers": "pinned"}
+
+    if args.check and rank == 0:
+        from oracle import oracle
+        refs = []
+        for f in range(f_lo, f_lo + F):
+            o = oracle.OracleFilter(m)
+            o.insert_fixed(workload.key_range(100 + f, kpf))
+            refs.append(o)
+        expect = oracle.probe_fixed(refs, look_np, threads=8)
+        got = hits.cpu().numpy().view(np.uint64)
+        assert np.array_equal(got, expect), "bench hits differ from the oracle"
+        log("[check] hits bit-exact vs oracle")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(look_np, F, m, kpf, args.build_keys, args.build_m_bits)
+        log(f"[cpu] {cpu}")
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "probes/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (splitmix64 hex keys, SURVEY.md §8d)",
+            "config": {"workload": f"C3 probe: {n} 16-B keys x {F} filters/GPU x {m // 8 // 2**20} MiB "
+                                   f"(m=2^{m.bit_length() - 1}), filters built from {kpf} keys each",
+                       "n_keys": n, "filters_per_gpu": F, "filters_total": nf_total, "m_bits": m,
+                       "keys_per_filter": kpf,
+                       "parallelism": "filter-sharded" + (", RCCL all-gather of hit bitmaps" if world > 1 else "")},
+            "path": {1: "direct", 2: "tiled"}.get(path_used, str(path_used)),
+            "kernels_us": {k: round(v["avg_us"], 2) for k, v in kprof.items()},
+            "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/pmc_*.json, FETCH_SIZE/WRITE_SIZE with the gfx950 corrections), or
+    None when no PMC run has been recorded for the current kernels."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as fh:
+            d = json.load(fh)
+        v = d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+        return int(v) if v else None
+    except Exception:
+        return None
+
+
+def cpu_baseline(look_np, F, m, kpf, build_keys, build_m):
+    """The C oracle (byte-per-bit restatement of src/bloom.rs, short-circuit
+    probe) on this host's cores: the full C3 probe (1M keys x F filters) on one
+    thread, the same on all cores, and the C2 build on one thread."""
+    from lsmt_amd import workload
+    from oracle import oracle
+    refs = []
+    for f in range(F):
+        o = oracle.OracleFilter(m)
+        o.insert_fixed(workload.key_range(100 + f, kpf))
+        refs.append(o)
+    n = look_np.shape[0]
+    t0 = time.perf_counter()
+    oracle.probe_fixed(refs, look_np, threads=1)
+    t1 = time.perf_counter() - t0
+    cores = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    oracle.probe_fixed(refs, look_np, threads=cores)
+    tn = time.perf_counter() - t0
+    del refs
+    bk = workload.c2_build_keys(build_keys)
+    o = oracle.OracleFilter(build_m)
+    t0 = time.perf_counter()
+    o.insert_fixed(bk)
+    tb = time.perf_counter() - t0
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(n * F / t1, 1), "unit": "probes/s", "cores": 1, "kind": "port",
+            "sample": f"full C3 probe: {n} keys x {F} filters (m=2^{m.bit_length() - 1}, byte-per-bit) on 1 thread, {t1:.2f}s",
+            "all_cores": {"value": round(n * F / tn, 1), "threads": cores, "seconds": round(tn, 3)},
+            "build": {"value": round(build_keys / tb, 1), "unit": "keys/s", "cores": 1,
+                      "sample": f"C2 build {build_keys} keys into m=2^{build_m.bit_length() - 1} bytes, {tb:.3f}s"},
+            "cpu_model": cpu_model, "nproc": os.cpu_count()}
+
+
+if __name__ == "__main__":
+    main()

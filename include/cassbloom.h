@@ -1,0 +1,136 @@
+/*
+ * cassbloom.h — C ABI of the MI355X-native Bloom-filter path for the `cass`
+ * LSM store (mweiden/lsmt). Drop-in for /root/reference/src/bloom.rs.
+ *
+ * Every entry point is plain C: opaque handles, pointers and sizes; no HIP,
+ * torch or C++ types. Streams are passed as `void*` (a hipStream_t; NULL = the
+ * device's null stream). Return value: CB_OK (0) or a negative CB_E* code;
+ * cb_last_error() gives a thread-local message for the last failure.
+ *
+ * Bit layout of a device filter (the "packed" form): bit p of the reference's
+ * Vec<bool> lives in 32-bit word p>>5 at bit p&31 (LSB-first), i.e. byte p>>3
+ * bit p&7 — little-endian packbits(bitorder="little") of the bool array.
+ *
+ * Pointer residency: key, offset and hit buffers may be device memory
+ * (hipMalloc / torch) or host memory (pageable or pinned). Device buffers are
+ * used in place and the call is asynchronous on `stream`. Host buffers are
+ * staged through library-owned device buffers and the call synchronises the
+ * stream before returning, so host outputs are valid on return.
+ *
+ * Reference interface replaced by each entry point (file:line in
+ * /root/reference):
+ *   cb_filter_create        BloomFilter::new(size)               src/bloom.rs:17-21
+ *   cb_filter_insert_*      BloomFilter::insert(&mut, &str)      src/bloom.rs:40-44
+ *                           batched over SsTable::create's loop  src/sstable.rs:62-65
+ *                           and SsTable::load's rebuild loop     src/sstable.rs:113-119
+ *   cb_probe_*              BloomFilter::may_contain(&, &str)    src/bloom.rs:48-51
+ *                           batched over Database::get's fan-out src/lib.rs:129-134
+ *   cb_may_contain          BloomFilter::may_contain (one key)   src/bloom.rs:48-51
+ *   cb_filter_export_bools  BloomFilter::to_proto (bits clone)   src/bloom.rs:54-58
+ *   cb_filter_import_bools  BloomFilter::from_proto              src/bloom.rs:61-63
+ *   cb_filter_to_bytes      BloomFilter::to_bytes (prost)        src/bloom.rs:66-70
+ *   cb_filter_from_bytes    BloomFilter::from_bytes (prost)      src/bloom.rs:74-77
+ *   cb_filter_destroy       Drop for BloomFilter (Vec<bool> free)
+ *
+ * Error behaviour mirrors the reference's panics as codes: inserting into or
+ * probing an m == 0 filter returns CB_EZEROM (`h % 0` panics at
+ * src/bloom.rs:36); malformed proto bytes return CB_EDECODE (`unwrap()` panics
+ * at src/bloom.rs:75). A Rust shim turns both back into panics.
+ *
+ * Threading: probes are reentrant and read-only on filters (the reference's
+ * concurrent `&self` readers under sstables.read(), src/lib.rs:129). Inserts
+ * need exclusive access to the target filter (the reference's `&mut self`).
+ */
+#ifndef CASSBLOOM_H
+#define CASSBLOOM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CB_OK 0
+#define CB_EINVAL (-1)  /* bad argument (null pointer, bad offsets, ...) */
+#define CB_EZEROM (-2)  /* m == 0: the reference panics with `% 0` */
+#define CB_ENOMEM (-3)  /* device or host allocation failed */
+#define CB_EHIP (-4)    /* HIP runtime error */
+#define CB_EDECODE (-5) /* malformed BloomProto bytes */
+#define CB_ENODEV (-6)  /* no usable gfx950 device */
+
+typedef struct cb_filter cb_filter;
+
+/* ---- device / library ---- */
+int cb_init(int device);
+int cb_device_count(int* out);
+const char* cb_last_error(void);
+const char* cb_version(void);
+int cb_stream_synchronize(void* stream);
+
+/* ---- filter lifetime (BloomFilter::new / Drop) ---- */
+/* m_bits may be 0 (legal in the reference; inserts/probes then fail with
+ * CB_EZEROM). The filter starts all-zero. */
+int cb_filter_create(uint64_t m_bits, int device, cb_filter** out);
+int cb_filter_destroy(cb_filter* f);
+int cb_filter_bits(const cb_filter* f, uint64_t* m_out);
+int cb_filter_device(const cb_filter* f, int* device_out);
+/* Device pointer to the packed words (ceil(m/32) uint32 LSB-first, padded
+ * with zero words to the allocation). Read-only use by callers. */
+int cb_filter_words(const cb_filter* f, const uint32_t** words_out, uint64_t* nwords_out);
+int cb_filter_clear(cb_filter* f, void* stream);
+
+/* ---- build (BloomFilter::insert, batched) ---- */
+/* n keys of key_len bytes each, contiguous. key_len may be 0. */
+int cb_filter_insert_fixed(cb_filter* f, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                           void* stream);
+/* n ragged keys: key i is bytes[offsets[i] .. offsets[i+1]) (offsets: n+1
+ * non-decreasing uint64). */
+int cb_filter_insert_var(cb_filter* f, const uint8_t* bytes, const uint64_t* offsets,
+                         uint64_t n, void* stream);
+
+/* ---- probe (BloomFilter::may_contain over many filters, batched) ---- */
+/* hits: [nf][ceil(n/64)] uint64; bit k%64 of word [f][k/64] is
+ * filters[f].may_contain(key k). Tail bits of the last word are zero. Filters
+ * may have different m; all must live on the same device. */
+int cb_probe_fixed(const cb_filter* const* filters, uint32_t nf, const uint8_t* keys,
+                   uint32_t key_len, uint64_t n, uint64_t* hits, void* stream);
+int cb_probe_var(const cb_filter* const* filters, uint32_t nf, const uint8_t* bytes,
+                 const uint64_t* offsets, uint64_t n, uint64_t* hits, void* stream);
+/* Single-key may_contain (host key, synchronous). *out = 0/1. */
+int cb_may_contain(const cb_filter* f, const uint8_t* key, uint64_t len, int* out);
+
+/* ---- persistence (to_proto / from_proto / to_bytes / from_bytes) ---- */
+/* Vec<bool> layout: m bytes of 0/1. */
+int cb_filter_export_bools(const cb_filter* f, uint8_t* out, void* stream);
+/* Replaces the filter's contents; m must equal the filter's m. */
+int cb_filter_import_bools(cb_filter* f, const uint8_t* in, uint64_t m, void* stream);
+/* Packed layout: ceil(m/32) uint32 words (bits >= m in the last word are 0). */
+int cb_filter_export_packed(const cb_filter* f, uint32_t* out, void* stream);
+int cb_filter_import_packed(cb_filter* f, const uint32_t* in, uint64_t nwords, void* stream);
+/* prost encoding of `BloomProto { repeated bool bits = 1; }` (packed): the
+ * exact bytes of BloomFilter::to_bytes. Writes at most `cap` bytes; *len_out
+ * always receives the full length (call with out=NULL, cap=0 to size). */
+int cb_filter_to_bytes(const cb_filter* f, uint8_t* out, uint64_t cap, uint64_t* len_out);
+/* BloomFilter::from_bytes: decodes (packed or unpacked elements, unknown
+ * fields skipped) into a new filter on `device`. */
+int cb_filter_from_bytes(const uint8_t* in, uint64_t len, int device, cb_filter** out);
+
+/* ---- tuning / introspection (bench + tests) ---- */
+/* Path selection: 0 = auto, 1 = force direct (per-key atomics / gathers),
+ * 2 = force tiled (LDS-staged filter tiles). Process-wide. */
+int cb_set_path(int path);
+/* Path the last insert/probe on this thread used (1 direct, 2 tiled). */
+int cb_last_path(void);
+/* Per-kernel timing with HIP events recorded on each launch's own stream
+ * (off by default). Kernel names: "k_insert_direct", "k_probe_direct",
+ * "k_part_build", "k_tile_build", "k_part_probe", "k_tile_probe",
+ * "k_masks_to_hits". cb_profile_read waits for pending events and returns the
+ * accumulated milliseconds and launch count for one kernel. */
+int cb_profile_enable(int on);
+int cb_profile_reset(void);
+int cb_profile_read(const char* kernel, double* total_ms, uint64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CASSBLOOM_H */

@@ -1,0 +1,25 @@
+"""lsmt_amd — MI355X-native Bloom-filter path for the `cass` LSM store
+(mweiden/lsmt, /root/reference/src/bloom.rs).
+
+The HIP extension (lsmt_amd/libcassbloom.so, C ABI in include/cassbloom.h) is
+loaded at import; there is no CPU fallback.
+"""
+from . import _lib
+
+_lib.load()  # fail loudly if the gfx950 extension is not built
+
+from .bloom import (  # noqa: E402
+    BloomFilter,
+    BloomProto,
+    DeviceKeys,
+    KeyBatch,
+    device_count,
+    last_path,
+    probe,
+    set_path,
+    unpack_hits,
+)
+
+__all__ = ["BloomFilter", "BloomProto", "DeviceKeys", "KeyBatch", "device_count", "last_path",
+           "probe", "set_path", "unpack_hits"]
+__version__ = "0.1.0"

@@ -1,0 +1,101 @@
+"""Loads the HIP extension ``lsmt_amd/libcassbloom.so`` (C ABI in
+``include/cassbloom.h``) with ctypes.
+
+There is no fallback: if the shared library is missing or cannot be loaded,
+importing the product API raises. Build it with ``__graft_entry__.build()`` or
+``make -C lsmt_amd/csrc``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcassbloom.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "cassbloom.h")
+
+CB_OK = 0
+CB_EINVAL = -1
+CB_EZEROM = -2
+CB_ENOMEM = -3
+CB_EHIP = -4
+CB_EDECODE = -5
+CB_ENODEV = -6
+
+PATH_AUTO, PATH_DIRECT, PATH_TILED = 0, 1, 2
+
+_lib = None
+
+
+class CassBloomError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"cassbloom error {code}: {msg}")
+        self.code = code
+
+
+class ExtensionMissing(ImportError):
+    pass
+
+
+def load():
+    """Load and prototype the C ABI. Raises ExtensionMissing if not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ExtensionMissing(
+            f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C lsmt_amd/csrc` (gfx950 HIP extension; no CPU fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, u8p, u32, u64, i32 = ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    pu64 = ctypes.POINTER(ctypes.c_uint64)
+    proto = {
+        "cb_init": ([i32], i32),
+        "cb_device_count": ([ctypes.POINTER(ctypes.c_int)], i32),
+        "cb_last_error": ([], ctypes.c_char_p),
+        "cb_version": ([], ctypes.c_char_p),
+        "cb_stream_synchronize": ([P], i32),
+        "cb_filter_create": ([u64, i32, pp], i32),
+        "cb_filter_destroy": ([P], i32),
+        "cb_filter_bits": ([P, pu64], i32),
+        "cb_filter_device": ([P, ctypes.POINTER(ctypes.c_int)], i32),
+        "cb_filter_words": ([P, pp, pu64], i32),
+        "cb_filter_clear": ([P, P], i32),
+        "cb_filter_insert_fixed": ([P, u8p, u32, u64, P], i32),
+        "cb_filter_insert_var": ([P, u8p, P, u64, P], i32),
+        "cb_probe_fixed": ([P, u32, u8p, u32, u64, P, P], i32),
+        "cb_probe_var": ([P, u32, u8p, P, u64, P, P], i32),
+        "cb_may_contain": ([P, u8p, u64, ctypes.POINTER(ctypes.c_int)], i32),
+        "cb_filter_export_bools": ([P, u8p, P], i32),
+        "cb_filter_import_bools": ([P, u8p, u64, P], i32),
+        "cb_filter_export_packed": ([P, P, P], i32),
+        "cb_filter_import_packed": ([P, P, u64, P], i32),
+        "cb_filter_to_bytes": ([P, u8p, u64, pu64], i32),
+        "cb_filter_from_bytes": ([u8p, u64, i32, pp], i32),
+        "cb_set_path": ([i32], i32),
+        "cb_last_path": ([], i32),
+        "cb_profile_enable": ([i32], i32),
+        "cb_profile_reset": ([], i32),
+        "cb_profile_read": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), pu64], i32),
+    }
+    for name, (args, res) in proto.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != CB_OK:
+        msg = load().cb_last_error()
+        raise CassBloomError(rc, msg.decode() if msg else "")
+
+
+def header_symbols() -> list[str]:
+    """Every function the public header declares (for the export test)."""
+    with open(HEADER_PATH) as fh:
+        text = fh.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(cb_\w+)\s*\(", text, re.M)))

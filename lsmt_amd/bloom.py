@@ -1,0 +1,311 @@
+"""Host-side mirror of the reference's ``BloomFilter`` over the gfx950 C ABI.
+
+Same surface as /root/reference/src/bloom.rs so the reference's callers and
+tests read the same:
+
+    BloomFilter.new(size)          src/bloom.rs:17-21
+    f.insert(item)                 src/bloom.rs:40-44
+    f.may_contain(item) -> bool    src/bloom.rs:48-51
+    f.to_proto() / from_proto(p)   src/bloom.rs:54-63
+    f.to_bytes() / from_bytes(b)   src/bloom.rs:66-77
+
+The filter bits live in HBM. Per-key ``insert`` calls are queued on the host
+and flushed as ONE batched build launch before the filter is next read: this
+is how SsTable::create's per-key loop (src/sstable.rs:62-65) turns into a
+single GPU build without changing the caller. ``may_contain`` on one key is a
+synchronous single-key probe; the read-path fan-out over many tables
+(src/lib.rs:129-134) uses the batched :func:`probe`.
+
+Errors follow the reference's panics: inserting into or probing an m == 0
+filter raises ZeroDivisionError (``h % 0``, src/bloom.rs:36); malformed proto
+bytes raise ValueError (``decode(..).unwrap()``, src/bloom.rs:75).
+
+There is no CPU fallback: every operation goes through libcassbloom.so.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import CassBloomError, check
+
+__all__ = ["BloomFilter", "BloomProto", "probe", "set_path", "last_path", "device_count",
+           "DeviceKeys", "KeyBatch"]
+
+
+def _L():
+    return _lib.load()
+
+
+def _raise(rc: int) -> None:
+    if rc == _lib.CB_EZEROM:
+        raise ZeroDivisionError("attempt to calculate the remainder with a divisor of zero")
+    if rc == _lib.CB_EDECODE:
+        msg = _L().cb_last_error()
+        raise ValueError(msg.decode() if msg else "BloomProto decode error")
+    check(rc)
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = _L().cb_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def set_path(path: int) -> None:
+    """0 auto, 1 direct (per-key atomics/gathers), 2 tiled (LDS tiles)."""
+    check(_L().cb_set_path(path))
+
+
+def last_path() -> int:
+    return int(_L().cb_last_path())
+
+
+# ---- key batches ---------------------------------------------------------------
+
+def _ptr_of(x):
+    """(address, keepalive) for numpy arrays, torch tensors, or raw ints."""
+    if x is None:
+        return None, None
+    if isinstance(x, int):
+        return x, None
+    if isinstance(x, np.ndarray):
+        if not x.flags["C_CONTIGUOUS"]:
+            x = np.ascontiguousarray(x)
+        return x.ctypes.data, x
+    if hasattr(x, "data_ptr"):  # torch tensor (device or host)
+        if not x.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+        return x.data_ptr(), x
+    raise TypeError(f"unsupported buffer type {type(x)!r}")
+
+
+@dataclass
+class KeyBatch:
+    """A batch of keys as the C ABI takes them: fixed-length rows
+    (``keys``: uint8[n, key_len]) or ragged (``data`` + ``offsets[n+1]``).
+    Buffers may be numpy (host) or device tensors."""
+    n: int
+    key_len: int = 0
+    keys: object = None
+    data: object = None
+    offsets: object = None
+
+    @property
+    def is_var(self) -> bool:
+        return self.offsets is not None
+
+
+def DeviceKeys(tensor) -> KeyBatch:
+    """Fixed-length keys already resident in HBM (torch uint8 [n, key_len])."""
+    n, kl = tensor.shape
+    return KeyBatch(n=int(n), key_len=int(kl), keys=tensor)
+
+
+def as_batch(keys) -> KeyBatch:
+    if isinstance(keys, KeyBatch):
+        return keys
+    if isinstance(keys, np.ndarray):
+        if keys.dtype != np.uint8 or keys.ndim != 2:
+            raise TypeError("fixed-length keys must be a uint8 array of shape [n, key_len]")
+        return KeyBatch(n=keys.shape[0], key_len=keys.shape[1], keys=np.ascontiguousarray(keys))
+    if hasattr(keys, "data_ptr") and getattr(keys, "ndim", 0) == 2:
+        return DeviceKeys(keys)
+    items = [k.encode() if isinstance(k, str) else bytes(k) for k in keys]
+    offs = np.zeros(len(items) + 1, np.uint64)
+    if items:
+        np.cumsum([len(k) for k in items], out=offs[1:])
+    data = np.frombuffer(b"".join(items), np.uint8) if offs[-1] else np.zeros(1, np.uint8)
+    return KeyBatch(n=len(items), data=np.ascontiguousarray(data), offsets=offs)
+
+
+def _stream(stream) -> int | None:
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return int(stream.cuda_stream)  # torch.cuda.Stream
+
+
+# ---- proto mirror ----------------------------------------------------------------
+
+@dataclass
+class BloomProto:
+    """Mirror of ``BloomProto { repeated bool bits = 1; }`` (src/bloom.rs:9-13)."""
+    bits: np.ndarray = field(default_factory=lambda: np.zeros(0, bool))
+
+
+# ---- the filter --------------------------------------------------------------------
+
+class BloomFilter:
+    """A Bloom filter of ``size`` bits resident in HBM (src/bloom.rs:4-7)."""
+
+    def __init__(self, size: int, device: int = 0, _handle: int | None = None):
+        self._h = ctypes.c_void_p()
+        if _handle is not None:
+            self._h = ctypes.c_void_p(_handle)
+        else:
+            _raise(_L().cb_filter_create(int(size), int(device), ctypes.byref(self._h)))
+        m = ctypes.c_uint64()
+        check(_L().cb_filter_bits(self._h, ctypes.byref(m)))
+        self._m = int(m.value)
+        self._pending: list[bytes] = []
+
+    # src/bloom.rs:17-21
+    @classmethod
+    def new(cls, size: int, device: int = 0) -> "BloomFilter":
+        return cls(size, device)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            _L().cb_filter_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def m(self) -> int:
+        return self._m
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def __len__(self) -> int:
+        return self._m
+
+    # ---- build -------------------------------------------------------------
+    def insert(self, item) -> None:
+        """src/bloom.rs:40-44. Queued; flushed as one batched launch."""
+        if self._m == 0:
+            raise ZeroDivisionError("attempt to calculate the remainder with a divisor of zero")
+        self._pending.append(item.encode() if isinstance(item, str) else bytes(item))
+
+    def flush(self, stream=None) -> None:
+        if self._pending:
+            batch, self._pending = self._pending, []
+            self.insert_batch(batch, stream=stream)
+
+    def insert_batch(self, keys, stream=None) -> None:
+        """Batched insert of every key (the flush build, src/sstable.rs:62-65)."""
+        b = as_batch(keys)
+        if self._pending:
+            pend, self._pending = self._pending, []
+            self.insert_batch(pend, stream=stream)
+        s = _stream(stream)
+        if b.is_var:
+            dp, k1 = _ptr_of(b.data)
+            op, k2 = _ptr_of(b.offsets)
+            _raise(_L().cb_filter_insert_var(self._h, dp, op, b.n, s))
+        else:
+            kp, k1 = _ptr_of(b.keys)
+            _raise(_L().cb_filter_insert_fixed(self._h, kp, b.key_len, b.n, s))
+
+    def clear(self, stream=None) -> None:
+        self._pending = []
+        check(_L().cb_filter_clear(self._h, _stream(stream)))
+
+    # ---- probe -------------------------------------------------------------
+    def may_contain(self, item) -> bool:
+        """src/bloom.rs:48-51 for one key (synchronous)."""
+        self.flush()
+        key = item.encode() if isinstance(item, str) else bytes(item)
+        buf = ctypes.create_string_buffer(key, max(len(key), 1))
+        out = ctypes.c_int(0)
+        _raise(_L().cb_may_contain(self._h, ctypes.cast(buf, ctypes.c_void_p), len(key), ctypes.byref(out)))
+        return bool(out.value)
+
+    def may_contain_batch(self, keys, stream=None) -> np.ndarray:
+        hits = probe([self], keys, stream=stream)
+        n = as_batch(keys).n
+        return unpack_hits(hits, n)[0]
+
+    # ---- persistence -------------------------------------------------------
+    def bools(self, stream=None) -> np.ndarray:
+        """The Vec<bool> contents as uint8 0/1 (to_proto's bits)."""
+        self.flush(stream)
+        out = np.zeros(max(self._m, 1), np.uint8)
+        _raise(_L().cb_filter_export_bools(self._h, out.ctypes.data, _stream(stream)))
+        return out[: self._m]
+
+    def packed(self, stream=None) -> np.ndarray:
+        self.flush(stream)
+        nw = (self._m + 31) // 32
+        out = np.zeros(max(nw, 1), np.uint32)
+        _raise(_L().cb_filter_export_packed(self._h, out.ctypes.data, _stream(stream)))
+        return out[:nw]
+
+    def load_packed(self, words: np.ndarray, stream=None) -> None:
+        self._pending = []
+        w = np.ascontiguousarray(words, dtype=np.uint32)
+        _raise(_L().cb_filter_import_packed(self._h, w.ctypes.data if w.size else None, w.size, _stream(stream)))
+
+    def to_proto(self) -> BloomProto:  # src/bloom.rs:54-58
+        return BloomProto(bits=self.bools().astype(bool))
+
+    @classmethod
+    def from_proto(cls, proto: BloomProto, device: int = 0) -> "BloomFilter":  # src/bloom.rs:61-63
+        bits = np.ascontiguousarray(np.asarray(proto.bits, dtype=bool).view(np.uint8))
+        f = cls(bits.shape[0], device)
+        if bits.shape[0]:
+            _raise(_L().cb_filter_import_bools(f._h, bits.ctypes.data, bits.shape[0], None))
+        return f
+
+    def to_bytes(self) -> bytes:  # src/bloom.rs:66-70
+        self.flush()
+        n = ctypes.c_uint64()
+        _raise(_L().cb_filter_to_bytes(self._h, None, 0, ctypes.byref(n)))
+        out = np.zeros(max(int(n.value), 1), np.uint8)
+        _raise(_L().cb_filter_to_bytes(self._h, out.ctypes.data, int(n.value), ctypes.byref(n)))
+        return out[: int(n.value)].tobytes()
+
+    @classmethod
+    def from_bytes(cls, data: bytes, device: int = 0) -> "BloomFilter":  # src/bloom.rs:74-77
+        buf = np.frombuffer(bytes(data), np.uint8) if data else np.zeros(1, np.uint8)
+        h = ctypes.c_void_p()
+        _raise(_L().cb_filter_from_bytes(buf.ctypes.data, len(data), device, ctypes.byref(h)))
+        return cls(0, _handle=h.value)
+
+
+# ---- batched multi-filter probe ------------------------------------------------------
+
+def probe(filters: Sequence[BloomFilter], keys, out=None, stream=None) -> np.ndarray:
+    """may_contain of every key against every filter (Database::get's fan-out,
+    src/lib.rs:129-134). Returns (or fills ``out``) uint64[nf, ceil(n/64)]:
+    bit k%64 of word [f][k/64] = filters[f].may_contain(key k)."""
+    b = as_batch(keys)
+    nf = len(filters)
+    for f in filters:
+        f.flush(stream)
+    words = (b.n + 63) // 64
+    if out is None:
+        out = np.zeros((nf, max(words, 1)), np.uint64)
+        result = out[:, :words]
+    else:
+        result = out
+    arr = (ctypes.c_void_p * max(nf, 1))(*[f.handle.value for f in filters])
+    op, keep = _ptr_of(out)
+    s = _stream(stream)
+    if b.is_var:
+        dp, k1 = _ptr_of(b.data)
+        offp, k2 = _ptr_of(b.offsets)
+        _raise(_L().cb_probe_var(ctypes.cast(arr, ctypes.c_void_p), nf, dp, offp, b.n, op, s))
+    else:
+        kp, k1 = _ptr_of(b.keys)
+        _raise(_L().cb_probe_fixed(ctypes.cast(arr, ctypes.c_void_p), nf, kp, b.key_len, b.n, op, s))
+    return result
+
+
+def unpack_hits(hits: np.ndarray, n: int) -> np.ndarray:
+    """uint64[nf, words] -> bool[nf, n]."""
+    h = np.ascontiguousarray(hits, dtype="<u8")
+    bits = np.unpackbits(h.view(np.uint8).reshape(h.shape[0], -1), axis=1, bitorder="little")
+    return bits[:, :n].astype(bool)

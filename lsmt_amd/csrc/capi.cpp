@@ -1,0 +1,733 @@
+// capi.cpp — the extern "C" boundary (include/cassbloom.h) over the gfx950
+// kernels in kernels.hip: filter handles in HBM, per-stream workspaces, host
+// buffer staging, path selection, and the BloomProto (prost) codec.
+//
+// Reference: /root/reference/src/bloom.rs (BloomFilter / BloomProto) and its
+// callers src/sstable.rs:59-65,96-119,138 and src/lib.rs:129-134.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "cassbloom.h"
+#include "kernels.hpp"
+
+using cb::FilterPtrs;
+using cb::KeySrc;
+using cb::ModP;
+using cb::TilePlan;
+
+struct cb_filter {
+  uint64_t m = 0;
+  int device = 0;
+  uint32_t* words = nullptr;  // device, nwords_alloc words
+  uint64_t nwords_alloc = 0;
+  bool known_zero = true;  // logically all-zero (lets the tiled build skip the read)
+  // cb_filter_clear is lazy: the memset is issued by the next operation that
+  // needs the words, and skipped by a fresh tiled build (which writes every
+  // tile). Exchanged atomically so concurrent readers issue it once.
+  std::atomic<bool> needs_zero{false};
+  int mode = 0;
+  ModP mp{};
+};
+
+namespace {
+
+thread_local std::string g_err;
+thread_local int g_last_path = 0;
+int g_path_override = 0;  // 0 auto, 1 direct, 2 tiled
+
+constexpr int PATH_DIRECT = 1, PATH_TILED = 2;
+
+int fail(int code, const char* what) {
+  g_err = what;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+  g_err = std::string(where) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
+  return CB_EHIP;
+}
+
+#define HIP_TRY(expr)                                \
+  do {                                               \
+    hipError_t _e = (expr);                          \
+    if (_e != hipSuccess) return hip_fail(_e, #expr); \
+  } while (0)
+
+// Device buffer that grows on demand. Growth synchronises the owning stream
+// first, so a buffer still read by queued work is never freed under it.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t bytes, hipStream_t s) {
+    if (bytes <= cap) return hipSuccess;
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+    want = (want + 4095) & ~size_t(4095);
+    e = hipMalloc(&p, want);
+    if (e != hipSuccess) return e;
+    cap = want;
+    return hipSuccess;
+  }
+};
+
+struct Workspace {
+  std::mutex mu;
+  DevBuf keys, offsets, hits, seg, ent, masks, bools;
+};
+
+std::mutex g_ws_mu;
+std::map<std::pair<int, void*>, std::unique_ptr<Workspace>> g_ws;
+
+Workspace& workspace(int device, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  auto& slot = g_ws[{device, (void*)s}];
+  if (!slot) slot.reset(new Workspace());
+  return *slot;
+}
+
+// Device-accessible memory (hipMalloc, managed) is used in place; anything
+// else (pageable or pinned host memory) is staged by the library.
+bool is_device_ptr(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t attr;
+  hipError_t e = hipPointerGetAttributes(&attr, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+uint64_t alloc_words_for(uint64_t m) {
+  // Pad to whole 2^18-bit tiles (the largest LDS tile) so tiled passes never
+  // read or write past the allocation; small filters pad to 2^12 bits.
+  const uint64_t align = m >= (1ull << 13) ? cb::kTileAlignBits : (1ull << 12);
+  const uint64_t bits = std::max<uint64_t>((m + align - 1) / align * align, align);
+  return bits / 32;
+}
+
+hipError_t ensure_zeroed(const cb_filter* cf, hipStream_t s) {
+  cb_filter* f = const_cast<cb_filter*>(cf);
+  if (f->needs_zero.exchange(false)) return hipMemsetAsync(f->words, 0, f->nwords_alloc * 4, s);
+  return hipSuccess;
+}
+
+bool tiled_ok(uint64_t m) { return m <= (1ull << 30) && m >= 1; }
+
+int choose_build_path(uint64_t m, uint64_t n) {
+  if (g_path_override == PATH_DIRECT || !tiled_ok(m)) return PATH_DIRECT;
+  if (g_path_override == PATH_TILED) return PATH_TILED;
+  return (m >= (1ull << 20) && n >= (1ull << 15)) ? PATH_TILED : PATH_DIRECT;
+}
+
+int choose_probe_path(uint64_t m, uint64_t n, uint32_t nf) {
+  if (g_path_override == PATH_DIRECT || !tiled_ok(m)) return PATH_DIRECT;
+  if (g_path_override == PATH_TILED) return PATH_TILED;
+  (void)nf;
+  return (m >= (1ull << 20) && n >= (1ull << 16)) ? PATH_TILED : PATH_DIRECT;
+}
+
+// Keys as the kernels see them (device pointers), staging host keys.
+struct StagedKeys {
+  KeySrc ks{};
+  int keyk = cb::KEY_FIXED;
+  bool staged = false;
+};
+
+int stage_fixed(Workspace& ws, const uint8_t* keys, uint32_t key_len, uint64_t n, hipStream_t s,
+                StagedKeys& out) {
+  const uint64_t bytes = (uint64_t)key_len * n;
+  const uint8_t* dk = keys;
+  if (bytes && !is_device_ptr(keys)) {
+    HIP_TRY(ws.keys.reserve(bytes, s));
+    HIP_TRY(hipMemcpyAsync(ws.keys.p, keys, bytes, hipMemcpyHostToDevice, s));
+    dk = (const uint8_t*)ws.keys.p;
+    out.staged = true;
+  }
+  out.ks.bytes = dk;
+  out.ks.offsets = nullptr;
+  out.ks.key_len = key_len;
+  out.keyk = (key_len == 16 && !((uintptr_t)dk & 15)) ? cb::KEY_FIXED16 : cb::KEY_FIXED;
+  return CB_OK;
+}
+
+int stage_var(Workspace& ws, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+              hipStream_t s, StagedKeys& out) {
+  // offsets are validated on the host when they live there; device offsets
+  // are the caller's contract (non-decreasing, n+1 entries).
+  const uint64_t* doff = offsets;
+  const uint8_t* db = bytes;
+  uint64_t total = 0;
+  if (!is_device_ptr(offsets)) {
+    for (uint64_t i = 0; i < n; ++i)
+      if (offsets[i + 1] < offsets[i]) return fail(CB_EINVAL, "offsets must be non-decreasing");
+    total = offsets[n];
+    HIP_TRY(ws.offsets.reserve((n + 1) * 8, s));
+    HIP_TRY(hipMemcpyAsync(ws.offsets.p, offsets, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    doff = (const uint64_t*)ws.offsets.p;
+    out.staged = true;
+  } else if (!is_device_ptr(bytes) && bytes) {
+    HIP_TRY(hipMemcpyAsync(&total, offsets + n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  if (bytes && total && !is_device_ptr(bytes)) {
+    HIP_TRY(ws.keys.reserve(total, s));
+    HIP_TRY(hipMemcpyAsync(ws.keys.p, bytes, total, hipMemcpyHostToDevice, s));
+    db = (const uint8_t*)ws.keys.p;
+    out.staged = true;
+  }
+  out.ks.bytes = db;
+  out.ks.offsets = doff;
+  out.ks.key_len = 0;
+  out.keyk = cb::KEY_VAR;
+  return CB_OK;
+}
+
+int insert_impl(cb_filter* f, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len,
+                uint64_t n, hipStream_t s) {
+  if (!f) return fail(CB_EINVAL, "null filter");
+  if (n == 0) return CB_OK;  // no hashes() call in the reference: no panic
+  if (f->m == 0) return fail(CB_EZEROM, "attempt to calculate the remainder with a divisor of zero");
+  if (offsets == nullptr && keys == nullptr && key_len) return fail(CB_EINVAL, "null keys");
+  DeviceGuard dg(f->device);
+  Workspace& ws = workspace(f->device, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  StagedKeys sk;
+  int rc = offsets ? stage_var(ws, keys, offsets, n, s, sk)
+                   : stage_fixed(ws, keys, key_len, n, s, sk);
+  if (rc) return rc;
+
+  const int path = choose_build_path(f->m, n);
+  g_last_path = path;
+  if (path == PATH_DIRECT) {
+    HIP_TRY(ensure_zeroed(f, s));
+    HIP_TRY(cb::launch_insert_direct(sk.keyk, f->mode, f->words, sk.ks, n, f->mp, s));
+  } else {
+    // a fresh tiled build writes every tile of [0, T * 2^tb): the words past
+    // it are padding that no insert ever sets, so a pending clear is moot.
+    if (f->known_zero)
+      f->needs_zero.store(false);
+    else
+      HIP_TRY(ensure_zeroed(f, s));
+    // chunks of at most 4096 partition blocks of the largest block size
+    const uint64_t chunk = 4096ull * 256 * 16;
+    for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
+      const uint64_t nk = std::min(chunk, n - k0);
+      KeySrc ks = sk.ks;
+      if (sk.keyk == cb::KEY_VAR)
+        ks.offsets += k0;
+      else
+        ks.bytes += k0 * key_len;
+      const int keyk = (sk.keyk == cb::KEY_FIXED16 && ((uintptr_t)ks.bytes & 15)) ? cb::KEY_FIXED
+                                                                                   : sk.keyk;
+      const TilePlan p = cb::plan_build(f->m, nk);
+      HIP_TRY(ws.seg.reserve(cb::build_seg_bytes(p), s));
+      HIP_TRY(ws.ent.reserve(cb::build_ent_bytes(p), s));
+      HIP_TRY(cb::launch_build_tiled(keyk, f->mode, f->words, f->known_zero, ks, nk, f->mp, p,
+                                     (uint32_t*)ws.seg.p, (uint32_t*)ws.ent.p, s));
+      f->known_zero = false;
+    }
+  }
+  f->known_zero = false;
+  if (sk.staged) HIP_TRY(hipStreamSynchronize(s));
+  return CB_OK;
+}
+
+int probe_impl(const cb_filter* const* filters, uint32_t nf, const uint8_t* keys,
+               const uint64_t* offsets, uint32_t key_len, uint64_t n, uint64_t* hits,
+               hipStream_t s) {
+  if (nf == 0 || n == 0) return CB_OK;
+  if (!filters || !hits) return fail(CB_EINVAL, "null filters or hits");
+  for (uint32_t i = 0; i < nf; ++i) {
+    if (!filters[i]) return fail(CB_EINVAL, "null filter");
+    if (filters[i]->device != filters[0]->device)
+      return fail(CB_EINVAL, "all filters of one probe must live on one device");
+    if (filters[i]->m == 0)
+      return fail(CB_EZEROM, "attempt to calculate the remainder with a divisor of zero");
+  }
+  for (uint32_t i = 0; i < nf; ++i) HIP_TRY(ensure_zeroed(filters[i], s));
+  if (offsets == nullptr && keys == nullptr && key_len) return fail(CB_EINVAL, "null keys");
+  const int dev = filters[0]->device;
+  DeviceGuard dg(dev);
+  Workspace& ws = workspace(dev, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  StagedKeys sk;
+  int rc = offsets ? stage_var(ws, keys, offsets, n, s, sk)
+                   : stage_fixed(ws, keys, key_len, n, s, sk);
+  if (rc) return rc;
+
+  const uint64_t hwords = (n + 63) / 64;
+  uint64_t* dhits = hits;
+  const bool host_hits = !is_device_ptr(hits);
+  if (host_hits) {
+    HIP_TRY(ws.hits.reserve((size_t)nf * hwords * 8, s));
+    dhits = (uint64_t*)ws.hits.p;
+  }
+
+  // Group filters by m (positions depend only on m), preserving hit rows.
+  std::map<uint64_t, std::vector<uint32_t>> groups;
+  for (uint32_t i = 0; i < nf; ++i) groups[filters[i]->m].push_back(i);
+
+  int last_path = PATH_DIRECT;
+  for (auto& kv : groups) {
+    const uint64_t m = kv.first;
+    const std::vector<uint32_t>& idx = kv.second;
+    const cb_filter* f0 = filters[idx[0]];
+    const int path = choose_probe_path(m, n, (uint32_t)idx.size());
+    last_path = path;
+    if (path == PATH_DIRECT) {
+      for (size_t g0 = 0; g0 < idx.size(); g0 += cb::kMaxFiltersPerLaunch) {
+        FilterPtrs fp{};
+        const uint32_t cnt = (uint32_t)std::min<size_t>(cb::kMaxFiltersPerLaunch, idx.size() - g0);
+        for (uint32_t j = 0; j < cnt; ++j) {
+          fp.w[j] = filters[idx[g0 + j]]->words;
+          fp.row[j] = idx[g0 + j];
+        }
+        HIP_TRY(cb::launch_probe_direct(sk.keyk, f0->mode, fp, cnt, sk.ks, n, f0->mp, dhits,
+                                        hwords, s));
+      }
+    } else {
+      const uint64_t chunk = 4096ull * 256 * 8;  // keys per partition pass (multiple of 64)
+      for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
+        const uint64_t nk = std::min(chunk, n - k0);
+        KeySrc ks = sk.ks;
+        if (sk.keyk == cb::KEY_VAR)
+          ks.offsets += k0;
+        else
+          ks.bytes += k0 * key_len;
+        const int keyk = (sk.keyk == cb::KEY_FIXED16 && ((uintptr_t)ks.bytes & 15))
+                             ? cb::KEY_FIXED
+                             : sk.keyk;
+        const TilePlan p = cb::plan_probe(m, nk);
+        HIP_TRY(ws.seg.reserve(cb::probe_seg_bytes(p), s));
+        HIP_TRY(ws.ent.reserve(cb::probe_ent_bytes(p), s));
+        HIP_TRY(ws.masks.reserve((size_t)2 * nk * 4, s));
+        HIP_TRY(cb::launch_probe_partition(keyk, f0->mode, ks, nk, f0->mp, p, (uint32_t*)ws.seg.p,
+                                           (uint4*)ws.ent.p, s));
+        for (size_t g0 = 0; g0 < idx.size(); g0 += cb::kMaxFiltersPerLaunch) {
+          FilterPtrs fp{};
+          const uint32_t cnt =
+              (uint32_t)std::min<size_t>(cb::kMaxFiltersPerLaunch, idx.size() - g0);
+          for (uint32_t j = 0; j < cnt; ++j) {
+            fp.w[j] = filters[idx[g0 + j]]->words;
+            fp.row[j] = idx[g0 + j];
+          }
+          HIP_TRY(cb::launch_probe_tiles(fp, cnt, nk, p, (const uint32_t*)ws.seg.p,
+                                         (const uint4*)ws.ent.p, (uint32_t*)ws.masks.p,
+                                         dhits + k0 / 64, hwords, s));
+        }
+      }
+    }
+  }
+  g_last_path = last_path;
+  if (host_hits) {
+    HIP_TRY(hipMemcpyAsync(hits, dhits, (size_t)nf * hwords * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  } else if (sk.staged) {
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  return CB_OK;
+}
+
+// ---- prost codec helpers (product side; see DESIGN.md "Persistence") ----
+
+uint64_t varint_len(uint64_t v) {
+  uint64_t n = 1;
+  while (v >= 0x80) {
+    v >>= 7;
+    ++n;
+  }
+  return n;
+}
+
+bool get_varint(const uint8_t*& p, const uint8_t* end, uint64_t& v) {
+  uint64_t r = 0;
+  for (int i = 0; i < 10; ++i) {
+    if (p >= end) return false;
+    const uint8_t b = *p++;
+    if (i == 9 && b > 1) return false;  // prost: overflowing varint
+    r |= (uint64_t)(b & 0x7F) << (7 * i);
+    if (!(b & 0x80)) {
+      v = r;
+      return true;
+    }
+  }
+  return false;
+}
+
+bool skip_field(const uint8_t*& p, const uint8_t* end, uint32_t wt, uint64_t field, int depth);
+
+bool skip_group(const uint8_t*& p, const uint8_t* end, uint64_t field, int depth) {
+  if (depth > 100) return false;
+  for (;;) {
+    uint64_t key;
+    if (!get_varint(p, end, key) || key > 0xFFFFFFFFull) return false;
+    const uint32_t wt = (uint32_t)(key & 7);
+    const uint64_t fn = key >> 3;
+    if (fn == 0) return false;
+    if (wt == 4) return fn == field;
+    if (!skip_field(p, end, wt, fn, depth + 1)) return false;
+  }
+}
+
+bool skip_field(const uint8_t*& p, const uint8_t* end, uint32_t wt, uint64_t field, int depth) {
+  uint64_t v;
+  switch (wt) {
+    case 0: return get_varint(p, end, v);
+    case 1:
+      if (end - p < 8) return false;
+      p += 8;
+      return true;
+    case 2:
+      if (!get_varint(p, end, v) || v > (uint64_t)(end - p)) return false;
+      p += v;
+      return true;
+    case 3: return skip_group(p, end, field, depth);
+    case 5:
+      if (end - p < 4) return false;
+      p += 4;
+      return true;
+    default: return false;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* cb_last_error(void) { return g_err.c_str(); }
+const char* cb_version(void) { return "cassbloom 0.1.0 (gfx950)"; }
+int cb_set_path(int path) {
+  if (path < 0 || path > 2) return fail(CB_EINVAL, "path must be 0, 1 or 2");
+  g_path_override = path;
+  return CB_OK;
+}
+int cb_last_path(void) { return g_last_path; }
+
+int cb_device_count(int* out) {
+  if (!out) return fail(CB_EINVAL, "null out");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    *out = 0;
+    return fail(CB_ENODEV, "no HIP device");
+  }
+  *out = n;
+  return CB_OK;
+}
+
+int cb_init(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    (void)hipGetLastError();
+    return fail(CB_ENODEV, "no HIP device");
+  }
+  if (device < 0 || device >= n) return fail(CB_ENODEV, "device index out of range");
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(CB_ENODEV, "device is not gfx950 (MI355X); this library carries gfx950 code only");
+  HIP_TRY(hipSetDevice(device));
+  return CB_OK;
+}
+
+int cb_stream_synchronize(void* stream) {
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return CB_OK;
+}
+
+int cb_filter_create(uint64_t m_bits, int device, cb_filter** out) {
+  if (!out) return fail(CB_EINVAL, "null out");
+  *out = nullptr;
+  int rc = cb_init(device);
+  if (rc) return rc;
+  DeviceGuard dg(device);
+  std::unique_ptr<cb_filter> f(new cb_filter());
+  f->m = m_bits;
+  f->device = device;
+  f->nwords_alloc = alloc_words_for(m_bits);
+  if (m_bits) f->mp = cb::make_modp(m_bits, &f->mode);
+  hipError_t e = hipMalloc(&f->words, f->nwords_alloc * 4);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(CB_ENOMEM, "hipMalloc failed for filter words");
+  }
+  HIP_TRY(hipMemsetAsync(f->words, 0, f->nwords_alloc * 4, nullptr));
+  HIP_TRY(hipStreamSynchronize(nullptr));
+  f->known_zero = true;
+  *out = f.release();
+  return CB_OK;
+}
+
+int cb_filter_destroy(cb_filter* f) {
+  if (!f) return CB_OK;
+  {
+    DeviceGuard dg(f->device);
+    if (f->words) (void)hipFree(f->words);
+  }
+  delete f;
+  return CB_OK;
+}
+
+int cb_filter_bits(const cb_filter* f, uint64_t* m_out) {
+  if (!f || !m_out) return fail(CB_EINVAL, "null argument");
+  *m_out = f->m;
+  return CB_OK;
+}
+
+int cb_filter_device(const cb_filter* f, int* device_out) {
+  if (!f || !device_out) return fail(CB_EINVAL, "null argument");
+  *device_out = f->device;
+  return CB_OK;
+}
+
+int cb_filter_words(const cb_filter* f, const uint32_t** words_out, uint64_t* nwords_out) {
+  if (!f || !words_out || !nwords_out) return fail(CB_EINVAL, "null argument");
+  if (f->needs_zero.load()) {
+    DeviceGuard dg(f->device);
+    HIP_TRY(ensure_zeroed(f, nullptr));
+    HIP_TRY(hipStreamSynchronize(nullptr));
+  }
+  *words_out = f->words;
+  *nwords_out = f->nwords_alloc;
+  return CB_OK;
+}
+
+int cb_filter_clear(cb_filter* f, void* stream) {
+  if (!f) return fail(CB_EINVAL, "null filter");
+  (void)stream;
+  f->known_zero = true;
+  f->needs_zero.store(true);
+  return CB_OK;
+}
+
+int cb_filter_insert_fixed(cb_filter* f, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                           void* stream) {
+  return insert_impl(f, keys, nullptr, key_len, n, (hipStream_t)stream);
+}
+
+int cb_filter_insert_var(cb_filter* f, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                         void* stream) {
+  if (!offsets) return fail(CB_EINVAL, "null offsets");
+  return insert_impl(f, bytes, offsets, 0, n, (hipStream_t)stream);
+}
+
+int cb_probe_fixed(const cb_filter* const* filters, uint32_t nf, const uint8_t* keys,
+                   uint32_t key_len, uint64_t n, uint64_t* hits, void* stream) {
+  return probe_impl(filters, nf, keys, nullptr, key_len, n, hits, (hipStream_t)stream);
+}
+
+int cb_probe_var(const cb_filter* const* filters, uint32_t nf, const uint8_t* bytes,
+                 const uint64_t* offsets, uint64_t n, uint64_t* hits, void* stream) {
+  if (!offsets) return fail(CB_EINVAL, "null offsets");
+  return probe_impl(filters, nf, bytes, offsets, 0, n, hits, (hipStream_t)stream);
+}
+
+int cb_may_contain(const cb_filter* f, const uint8_t* key, uint64_t len, int* out) {
+  if (!f || !out || (!key && len)) return fail(CB_EINVAL, "null argument");
+  if (f->m == 0) return fail(CB_EZEROM, "attempt to calculate the remainder with a divisor of zero");
+  uint64_t offs[2] = {0, len};
+  uint64_t hit = 0;
+  const cb_filter* fs[1] = {f};
+  int rc = probe_impl(fs, 1, key ? key : (const uint8_t*)"", offs, 0, 1, &hit, nullptr);
+  if (rc) return rc;
+  *out = (int)(hit & 1);
+  return CB_OK;
+}
+
+int cb_filter_export_bools(const cb_filter* f, uint8_t* out, void* stream) {
+  if (!f) return fail(CB_EINVAL, "null filter");
+  if (f->m == 0) return CB_OK;
+  if (!out) return fail(CB_EINVAL, "null out");
+  hipStream_t s = (hipStream_t)stream;
+  DeviceGuard dg(f->device);
+  HIP_TRY(ensure_zeroed(f, s));
+  if (is_device_ptr(out)) {
+    HIP_TRY(cb::launch_export_bools(f->words, f->m, out, s));
+    return CB_OK;
+  }
+  Workspace& ws = workspace(f->device, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  HIP_TRY(ws.bools.reserve(f->m, s));
+  HIP_TRY(cb::launch_export_bools(f->words, f->m, (uint8_t*)ws.bools.p, s));
+  HIP_TRY(hipMemcpyAsync(out, ws.bools.p, f->m, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return CB_OK;
+}
+
+int cb_filter_import_bools(cb_filter* f, const uint8_t* in, uint64_t m, void* stream) {
+  if (!f) return fail(CB_EINVAL, "null filter");
+  if (m != f->m) return fail(CB_EINVAL, "bool array length differs from the filter's m");
+  if (m == 0) return CB_OK;
+  if (!in) return fail(CB_EINVAL, "null input");
+  hipStream_t s = (hipStream_t)stream;
+  DeviceGuard dg(f->device);
+  if (is_device_ptr(in)) {
+    HIP_TRY(cb::launch_import_bools(f->words, m, in, s));
+  } else {
+    Workspace& ws = workspace(f->device, s);
+    std::lock_guard<std::mutex> lk(ws.mu);
+    HIP_TRY(ws.bools.reserve(m, s));
+    HIP_TRY(hipMemcpyAsync(ws.bools.p, in, m, hipMemcpyHostToDevice, s));
+    HIP_TRY(cb::launch_import_bools(f->words, m, (const uint8_t*)ws.bools.p, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  f->needs_zero.store(false);  // every word < ceil(m/32) was rewritten; padding is never set
+  f->known_zero = false;
+  return CB_OK;
+}
+
+int cb_filter_export_packed(const cb_filter* f, uint32_t* out, void* stream) {
+  if (!f) return fail(CB_EINVAL, "null filter");
+  const uint64_t nw = (f->m + 31) / 32;
+  if (!nw) return CB_OK;
+  if (!out) return fail(CB_EINVAL, "null out");
+  hipStream_t s = (hipStream_t)stream;
+  DeviceGuard dg(f->device);
+  HIP_TRY(ensure_zeroed(f, s));
+  const bool dev = is_device_ptr(out);
+  HIP_TRY(hipMemcpyAsync(out, f->words, nw * 4, dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                         s));
+  if (!dev) HIP_TRY(hipStreamSynchronize(s));
+  return CB_OK;
+}
+
+int cb_filter_import_packed(cb_filter* f, const uint32_t* in, uint64_t nwords, void* stream) {
+  if (!f) return fail(CB_EINVAL, "null filter");
+  const uint64_t nw = (f->m + 31) / 32;
+  if (nwords != nw) return fail(CB_EINVAL, "word count differs from ceil(m/32)");
+  if (!nw) return CB_OK;
+  if (!in) return fail(CB_EINVAL, "null input");
+  hipStream_t s = (hipStream_t)stream;
+  DeviceGuard dg(f->device);
+  const bool dev = is_device_ptr(in);
+  HIP_TRY(hipMemcpyAsync(f->words, in, nw * 4, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                         s));
+  HIP_TRY(cb::launch_mask_tail(f->words, f->m, s));
+  if (!dev) HIP_TRY(hipStreamSynchronize(s));
+  f->needs_zero.store(false);
+  f->known_zero = false;
+  return CB_OK;
+}
+
+int cb_filter_to_bytes(const cb_filter* f, uint8_t* out, uint64_t cap, uint64_t* len_out) {
+  if (!f || !len_out) return fail(CB_EINVAL, "null argument");
+  // prost: proto3 repeated scalars are packed; an empty field is omitted.
+  const uint64_t total = f->m ? 1 + varint_len(f->m) + f->m : 0;
+  *len_out = total;
+  if (!out || cap < total || !total) return CB_OK;
+  uint8_t* p = out;
+  *p++ = 0x0A;  // field 1, wire type 2
+  uint64_t v = f->m;
+  while (v >= 0x80) {
+    *p++ = (uint8_t)(v | 0x80);
+    v >>= 7;
+  }
+  *p++ = (uint8_t)v;
+  return cb_filter_export_bools(f, p, nullptr);
+}
+
+int cb_filter_from_bytes(const uint8_t* in, uint64_t len, int device, cb_filter** out) {
+  if (!out || (!in && len)) return fail(CB_EINVAL, "null argument");
+  *out = nullptr;
+  const uint8_t* p = in;
+  const uint8_t* end = in + len;
+  // Fast path: exactly one packed field-1 run of single-byte 0/1 varints (what
+  // to_bytes writes) is imported straight from the input buffer.
+  std::vector<uint8_t> bits;
+  const uint8_t* direct = nullptr;
+  uint64_t direct_len = 0;
+  int runs = 0;
+  while (p < end) {
+    uint64_t key;
+    if (!get_varint(p, end, key) || key > 0xFFFFFFFFull)
+      return fail(CB_EDECODE, "BloomProto decode: invalid key");
+    const uint32_t wt = (uint32_t)(key & 7);
+    const uint64_t fn = key >> 3;
+    if (fn == 0) return fail(CB_EDECODE, "BloomProto decode: invalid tag value 0");
+    if (fn == 1 && wt == 2) {
+      uint64_t l;
+      if (!get_varint(p, end, l) || l > (uint64_t)(end - p))
+        return fail(CB_EDECODE, "BloomProto decode: bad length");
+      const uint8_t* lim = p + l;
+      bool simple = true;
+      for (const uint8_t* q = p; q < lim; ++q)
+        if (*q > 1) {
+          simple = false;
+          break;
+        }
+      if (simple && runs == 0 && bits.empty()) {
+        direct = p;
+        direct_len = l;
+        p = lim;
+        ++runs;
+        continue;
+      }
+      if (direct) {
+        bits.assign(direct, direct + direct_len);
+        direct = nullptr;
+      }
+      while (p < lim) {
+        uint64_t v;
+        if (!get_varint(p, lim, v)) return fail(CB_EDECODE, "BloomProto decode: bad varint");
+        bits.push_back(v != 0);
+      }
+      ++runs;
+    } else if (fn == 1 && wt == 0) {
+      uint64_t v;
+      if (!get_varint(p, end, v)) return fail(CB_EDECODE, "BloomProto decode: bad varint");
+      if (direct) {
+        bits.assign(direct, direct + direct_len);
+        direct = nullptr;
+      }
+      bits.push_back(v != 0);
+      ++runs;
+    } else if (fn == 1) {
+      return fail(CB_EDECODE, "BloomProto decode: invalid wire type for field 1");
+    } else if (!skip_field(p, end, wt, fn, 0)) {
+      return fail(CB_EDECODE, "BloomProto decode: malformed unknown field");
+    }
+  }
+  const uint8_t* src = direct ? direct : bits.data();
+  const uint64_t m = direct ? direct_len : bits.size();
+  cb_filter* f = nullptr;
+  int rc = cb_filter_create(m, device, &f);
+  if (rc) return rc;
+  if (m) {
+    rc = cb_filter_import_bools(f, src, m, nullptr);
+    if (rc) {
+      cb_filter_destroy(f);
+      return rc;
+    }
+  }
+  *out = f;
+  return CB_OK;
+}
+
+}  // extern "C"

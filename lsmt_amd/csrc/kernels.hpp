@@ -1,0 +1,63 @@
+// kernels.hpp — host-side launchers for the gfx950 Bloom kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hash.hpp"
+
+namespace cb {
+
+constexpr uint32_t kMaxFiltersPerLaunch = 64;  // filter pointers carried in kernargs
+constexpr uint32_t kFiltersPerGroup = 32;      // one uint32 result mask per key
+constexpr uint32_t kMaxTiles = 4096;           // LDS histogram bound in the partition pass
+constexpr uint32_t kMaxTileBits = 18;          // 32 KiB LDS tiles at most
+constexpr uint32_t kMinTileBits = 12;          // 512 B tiles at least
+constexpr uint32_t kTileAlignBits = 1u << kMaxTileBits;  // filters >= 2^20 bits pad to this
+
+struct FilterPtrs {
+  const uint32_t* w[kMaxFiltersPerLaunch];
+  uint32_t row[kMaxFiltersPerLaunch];  // hits row for filter i of this launch
+};
+
+// Geometry of one tiled pass (build or probe) over filters of m bits.
+struct TilePlan {
+  uint32_t tb;    // log2(tile bits)
+  uint32_t T;     // number of tiles = ceil(m / 2^tb)
+  uint32_t kpt;   // keys per thread in the partition pass
+  uint32_t C;     // keys per partition block = 256 * kpt
+  uint32_t nblk;  // partition blocks = ceil(n / C)
+};
+
+TilePlan plan_build(uint64_t m, uint64_t n);
+TilePlan plan_probe(uint64_t m, uint64_t n);
+
+// Workspace bytes a tiled pass needs.
+size_t build_seg_bytes(const TilePlan& p);
+size_t build_ent_bytes(const TilePlan& p);
+size_t probe_seg_bytes(const TilePlan& p);
+size_t probe_ent_bytes(const TilePlan& p);
+
+hipError_t launch_insert_direct(int keyk, int mode, uint32_t* words, const KeySrc& ks, uint64_t n,
+                                const ModP& mp, hipStream_t s);
+hipError_t launch_probe_direct(int keyk, int mode, const FilterPtrs& fp, uint32_t nf,
+                               const KeySrc& ks, uint64_t n, const ModP& mp, uint64_t* hits,
+                               uint64_t hwords, hipStream_t s);
+
+hipError_t launch_build_tiled(int keyk, int mode, uint32_t* words, bool fresh, const KeySrc& ks,
+                              uint64_t n, const ModP& mp, const TilePlan& p, uint32_t* seg,
+                              uint32_t* ent, hipStream_t s);
+// Probe = partition the key batch once per filter size (K1), then per launch
+// of <= 64 filters: tile pass (K2) into masks (ceil(nf/32) * n uint32) and the
+// ballot transpose into hits (K3).
+hipError_t launch_probe_partition(int keyk, int mode, const KeySrc& ks, uint64_t n,
+                                  const ModP& mp, const TilePlan& p, uint32_t* seg, uint4* ent,
+                                  hipStream_t s);
+hipError_t launch_probe_tiles(const FilterPtrs& fp, uint32_t nf, uint64_t n, const TilePlan& p,
+                              const uint32_t* seg, const uint4* ent, uint32_t* masks,
+                              uint64_t* hits, uint64_t hwords, hipStream_t s);
+hipError_t launch_mask_tail(uint32_t* words, uint64_t m, hipStream_t s);
+
+hipError_t launch_export_bools(const uint32_t* words, uint64_t m, uint8_t* out, hipStream_t s);
+hipError_t launch_import_bools(uint32_t* words, uint64_t m, const uint8_t* in, hipStream_t s);
+
+}  // namespace cb

@@ -1,0 +1,100 @@
+"""Synthetic, deterministic key batches for the BASELINE configs.
+
+``key(seed, i)`` is the 16 lowercase hex characters (most-significant nibble
+first) of ``splitmix64(seed * 2**32 + i)`` — 16 bytes of valid UTF-8, i.e. a
+legal Rust ``&str`` for ``BloomFilter::insert``/``may_contain``
+(/root/reference/src/bloom.rs:40,48). Generated with numpy on the host; the
+bench copies them to HBM before the timed region.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+_HEX = np.frombuffer(b"0123456789abcdef", dtype=np.uint8)
+_M64 = (1 << 64) - 1
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint64, copy=False)
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def hex16(v: np.ndarray) -> np.ndarray:
+    """uint64[n] -> uint8[n,16] lowercase hex, most-significant nibble first."""
+    v = v.astype(np.uint64, copy=False)
+    shifts = np.arange(60, -4, -4, dtype=np.uint64)  # 60, 56, ..., 0
+    nib = (v[:, None] >> shifts[None, :]) & np.uint64(15)
+    return _HEX[nib.astype(np.intp)]
+
+
+def keys(seed: int, idx) -> np.ndarray:
+    """key(seed, i) for every i in ``idx`` (array-like of ints) -> uint8[n,16]."""
+    idx = np.asarray(idx, dtype=np.uint64)
+    return hex16(splitmix64(np.uint64((seed << 32) & _M64) + idx))
+
+
+def key_range(seed: int, n: int, first: int = 0) -> np.ndarray:
+    return keys(seed, np.arange(first, first + n, dtype=np.uint64))
+
+
+# ---- BASELINE configs ---------------------------------------
+
+def c2_build_keys(n: int = 1 << 20) -> np.ndarray:
+    """C2: N keys key(1, i) -> one m = 2^27 (16 MiB) filter."""
+    return key_range(1, n)
+
+
+def probe_lookups(n: int, nf: int, keys_per_filter: int, seed_base: int, absent_seed: int) -> np.ndarray:
+    """Lookup batch of the probe configs: even i -> present key
+    key(seed_base + j mod nf, (j div nf) mod keys_per_filter) with j = i/2;
+    odd i -> absent key key(absent_seed, i)."""
+    i = np.arange(n, dtype=np.uint64)
+    out = np.empty((n, 16), np.uint8)
+    even = i[0::2]
+    j = even // np.uint64(2)
+    f = (j % np.uint64(nf)).astype(np.int64)
+    kidx = (j // np.uint64(nf)) % np.uint64(keys_per_filter)
+    ev = np.empty((len(even), 16), np.uint8)
+    for fs in np.unique(f):
+        sel = f == fs
+        ev[sel] = keys(seed_base + int(fs), kidx[sel])
+    out[0::2] = ev
+    out[1::2] = keys(absent_seed, i[1::2])
+    return out
+
+
+def c3_filter_keys(f: int, keys_per_filter: int = 1 << 19) -> np.ndarray:
+    """C3: filter f is built from key(100 + f, i), i < 2^19."""
+    return key_range(100 + f, keys_per_filter)
+
+
+def c3_lookups(n: int = 1 << 20, nf: int = 32, keys_per_filter: int = 1 << 19) -> np.ndarray:
+    return probe_lookups(n, nf, keys_per_filter, seed_base=100, absent_seed=999)
+
+
+def c4_filter_keys(f: int, keys_per_filter: int = 1 << 18) -> np.ndarray:
+    """C4: filter f (of 64, m = 2^25) is built from key(200 + f, i)."""
+    return key_range(200 + f, keys_per_filter)
+
+
+def c5_filter_keys(f: int, keys_per_filter: int = 1 << 19) -> np.ndarray:
+    """C5: filter f (of 256, m = 2^26) is built from key(1000 + f, i)."""
+    return key_range(1000 + f, keys_per_filter)
+
+
+def c5_lookups(n: int = 10_000_000, nf: int = 256, keys_per_filter: int = 1 << 19) -> np.ndarray:
+    return probe_lookups(n, nf, keys_per_filter, seed_base=1000, absent_seed=9999)
+
+
+def var_keys(rng: np.random.Generator, n: int, max_len: int = 48):
+    """Ragged UTF-8-ish keys (bytes + offsets[n+1]) for the var-length paths,
+    shaped like the product's "ns:pk|ck" keys (src/lib.rs:155)."""
+    lens = rng.integers(0, max_len + 1, size=n, dtype=np.int64)
+    offsets = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=offsets[1:])
+    data = rng.integers(0x20, 0x7F, size=int(offsets[-1]), dtype=np.uint8)
+    return data, offsets

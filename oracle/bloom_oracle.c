@@ -1,0 +1,338 @@
+/*
+ * bloom_oracle.c — plain-C restatement of /root/reference/src/bloom.rs.
+ * TEST INFRASTRUCTURE ONLY (see bloom_oracle.h): parity checker and CPU
+ * baseline, never linked into the product library.
+ */
+#include "bloom_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+int ob_new(ob_filter* f, uint64_t m) {
+  /* src/bloom.rs:17-21 — vec![false; size] */
+  f->m = m;
+  f->bits = NULL;
+  if (m == 0) return OB_OK;
+  f->bits = (uint8_t*)calloc(m, 1);
+  return f->bits ? OB_OK : OB_ENOMEM;
+}
+
+void ob_free(ob_filter* f) {
+  free(f->bits);
+  f->bits = NULL;
+  f->m = 0;
+}
+
+void ob_raw_hashes(const uint8_t* key, uint64_t len, uint64_t* h1o, uint64_t* h2o) {
+  /* src/bloom.rs:28-34 — u64 wrapping arithmetic (unsigned overflow in C is
+   * modulo 2^64, which is exactly Rust's wrapping_*). */
+  uint64_t h1 = 5381, h2 = 0;
+  for (uint64_t i = 0; i < len; ++i) {
+    uint64_t b = key[i];
+    h1 = ((h1 << 5) + h1) + b; /* (h1 << 5).wrapping_add(h1).wrapping_add(b) */
+    h2 = h2 * 31u + b;         /* h2.wrapping_mul(31).wrapping_add(b) */
+  }
+  *h1o = h1;
+  *h2o = h2;
+}
+
+int ob_hashes(const uint8_t* key, uint64_t len, uint64_t m, uint64_t* a, uint64_t* b) {
+  uint64_t h1, h2;
+  if (m == 0) return OB_EZEROM; /* src/bloom.rs:36 panics on % 0 */
+  ob_raw_hashes(key, len, &h1, &h2);
+  *a = h1 % m; /* src/bloom.rs:35-36 */
+  *b = h2 % m;
+  return OB_OK;
+}
+
+int ob_insert(ob_filter* f, const uint8_t* key, uint64_t len) {
+  uint64_t a, b;
+  int rc = ob_hashes(key, len, f->m, &a, &b);
+  if (rc) return rc;
+  f->bits[a] = 1; /* src/bloom.rs:42-43 */
+  f->bits[b] = 1;
+  return OB_OK;
+}
+
+int ob_may_contain(const ob_filter* f, const uint8_t* key, uint64_t len) {
+  uint64_t a, b;
+  int rc = ob_hashes(key, len, f->m, &a, &b);
+  if (rc) return rc;
+  /* src/bloom.rs:50 — `&&` short-circuits: bit b is only read if bit a is set */
+  return f->bits[a] && f->bits[b];
+}
+
+int ob_insert_fixed(ob_filter* f, const uint8_t* keys, uint32_t key_len, uint64_t n) {
+  if (n && f->m == 0) return OB_EZEROM;
+  for (uint64_t i = 0; i < n; ++i) ob_insert(f, keys + i * (uint64_t)key_len, key_len);
+  return OB_OK;
+}
+
+int ob_insert_var(ob_filter* f, const uint8_t* bytes, const uint64_t* off, uint64_t n) {
+  if (n && f->m == 0) return OB_EZEROM;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (off[i + 1] < off[i]) return OB_EINVAL;
+    ob_insert(f, bytes + off[i], off[i + 1] - off[i]);
+  }
+  return OB_OK;
+}
+
+typedef struct {
+  const ob_filter* const* fs;
+  uint32_t nf;
+  const uint8_t* bytes;
+  const uint64_t* off; /* NULL for fixed-length keys */
+  uint32_t key_len;
+  uint64_t n, words, k0, k1;
+  uint64_t* hits;
+} probe_job;
+
+static void* probe_range(void* arg) {
+  probe_job* j = (probe_job*)arg;
+  for (uint64_t k = j->k0; k < j->k1; ++k) {
+    const uint8_t* key;
+    uint64_t len;
+    if (j->off) {
+      key = j->bytes + j->off[k];
+      len = j->off[k + 1] - j->off[k];
+    } else {
+      key = j->bytes + k * (uint64_t)j->key_len;
+      len = j->key_len;
+    }
+    /* Database::get walks tables newest-first (src/lib.rs:130); the per-table
+     * answer is independent of the order, so filters are visited 0..nf-1. */
+    for (uint32_t f = 0; f < j->nf; ++f) {
+      if (ob_may_contain(j->fs[f], key, len) == 1)
+        j->hits[(uint64_t)f * j->words + (k >> 6)] |= (uint64_t)1 << (k & 63);
+    }
+  }
+  return NULL;
+}
+
+static int probe_common(const ob_filter* const* fs, uint32_t nf, const uint8_t* bytes,
+                        const uint64_t* off, uint32_t key_len, uint64_t n, uint64_t* hits,
+                        int threads) {
+  uint64_t words = (n + 63) / 64;
+  for (uint32_t f = 0; f < nf; ++f)
+    if (n && fs[f]->m == 0) return OB_EZEROM;
+  if (off)
+    for (uint64_t i = 0; i < n; ++i)
+      if (off[i + 1] < off[i]) return OB_EINVAL;
+  memset(hits, 0, (size_t)(words * nf * sizeof(uint64_t)));
+  if (threads < 1) threads = 1;
+  if ((uint64_t)threads > words) threads = words ? (int)words : 1;
+  probe_job* jobs = (probe_job*)calloc((size_t)threads, sizeof(probe_job));
+  pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+  if (!jobs || !tids) {
+    free(jobs);
+    free(tids);
+    return OB_ENOMEM;
+  }
+  /* ranges aligned to 64 keys so every hit word has exactly one writer */
+  uint64_t per = ((words + threads - 1) / threads) * 64;
+  for (int t = 0; t < threads; ++t) {
+    probe_job* j = &jobs[t];
+    j->fs = fs;
+    j->nf = nf;
+    j->bytes = bytes;
+    j->off = off;
+    j->key_len = key_len;
+    j->n = n;
+    j->words = words;
+    j->hits = hits;
+    j->k0 = per * t < n ? per * t : n;
+    j->k1 = per * (t + 1) < n ? per * (t + 1) : n;
+  }
+  if (threads == 1) {
+    probe_range(&jobs[0]);
+  } else {
+    for (int t = 0; t < threads; ++t) pthread_create(&tids[t], NULL, probe_range, &jobs[t]);
+    for (int t = 0; t < threads; ++t) pthread_join(tids[t], NULL);
+  }
+  free(jobs);
+  free(tids);
+  return OB_OK;
+}
+
+int ob_probe_fixed(const ob_filter* const* fs, uint32_t nf, const uint8_t* keys,
+                   uint32_t key_len, uint64_t n, uint64_t* hits, int threads) {
+  return probe_common(fs, nf, keys, NULL, key_len, n, hits, threads);
+}
+
+int ob_probe_var(const ob_filter* const* fs, uint32_t nf, const uint8_t* bytes,
+                 const uint64_t* offsets, uint64_t n, uint64_t* hits, int threads) {
+  return probe_common(fs, nf, bytes, offsets, 0, n, hits, threads);
+}
+
+/* ---- prost codec for `message BloomProto { repeated bool bits = 1; }` ---- */
+
+static uint64_t varint_len(uint64_t v) {
+  uint64_t n = 1;
+  while (v >= 0x80) {
+    v >>= 7;
+    ++n;
+  }
+  return n;
+}
+
+static uint8_t* put_varint(uint8_t* p, uint64_t v) {
+  while (v >= 0x80) {
+    *p++ = (uint8_t)(v | 0x80);
+    v >>= 7;
+  }
+  *p++ = (uint8_t)v;
+  return p;
+}
+
+uint64_t ob_encode(const ob_filter* f, uint8_t* out, uint64_t cap) {
+  /* prost encodes proto3 repeated scalars packed and omits empty fields */
+  if (f->m == 0) return 0;
+  uint64_t total = 1 + varint_len(f->m) + f->m;
+  if (out && cap >= total) {
+    uint8_t* p = out;
+    *p++ = 0x0A; /* field 1, wire type 2 (length-delimited) */
+    p = put_varint(p, f->m);
+    for (uint64_t i = 0; i < f->m; ++i) p[i] = f->bits[i] ? 1 : 0;
+  }
+  return total;
+}
+
+/* prost's decode_varint: at most 10 bytes, the 10th must be <= 1. */
+static int get_varint(const uint8_t** pp, const uint8_t* end, uint64_t* v) {
+  const uint8_t* p = *pp;
+  uint64_t r = 0;
+  for (int i = 0; i < 10; ++i) {
+    if (p >= end) return OB_EDECODE;
+    uint8_t b = *p++;
+    if (i == 9 && b > 1) return OB_EDECODE;
+    r |= (uint64_t)(b & 0x7F) << (7 * i);
+    if (!(b & 0x80)) {
+      *pp = p;
+      *v = r;
+      return OB_OK;
+    }
+  }
+  return OB_EDECODE;
+}
+
+typedef struct {
+  uint8_t* v;
+  uint64_t n, cap;
+} bvec;
+
+static int bvec_push(bvec* b, uint8_t x) {
+  if (b->n == b->cap) {
+    uint64_t nc = b->cap ? b->cap * 2 : 64;
+    uint8_t* nv = (uint8_t*)realloc(b->v, nc);
+    if (!nv) return OB_ENOMEM;
+    b->v = nv;
+    b->cap = nc;
+  }
+  b->v[b->n++] = x;
+  return OB_OK;
+}
+
+static int skip_field(const uint8_t** pp, const uint8_t* end, uint32_t wt, uint64_t field,
+                      int depth);
+
+static int skip_group(const uint8_t** pp, const uint8_t* end, uint64_t field, int depth) {
+  if (depth > 100) return OB_EDECODE; /* prost's recursion limit */
+  for (;;) {
+    uint64_t key;
+    if (get_varint(pp, end, &key)) return OB_EDECODE;
+    uint32_t wt = (uint32_t)(key & 7);
+    uint64_t fn = key >> 3;
+    if (fn == 0 || key > 0xFFFFFFFFull) return OB_EDECODE;
+    if (wt == 4) return fn == field ? OB_OK : OB_EDECODE;
+    if (skip_field(pp, end, wt, fn, depth + 1)) return OB_EDECODE;
+  }
+}
+
+static int skip_field(const uint8_t** pp, const uint8_t* end, uint32_t wt, uint64_t field,
+                      int depth) {
+  uint64_t v;
+  switch (wt) {
+    case 0:
+      return get_varint(pp, end, &v);
+    case 1:
+      if ((uint64_t)(end - *pp) < 8) return OB_EDECODE;
+      *pp += 8;
+      return OB_OK;
+    case 2:
+      if (get_varint(pp, end, &v)) return OB_EDECODE;
+      if (v > (uint64_t)(end - *pp)) return OB_EDECODE;
+      *pp += v;
+      return OB_OK;
+    case 3:
+      return skip_group(pp, end, field, depth);
+    case 5:
+      if ((uint64_t)(end - *pp) < 4) return OB_EDECODE;
+      *pp += 4;
+      return OB_OK;
+    default:
+      return OB_EDECODE; /* 4 (unmatched end group), 6, 7 */
+  }
+}
+
+int ob_decode(const uint8_t* in, uint64_t len, ob_filter* out) {
+  const uint8_t* p = in;
+  const uint8_t* end = in + len;
+  bvec bits = {NULL, 0, 0};
+  while (p < end) {
+    uint64_t key, v;
+    if (get_varint(&p, end, &key) || key > 0xFFFFFFFFull) goto bad;
+    uint32_t wt = (uint32_t)(key & 7);
+    uint64_t fn = key >> 3;
+    if (fn == 0) goto bad;
+    if (fn == 1) {
+      if (wt == 2) { /* packed */
+        uint64_t l;
+        if (get_varint(&p, end, &l) || l > (uint64_t)(end - p)) goto bad;
+        const uint8_t* lim = p + l;
+        while (p < lim) {
+          if (get_varint(&p, lim, &v)) goto bad;
+          if (bvec_push(&bits, v != 0)) goto nomem;
+        }
+      } else if (wt == 0) { /* unpacked element */
+        if (get_varint(&p, end, &v)) goto bad;
+        if (bvec_push(&bits, v != 0)) goto nomem;
+      } else {
+        goto bad; /* wire-type mismatch on a known field */
+      }
+    } else if (skip_field(&p, end, wt, fn, 0)) {
+      goto bad;
+    }
+  }
+  out->m = bits.n;
+  out->bits = bits.v;
+  if (out->m == 0) {
+    free(out->bits);
+    out->bits = NULL;
+  }
+  return OB_OK;
+bad:
+  free(bits.v);
+  return OB_EDECODE;
+nomem:
+  free(bits.v);
+  return OB_ENOMEM;
+}
+
+/* ---- synthetic workload ---- */
+
+uint64_t ob_splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+void ob_gen_keys(uint64_t seed, uint64_t first, uint64_t n, uint8_t* out) {
+  static const char hex[] = "0123456789abcdef";
+  for (uint64_t i = 0; i < n; ++i) {
+    uint64_t v = ob_splitmix64((seed << 32) + first + i);
+    uint8_t* o = out + i * 16;
+    for (int d = 0; d < 16; ++d) o[d] = (uint8_t)hex[(v >> (60 - 4 * d)) & 15];
+  }
+}

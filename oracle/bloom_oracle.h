@@ -1,0 +1,86 @@
+/*
+ * bloom_oracle.h — CPU restatement of the reference Bloom filter.
+ *
+ * TEST INFRASTRUCTURE ONLY. This is the parity checker for the HIP path in
+ * lsmt_amd/csrc. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it. The product path (libcassbloom.so) never
+ * links, calls or falls back to it.
+ *
+ * Restates /root/reference/src/bloom.rs (mweiden/lsmt, crate `cass`):
+ *   storage    : one byte per bit, 0/1         (Vec<bool>, src/bloom.rs:4-7,17-21)
+ *   hashes     : u64 wrapping djb2 (x33, seed 5381) and x31 (seed 0) over
+ *                the key's bytes, index = h % m  (src/bloom.rs:26-37)
+ *   insert     : sets bits[a] and bits[b]       (src/bloom.rs:40-44)
+ *   may_contain: bits[a] && bits[b], short-circuit (src/bloom.rs:48-51)
+ *   to/from_bytes: prost encoding of `repeated bool bits = 1` (packed)
+ *                  (src/bloom.rs:9-13,54-77)
+ *
+ * Parity pinning: the Rust reference cannot be compiled in this image (no
+ * cargo/rustc). This restatement is pinned by the reference's own test
+ * assertions (tests/bloom_test.rs:3-8, tests/sstable_local_test.rs:12) and by
+ * known-answer vectors from an independent Python big-int restatement
+ * (tests/golden/make_golden.py). See DESIGN.md "Parity".
+ */
+#ifndef CASSBLOOM_ORACLE_H
+#define CASSBLOOM_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OB_OK 0
+#define OB_EINVAL (-1)
+#define OB_EZEROM (-2)   /* reference panics: `h % 0` at src/bloom.rs:36 */
+#define OB_ENOMEM (-3)
+#define OB_EDECODE (-5)  /* reference panics: `decode(..).unwrap()` at src/bloom.rs:75 */
+
+typedef struct ob_filter {
+  uint8_t* bits; /* m bytes, each 0 or 1 — the Vec<bool> layout */
+  uint64_t m;
+} ob_filter;
+
+/* BloomFilter::new(size) — src/bloom.rs:17-21. m == 0 is legal (the panic is
+ * deferred to the first hashes() call, as in the reference). */
+int ob_new(ob_filter* f, uint64_t m);
+void ob_free(ob_filter* f);
+
+/* The two raw u64 hashes before the modulo — src/bloom.rs:28-34. */
+void ob_raw_hashes(const uint8_t* key, uint64_t len, uint64_t* h1, uint64_t* h2);
+/* hashes(): (h1 % m, h2 % m) — src/bloom.rs:35-36. OB_EZEROM if m == 0. */
+int ob_hashes(const uint8_t* key, uint64_t len, uint64_t m, uint64_t* a, uint64_t* b);
+
+int ob_insert(ob_filter* f, const uint8_t* key, uint64_t len);
+/* returns 1/0, or OB_EZEROM */
+int ob_may_contain(const ob_filter* f, const uint8_t* key, uint64_t len);
+
+/* Batched restatements of the callers' per-key loops:
+ * build  — SsTable::create's loop (src/sstable.rs:62-65), keys in order;
+ * probe  — Database::get's per-table probe (src/lib.rs:129-134) for every
+ *          (key, table) pair. hits is [nf][ceil(n/64)] u64, bit k%64 of word
+ *          k/64 set iff filter f may_contain key k; tail bits are zero. */
+int ob_insert_fixed(ob_filter* f, const uint8_t* keys, uint32_t key_len, uint64_t n);
+int ob_insert_var(ob_filter* f, const uint8_t* bytes, const uint64_t* offsets, uint64_t n);
+int ob_probe_fixed(const ob_filter* const* fs, uint32_t nf, const uint8_t* keys,
+                   uint32_t key_len, uint64_t n, uint64_t* hits, int threads);
+int ob_probe_var(const ob_filter* const* fs, uint32_t nf, const uint8_t* bytes,
+                 const uint64_t* offsets, uint64_t n, uint64_t* hits, int threads);
+
+/* prost encoding of BloomProto{bits} (to_bytes, src/bloom.rs:66-70):
+ * m == 0 -> empty; else 0x0A, varint(m), m bytes of 0/1. Returns the encoded
+ * length; writes only if cap is large enough. */
+uint64_t ob_encode(const ob_filter* f, uint8_t* out, uint64_t cap);
+/* prost decoding (from_bytes, src/bloom.rs:74-77): accepts packed and
+ * unpacked field-1 elements, skips unknown fields; OB_EDECODE on malformed. */
+int ob_decode(const uint8_t* in, uint64_t len, ob_filter* out);
+
+/* Synthetic workload keys: 16 lowercase hex chars, MSB
+ * nibble first, of splitmix64(seed * 2^32 + i). out is n*16 bytes. */
+void ob_gen_keys(uint64_t seed, uint64_t first, uint64_t n, uint8_t* out);
+uint64_t ob_splitmix64(uint64_t x);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

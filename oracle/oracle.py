@@ -1,0 +1,183 @@
+"""ctypes wrapper over the C oracle (oracle/bloom_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the parity checker / CPU baseline. The product
+path (lsmt_amd) never imports this module.
+
+Restates /root/reference/src/bloom.rs:17-77 (see bloom_oracle.h for the
+line-by-line mapping).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+OB_OK = 0
+OB_EINVAL = -1
+OB_EZEROM = -2
+OB_ENOMEM = -3
+OB_EDECODE = -5
+
+
+class _Filter(ctypes.Structure):
+    _fields_ = [("bits", ctypes.POINTER(ctypes.c_uint8)), ("m", ctypes.c_uint64)]
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+        FP = ctypes.POINTER(_Filter)
+        L.ob_new.argtypes = [FP, u64]
+        L.ob_free.argtypes = [FP]
+        L.ob_free.restype = None
+        L.ob_raw_hashes.argtypes = [P, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+        L.ob_raw_hashes.restype = None
+        L.ob_hashes.argtypes = [P, u64, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+        L.ob_insert.argtypes = [FP, P, u64]
+        L.ob_may_contain.argtypes = [FP, P, u64]
+        L.ob_insert_fixed.argtypes = [FP, P, u32, u64]
+        L.ob_insert_var.argtypes = [FP, P, P, u64]
+        L.ob_probe_fixed.argtypes = [P, u32, P, u32, u64, P, i32]
+        L.ob_probe_var.argtypes = [P, u32, P, P, u64, P, i32]
+        L.ob_encode.argtypes = [FP, P, u64]
+        L.ob_encode.restype = u64
+        L.ob_decode.argtypes = [P, u64, FP]
+        L.ob_gen_keys.argtypes = [u64, u64, u64, P]
+        L.ob_gen_keys.restype = None
+        L.ob_splitmix64.argtypes = [u64]
+        L.ob_splitmix64.restype = u64
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OracleFilter:
+    """Byte-per-bit Bloom filter — the reference's `BloomFilter` on the CPU."""
+
+    def __init__(self, m: int, _raw: _Filter | None = None):
+        self._f = _Filter()
+        if _raw is not None:
+            self._f = _raw
+        else:
+            rc = lib().ob_new(ctypes.byref(self._f), m)
+            if rc:
+                raise MemoryError(rc)
+
+    def __del__(self):
+        try:
+            lib().ob_free(ctypes.byref(self._f))
+        except Exception:
+            pass
+
+    @property
+    def m(self) -> int:
+        return int(self._f.m)
+
+    def bools(self) -> np.ndarray:
+        """The Vec<bool> array (m bytes of 0/1), copied."""
+        if self.m == 0:
+            return np.zeros(0, np.uint8)
+        return np.ctypeslib.as_array(self._f.bits, shape=(self.m,)).copy()
+
+    def insert(self, key: bytes) -> None:
+        buf = ctypes.create_string_buffer(key, len(key))
+        rc = lib().ob_insert(ctypes.byref(self._f), buf, len(key))
+        if rc == OB_EZEROM:
+            raise ZeroDivisionError("attempt to calculate the remainder with a divisor of zero")
+
+    def may_contain(self, key: bytes) -> bool:
+        buf = ctypes.create_string_buffer(key, len(key))
+        rc = lib().ob_may_contain(ctypes.byref(self._f), buf, len(key))
+        if rc == OB_EZEROM:
+            raise ZeroDivisionError("attempt to calculate the remainder with a divisor of zero")
+        return bool(rc)
+
+    def insert_fixed(self, keys: np.ndarray) -> None:
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        n, kl = keys.shape
+        rc = lib().ob_insert_fixed(ctypes.byref(self._f), _ptr(keys), kl, n)
+        if rc:
+            raise RuntimeError(f"ob_insert_fixed rc={rc}")
+
+    def insert_var(self, data: np.ndarray, offsets: np.ndarray) -> None:
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        rc = lib().ob_insert_var(ctypes.byref(self._f), _ptr(data), _ptr(offsets), len(offsets) - 1)
+        if rc:
+            raise RuntimeError(f"ob_insert_var rc={rc}")
+
+    def to_bytes(self) -> bytes:
+        L = lib()
+        n = L.ob_encode(ctypes.byref(self._f), None, 0)
+        out = np.zeros(max(n, 1), np.uint8)
+        L.ob_encode(ctypes.byref(self._f), _ptr(out), n)
+        return out[:n].tobytes()
+
+    @classmethod
+    def from_bytes(cls, data: bytes) -> "OracleFilter":
+        raw = _Filter()
+        buf = np.frombuffer(data, np.uint8).copy() if data else np.zeros(1, np.uint8)
+        rc = lib().ob_decode(_ptr(buf), len(data), ctypes.byref(raw))
+        if rc:
+            raise ValueError(f"decode error rc={rc}")
+        return cls(0, _raw=raw)
+
+
+def raw_hashes(key: bytes) -> tuple[int, int]:
+    h1, h2 = ctypes.c_uint64(), ctypes.c_uint64()
+    buf = ctypes.create_string_buffer(key, len(key))
+    lib().ob_raw_hashes(buf, len(key), ctypes.byref(h1), ctypes.byref(h2))
+    return h1.value, h2.value
+
+
+def probe_fixed(filters, keys: np.ndarray, threads: int = 1) -> np.ndarray:
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    n, kl = keys.shape
+    nf = len(filters)
+    words = (n + 63) // 64
+    hits = np.zeros((nf, words), np.uint64)
+    arr = (ctypes.POINTER(_Filter) * max(nf, 1))(*[ctypes.pointer(f._f) for f in filters])
+    rc = lib().ob_probe_fixed(ctypes.cast(arr, ctypes.c_void_p), nf, _ptr(keys), kl, n, _ptr(hits), threads)
+    if rc:
+        raise RuntimeError(f"ob_probe_fixed rc={rc}")
+    return hits
+
+
+def probe_var(filters, data: np.ndarray, offsets: np.ndarray, threads: int = 1) -> np.ndarray:
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offsets) - 1
+    nf = len(filters)
+    hits = np.zeros((nf, (n + 63) // 64), np.uint64)
+    arr = (ctypes.POINTER(_Filter) * max(nf, 1))(*[ctypes.pointer(f._f) for f in filters])
+    rc = lib().ob_probe_var(ctypes.cast(arr, ctypes.c_void_p), nf, _ptr(data if len(data) else np.zeros(1, np.uint8)),
+                            _ptr(offsets), n, _ptr(hits), threads)
+    if rc:
+        raise RuntimeError(f"ob_probe_var rc={rc}")
+    return hits
+
+
+def gen_keys(seed: int, n: int, first: int = 0) -> np.ndarray:
+    out = np.empty((n, 16), np.uint8)
+    if n:
+        lib().ob_gen_keys(seed, first, n, _ptr(out))
+    return out

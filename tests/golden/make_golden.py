@@ -1,0 +1,234 @@
+"""Generate the committed golden fixtures for the Bloom-filter path.
+
+Independent restatement of /root/reference/src/bloom.rs:26-51 in Python
+big-int arithmetic (masked to 64 bits = Rust's wrapping u64), plus a numpy
+vectorised restatement for the large configs; the two are cross-checked here
+on every small case before anything is written. Neither imports the C oracle
+or the product library, so the fixtures pin both of them independently.
+
+The Rust reference cannot be built in this image (no cargo/rustc): the
+fixtures therefore follow the reference's formula, and are anchored on the
+reference's own tests: tests/bloom_test.rs:3-8 (m=128, "hello" present),
+tests/sstable_test.rs:10-14 ("a","b","c" at m=1024), tests/lsm_flush_test.rs
+(m=1024, "k1","k2","missing"), tests/sstable_local_test.rs:7-12 ("k").
+
+Usage:  python tests/golden/make_golden.py      (~1-2 min; writes golden.json)
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+
+import numpy as np
+
+M64 = (1 << 64) - 1
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+# ---- pure-Python big-int restatement -----------------------------------------
+
+def raw_hashes(key: bytes) -> tuple[int, int]:
+    h1, h2 = 5381, 0  # src/bloom.rs:28,30
+    for b in key:  # src/bloom.rs:31-34
+        h1 = ((h1 << 5) + h1 + b) & M64
+        h2 = (h2 * 31 + b) & M64
+    return h1, h2
+
+
+def positions(key: bytes, m: int) -> tuple[int, int]:
+    h1, h2 = raw_hashes(key)
+    return h1 % m, h2 % m  # src/bloom.rs:35-36
+
+
+def splitmix64(x: int) -> int:
+    z = (x + 0x9E3779B97F4A7C15) & M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
+
+
+def key(seed: int, i: int) -> bytes:
+    return format(splitmix64(((seed << 32) + i) & M64), "016x").encode()
+
+
+# ---- numpy restatement (large configs) -----------------------------------------
+
+def np_keys(seed: int, idx: np.ndarray) -> np.ndarray:
+    x = np.uint64((seed << 32) & M64) + idx.astype(np.uint64)
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    z = z ^ (z >> np.uint64(31))
+    hexd = np.frombuffer(b"0123456789abcdef", np.uint8)
+    sh = np.arange(60, -4, -4, dtype=np.uint64)
+    return hexd[((z[:, None] >> sh[None, :]) & np.uint64(15)).astype(np.intp)]
+
+
+def np_raw_hashes(keys: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    n = keys.shape[0]
+    h1 = np.full(n, 5381, np.uint64)
+    h2 = np.zeros(n, np.uint64)
+    with np.errstate(over="ignore"):
+        for j in range(keys.shape[1]):
+            b = keys[:, j].astype(np.uint64)
+            h1 = (h1 << np.uint64(5)) + h1 + b
+            h2 = h2 * np.uint64(31) + b
+    return h1, h2
+
+
+def np_build(keys: np.ndarray, m: int) -> np.ndarray:
+    h1, h2 = np_raw_hashes(keys)
+    bits = np.zeros(m, np.uint8)
+    bits[(h1 % np.uint64(m)).astype(np.int64)] = 1
+    bits[(h2 % np.uint64(m)).astype(np.int64)] = 1
+    return bits
+
+
+def np_probe(bits: np.ndarray, keys: np.ndarray) -> np.ndarray:
+    m = bits.shape[0]
+    h1, h2 = np_raw_hashes(keys)
+    a = bits[(h1 % np.uint64(m)).astype(np.int64)]
+    b = bits[(h2 % np.uint64(m)).astype(np.int64)]
+    return (a & b).astype(bool)
+
+
+def _pack64(bits01: np.ndarray) -> np.ndarray:
+    """bool[n] -> uint64[ceil(n/64)]: bit k%64 of word k/64, LSB-first, tail zero."""
+    words = (bits01.shape[0] + 63) // 64
+    padded = np.zeros(words * 64, np.uint8)
+    padded[: bits01.shape[0]] = bits01
+    return np.packbits(padded, bitorder="little").view("<u8").astype(np.uint64)
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def lookups(n: int, nf: int, kpf: int, base: int, absent: int) -> np.ndarray:
+    i = np.arange(n, dtype=np.uint64)
+    out = np.empty((n, 16), np.uint8)
+    j = i[0::2] // np.uint64(2)
+    f = j % np.uint64(nf)
+    kidx = (j // np.uint64(nf)) % np.uint64(kpf)
+    ev = np.empty((len(j), 16), np.uint8)
+    for fs in range(nf):
+        sel = f == np.uint64(fs)
+        ev[sel] = np_keys(base + fs, kidx[sel])
+    out[0::2] = ev
+    out[1::2] = np_keys(absent, i[1::2])
+    return out
+
+
+def main() -> None:
+    g: dict = {"source": "tests/golden/make_golden.py (Python big-int + numpy restatement of src/bloom.rs:26-51)"}
+
+    # 1. known-answer raw hashes and positions
+    kat_keys = [b"", b"hello", b"k", b"a", b"b", b"c", b"k1", b"k2", b"missing", b"0123456789abcdef",
+                "ns:pk|ck".encode(), "utf8-é✓".encode(), bytes(range(256)), b"\xff" * 40]
+    ms = [1, 2, 3, 128, 1000, 1024, 100003, 1 << 17, 1 << 25, 1 << 26, 1 << 27, (1 << 32) + 15, (1 << 61) - 1]
+    kat = []
+    for k in kat_keys:
+        h1, h2 = raw_hashes(k)
+        kat.append({"key_hex": k.hex(), "h1": str(h1), "h2": str(h2),
+                    "pos": {str(m): [h1 % m, h2 % m] for m in ms}})
+    g["kat"] = kat
+    assert positions(b"hello", 128) == (25, 82)          # pins tests/bloom_test.rs:5-7
+    assert positions(b"hello", 1024) == (153, 210)
+    assert positions(b"k", 1024) == (528, 107)            # tests/sstable_local_test.rs:7
+    assert positions(b"0123456789abcdef", 1 << 27) == (84411015, 17008296)
+
+    # 2. the reference's own test scenarios as bit arrays (m = 1024 everywhere in the product)
+    def build_py(keys, m):
+        bits = bytearray(m)
+        for k in keys:
+            a, b = positions(k, m)
+            bits[a] = 1
+            bits[b] = 1
+        return bytes(bits)
+
+    def may_py(bits, k):
+        a, b = positions(k, len(bits))
+        return bool(bits[a]) and bool(bits[b])
+
+    scen = {}
+    for name, m, ins, probes in [
+        ("bloom_test", 128, [b"hello"], [b"hello", b"world", b""]),
+        ("sstable_test", 1024, [b"a", b"b", b"c"], [b"a", b"b", b"c", b"d"]),
+        ("lsm_flush_test", 1024, [b"k1", b"k2"], [b"k1", b"k2", b"missing"]),
+        ("sstable_local_test", 1024, [b"k"], [b"k", b"v"]),
+    ]:
+        bits = build_py(ins, m)
+        scen[name] = {"m": m, "insert_hex": [k.hex() for k in ins], "set_bits": [i for i, v in enumerate(bits) if v],
+                      "probe_hex": [k.hex() for k in probes], "probe": [may_py(bits, k) for k in probes],
+                      "to_bytes_hex": (bytes([0x0A]) + _varint(m) + bits).hex()}
+    assert scen["bloom_test"]["probe"][0] is True
+    assert scen["lsm_flush_test"]["probe"][2] is False
+    g["scenarios"] = scen
+
+    # 3. synthetic keys: python vs numpy, first 2000 keys of seed 1 and their positions
+    idx = np.arange(2000, dtype=np.uint64)
+    npk = np_keys(1, idx)
+    pyk = [key(1, i) for i in range(2000)]
+    assert all(npk[i].tobytes() == pyk[i] for i in range(2000))
+    h1n, h2n = np_raw_hashes(npk)
+    for i in range(2000):
+        assert (int(h1n[i]), int(h2n[i])) == raw_hashes(pyk[i])
+    g["keys_seed1_first8"] = [k.decode() for k in pyk[:8]]
+    g["keys_seed1_2000_sha256"] = hashlib.sha256(b"".join(pyk)).hexdigest()
+    g["hashes_seed1_2000"] = {"h1_sha256": sha(h1n.astype("<u8")), "h2_sha256": sha(h2n.astype("<u8"))}
+
+    # 4. C1: 10k keys key(1,i) into m=2^17 and m=100003; FP on 100k absent keys key(2,i)
+    c1 = {}
+    k10 = np_keys(1, np.arange(10_000, dtype=np.uint64))
+    absent = np_keys(2, np.arange(100_000, dtype=np.uint64))
+    for m in (1 << 17, 100003):
+        bits = np_build(k10, m)
+        # cross-check the numpy build against the big-int one
+        assert bits.tobytes() == build_py([bytes(r) for r in k10], m)
+        present = np_probe(bits, k10)
+        assert present.all()
+        fp = np_probe(bits, absent)
+        c1[str(m)] = {"n": 10_000, "bools_sha256": sha(bits), "popcount": int(bits.sum()),
+                      "fp_absent_100k": int(fp.sum()), "fp_hits_sha256": sha(_pack64(fp))}
+    g["c1"] = c1
+
+    # 5. C2: 1M keys key(1,i) -> m = 2^27
+    n2, m2 = 1 << 20, 1 << 27
+    bits = np_build(np_keys(1, np.arange(n2, dtype=np.uint64)), m2)
+    g["c2"] = {"n": n2, "m": m2, "bools_sha256": sha(bits), "popcount": int(bits.sum()),
+               "packed_sha256": sha(np.packbits(bits, bitorder="little"))}
+    del bits
+
+    # 6. C3: 32 filters m=2^26 from key(100+f, i<2^19); 2^20 lookups
+    nf, m3, kpf, nl = 32, 1 << 26, 1 << 19, 1 << 20
+    lk = lookups(nl, nf, kpf, 100, 999)
+    rows = []
+    pops = []
+    for f in range(nf):
+        b = np_build(np_keys(100 + f, np.arange(kpf, dtype=np.uint64)), m3)
+        pops.append(int(b.sum()))
+        rows.append(np_probe(b, lk))
+    hits = np.stack([_pack64(r) for r in rows])
+    g["c3"] = {"nf": nf, "m": m3, "keys_per_filter": kpf, "n_lookups": nl,
+               "lookups_sha256": sha(lk), "filter_popcounts": pops,
+               "hits_sha256": sha(hits.astype("<u8")), "hits_popcount": int(sum(int(r.sum()) for r in rows)),
+               "hits_per_filter": [int(r.sum()) for r in rows]}
+
+    with open(os.path.join(HERE, "golden.json"), "w") as fh:
+        json.dump(g, fh, indent=1, sort_keys=True)
+    print("wrote", os.path.join(HERE, "golden.json"))
+
+
+def _varint(v: int) -> bytes:
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,281 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the
+golden fixtures. Bit-exact for every bit array and every hit bitmap.
+
+Reference semantics: /root/reference/src/bloom.rs:17-77; callers
+src/sstable.rs:59-65,138 and src/lib.rs:129-134.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from lsmt_amd import workload
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+DIRECT, TILED, AUTO = 1, 2, 0
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(params=[DIRECT, TILED], ids=["direct", "tiled"])
+def path(request, gpu):
+    gpu.set_path(request.param)
+    yield request.param
+    gpu.set_path(AUTO)
+
+
+def build_pair(gpu, m, keys):
+    g = gpu.BloomFilter(m)
+    g.insert_batch(keys)
+    o = oracle.OracleFilter(m)
+    if isinstance(keys, np.ndarray):
+        o.insert_fixed(keys)
+    else:
+        for k in keys:
+            o.insert(k.encode() if isinstance(k, str) else k)
+    return g, o
+
+
+# ---- the reference's own tests, through the GPU path ----------------------------
+
+def test_reference_bloom_test(gpu):
+    # tests/bloom_test.rs:3-8
+    b = gpu.BloomFilter.new(128)
+    b.insert("hello")
+    assert b.may_contain("hello")
+    assert list(np.flatnonzero(b.bools())) == [25, 82]
+
+
+def test_reference_scenarios(gpu, golden):
+    for name, s in golden["scenarios"].items():
+        b = gpu.BloomFilter(s["m"])
+        for k in s["insert_hex"]:
+            b.insert(bytes.fromhex(k))  # queued, flushed as one batch
+        assert [b.may_contain(bytes.fromhex(k)) for k in s["probe_hex"]] == s["probe"], name
+        assert list(np.flatnonzero(b.bools())) == s["set_bits"], name
+        assert b.to_bytes().hex() == s["to_bytes_hex"], name
+
+
+def test_sstable_local_roundtrip(gpu):
+    # tests/sstable_local_test.rs:12 — loaded.bloom.to_bytes() == table.bloom.to_bytes()
+    b = gpu.BloomFilter(1024)
+    b.insert("k")
+    data = b.to_bytes()
+    assert gpu.BloomFilter.from_bytes(data).to_bytes() == data
+    p = b.to_proto()
+    assert gpu.BloomFilter.from_proto(p).to_bytes() == data
+
+
+# ---- build parity ---------------------------------------------------------------------
+
+@pytest.mark.parametrize("m", [1, 2, 3, 64, 1000, 1024, 4097, 100003, 1 << 17, (1 << 20) + 7,
+                               1 << 21, 3 << 20, 1 << 22])
+def test_build_fixed16(gpu, path, m):
+    keys = workload.key_range(1, 20_000)
+    g, o = build_pair(gpu, m, keys)
+    assert np.array_equal(g.bools(), o.bools())
+
+
+@pytest.mark.parametrize("key_len", [0, 1, 7, 15, 17, 33])
+def test_build_fixed_other_lengths(gpu, path, key_len):
+    rng = np.random.default_rng(key_len)
+    keys = rng.integers(0, 256, size=(5000, key_len), dtype=np.uint8)
+    for m in (4099, 1 << 20):
+        g, o = build_pair(gpu, m, keys)
+        assert np.array_equal(g.bools(), o.bools()), (key_len, m)
+
+
+def test_build_var(gpu, path):
+    rng = np.random.default_rng(7)
+    data, offs = workload.var_keys(rng, 30_000, max_len=64)
+    keys = [bytes(data[offs[i]:offs[i + 1]]) for i in range(len(offs) - 1)]
+    for m in (100003, 1 << 20, (1 << 21) + 1):
+        g = gpu.BloomFilter(m)
+        g.insert_batch(gpu.KeyBatch(n=len(keys), data=data, offsets=offs))
+        o = oracle.OracleFilter(m)
+        o.insert_var(data, offs)
+        assert np.array_equal(g.bools(), o.bools()), m
+        # the list-of-bytes form builds the same ragged batch
+        h = gpu.BloomFilter(m)
+        h.insert_batch(keys)
+        assert np.array_equal(h.bools(), o.bools())
+
+
+def test_build_unaligned_fixed16(gpu, path):
+    keys = workload.key_range(9, 10_001)
+    raw = np.zeros(16 * 10_001 + 3, np.uint8)
+    view = raw[3:].reshape(10_001, 16)  # 3-byte misaligned rows
+    view[:] = keys
+    g = gpu.BloomFilter(1 << 20)
+    g.insert_batch(gpu.KeyBatch(n=10_001, key_len=16, keys=view))
+    o = oracle.OracleFilter(1 << 20)
+    o.insert_fixed(keys)
+    assert np.array_equal(g.bools(), o.bools())
+
+
+def test_build_incremental_and_idempotent(gpu, path):
+    a = workload.key_range(11, 50_000)
+    b = workload.key_range(12, 70_000)
+    m = 1 << 21
+    g1 = gpu.BloomFilter(m)
+    g1.insert_batch(a)
+    g1.insert_batch(b)  # second batch ORs into a non-empty filter
+    g2 = gpu.BloomFilter(m)
+    g2.insert_batch(np.concatenate([b, a]))
+    g2.insert_batch(a)  # idempotent
+    o = oracle.OracleFilter(m)
+    o.insert_fixed(a)
+    o.insert_fixed(b)
+    assert np.array_equal(g1.bools(), o.bools())
+    assert np.array_equal(g2.packed(), g1.packed())
+
+
+@pytest.mark.parametrize("m", [(1 << 32) + 15, 1 << 33])
+def test_build_64bit_modes(gpu, m):
+    # m > 2^32: 64-bit state (mask or exact 64-bit fastmod). Checked by set positions.
+    keys = workload.key_range(21, 4000)
+    g = gpu.BloomFilter(m)
+    g.insert_batch(keys)
+    pos = set()
+    for k in keys:
+        h1, h2 = oracle.raw_hashes(bytes(k))
+        pos.add(h1 % m)
+        pos.add(h2 % m)
+    words = g.packed()
+    nz = np.flatnonzero(words)
+    got = set()
+    for w in nz:
+        v = int(words[w])
+        while v:
+            lsb = v & -v
+            got.add(int(w) * 32 + lsb.bit_length() - 1)
+            v ^= lsb
+    assert got == pos
+    assert g.may_contain_batch(keys).all()
+
+
+def test_c2_build_golden(gpu, golden, path):
+    g = golden["c2"]
+    f = gpu.BloomFilter(g["m"])
+    f.insert_batch(workload.c2_build_keys(g["n"]))
+    assert sha(f.bools()) == g["bools_sha256"]
+    assert sha(f.packed().view(np.uint8)) == g["packed_sha256"]
+
+
+# ---- probe parity ------------------------------------------------------------------
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 4095, 70_001])
+def test_probe_sizes(gpu, path, n):
+    m = 1 << 20
+    filters, refs = [], []
+    for f in range(5):
+        g, o = build_pair(gpu, m, workload.key_range(100 + f, 30_000))
+        filters.append(g)
+        refs.append(o)
+    look = workload.probe_lookups(n, 5, 30_000, seed_base=100, absent_seed=999)
+    assert np.array_equal(gpu.probe(filters, look), oracle.probe_fixed(refs, look))
+
+
+def test_probe_mixed_m_and_many_filters(gpu, path):
+    ms = [1024, 100003, 1 << 20, (1 << 20) + 5, 1 << 21]
+    filters, refs = [], []
+    for f in range(70):  # > 64 filters: several launches per size group
+        m = ms[f % len(ms)]
+        g, o = build_pair(gpu, m, workload.key_range(300 + f, 3000))
+        filters.append(g)
+        refs.append(o)
+    look = workload.probe_lookups(100_000, 70, 3000, seed_base=300, absent_seed=998)
+    assert np.array_equal(gpu.probe(filters, look), oracle.probe_fixed(refs, look))
+
+
+def test_probe_var_keys(gpu, path):
+    rng = np.random.default_rng(3)
+    data, offs = workload.var_keys(rng, 80_000, max_len=40)
+    half = 40_000
+    filters, refs = [], []
+    for m in (4099, 1 << 20, 1 << 21):
+        g = gpu.BloomFilter(m)
+        g.insert_batch(gpu.KeyBatch(n=half, data=data, offsets=offs[: half + 1]))
+        o = oracle.OracleFilter(m)
+        o.insert_var(data, offs[: half + 1])
+        filters.append(g)
+        refs.append(o)
+    hits = gpu.probe(filters, gpu.KeyBatch(n=80_000, data=data, offsets=offs))
+    assert np.array_equal(hits, oracle.probe_var(refs, data, offs))
+
+
+def test_probe_empty_and_zero(gpu):
+    f = gpu.BloomFilter(1 << 20)
+    f.insert_batch(workload.key_range(1, 10))
+    h = gpu.probe([f], np.zeros((0, 16), np.uint8))
+    assert h.shape == (1, 0)
+    z = gpu.BloomFilter(0)
+    with pytest.raises(ZeroDivisionError):
+        z.insert("x")
+    with pytest.raises(ZeroDivisionError):
+        z.may_contain("x")
+    with pytest.raises(ZeroDivisionError):
+        gpu.probe([f, z], workload.key_range(1, 3))
+    assert z.to_bytes() == b""
+    assert gpu.BloomFilter.from_bytes(b"").m == 0
+
+
+def test_c3_probe_golden(gpu, golden, path):
+    g = golden["c3"]
+    filters = []
+    for f in range(g["nf"]):
+        b = gpu.BloomFilter(g["m"])
+        b.insert_batch(workload.c3_filter_keys(f, g["keys_per_filter"]))
+        filters.append(b)
+    look = workload.c3_lookups(g["n_lookups"], g["nf"], g["keys_per_filter"])
+    hits = gpu.probe(filters, look)
+    assert sha(hits.astype("<u8")) == g["hits_sha256"]
+
+
+# ---- codec -------------------------------------------------------------------------
+
+def test_codec_matches_oracle(gpu):
+    for m in (1, 127, 128, 129, 16384, 100003):
+        g, o = build_pair(gpu, m, workload.key_range(4, 500))
+        data = g.to_bytes()
+        assert data == o.to_bytes()
+        back = gpu.BloomFilter.from_bytes(data)
+        assert back.m == m and np.array_equal(back.bools(), o.bools())
+    unpacked = bytes([0x08, 0x01, 0x08, 0x00, 0x08, 0x05, 0x10, 0x07, 0x0A, 0x02, 0x00, 0x81, 0x01])
+    f = gpu.BloomFilter.from_bytes(unpacked)
+    assert list(f.bools()) == list(oracle.OracleFilter.from_bytes(unpacked).bools())
+    for bad in (b"\x0a", b"\x0a\x05\x01", b"\x00", b"\x0d\x00\x00\x00\x00", b"\xff" * 11):
+        with pytest.raises(ValueError):
+            gpu.BloomFilter.from_bytes(bad)
+
+
+def test_packed_import_masks_tail(gpu):
+    f = gpu.BloomFilter(40)
+    f.load_packed(np.array([0xFFFFFFFF, 0xFFFFFFFF], np.uint32))
+    assert int(f.bools().sum()) == 40
+    assert f.packed()[1] == 0xFF
+
+
+# ---- device-resident buffers and streams ----------------------------------------
+
+def test_device_resident_keys_and_hits(gpu):
+    import torch
+    dev = torch.device("cuda:0")
+    keys = workload.key_range(100, 200_000)
+    dk = torch.from_numpy(keys).to(dev)
+    s = torch.cuda.Stream()
+    f = gpu.BloomFilter(1 << 22)
+    with torch.cuda.stream(s):
+        f.insert_batch(gpu.DeviceKeys(dk), stream=s)
+        look = torch.from_numpy(workload.probe_lookups(300_000, 1, 200_000, 100, 999)).to(dev)
+        out = torch.zeros((1, (300_000 + 63) // 64), dtype=torch.int64, device=dev)
+        gpu.probe([f], gpu.DeviceKeys(look), out=out, stream=s)
+    s.synchronize()
+    o = oracle.OracleFilter(1 << 22)
+    o.insert_fixed(keys)
+    expect = oracle.probe_fixed([o], look.cpu().numpy())
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), expect)
