@@ -47,6 +47,14 @@ def load():
         raise ExtensionMissing(
             f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
             "or `make -C lsmt_amd/csrc` (gfx950 HIP extension; no CPU fallback exists)")
+    # torch wheels bundle their own libamdhip64.so.7 (same soname as
+    # /opt/rocm's). Whichever loads first serves the whole process, and torch
+    # cannot run on a runtime it did not load itself, so when torch is present
+    # it is imported first and this library binds to torch's HIP runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     P, u8p, u32, u64, i32 = ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
     pp = ctypes.POINTER(ctypes.c_void_p)

@@ -125,8 +125,9 @@ struct DeviceGuard {
 
 uint64_t alloc_words_for(uint64_t m) {
   // Pad to whole 2^18-bit tiles (the largest LDS tile) so tiled passes never
-  // read or write past the allocation; small filters pad to 2^12 bits.
-  const uint64_t align = m >= (1ull << 13) ? cb::kTileAlignBits : (1ull << 12);
+  // read or write past the allocation; small filters pad to one 2^16-bit
+  // tile (the smallest probe tile).
+  const uint64_t align = m >= cb::kSmallAlignBits ? cb::kTileAlignBits : cb::kSmallAlignBits;
   const uint64_t bits = std::max<uint64_t>((m + align - 1) / align * align, align);
   return bits / 32;
 }
@@ -137,16 +138,26 @@ hipError_t ensure_zeroed(const cb_filter* cf, hipStream_t s) {
   return hipSuccess;
 }
 
-bool tiled_ok(uint64_t m) { return m <= (1ull << 30) && m >= 1; }
+// Every tiled pass reads/writes whole tiles [0, T * 2^tb): refuse to launch
+// one the allocation does not cover (a safety net over alloc_words_for).
+bool covers(const cb_filter* f, const TilePlan& p) {
+  return cb::plan_ok(p) && ((uint64_t)p.T << p.tb) <= f->nwords_alloc * 32;
+}
+
+// Largest m a tiled pass covers: kMaxTiles tiles of the largest tile size.
+bool build_tiled_ok(uint64_t m) { return m >= 1 && m <= (uint64_t)cb::kMaxTiles << cb::kMaxTileBits; }
+bool probe_tiled_ok(uint64_t m) {
+  return m >= 1 && m <= (uint64_t)cb::kMaxTiles << cb::kMaxProbeTileBits;
+}
 
 int choose_build_path(uint64_t m, uint64_t n) {
-  if (g_path_override == PATH_DIRECT || !tiled_ok(m)) return PATH_DIRECT;
+  if (g_path_override == PATH_DIRECT || !build_tiled_ok(m)) return PATH_DIRECT;
   if (g_path_override == PATH_TILED) return PATH_TILED;
   return (m >= (1ull << 20) && n >= (1ull << 15)) ? PATH_TILED : PATH_DIRECT;
 }
 
 int choose_probe_path(uint64_t m, uint64_t n, uint32_t nf) {
-  if (g_path_override == PATH_DIRECT || !tiled_ok(m)) return PATH_DIRECT;
+  if (g_path_override == PATH_DIRECT || !probe_tiled_ok(m)) return PATH_DIRECT;
   if (g_path_override == PATH_TILED) return PATH_TILED;
   (void)nf;
   return (m >= (1ull << 20) && n >= (1ull << 16)) ? PATH_TILED : PATH_DIRECT;
@@ -246,6 +257,7 @@ int insert_impl(cb_filter* f, const uint8_t* keys, const uint64_t* offsets, uint
       const int keyk = (sk.keyk == cb::KEY_FIXED16 && ((uintptr_t)ks.bytes & 15)) ? cb::KEY_FIXED
                                                                                    : sk.keyk;
       const TilePlan p = cb::plan_build(f->m, nk);
+      if (!covers(f, p)) return fail(CB_EINVAL, "internal: build tile plan exceeds the filter allocation");
       HIP_TRY(ws.seg.reserve(cb::build_seg_bytes(p), s));
       HIP_TRY(ws.ent.reserve(cb::build_ent_bytes(p), s));
       HIP_TRY(cb::launch_build_tiled(keyk, f->mode, f->words, f->known_zero, ks, nk, f->mp, p,
@@ -324,11 +336,14 @@ int probe_impl(const cb_filter* const* filters, uint32_t nf, const uint8_t* keys
                              ? cb::KEY_FIXED
                              : sk.keyk;
         const TilePlan p = cb::plan_probe(m, nk);
+        for (uint32_t i : idx)
+          if (!covers(filters[i], p))
+            return fail(CB_EINVAL, "internal: probe tile plan exceeds the filter allocation");
         HIP_TRY(ws.seg.reserve(cb::probe_seg_bytes(p), s));
         HIP_TRY(ws.ent.reserve(cb::probe_ent_bytes(p), s));
         HIP_TRY(ws.masks.reserve((size_t)2 * nk * 4, s));
         HIP_TRY(cb::launch_probe_partition(keyk, f0->mode, ks, nk, f0->mp, p, (uint32_t*)ws.seg.p,
-                                           (uint4*)ws.ent.p, s));
+                                           (uint2*)ws.ent.p, s));
         for (size_t g0 = 0; g0 < idx.size(); g0 += cb::kMaxFiltersPerLaunch) {
           FilterPtrs fp{};
           const uint32_t cnt =
@@ -338,7 +353,7 @@ int probe_impl(const cb_filter* const* filters, uint32_t nf, const uint8_t* keys
             fp.row[j] = idx[g0 + j];
           }
           HIP_TRY(cb::launch_probe_tiles(fp, cnt, nk, p, (const uint32_t*)ws.seg.p,
-                                         (const uint4*)ws.ent.p, (uint32_t*)ws.masks.p,
+                                         (const uint2*)ws.ent.p, (uint32_t*)ws.masks.p,
                                          dhits + k0 / 64, hwords, s));
         }
       }

@@ -13,6 +13,12 @@
 //            each filter's tile through LDS, tests bit a from LDS, and reads
 //            bit b from HBM only when bit a is set (the reference's `&&`
 //            short-circuit, src/bloom.rs:50). Results leave as wave64 ballots.
+//
+// Partition layout shared by the tiled kernels: partition block b (C keys)
+// writes its entries sorted by tile into ent[b*estride ...] and, in
+// seg[b*(T+1) + t], the start of tile t's run inside that region
+// (seg[b*(T+1) + T] = the block's total). Tile t's entries are therefore the
+// runs [seg[b][t], seg[b][t+1]) of every block b.
 #include <hip/hip_runtime.h>
 
 #include "kernels.hpp"
@@ -22,15 +28,20 @@ namespace cb {
 
 namespace {
 
-constexpr uint32_t kBlock = 256;
-
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
-// Exclusive scan of arr[0..len) in LDS by the whole 256-thread block; returns
-// the total. wsum: 4 words of LDS scratch. Contains barriers: all threads call.
+// Global (address space 1) pointer types: loads through them are global_load
+// with counted vmcnt waits, never flat_load (which also waits on lgkmcnt).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4* gptr_u4;
+typedef const __attribute__((address_space(1))) uint32_t* gptr_u32;
+
+// Exclusive scan of arr[0..len) in LDS by a whole NT-thread block; returns the
+// total. wsum: NT/64 words of LDS scratch. Contains barriers: all threads call.
+template <uint32_t NT>
 __device__ uint32_t block_exclusive_scan(uint32_t* arr, uint32_t len, uint32_t* wsum) {
   const uint32_t tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
-  const uint32_t per = (len + kBlock - 1) / kBlock;
+  const uint32_t per = (len + NT - 1) / NT;
   const uint32_t beg = min(tid * per, len), end = min(beg + per, len);
   uint32_t s = 0;
   for (uint32_t i = beg; i < end; ++i) s += arr[i];
@@ -44,7 +55,7 @@ __device__ uint32_t block_exclusive_scan(uint32_t* arr, uint32_t len, uint32_t* 
   __syncthreads();
   uint32_t wpre = 0, total = 0;
 #pragma unroll
-  for (uint32_t w = 0; w < kBlock / 64; ++w) {
+  for (uint32_t w = 0; w < NT / 64; ++w) {
     const uint32_t v = wsum[w];
     wpre += (w < wid) ? v : 0u;
     total += v;
@@ -59,11 +70,9 @@ __device__ uint32_t block_exclusive_scan(uint32_t* arr, uint32_t len, uint32_t* 
   return total;
 }
 
-// Segment bookkeeping shared by the tile kernels. For tile t, partition block
-// b wrote its entries for t at ent[b*estride + S[b] .. + cnt_b). After the
-// scan, P[b] is the exclusive prefix of cnt over b ("tile order").
+// Last b with P[b] <= j (P: exclusive prefix of the runs' lengths, P[0] = 0).
 __device__ __forceinline__ uint32_t seg_find(const uint32_t* P, uint32_t nblk, uint32_t j) {
-  uint32_t lo = 0, hi = nblk;  // first b with P[b] > j, minus one
+  uint32_t lo = 0, hi = nblk;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
     if (P[mid] <= j)
@@ -74,7 +83,24 @@ __device__ __forceinline__ uint32_t seg_find(const uint32_t* P, uint32_t nblk, u
   return lo - 1;
 }
 
+// Loads tile t's run table into LDS: S[b] = run start in block b's region,
+// P[b] = exclusive prefix of run lengths. Returns the tile's entry count.
+template <uint32_t NT>
+__device__ uint32_t load_runs(const uint32_t* __restrict__ seg, uint32_t nblk, uint32_t T,
+                              uint32_t t, uint32_t* S, uint32_t* P, uint32_t* wsum) {
+  for (uint32_t b = threadIdx.x; b < nblk; b += NT) {
+    const uint32_t* row = seg + (size_t)b * (T + 1) + t;
+    const uint32_t s0 = row[0], s1 = row[1];
+    S[b] = s0;
+    P[b] = s1 - s0;
+  }
+  __syncthreads();
+  return block_exclusive_scan<NT>(P, nblk, wsum);
+}
+
 // ---------------------------------------------------------------- direct ---
+
+constexpr uint32_t kBlock = 256;
 
 template <int KEYK, int MODE>
 __global__ __launch_bounds__(kBlock) void k_insert_direct(uint32_t* __restrict__ words, KeySrc ks,
@@ -109,8 +135,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_direct(FilterPtrs fp, uint32_t
     for (uint32_t f0 = 0; f0 < nf; f0 += 8) {
       uint32_t va[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        va[i] = (valid && f0 + i < nf) ? fp.w[f0 + i][wa] : 0u;
+      for (int i = 0; i < 8; ++i) va[i] = (valid && f0 + i < nf) ? fp.w[f0 + i][wa] : 0u;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         bool hit = false;
@@ -125,21 +150,24 @@ __global__ __launch_bounds__(kBlock) void k_probe_direct(FilterPtrs fp, uint32_t
 
 // ---------------------------------------------------------------- tiled ----
 
+constexpr uint32_t kPartThreads = 256;
+
 // Partition for build: every key contributes two entries (bit a, bit b), each
-// bucketed by its tile. Per block: LDS histogram with ranks, block scan,
-// LDS staging in tile order, coalesced write of the block's run.
+// bucketed by its tile. Per block: LDS histogram with ranks, block scan, LDS
+// staging in tile order, coalesced writes of the block's run and run table.
 template <int KEYK, int MODE, int KPT>
-__global__ __launch_bounds__(kBlock) void k_part_build(KeySrc ks, uint64_t n, ModP mp, uint32_t tb,
-                                                       uint32_t T, uint32_t* __restrict__ seg,
-                                                       uint32_t nblk, uint32_t* __restrict__ ent) {
-  constexpr uint32_t C = kBlock * KPT;
+__global__ __launch_bounds__(kPartThreads) void k_part_build(KeySrc ks, uint64_t n, ModP mp,
+                                                             uint32_t tb, uint32_t T,
+                                                             uint32_t* __restrict__ seg,
+                                                             uint32_t* __restrict__ ent) {
+  constexpr uint32_t C = kPartThreads * KPT;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t Tp = (T + 4) & ~3u;
   uint32_t* hist = smem;
   uint32_t* stage = smem + Tp;
   uint32_t* wsum = stage + 2 * C;
   const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < Tp; i += kBlock) hist[i] = 0;
+  for (uint32_t i = tid; i < Tp; i += kPartThreads) hist[i] = 0;
   __syncthreads();
 
   const uint64_t kbase = (uint64_t)blockIdx.x * C;
@@ -147,7 +175,7 @@ __global__ __launch_bounds__(kBlock) void k_part_build(KeySrc ks, uint64_t n, Mo
   uint32_t et[2 * KPT], er[2 * KPT], eo[2 * KPT];
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
-    const uint64_t k = kbase + (uint64_t)j * kBlock + tid;
+    const uint64_t k = kbase + (uint64_t)j * kPartThreads + tid;
     et[2 * j] = et[2 * j + 1] = 0xFFFFFFFFu;
     if (k < n) {
       uint64_t a, b;
@@ -162,26 +190,27 @@ __global__ __launch_bounds__(kBlock) void k_part_build(KeySrc ks, uint64_t n, Mo
     }
   }
   __syncthreads();
-  const uint32_t total = block_exclusive_scan(hist, T, wsum);
+  const uint32_t total = block_exclusive_scan<kPartThreads>(hist, T, wsum);
   if (tid == 0) hist[T] = total;
   __syncthreads();
-  for (uint32_t t = tid; t <= T; t += kBlock) seg[(size_t)t * nblk + blockIdx.x] = hist[t];
+  uint32_t* srow = seg + (size_t)blockIdx.x * (T + 1);
+  for (uint32_t t = tid; t <= T; t += kPartThreads) srow[t] = hist[t];
 #pragma unroll
   for (int e = 0; e < 2 * KPT; ++e)
     if (et[e] != 0xFFFFFFFFu) stage[hist[et[e]] + er[e]] = eo[e];
   __syncthreads();
   uint32_t* out = ent + (size_t)blockIdx.x * (2 * C);
-  for (uint32_t i = tid; i < total; i += kBlock) out[i] = stage[i];
+  for (uint32_t i = tid; i < total; i += kPartThreads) out[i] = stage[i];
 }
+
+constexpr uint32_t kTileBuildThreads = 256;
 
 // One workgroup per tile: stage the tile in LDS (zeros if the filter is known
 // empty), OR in every entry of the tile with LDS atomics, write it back.
-__global__ __launch_bounds__(kBlock) void k_tile_build(uint32_t* __restrict__ words, uint32_t tb,
-                                                       uint32_t T,
-                                                       const uint32_t* __restrict__ seg,
-                                                       uint32_t nblk,
-                                                       const uint32_t* __restrict__ ent,
-                                                       uint32_t estride, int fresh) {
+__global__ __launch_bounds__(kTileBuildThreads) void k_tile_build(
+    uint32_t* __restrict__ words, uint32_t tb, uint32_t T, const uint32_t* __restrict__ seg,
+    uint32_t nblk, const uint32_t* __restrict__ ent, uint32_t estride, int fresh) {
+  constexpr uint32_t NT = kTileBuildThreads;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t tw = 1u << (tb - 5);
   const uint32_t nbp = (nblk + 3) & ~3u;
@@ -194,15 +223,9 @@ __global__ __launch_bounds__(kBlock) void k_tile_build(uint32_t* __restrict__ wo
 
   uint4* gt = reinterpret_cast<uint4*>(words + (size_t)t * tw);
   uint4* lt = reinterpret_cast<uint4*>(tile);
-  for (uint32_t i = tid; i < tw / 4; i += kBlock) lt[i] = fresh ? make_uint4(0, 0, 0, 0) : gt[i];
-  for (uint32_t b = tid; b < nblk; b += kBlock) {
-    const uint32_t s0 = seg[(size_t)t * nblk + b], s1 = seg[(size_t)(t + 1) * nblk + b];
-    S[b] = s0;
-    P[b] = s1 - s0;
-  }
-  __syncthreads();
-  const uint32_t E = block_exclusive_scan(P, nblk, wsum);
-  const uint32_t per = (E + kBlock - 1) / kBlock;
+  for (uint32_t i = tid; i < tw / 4; i += NT) lt[i] = fresh ? make_uint4(0, 0, 0, 0) : gt[i];
+  const uint32_t E = load_runs<NT>(seg, nblk, T, t, S, P, wsum);
+  const uint32_t per = (E + NT - 1) / NT;
   const uint32_t j0 = min(tid * per, E), j1 = min(j0 + per, E);
   if (j0 < j1) {
     uint32_t b = seg_find(P, nblk, j0);
@@ -217,93 +240,93 @@ __global__ __launch_bounds__(kBlock) void k_tile_build(uint32_t* __restrict__ wo
     }
   }
   __syncthreads();
-  for (uint32_t i = tid; i < tw / 4; i += kBlock) gt[i] = lt[i];
+  for (uint32_t i = tid; i < tw / 4; i += NT) gt[i] = lt[i];
 }
 
-// Partition for probe: one entry per key, bucketed by the tile of bit a. The
-// entry carries (offset of a in its tile, b, key index, b >> 32).
+// Partition for probe: one 8-byte entry per key, bucketed by the tile of bit
+// a: x = (offset of a in its tile) | (key index within the block << tb),
+// y = b. Requires tb + log2(C) <= 32 and m <= 2^32 (checked on the host).
 template <int KEYK, int MODE, int KPT>
-__global__ __launch_bounds__(kBlock) void k_part_probe(KeySrc ks, uint64_t n, ModP mp, uint32_t tb,
-                                                       uint32_t T, uint32_t* __restrict__ seg,
-                                                       uint32_t nblk, uint4* __restrict__ ent) {
-  constexpr uint32_t C = kBlock * KPT;
+__global__ __launch_bounds__(kPartThreads) void k_part_probe(KeySrc ks, uint64_t n, ModP mp,
+                                                             uint32_t tb, uint32_t T,
+                                                             uint32_t* __restrict__ seg,
+                                                             uint2* __restrict__ ent) {
+  constexpr uint32_t C = kPartThreads * KPT;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t Tp = (T + 4) & ~3u;
   uint32_t* hist = smem;
-  uint4* stage = reinterpret_cast<uint4*>(smem + Tp);
+  uint2* stage = reinterpret_cast<uint2*>(smem + Tp);
   uint32_t* wsum = reinterpret_cast<uint32_t*>(stage + C);
   const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < Tp; i += kBlock) hist[i] = 0;
+  for (uint32_t i = tid; i < Tp; i += kPartThreads) hist[i] = 0;
   __syncthreads();
 
   const uint64_t kbase = (uint64_t)blockIdx.x * C;
   const uint32_t tmask = (1u << tb) - 1u;
   uint32_t et[KPT], er[KPT];
-  uint4 rec[KPT];
+  uint2 rec[KPT];
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
-    const uint64_t k = kbase + (uint64_t)j * kBlock + tid;
+    const uint32_t local = (uint32_t)j * kPartThreads + tid;
+    const uint64_t k = kbase + local;
     et[j] = 0xFFFFFFFFu;
     if (k < n) {
       uint64_t a, b;
       key_positions<KEYK, MODE>(ks, k, mp, a, b);
       et[j] = (uint32_t)(a >> tb);
       er[j] = atomicAdd(&hist[et[j]], 1u);
-      rec[j] = make_uint4((uint32_t)a & tmask, (uint32_t)b, (uint32_t)k, (uint32_t)(b >> 32));
+      rec[j] = make_uint2(((uint32_t)a & tmask) | (local << tb), (uint32_t)b);
     }
   }
   __syncthreads();
-  const uint32_t total = block_exclusive_scan(hist, T, wsum);
+  const uint32_t total = block_exclusive_scan<kPartThreads>(hist, T, wsum);
   if (tid == 0) hist[T] = total;
   __syncthreads();
-  for (uint32_t t = tid; t <= T; t += kBlock) seg[(size_t)t * nblk + blockIdx.x] = hist[t];
+  uint32_t* srow = seg + (size_t)blockIdx.x * (T + 1);
+  for (uint32_t t = tid; t <= T; t += kPartThreads) srow[t] = hist[t];
 #pragma unroll
   for (int j = 0; j < KPT; ++j)
     if (et[j] != 0xFFFFFFFFu) stage[hist[et[j]] + er[j]] = rec[j];
   __syncthreads();
-  uint4* out = ent + (size_t)blockIdx.x * C;
-  for (uint32_t i = tid; i < total; i += kBlock) out[i] = stage[i];
+  uint2* out = ent + (size_t)blockIdx.x * C;
+  for (uint32_t i = tid; i < total; i += kPartThreads) out[i] = stage[i];
 }
 
+constexpr uint32_t kTileProbeThreads = 512;
+
 // Probe one tile against up to 32 filters (group blockIdx.y). Each filter's
-// tile is streamed HBM -> registers -> LDS, double-buffered so the next
-// filter's loads are in flight while the current tile is tested. Bit a is
-// tested in LDS; bit b is gathered from HBM only for (key, filter) pairs whose
-// bit a was set. Output: masks[g*n + key] = per-filter result bits.
-template <int EPT>
-__global__ __launch_bounds__(kBlock) void k_tile_probe(FilterPtrs fp, uint32_t nf, uint32_t tb,
-                                                       const uint32_t* __restrict__ seg,
-                                                       uint32_t nblk, const uint4* __restrict__ ent,
-                                                       uint32_t estride, uint64_t n,
-                                                       uint32_t* __restrict__ masks) {
-  constexpr uint32_t RPT = 8;  // uint4 per thread per tile: tiles up to 2^18 bits
+// tile is streamed HBM -> registers -> LDS through a D-deep register ring, so
+// D tiles are in flight while the current one is tested. Bit a is tested in
+// LDS; bit b is gathered from HBM only for (key, filter) pairs whose bit a was
+// set. Output: masks[g*n + key] = per-filter result bits.
+// RPT = uint4 per thread per tile (tile bits = RPT * 16 * 8 * NT).
+template <int EPT, int RPT, int D>
+__global__ __launch_bounds__(kTileProbeThreads) void k_tile_probe(
+    FilterPtrs fp, uint32_t nf, uint32_t tb, uint32_t T, const uint32_t* __restrict__ seg,
+    uint32_t nblk, const uint2* __restrict__ ent, uint32_t C, uint64_t n,
+    uint32_t* __restrict__ masks) {
+  constexpr uint32_t NT = kTileProbeThreads;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t tw = 1u << (tb - 5);
+  const uint32_t tw = 1u << (tb - 5);  // == RPT * 4 * NT
   const uint32_t nbp = (nblk + 3) & ~3u;
   uint32_t* buf = smem;  // 2 * tw
   uint32_t* P = buf + 2 * tw;
   uint32_t* S = P + nbp;
-  uint32_t* wsum = S + nbp;
-  const uint32_t** fw = reinterpret_cast<const uint32_t**>(wsum + 4);  // 32 pointers
+  uint32_t* wsum = S + nbp;                                                  // NT/64 words
+  const uint32_t** fw = reinterpret_cast<const uint32_t**>(wsum + NT / 64);  // 32 pointers
   const uint32_t tid = threadIdx.x;
   const uint32_t t = blockIdx.x, g = blockIdx.y;
   const uint32_t f0 = g * kFiltersPerGroup;
   const uint32_t nfg = min(kFiltersPerGroup, nf - f0);
+  const uint32_t tmask = (1u << tb) - 1u;
   if (tid < nfg) fw[tid] = fp.w[f0 + tid];
 
-  for (uint32_t b = tid; b < nblk; b += kBlock) {
-    const uint32_t s0 = seg[(size_t)t * nblk + b], s1 = seg[(size_t)(t + 1) * nblk + b];
-    S[b] = s0;
-    P[b] = s1 - s0;
-  }
-  __syncthreads();
-  const uint32_t E = block_exclusive_scan(P, nblk, wsum);
-  const uint32_t q = tw / 4;  // uint4 per tile
+  const uint32_t E = load_runs<NT>(seg, nblk, T, t, S, P, wsum);
   uint32_t* mg = masks + (size_t)g * n;
 
-  for (uint32_t cbase = 0; cbase < E; cbase += kBlock * EPT) {
-    const uint32_t cn = min(E - cbase, kBlock * EPT);
-    const uint32_t per = (cn + kBlock - 1) / kBlock;
+  for (uint32_t cbase = 0; cbase < E; cbase += NT * EPT) {
+    const uint32_t cn = min(E - cbase, NT * EPT);
+    const uint32_t per = (cn + NT - 1) / NT;
     const uint32_t j0 = cbase + min(tid * per, cn);
     const uint32_t cnt = cbase + min(tid * per + per, cn) - j0;
     uint32_t off[EPT], pb[EPT], kk[EPT], am[EPT];
@@ -313,45 +336,59 @@ __global__ __launch_bounds__(kBlock) void k_tile_probe(FilterPtrs fp, uint32_t n
 #pragma unroll
       for (int i = 0; i < EPT; ++i) {
         am[i] = 0;
+        off[i] = 0;  // unused slots test bit 0 (branch-free LDS reads) and are dropped
         if ((uint32_t)i < cnt) {
           const uint32_t j = j0 + i;
           while (j >= pnext) {
             ++b;
             pnext = (b + 1 < nblk) ? P[b + 1] : E;
           }
-          const uint4 r = ent[(size_t)b * estride + S[b] + (j - P[b])];
-          off[i] = r.x;
+          const uint2 r = ent[(size_t)b * C + S[b] + (j - P[b])];
+          off[i] = r.x & tmask;
+          kk[i] = b * C + (r.x >> tb);
           pb[i] = r.y;
-          kk[i] = r.z;
         }
       }
     }
 
-    uint4 pre[RPT];
-    {
-      const uint4* src = reinterpret_cast<const uint4*>(fw[0] + (size_t)t * tw);
-#pragma unroll
-      for (uint32_t r = 0; r < RPT; ++r)
-        if (tid + r * kBlock < q) pre[r] = src[tid + r * kBlock];
+    // Register ring: slot s holds filter fb+s's tile. Each slot is its own
+    // named array so every index is static (no scratch); a slot is refilled
+    // right after it is committed to LDS, keeping D tiles in flight. Loads go
+    // through address-space-1 pointers (global_load, counted vmcnt waits).
+    u32x4 r0[RPT], r1[RPT], r2[RPT], r3[RPT];
+#define TP_FETCH(R, F)                                                        \
+  {                                                                           \
+    const gptr_u4 src = (gptr_u4)(fp.w[f0 + (F)] + (size_t)t * tw);           \
+    _Pragma("unroll") for (int q = 0; q < RPT; ++q) R[q] = src[tid + q * NT]; \
+  }
+#define TP_STAGE(R, F)                                                                     \
+  {                                                                                        \
+    const uint32_t f_ = (F);                                                               \
+    u32x4* dst = reinterpret_cast<u32x4*>(buf + (f_ & 1) * tw);                            \
+    _Pragma("unroll") for (int q = 0; q < RPT; ++q) dst[tid + q * NT] = R[q];              \
+    __syncthreads();                                                                       \
+    if (f_ + D < nfg) TP_FETCH(R, f_ + D);                                                 \
+    const uint32_t* lb = buf + (f_ & 1) * tw;                                              \
+    _Pragma("unroll") for (int i = 0; i < EPT; ++i) am[i] |=                               \
+        ((lb[off[i] >> 5] >> (off[i] & 31)) & 1u) << f_;                                   \
+  }
+    TP_FETCH(r0, 0);
+    if (1 < nfg) TP_FETCH(r1, 1);
+    if constexpr (D == 4) {
+      if (2 < nfg) TP_FETCH(r2, 2);
+      if (3 < nfg) TP_FETCH(r3, 3);
     }
-    for (uint32_t f = 0; f < nfg; ++f) {
-      uint4* dst = reinterpret_cast<uint4*>(buf + (f & 1) * tw);
-#pragma unroll
-      for (uint32_t r = 0; r < RPT; ++r)
-        if (tid + r * kBlock < q) dst[tid + r * kBlock] = pre[r];
-      __syncthreads();
-      if (f + 1 < nfg) {
-        const uint4* src = reinterpret_cast<const uint4*>(fw[f + 1] + (size_t)t * tw);
-#pragma unroll
-        for (uint32_t r = 0; r < RPT; ++r)
-          if (tid + r * kBlock < q) pre[r] = src[tid + r * kBlock];
+    for (uint32_t fb = 0; fb < nfg; fb += D) {
+      TP_STAGE(r0, fb);
+      if (fb + 1 < nfg) TP_STAGE(r1, fb + 1);
+      if constexpr (D == 4) {
+        if (fb + 2 < nfg) TP_STAGE(r2, fb + 2);
+        if (fb + 3 < nfg) TP_STAGE(r3, fb + 3);
       }
-      const uint32_t* lb = buf + (f & 1) * tw;
-#pragma unroll
-      for (int i = 0; i < EPT; ++i)
-        if ((uint32_t)i < cnt) am[i] |= ((lb[off[i] >> 5] >> (off[i] & 31)) & 1u) << f;
     }
-    __syncthreads();  // buffers are reused by the next chunk
+#undef TP_STAGE
+#undef TP_FETCH
+    __syncthreads();  // the LDS buffers are rewritten by the next chunk
 
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
@@ -361,7 +398,7 @@ __global__ __launch_bounds__(kBlock) void k_tile_probe(FilterPtrs fp, uint32_t n
         while (x) {
           const uint32_t f = __builtin_ctz(x);
           x &= x - 1;
-          mask |= ((fw[f][wb] >> sb) & 1u) << f;
+          mask |= ((((gptr_u32)fw[f])[wb] >> sb) & 1u) << f;
         }
         mg[kk[i]] = mask;
       }
@@ -369,27 +406,41 @@ __global__ __launch_bounds__(kBlock) void k_tile_probe(FilterPtrs fp, uint32_t n
   }
 }
 
+constexpr uint32_t kHitsThreads = 256;
+constexpr uint32_t kHitsWordsPerBlock = 16;  // 1024 keys: 128 contiguous bytes per filter row
+
 // Transpose per-key masks into the [filter][n/64] hit bitmaps with wave64
-// ballots: wave w owns keys [64w, 64w+64), lane f stores filter f's word.
-__global__ __launch_bounds__(kBlock) void k_masks_to_hits(const uint32_t* __restrict__ masks,
-                                                          FilterPtrs fp, uint32_t nf, uint64_t n,
-                                                          uint64_t* __restrict__ hits,
-                                                          uint64_t hwords) {
-  const uint32_t lane = lane_id();
-  const uint64_t nwaves = ((uint64_t)gridDim.x * kBlock) >> 6;
+// ballots, staged in LDS so each filter row leaves as whole 128-byte lines.
+__global__ __launch_bounds__(kHitsThreads) void k_masks_to_hits(const uint32_t* __restrict__ masks,
+                                                                FilterPtrs fp, uint32_t nf,
+                                                                uint64_t n,
+                                                                uint64_t* __restrict__ hits,
+                                                                uint64_t hwords) {
+  __shared__ uint64_t hb[kMaxFiltersPerLaunch][kHitsWordsPerBlock];
+  __shared__ uint32_t rows[kMaxFiltersPerLaunch];
+  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
   const uint64_t nw = (n + 63) / 64;
-  for (uint64_t wv = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; wv < nw; wv += nwaves) {
-    const uint64_t k = wv * 64 + lane;
-    uint64_t mine = 0;
+  const uint64_t wbase = (uint64_t)blockIdx.x * kHitsWordsPerBlock;
+  if (threadIdx.x < nf) rows[threadIdx.x] = fp.row[threadIdx.x];
+#pragma unroll
+  for (uint32_t p = 0; p < kHitsWordsPerBlock / (kHitsThreads / 64); ++p) {
+    const uint32_t w = p * (kHitsThreads / 64) + wave;
+    const uint64_t k = (wbase + w) * 64 + lane;
     for (uint32_t g = 0; g * kFiltersPerGroup < nf; ++g) {
       const uint32_t mask = k < n ? masks[(size_t)g * n + k] : 0u;
       const uint32_t nfg = min(kFiltersPerGroup, nf - g * kFiltersPerGroup);
+      uint64_t mine = 0;
       for (uint32_t f = 0; f < nfg; ++f) {
         const uint64_t bal = __ballot((mask >> f) & 1u);
-        if (lane == g * kFiltersPerGroup + f) mine = bal;
+        if (lane == f) mine = bal;
       }
+      if (lane < nfg) hb[g * kFiltersPerGroup + lane][w] = mine;
     }
-    if (lane < nf) hits[(uint64_t)fp.row[lane] * hwords + wv] = mine;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nf * kHitsWordsPerBlock; i += kHitsThreads) {
+    const uint32_t f = i / kHitsWordsPerBlock, w = i % kHitsWordsPerBlock;
+    if (wbase + w < nw) hits[(uint64_t)rows[f] * hwords + wbase + w] = hb[f][w];
   }
 }
 
@@ -453,8 +504,8 @@ __global__ void k_mask_tail(uint32_t* words, uint64_t m) {
 
 // Instantiates CALL for the (key source, modulo mode) pair with KK / MM bound
 // as compile-time constants.
-#define CB_DISPATCH(keyk, mode, CALL)                                  \
-  switch ((keyk) * 3 + (mode)) {                                       \
+#define CB_DISPATCH(keyk, mode, CALL)                                          \
+  switch ((keyk) * 3 + (mode)) {                                               \
     case 0: { constexpr int KK = KEY_FIXED16, MM = MOD_POW2_32; CALL; } break; \
     case 1: { constexpr int KK = KEY_FIXED16, MM = MOD_POW2_64; CALL; } break; \
     case 2: { constexpr int KK = KEY_FIXED16, MM = MOD_GENERIC; CALL; } break; \
@@ -464,7 +515,7 @@ __global__ void k_mask_tail(uint32_t* words, uint64_t m) {
     case 6: { constexpr int KK = KEY_VAR, MM = MOD_POW2_32; CALL; } break;     \
     case 7: { constexpr int KK = KEY_VAR, MM = MOD_POW2_64; CALL; } break;     \
     case 8: { constexpr int KK = KEY_VAR, MM = MOD_GENERIC; CALL; } break;     \
-    default: return hipErrorInvalidValue;                              \
+    default: return hipErrorInvalidValue;                                      \
   }
 
 inline uint32_t grid_for(uint64_t items, uint32_t cap = 2048) {
@@ -481,52 +532,55 @@ inline void allow_lds(K kernel, size_t bytes) {
 }
 
 inline uint32_t ilog2_floor(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
-inline uint32_t ilog2_ceil(uint64_t x) { return x <= 1 ? 0 : ilog2_floor(x - 1) + 1; }
 
 }  // namespace
 
 // ------------------------------------------------------------- plans -------
 
-static uint32_t clamp_u32(int64_t v, int64_t lo, int64_t hi) {
-  return (uint32_t)(v < lo ? lo : (v > hi ? hi : v));
+static int64_t clamp64(int64_t v, int64_t lo, int64_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// Raise tb (up to hi) until the tile count fits the partition histogram.
+static uint32_t fit_tiles(uint64_t m, int64_t tb, int64_t hi) {
+  while (tb < hi && ((m + (1ull << tb) - 1) >> tb) > kMaxTiles) ++tb;
+  return (uint32_t)tb;
 }
 
 TilePlan plan_build(uint64_t m, uint64_t n) {
   TilePlan p{};
-  // ~512 tiles (2 workgroups per CU), tiles within [2^12, 2^18] bits, T <= 4096.
-  int64_t tb = (int64_t)ilog2_floor(m > 512 ? m / 512 : 1);
-  tb = clamp_u32(tb, kMinTileBits, kMaxTileBits);
-  if (((m + (1ull << tb) - 1) >> tb) > kMaxTiles) tb = ilog2_ceil((m + kMaxTiles - 1) / kMaxTiles);
-  p.tb = (uint32_t)tb;
-  p.T = (uint32_t)((m + (1ull << tb) - 1) >> tb);
+  // ~512 tiles (2 workgroups per CU), tiles within [2^12, 2^18] bits.
+  int64_t tb = clamp64((int64_t)ilog2_floor(m > 512 ? m / 512 : 1), kMinTileBits, kMaxTileBits);
+  p.tb = fit_tiles(m, tb, kMaxTileBits);
+  p.T = (uint32_t)((m + (1ull << p.tb) - 1) >> p.tb);
   p.kpt = 4;
   while (p.kpt < 16 && (n + 256ull * p.kpt - 1) / (256ull * p.kpt) > 2048) p.kpt *= 2;
-  p.C = 256 * p.kpt;
+  p.C = kPartThreads * p.kpt;
   p.nblk = (uint32_t)((n + p.C - 1) / p.C);
   return p;
 }
 
 TilePlan plan_probe(uint64_t m, uint64_t n) {
   TilePlan p{};
-  // ~512 tiles, and about <= 4096 entries (16 per thread) per tile.
+  // The probe kernel is instantiated for tiles of 2^16..2^18 bits. Aim for
+  // ~512 tiles and <= ~4096 entries per tile.
   int64_t tb1 = (int64_t)ilog2_floor(m > 512 ? m / 512 : 1);
   const uint64_t want = n ? (m * 4096ull) / n : m;
   int64_t tb2 = (int64_t)ilog2_floor(want ? want : 1);
-  int64_t tb = clamp_u32(tb1 < tb2 ? tb1 : tb2, kMinTileBits, kMaxTileBits);
-  if (((m + (1ull << tb) - 1) >> tb) > kMaxTiles) tb = ilog2_ceil((m + kMaxTiles - 1) / kMaxTiles);
-  p.tb = (uint32_t)tb;
-  p.T = (uint32_t)((m + (1ull << tb) - 1) >> tb);
+  p.tb = fit_tiles(m, clamp64(tb1 < tb2 ? tb1 : tb2, kMinProbeTileBits, kMaxProbeTileBits),
+                   kMaxProbeTileBits);
+  p.T = (uint32_t)((m + (1ull << p.tb) - 1) >> p.tb);
   p.kpt = 4;
   while (p.kpt < 8 && (n + 256ull * p.kpt - 1) / (256ull * p.kpt) > 2048) p.kpt *= 2;
-  p.C = 256 * p.kpt;
+  p.C = kPartThreads * p.kpt;
   p.nblk = (uint32_t)((n + p.C - 1) / p.C);
   return p;
 }
 
+bool plan_ok(const TilePlan& p) { return p.T <= kMaxTiles; }
+
 size_t build_seg_bytes(const TilePlan& p) { return (size_t)(p.T + 1) * p.nblk * 4; }
 size_t build_ent_bytes(const TilePlan& p) { return (size_t)p.nblk * 2 * p.C * 4; }
 size_t probe_seg_bytes(const TilePlan& p) { return (size_t)(p.T + 1) * p.nblk * 4; }
-size_t probe_ent_bytes(const TilePlan& p) { return (size_t)p.nblk * p.C * 16; }
+size_t probe_ent_bytes(const TilePlan& p) { return (size_t)p.nblk * p.C * 8; }
 
 // ------------------------------------------------------------- launchers ---
 
@@ -558,32 +612,33 @@ template <int KK, int MM, int KPT>
 static void part_build(const TilePlan& p, const KeySrc& ks, uint64_t n, const ModP& mp,
                        uint32_t* seg, uint32_t* ent, size_t lds, hipStream_t s) {
   allow_lds(k_part_build<KK, MM, KPT>, lds);
-  hipLaunchKernelGGL((k_part_build<KK, MM, KPT>), dim3(p.nblk), dim3(kBlock), lds, s, ks, n, mp,
-                     p.tb, p.T, seg, p.nblk, ent);
+  hipLaunchKernelGGL((k_part_build<KK, MM, KPT>), dim3(p.nblk), dim3(kPartThreads), lds, s, ks, n,
+                     mp, p.tb, p.T, seg, ent);
 }
 
 template <int KK, int MM, int KPT>
 static void part_probe(const TilePlan& p, const KeySrc& ks, uint64_t n, const ModP& mp,
-                       uint32_t* seg, uint4* ent, size_t lds, hipStream_t s) {
+                       uint32_t* seg, uint2* ent, size_t lds, hipStream_t s) {
   allow_lds(k_part_probe<KK, MM, KPT>, lds);
-  hipLaunchKernelGGL((k_part_probe<KK, MM, KPT>), dim3(p.nblk), dim3(kBlock), lds, s, ks, n, mp,
-                     p.tb, p.T, seg, p.nblk, ent);
+  hipLaunchKernelGGL((k_part_probe<KK, MM, KPT>), dim3(p.nblk), dim3(kPartThreads), lds, s, ks, n,
+                     mp, p.tb, p.T, seg, ent);
 }
 
 hipError_t launch_build_tiled(int keyk, int mode, uint32_t* words, bool fresh, const KeySrc& ks,
                               uint64_t n, const ModP& mp, const TilePlan& p, uint32_t* seg,
                               uint32_t* ent, hipStream_t s) {
   if (!n) return hipSuccess;
+  if (!plan_ok(p)) return hipErrorInvalidValue;
   const size_t lds1 = ((size_t)((p.T + 4) & ~3u) + 2 * p.C + 8) * 4;
   {
-  ProfScope ps("k_part_build", s);
-  if (p.kpt == 4) {
-    CB_DISPATCH(keyk, mode, (part_build<KK, MM, 4>(p, ks, n, mp, seg, ent, lds1, s)));
-  } else if (p.kpt == 8) {
-    CB_DISPATCH(keyk, mode, (part_build<KK, MM, 8>(p, ks, n, mp, seg, ent, lds1, s)));
-  } else {
-    CB_DISPATCH(keyk, mode, (part_build<KK, MM, 16>(p, ks, n, mp, seg, ent, lds1, s)));
-  }
+    ProfScope ps("k_part_build", s);
+    if (p.kpt == 4) {
+      CB_DISPATCH(keyk, mode, (part_build<KK, MM, 4>(p, ks, n, mp, seg, ent, lds1, s)));
+    } else if (p.kpt == 8) {
+      CB_DISPATCH(keyk, mode, (part_build<KK, MM, 8>(p, ks, n, mp, seg, ent, lds1, s)));
+    } else {
+      CB_DISPATCH(keyk, mode, (part_build<KK, MM, 16>(p, ks, n, mp, seg, ent, lds1, s)));
+    }
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -591,16 +646,17 @@ hipError_t launch_build_tiled(int keyk, int mode, uint32_t* words, bool fresh, c
   const size_t lds2 = ((size_t)(1u << (p.tb - 5)) + 2 * nbp + 8) * 4;
   allow_lds(k_tile_build, lds2);
   ProfScope ps("k_tile_build", s);
-  hipLaunchKernelGGL(k_tile_build, dim3(p.T), dim3(kBlock), lds2, s, words, p.tb, p.T, seg, p.nblk,
-                     ent, 2 * p.C, fresh ? 1 : 0);
+  hipLaunchKernelGGL(k_tile_build, dim3(p.T), dim3(kTileBuildThreads), lds2, s, words, p.tb, p.T,
+                     seg, p.nblk, ent, 2 * p.C, fresh ? 1 : 0);
   return hipGetLastError();
 }
 
 hipError_t launch_probe_partition(int keyk, int mode, const KeySrc& ks, uint64_t n,
-                                  const ModP& mp, const TilePlan& p, uint32_t* seg, uint4* ent,
+                                  const ModP& mp, const TilePlan& p, uint32_t* seg, uint2* ent,
                                   hipStream_t s) {
   if (!n) return hipSuccess;
-  const size_t lds1 = ((size_t)((p.T + 4) & ~3u) + 4 * p.C + 8) * 4;
+  if (!plan_ok(p) || p.tb + 12 > 32) return hipErrorInvalidValue;
+  const size_t lds1 = ((size_t)((p.T + 4) & ~3u) + 2 * p.C + 8) * 4;
   ProfScope ps("k_part_probe", s);
   if (p.kpt == 4) {
     CB_DISPATCH(keyk, mode, (part_probe<KK, MM, 4>(p, ks, n, mp, seg, ent, lds1, s)));
@@ -610,25 +666,44 @@ hipError_t launch_probe_partition(int keyk, int mode, const KeySrc& ks, uint64_t
   return hipGetLastError();
 }
 
+template <int RPT>
+static hipError_t tile_probe(const FilterPtrs& fp, uint32_t nf, uint64_t n, const TilePlan& p,
+                             const uint32_t* seg, const uint2* ent, uint32_t* masks, size_t lds,
+                             uint32_t G, hipStream_t s) {
+  // The instantiation must cover the tile exactly: RPT uint4 per thread.
+  if ((1u << (p.tb - 5)) != (uint32_t)RPT * 4u * kTileProbeThreads) return hipErrorInvalidValue;
+  constexpr int D = RPT >= 2 ? 2 : 4;  // 32-64 KiB of tiles in flight per workgroup
+  allow_lds(k_tile_probe<8, RPT, D>, lds);
+  hipLaunchKernelGGL((k_tile_probe<8, RPT, D>), dim3(p.T, G), dim3(kTileProbeThreads), lds, s, fp,
+                     nf, p.tb, p.T, seg, p.nblk, ent, p.C, n, masks);
+  return hipGetLastError();
+}
+
 hipError_t launch_probe_tiles(const FilterPtrs& fp, uint32_t nf, uint64_t n, const TilePlan& p,
-                              const uint32_t* seg, const uint4* ent, uint32_t* masks,
+                              const uint32_t* seg, const uint2* ent, uint32_t* masks,
                               uint64_t* hits, uint64_t hwords, hipStream_t s) {
   if (!n || !nf) return hipSuccess;
   const uint32_t nbp = (p.nblk + 3) & ~3u;
-  const size_t lds2 = ((size_t)2 * (1u << (p.tb - 5)) + 2 * nbp + 4) * 4 + kFiltersPerGroup * 8;
+  const size_t lds2 = ((size_t)2 * (1u << (p.tb - 5)) + 2 * nbp + kTileProbeThreads / 64) * 4 +
+                      kFiltersPerGroup * 8;
   const uint32_t G = (nf + kFiltersPerGroup - 1) / kFiltersPerGroup;
-  allow_lds(k_tile_probe<16>, lds2);
+  hipError_t e;
   {
     ProfScope ps("k_tile_probe", s);
-    hipLaunchKernelGGL((k_tile_probe<16>), dim3(p.T, G), dim3(kBlock), lds2, s, fp, nf, p.tb, seg,
-                       p.nblk, ent, p.C, n, masks);
+    // tile bits = RPT * 16 B * 8 * 512 threads = RPT * 2^16
+    switch (p.tb) {
+      case 16: e = tile_probe<1>(fp, nf, n, p, seg, ent, masks, lds2, G, s); break;
+      case 17: e = tile_probe<2>(fp, nf, n, p, seg, ent, masks, lds2, G, s); break;
+      case 18: e = tile_probe<4>(fp, nf, n, p, seg, ent, masks, lds2, G, s); break;
+      default: e = hipErrorInvalidValue;
+    }
   }
-  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint64_t nw = (n + 63) / 64;
   ProfScope ps("k_masks_to_hits", s);
-  hipLaunchKernelGGL(k_masks_to_hits, dim3(grid_for(nw * 64, 4096)), dim3(kBlock), 0, s, masks,
-                     fp, nf, n, hits, hwords);
+  hipLaunchKernelGGL(k_masks_to_hits,
+                     dim3((uint32_t)((nw + kHitsWordsPerBlock - 1) / kHitsWordsPerBlock)),
+                     dim3(kHitsThreads), 0, s, masks, fp, nf, n, hits, hwords);
   return hipGetLastError();
 }
 

@@ -10,9 +10,14 @@ namespace cb {
 constexpr uint32_t kMaxFiltersPerLaunch = 64;  // filter pointers carried in kernargs
 constexpr uint32_t kFiltersPerGroup = 32;      // one uint32 result mask per key
 constexpr uint32_t kMaxTiles = 4096;           // LDS histogram bound in the partition pass
-constexpr uint32_t kMaxTileBits = 18;          // 32 KiB LDS tiles at most
-constexpr uint32_t kMinTileBits = 12;          // 512 B tiles at least
-constexpr uint32_t kTileAlignBits = 1u << kMaxTileBits;  // filters >= 2^20 bits pad to this
+constexpr uint32_t kMaxTileBits = 18;          // build: 32 KiB LDS tiles at most
+constexpr uint32_t kMinTileBits = 12;          // build: 512 B tiles at least
+constexpr uint32_t kMinProbeTileBits = 16;     // probe kernel instantiations: 2^16..2^18
+constexpr uint32_t kMaxProbeTileBits = 18;
+// Filter allocations are padded to whole tiles of the largest tile size a pass
+// may use, so no tiled pass reads or writes past the allocation.
+constexpr uint64_t kTileAlignBits = 1ull << kMaxTileBits;
+constexpr uint64_t kSmallAlignBits = 1ull << kMinProbeTileBits;
 
 struct FilterPtrs {
   const uint32_t* w[kMaxFiltersPerLaunch];
@@ -30,6 +35,7 @@ struct TilePlan {
 
 TilePlan plan_build(uint64_t m, uint64_t n);
 TilePlan plan_probe(uint64_t m, uint64_t n);
+bool plan_ok(const TilePlan& p);  // tile count fits the partition histogram
 
 // Workspace bytes a tiled pass needs.
 size_t build_seg_bytes(const TilePlan& p);
@@ -50,10 +56,10 @@ hipError_t launch_build_tiled(int keyk, int mode, uint32_t* words, bool fresh, c
 // of <= 64 filters: tile pass (K2) into masks (ceil(nf/32) * n uint32) and the
 // ballot transpose into hits (K3).
 hipError_t launch_probe_partition(int keyk, int mode, const KeySrc& ks, uint64_t n,
-                                  const ModP& mp, const TilePlan& p, uint32_t* seg, uint4* ent,
+                                  const ModP& mp, const TilePlan& p, uint32_t* seg, uint2* ent,
                                   hipStream_t s);
 hipError_t launch_probe_tiles(const FilterPtrs& fp, uint32_t nf, uint64_t n, const TilePlan& p,
-                              const uint32_t* seg, const uint4* ent, uint32_t* masks,
+                              const uint32_t* seg, const uint2* ent, uint32_t* masks,
                               uint64_t* hits, uint64_t hwords, hipStream_t s);
 hipError_t launch_mask_tail(uint32_t* words, uint64_t m, hipStream_t s);
 

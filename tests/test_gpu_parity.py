@@ -245,7 +245,7 @@ def test_codec_matches_oracle(gpu):
         assert data == o.to_bytes()
         back = gpu.BloomFilter.from_bytes(data)
         assert back.m == m and np.array_equal(back.bools(), o.bools())
-    unpacked = bytes([0x08, 0x01, 0x08, 0x00, 0x08, 0x05, 0x10, 0x07, 0x0A, 0x02, 0x00, 0x81, 0x01])
+    unpacked = bytes([0x08, 0x01, 0x08, 0x00, 0x08, 0x05, 0x10, 0x07, 0x0A, 0x03, 0x00, 0x81, 0x01])
     f = gpu.BloomFilter.from_bytes(unpacked)
     assert list(f.bools()) == list(oracle.OracleFilter.from_bytes(unpacked).bools())
     for bad in (b"\x0a", b"\x0a\x05\x01", b"\x00", b"\x0d\x00\x00\x00\x00", b"\xff" * 11):
