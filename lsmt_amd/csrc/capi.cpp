@@ -85,7 +85,7 @@ struct DevBuf {
 
 struct Workspace {
   std::mutex mu;
-  DevBuf keys, offsets, hits, seg, ent, masks, bools;
+  DevBuf keys, offsets, hits, seg, ent, masks, bools, lkey;
 };
 
 std::mutex g_ws_mu;
@@ -342,8 +342,9 @@ int probe_impl(const cb_filter* const* filters, uint32_t nf, const uint8_t* keys
         HIP_TRY(ws.seg.reserve(cb::probe_seg_bytes(p), s));
         HIP_TRY(ws.ent.reserve(cb::probe_ent_bytes(p), s));
         HIP_TRY(ws.masks.reserve((size_t)2 * nk * 4, s));
+        HIP_TRY(ws.lkey.reserve(cb::probe_lkey_bytes(p), s));
         HIP_TRY(cb::launch_probe_partition(keyk, f0->mode, ks, nk, f0->mp, p, (uint32_t*)ws.seg.p,
-                                           (uint2*)ws.ent.p, s));
+                                           (uint2*)ws.ent.p, (uint16_t*)ws.lkey.p, s));
         for (size_t g0 = 0; g0 < idx.size(); g0 += cb::kMaxFiltersPerLaunch) {
           FilterPtrs fp{};
           const uint32_t cnt =
@@ -353,8 +354,8 @@ int probe_impl(const cb_filter* const* filters, uint32_t nf, const uint8_t* keys
             fp.row[j] = idx[g0 + j];
           }
           HIP_TRY(cb::launch_probe_tiles(fp, cnt, nk, p, (const uint32_t*)ws.seg.p,
-                                         (const uint2*)ws.ent.p, (uint32_t*)ws.masks.p,
-                                         dhits + k0 / 64, hwords, s));
+                                         (const uint2*)ws.ent.p, (const uint16_t*)ws.lkey.p,
+                                         (uint32_t*)ws.masks.p, dhits + k0 / 64, hwords, s));
         }
       }
     }

@@ -21,6 +21,8 @@
 // runs [seg[b][t], seg[b][t+1]) of every block b.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kernels.hpp"
 #include "profile.hpp"
 
@@ -66,6 +68,23 @@ __device__ uint32_t block_exclusive_scan(uint32_t* arr, uint32_t len, uint32_t* 
     arr[i] = run;
     run += v;
   }
+  __syncthreads();
+  return total;
+}
+
+// Sum of arr[0..len) in LDS by a whole NT-thread block (barriers inside).
+template <uint32_t NT>
+__device__ uint32_t block_sum(const uint32_t* arr, uint32_t len, uint32_t* wsum) {
+  uint32_t x = 0;
+  for (uint32_t i = threadIdx.x; i < len; i += NT) x += arr[i];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  __syncthreads();  // wsum may still be read by a preceding scan
+  if (lane_id() == 0) wsum[threadIdx.x >> 6] = x;
+  __syncthreads();
+  uint32_t total = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < NT / 64; ++w) total += wsum[w];
   __syncthreads();
   return total;
 }
@@ -230,13 +249,24 @@ __global__ __launch_bounds__(kTileBuildThreads) void k_tile_build(
   if (j0 < j1) {
     uint32_t b = seg_find(P, nblk, j0);
     uint32_t pnext = (b + 1 < nblk) ? P[b + 1] : E;
-    for (uint32_t j = j0; j < j1; ++j) {
-      while (j >= pnext) {
-        ++b;
-        pnext = (b + 1 < nblk) ? P[b + 1] : E;
+    // 8 entries per round: the 8 loads issue back to back, then 8 ds_or.
+    for (uint32_t jb = j0; jb < j1; jb += 8) {
+      uint32_t o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t j = jb + i;
+        o[i] = 0xFFFFFFFFu;
+        if (j < j1) {
+          while (j >= pnext) {
+            ++b;
+            pnext = (b + 1 < nblk) ? P[b + 1] : E;
+          }
+          o[i] = ent[(size_t)b * estride + S[b] + (j - P[b])];
+        }
       }
-      const uint32_t off = ent[(size_t)b * estride + S[b] + (j - P[b])];
-      atomicOr(&tile[off >> 5], 1u << (off & 31));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (o[i] != 0xFFFFFFFFu) atomicOr(&tile[o[i] >> 5], 1u << (o[i] & 31));
     }
   }
   __syncthreads();
@@ -246,17 +276,22 @@ __global__ __launch_bounds__(kTileBuildThreads) void k_tile_build(
 // Partition for probe: one 8-byte entry per key, bucketed by the tile of bit
 // a: x = (offset of a in its tile) | (key index within the block << tb),
 // y = b. Requires tb + log2(C) <= 32 and m <= 2^32 (checked on the host).
+// lkey[b*C + i] = the block-local key index of region slot i: k_tile_probe
+// writes each key's result mask at its entry's slot, and k_masks_to_hits
+// reads a block's region back in order and un-permutes it in LDS.
 template <int KEYK, int MODE, int KPT>
 __global__ __launch_bounds__(kPartThreads) void k_part_probe(KeySrc ks, uint64_t n, ModP mp,
                                                              uint32_t tb, uint32_t T,
                                                              uint32_t* __restrict__ seg,
-                                                             uint2* __restrict__ ent) {
+                                                             uint2* __restrict__ ent,
+                                                             uint16_t* __restrict__ lkey) {
   constexpr uint32_t C = kPartThreads * KPT;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t Tp = (T + 4) & ~3u;
   uint32_t* hist = smem;
   uint2* stage = reinterpret_cast<uint2*>(smem + Tp);
-  uint32_t* wsum = reinterpret_cast<uint32_t*>(stage + C);
+  uint16_t* lstage = reinterpret_cast<uint16_t*>(stage + C);
+  uint32_t* wsum = reinterpret_cast<uint32_t*>(lstage + C);
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < Tp; i += kPartThreads) hist[i] = 0;
   __syncthreads();
@@ -285,14 +320,27 @@ __global__ __launch_bounds__(kPartThreads) void k_part_probe(KeySrc ks, uint64_t
   uint32_t* srow = seg + (size_t)blockIdx.x * (T + 1);
   for (uint32_t t = tid; t <= T; t += kPartThreads) srow[t] = hist[t];
 #pragma unroll
-  for (int j = 0; j < KPT; ++j)
-    if (et[j] != 0xFFFFFFFFu) stage[hist[et[j]] + er[j]] = rec[j];
+  for (int j = 0; j < KPT; ++j) {
+    if (et[j] != 0xFFFFFFFFu) {
+      const uint32_t slot = hist[et[j]] + er[j];
+      stage[slot] = rec[j];
+      lstage[slot] = (uint16_t)(j * kPartThreads + tid);
+    }
+  }
   __syncthreads();
   uint2* out = ent + (size_t)blockIdx.x * C;
-  for (uint32_t i = tid; i < total; i += kPartThreads) out[i] = stage[i];
+  uint16_t* lout = lkey + (size_t)blockIdx.x * C;
+  for (uint32_t i = tid; i < total; i += kPartThreads) {
+    out[i] = stage[i];
+    lout[i] = lstage[i];
+  }
 }
 
 constexpr uint32_t kTileProbeThreads = 512;
+
+// Timing-only experiment switches for k_tile_probe (CB_PROBE_XFLAGS; results
+// are wrong when set — bench attribution only, never set in production).
+constexpr uint32_t kXSkipGather = 1, kXSkipStream = 2, kXSkipStore = 4;
 
 // Probe one tile against up to 32 filters (group blockIdx.y). Each filter's
 // tile is streamed HBM -> registers -> LDS through a D-deep register ring, so
@@ -304,7 +352,7 @@ template <int EPT, int RPT, int D>
 __global__ __launch_bounds__(kTileProbeThreads) void k_tile_probe(
     FilterPtrs fp, uint32_t nf, uint32_t tb, uint32_t T, const uint32_t* __restrict__ seg,
     uint32_t nblk, const uint2* __restrict__ ent, uint32_t C, uint64_t n,
-    uint32_t* __restrict__ masks) {
+    uint32_t* __restrict__ masks, uint32_t xflags) {
   constexpr uint32_t NT = kTileProbeThreads;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t tw = 1u << (tb - 5);  // == RPT * 4 * NT
@@ -321,15 +369,39 @@ __global__ __launch_bounds__(kTileProbeThreads) void k_tile_probe(
   const uint32_t tmask = (1u << tb) - 1u;
   if (tid < nfg) fw[tid] = fp.w[f0 + tid];
 
+  // Register ring: slot s holds filter fb+s's tile. Each slot is its own
+  // named array so every index is static (no scratch); a slot is refilled
+  // right after it is committed to LDS, keeping D tiles in flight. Loads go
+  // through address-space-1 pointers (global_load, counted vmcnt waits).
+  u32x4 r0[RPT], r1[RPT], r2[RPT], r3[RPT];
+#define TP_FETCH(R, F)                                                        \
+  if (!(xflags & kXSkipStream)) {                                             \
+    const gptr_u4 src = (gptr_u4)(fp.w[f0 + (F)] + (size_t)t * tw);           \
+    _Pragma("unroll") for (int q = 0; q < RPT; ++q) R[q] = src[tid + q * NT]; \
+  }
+#define TP_FETCH_FIRST()                  \
+  {                                       \
+    TP_FETCH(r0, 0);                      \
+    if (1 < nfg) TP_FETCH(r1, 1);         \
+    if constexpr (D == 4) {               \
+      if (2 < nfg) TP_FETCH(r2, 2);       \
+      if (3 < nfg) TP_FETCH(r3, 3);       \
+    }                                     \
+  }
+  // The first D tiles are requested before the run table and entries are
+  // read, so their HBM latency overlaps the prologue.
+  TP_FETCH_FIRST();
+
   const uint32_t E = load_runs<NT>(seg, nblk, T, t, S, P, wsum);
-  uint32_t* mg = masks + (size_t)g * n;
+  uint32_t* mg = masks + (size_t)g * n;  // results go to each entry's region slot
 
   for (uint32_t cbase = 0; cbase < E; cbase += NT * EPT) {
+    if (cbase) TP_FETCH_FIRST();  // rare extra chunk: stream the tiles again
     const uint32_t cn = min(E - cbase, NT * EPT);
     const uint32_t per = (cn + NT - 1) / NT;
     const uint32_t j0 = cbase + min(tid * per, cn);
     const uint32_t cnt = cbase + min(tid * per + per, cn) - j0;
-    uint32_t off[EPT], pb[EPT], kk[EPT], am[EPT];
+    uint32_t off[EPT], pb[EPT], am[EPT], slot[EPT];
     {
       uint32_t b = cnt ? seg_find(P, nblk, j0) : 0;
       uint32_t pnext = (b + 1 < nblk) ? P[b + 1] : E;
@@ -343,24 +415,14 @@ __global__ __launch_bounds__(kTileProbeThreads) void k_tile_probe(
             ++b;
             pnext = (b + 1 < nblk) ? P[b + 1] : E;
           }
-          const uint2 r = ent[(size_t)b * C + S[b] + (j - P[b])];
+          slot[i] = b * C + S[b] + (j - P[b]);
+          const uint2 r = ent[slot[i]];
           off[i] = r.x & tmask;
-          kk[i] = b * C + (r.x >> tb);
           pb[i] = r.y;
         }
       }
     }
 
-    // Register ring: slot s holds filter fb+s's tile. Each slot is its own
-    // named array so every index is static (no scratch); a slot is refilled
-    // right after it is committed to LDS, keeping D tiles in flight. Loads go
-    // through address-space-1 pointers (global_load, counted vmcnt waits).
-    u32x4 r0[RPT], r1[RPT], r2[RPT], r3[RPT];
-#define TP_FETCH(R, F)                                                        \
-  {                                                                           \
-    const gptr_u4 src = (gptr_u4)(fp.w[f0 + (F)] + (size_t)t * tw);           \
-    _Pragma("unroll") for (int q = 0; q < RPT; ++q) R[q] = src[tid + q * NT]; \
-  }
 #define TP_STAGE(R, F)                                                                     \
   {                                                                                        \
     const uint32_t f_ = (F);                                                               \
@@ -372,12 +434,6 @@ __global__ __launch_bounds__(kTileProbeThreads) void k_tile_probe(
     _Pragma("unroll") for (int i = 0; i < EPT; ++i) am[i] |=                               \
         ((lb[off[i] >> 5] >> (off[i] & 31)) & 1u) << f_;                                   \
   }
-    TP_FETCH(r0, 0);
-    if (1 < nfg) TP_FETCH(r1, 1);
-    if constexpr (D == 4) {
-      if (2 < nfg) TP_FETCH(r2, 2);
-      if (3 < nfg) TP_FETCH(r3, 3);
-    }
     for (uint32_t fb = 0; fb < nfg; fb += D) {
       TP_STAGE(r0, fb);
       if (fb + 1 < nfg) TP_STAGE(r1, fb + 1);
@@ -387,59 +443,92 @@ __global__ __launch_bounds__(kTileProbeThreads) void k_tile_probe(
       }
     }
 #undef TP_STAGE
-#undef TP_FETCH
     __syncthreads();  // the LDS buffers are rewritten by the next chunk
 
+    // Bit b of every (entry, filter) pair whose bit a was set, gathered from
+    // HBM in rounds: each round issues one independent load per entry.
+    uint32_t mask[EPT], x[EPT];
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
-      if ((uint32_t)i < cnt) {
-        uint32_t mask = 0, x = am[i];
-        const uint32_t wb = pb[i] >> 5, sb = pb[i] & 31;
-        while (x) {
-          const uint32_t f = __builtin_ctz(x);
-          x &= x - 1;
-          mask |= ((((gptr_u32)fw[f])[wb] >> sb) & 1u) << f;
+      mask[i] = 0;
+      x[i] = ((uint32_t)i < cnt && !(xflags & kXSkipGather)) ? am[i] : 0u;
+    }
+    for (;;) {
+      uint32_t any = 0, v[EPT];
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        any |= x[i];
+        v[i] = x[i] ? ((gptr_u32)fw[__builtin_ctz(x[i])])[pb[i] >> 5] : 0u;
+      }
+      if (!any) break;
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) {
+        if (x[i]) {
+          const uint32_t f = __builtin_ctz(x[i]);
+          mask[i] |= ((v[i] >> (pb[i] & 31)) & 1u) << f;
+          x[i] &= x[i] - 1;
         }
-        mg[kk[i]] = mask;
       }
     }
+    if (!(xflags & kXSkipStore)) {
+#pragma unroll
+      for (int i = 0; i < EPT; ++i)
+        if ((uint32_t)i < cnt) mg[slot[i]] = mask[i];
+    }
   }
+#undef TP_FETCH_FIRST
+#undef TP_FETCH
 }
 
-constexpr uint32_t kHitsThreads = 256;
-constexpr uint32_t kHitsWordsPerBlock = 16;  // 1024 keys: 128 contiguous bytes per filter row
+constexpr uint32_t kHitsThreads = 512;
 
-// Transpose per-key masks into the [filter][n/64] hit bitmaps with wave64
-// ballots, staged in LDS so each filter row leaves as whole 128-byte lines.
-__global__ __launch_bounds__(kHitsThreads) void k_masks_to_hits(const uint32_t* __restrict__ masks,
-                                                                FilterPtrs fp, uint32_t nf,
-                                                                uint64_t n,
-                                                                uint64_t* __restrict__ hits,
-                                                                uint64_t hwords) {
-  __shared__ uint64_t hb[kMaxFiltersPerLaunch][kHitsWordsPerBlock];
+// Un-permute one partition block's results and transpose them into the
+// [filter][n/64] hit bitmaps. Block b reads its region's masks and local key
+// indices in order (coalesced), scatters the masks into LDS by key, then each
+// wave turns 64 keys into one word per filter with wave64 ballots; the words
+// are staged in LDS so every filter row leaves as whole contiguous segments.
+template <int KPT>
+__global__ __launch_bounds__(kHitsThreads) void k_masks_to_hits(
+    const uint32_t* __restrict__ masks, const uint16_t* __restrict__ lkey, FilterPtrs fp,
+    uint32_t nf, uint64_t n, uint64_t* __restrict__ hits, uint64_t hwords) {
+  constexpr uint32_t C = kPartThreads * KPT;  // keys per partition block
+  constexpr uint32_t W = C / 64;              // hit words per filter row
+  constexpr uint32_t G = kMaxFiltersPerLaunch / kFiltersPerGroup;
+  __shared__ uint32_t km[G][C];
+  __shared__ uint64_t hb[kMaxFiltersPerLaunch][W];
   __shared__ uint32_t rows[kMaxFiltersPerLaunch];
-  const uint32_t lane = lane_id(), wave = threadIdx.x >> 6;
-  const uint64_t nw = (n + 63) / 64;
-  const uint64_t wbase = (uint64_t)blockIdx.x * kHitsWordsPerBlock;
-  if (threadIdx.x < nf) rows[threadIdx.x] = fp.row[threadIdx.x];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t ng = (nf + kFiltersPerGroup - 1) / kFiltersPerGroup;
+  const uint64_t kbase = (uint64_t)blockIdx.x * C;
+  const uint32_t cnt = (uint32_t)min((uint64_t)C, n - kbase);
+  if (tid < nf) rows[tid] = fp.row[tid];
+  for (uint32_t i = tid; i < cnt; i += kHitsThreads) {
+    const uint32_t lk = lkey[kbase + i];
+    km[0][lk] = masks[kbase + i];
+    if (ng > 1) km[1][lk] = masks[n + kbase + i];
+  }
+  __syncthreads();
+  for (uint32_t w = wave; w < W; w += kHitsThreads / 64) {
+    const uint32_t kl = w * 64 + lane;
 #pragma unroll
-  for (uint32_t p = 0; p < kHitsWordsPerBlock / (kHitsThreads / 64); ++p) {
-    const uint32_t w = p * (kHitsThreads / 64) + wave;
-    const uint64_t k = (wbase + w) * 64 + lane;
-    for (uint32_t g = 0; g * kFiltersPerGroup < nf; ++g) {
-      const uint32_t mask = k < n ? masks[(size_t)g * n + k] : 0u;
-      const uint32_t nfg = min(kFiltersPerGroup, nf - g * kFiltersPerGroup);
-      uint64_t mine = 0;
-      for (uint32_t f = 0; f < nfg; ++f) {
-        const uint64_t bal = __ballot((mask >> f) & 1u);
-        if (lane == f) mine = bal;
+    for (uint32_t g = 0; g < G; ++g) {
+      if (g < ng) {
+        const uint32_t m = kl < cnt ? km[g][kl] : 0u;
+        uint64_t mine = 0;
+#pragma unroll
+        for (uint32_t f = 0; f < kFiltersPerGroup; ++f) {
+          const uint64_t bal = __ballot((m >> f) & 1u);
+          mine = (lane == f) ? bal : mine;
+        }
+        if (lane < min(kFiltersPerGroup, nf - g * kFiltersPerGroup))
+          hb[g * kFiltersPerGroup + lane][w] = mine;
       }
-      if (lane < nfg) hb[g * kFiltersPerGroup + lane][w] = mine;
     }
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nf * kHitsWordsPerBlock; i += kHitsThreads) {
-    const uint32_t f = i / kHitsWordsPerBlock, w = i % kHitsWordsPerBlock;
+  const uint64_t wbase = kbase / 64, nw = (n + 63) / 64;
+  for (uint32_t i = tid; i < nf * W; i += kHitsThreads) {
+    const uint32_t f = i / W, w = i % W;
     if (wbase + w < nw) hits[(uint64_t)rows[f] * hwords + wbase + w] = hb[f][w];
   }
 }
@@ -558,6 +647,13 @@ TilePlan plan_build(uint64_t m, uint64_t n) {
   return p;
 }
 
+// Tuning overrides for experiments (unset in production): CB_PROBE_TB fixes
+// the probe tile bits, CB_PROBE_KPT the partition keys per thread (4 or 8).
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
 TilePlan plan_probe(uint64_t m, uint64_t n) {
   TilePlan p{};
   // The probe kernel is instantiated for tiles of 2^16..2^18 bits. Aim for
@@ -565,11 +661,16 @@ TilePlan plan_probe(uint64_t m, uint64_t n) {
   int64_t tb1 = (int64_t)ilog2_floor(m > 512 ? m / 512 : 1);
   const uint64_t want = n ? (m * 4096ull) / n : m;
   int64_t tb2 = (int64_t)ilog2_floor(want ? want : 1);
-  p.tb = fit_tiles(m, clamp64(tb1 < tb2 ? tb1 : tb2, kMinProbeTileBits, kMaxProbeTileBits),
-                   kMaxProbeTileBits);
+  int64_t tb = clamp64(tb1 < tb2 ? tb1 : tb2, kMinProbeTileBits, kMaxProbeTileBits);
+  static const int env_tb = env_int("CB_PROBE_TB", 0);
+  if (env_tb) tb = clamp64(env_tb, kMinProbeTileBits, kMaxProbeTileBits);
+  p.tb = fit_tiles(m, tb, kMaxProbeTileBits);
   p.T = (uint32_t)((m + (1ull << p.tb) - 1) >> p.tb);
-  p.kpt = 4;
-  while (p.kpt < 8 && (n + 256ull * p.kpt - 1) / (256ull * p.kpt) > 2048) p.kpt *= 2;
+  // Longer runs per (block, tile) with C = 2048 once that still leaves >= 512
+  // partition blocks; never more than 4096 blocks (the host chunks keys).
+  p.kpt = n >= 512ull * 2048 ? 8 : 4;
+  static const int env_kpt = env_int("CB_PROBE_KPT", 0);
+  if (env_kpt == 4 || env_kpt == 8) p.kpt = env_kpt;
   p.C = kPartThreads * p.kpt;
   p.nblk = (uint32_t)((n + p.C - 1) / p.C);
   return p;
@@ -581,6 +682,7 @@ size_t build_seg_bytes(const TilePlan& p) { return (size_t)(p.T + 1) * p.nblk * 
 size_t build_ent_bytes(const TilePlan& p) { return (size_t)p.nblk * 2 * p.C * 4; }
 size_t probe_seg_bytes(const TilePlan& p) { return (size_t)(p.T + 1) * p.nblk * 4; }
 size_t probe_ent_bytes(const TilePlan& p) { return (size_t)p.nblk * p.C * 8; }
+size_t probe_lkey_bytes(const TilePlan& p) { return (size_t)p.nblk * p.C * 2; }
 
 // ------------------------------------------------------------- launchers ---
 
@@ -618,10 +720,10 @@ static void part_build(const TilePlan& p, const KeySrc& ks, uint64_t n, const Mo
 
 template <int KK, int MM, int KPT>
 static void part_probe(const TilePlan& p, const KeySrc& ks, uint64_t n, const ModP& mp,
-                       uint32_t* seg, uint2* ent, size_t lds, hipStream_t s) {
+                       uint32_t* seg, uint2* ent, uint16_t* lkey, size_t lds, hipStream_t s) {
   allow_lds(k_part_probe<KK, MM, KPT>, lds);
   hipLaunchKernelGGL((k_part_probe<KK, MM, KPT>), dim3(p.nblk), dim3(kPartThreads), lds, s, ks, n,
-                     mp, p.tb, p.T, seg, ent);
+                     mp, p.tb, p.T, seg, ent, lkey);
 }
 
 hipError_t launch_build_tiled(int keyk, int mode, uint32_t* words, bool fresh, const KeySrc& ks,
@@ -653,15 +755,15 @@ hipError_t launch_build_tiled(int keyk, int mode, uint32_t* words, bool fresh, c
 
 hipError_t launch_probe_partition(int keyk, int mode, const KeySrc& ks, uint64_t n,
                                   const ModP& mp, const TilePlan& p, uint32_t* seg, uint2* ent,
-                                  hipStream_t s) {
+                                  uint16_t* lkey, hipStream_t s) {
   if (!n) return hipSuccess;
   if (!plan_ok(p) || p.tb + 12 > 32) return hipErrorInvalidValue;
-  const size_t lds1 = ((size_t)((p.T + 4) & ~3u) + 2 * p.C + 8) * 4;
+  const size_t lds1 = ((size_t)((p.T + 4) & ~3u) + 2 * p.C + p.C / 2 + 8) * 4;
   ProfScope ps("k_part_probe", s);
   if (p.kpt == 4) {
-    CB_DISPATCH(keyk, mode, (part_probe<KK, MM, 4>(p, ks, n, mp, seg, ent, lds1, s)));
+    CB_DISPATCH(keyk, mode, (part_probe<KK, MM, 4>(p, ks, n, mp, seg, ent, lkey, lds1, s)));
   } else {
-    CB_DISPATCH(keyk, mode, (part_probe<KK, MM, 8>(p, ks, n, mp, seg, ent, lds1, s)));
+    CB_DISPATCH(keyk, mode, (part_probe<KK, MM, 8>(p, ks, n, mp, seg, ent, lkey, lds1, s)));
   }
   return hipGetLastError();
 }
@@ -670,18 +772,19 @@ template <int RPT>
 static hipError_t tile_probe(const FilterPtrs& fp, uint32_t nf, uint64_t n, const TilePlan& p,
                              const uint32_t* seg, const uint2* ent, uint32_t* masks, size_t lds,
                              uint32_t G, hipStream_t s) {
+  static const uint32_t xflags = (uint32_t)env_int("CB_PROBE_XFLAGS", 0);
   // The instantiation must cover the tile exactly: RPT uint4 per thread.
   if ((1u << (p.tb - 5)) != (uint32_t)RPT * 4u * kTileProbeThreads) return hipErrorInvalidValue;
-  constexpr int D = RPT >= 2 ? 2 : 4;  // 32-64 KiB of tiles in flight per workgroup
+  constexpr int D = RPT >= 4 ? 2 : 4;  // 32-64 KiB of tiles in flight per workgroup
   allow_lds(k_tile_probe<8, RPT, D>, lds);
   hipLaunchKernelGGL((k_tile_probe<8, RPT, D>), dim3(p.T, G), dim3(kTileProbeThreads), lds, s, fp,
-                     nf, p.tb, p.T, seg, p.nblk, ent, p.C, n, masks);
+                     nf, p.tb, p.T, seg, p.nblk, ent, p.C, n, masks, xflags);
   return hipGetLastError();
 }
 
 hipError_t launch_probe_tiles(const FilterPtrs& fp, uint32_t nf, uint64_t n, const TilePlan& p,
-                              const uint32_t* seg, const uint2* ent, uint32_t* masks,
-                              uint64_t* hits, uint64_t hwords, hipStream_t s) {
+                              const uint32_t* seg, const uint2* ent, const uint16_t* lkey,
+                              uint32_t* masks, uint64_t* hits, uint64_t hwords, hipStream_t s) {
   if (!n || !nf) return hipSuccess;
   const uint32_t nbp = (p.nblk + 3) & ~3u;
   const size_t lds2 = ((size_t)2 * (1u << (p.tb - 5)) + 2 * nbp + kTileProbeThreads / 64) * 4 +
@@ -699,11 +802,13 @@ hipError_t launch_probe_tiles(const FilterPtrs& fp, uint32_t nf, uint64_t n, con
     }
   }
   if (e != hipSuccess) return e;
-  const uint64_t nw = (n + 63) / 64;
   ProfScope ps("k_masks_to_hits", s);
-  hipLaunchKernelGGL(k_masks_to_hits,
-                     dim3((uint32_t)((nw + kHitsWordsPerBlock - 1) / kHitsWordsPerBlock)),
-                     dim3(kHitsThreads), 0, s, masks, fp, nf, n, hits, hwords);
+  if (p.kpt == 4)
+    hipLaunchKernelGGL((k_masks_to_hits<4>), dim3(p.nblk), dim3(kHitsThreads), 0, s, masks, lkey,
+                       fp, nf, n, hits, hwords);
+  else
+    hipLaunchKernelGGL((k_masks_to_hits<8>), dim3(p.nblk), dim3(kHitsThreads), 0, s, masks, lkey,
+                       fp, nf, n, hits, hwords);
   return hipGetLastError();
 }
 

@@ -42,6 +42,7 @@ size_t build_seg_bytes(const TilePlan& p);
 size_t build_ent_bytes(const TilePlan& p);
 size_t probe_seg_bytes(const TilePlan& p);
 size_t probe_ent_bytes(const TilePlan& p);
+size_t probe_lkey_bytes(const TilePlan& p);
 
 hipError_t launch_insert_direct(int keyk, int mode, uint32_t* words, const KeySrc& ks, uint64_t n,
                                 const ModP& mp, hipStream_t s);
@@ -57,10 +58,10 @@ hipError_t launch_build_tiled(int keyk, int mode, uint32_t* words, bool fresh, c
 // ballot transpose into hits (K3).
 hipError_t launch_probe_partition(int keyk, int mode, const KeySrc& ks, uint64_t n,
                                   const ModP& mp, const TilePlan& p, uint32_t* seg, uint2* ent,
-                                  hipStream_t s);
+                                  uint16_t* lkey, hipStream_t s);
 hipError_t launch_probe_tiles(const FilterPtrs& fp, uint32_t nf, uint64_t n, const TilePlan& p,
-                              const uint32_t* seg, const uint2* ent, uint32_t* masks,
-                              uint64_t* hits, uint64_t hwords, hipStream_t s);
+                              const uint32_t* seg, const uint2* ent, const uint16_t* lkey,
+                              uint32_t* masks, uint64_t* hits, uint64_t hwords, hipStream_t s);
 hipError_t launch_mask_tail(uint32_t* words, uint64_t m, hipStream_t s);
 
 hipError_t launch_export_bools(const uint32_t* words, uint64_t m, uint8_t* out, hipStream_t s);
