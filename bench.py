@@ -96,8 +96,22 @@ def main():
     log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: {F} filters m={m} built, {n} lookups in HBM")
     keys_batch = lsmt_amd.DeviceKeys(look)
 
-    def step():
+    # FilterSet: the same F filters bit-sliced ([m][F]); built once from the
+    # filters (a full transpose) and timed separately as a maintenance cost.
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    fset = lsmt_amd.FilterSet(m, width=32 if F <= 32 else 64, device=local)
+    fset.assign_all(filters, stream=sh)
+    torch.cuda.synchronize(dev)
+    set_build_ms = (time.perf_counter() - t0) * 1e3
+
+    def step_tiled():
         lsmt_amd.probe(filters, keys_batch, out=hits, stream=sh)
+        if world > 1:
+            dist.all_gather_into_tensor(hits_all, hits)
+
+    def step_set():
+        fset.probe(keys_batch, out=hits, stream=sh)
         if world > 1:
             dist.all_gather_into_tensor(hits_all, hits)
 
@@ -118,13 +132,19 @@ def main():
             el = float(t.item())
         return el
 
-    for _ in range(args.warmup):
-        step()
-    el = timed(step, args.steps)
-    ms_step = el / args.steps * 1e3
     probes_per_step = n * nf_total
-    value = probes_per_step / (el / args.steps)
-    path_used = int(L.cb_last_path())
+    legs = {}
+    for name, fn in (("tiled", step_tiled), ("filterset", step_set)):
+        for _ in range(args.warmup):
+            fn()
+        el_leg = timed(fn, args.steps)
+        legs[name] = {"el": el_leg, "value": probes_per_step / (el_leg / args.steps),
+                      "ms_per_step": el_leg / args.steps * 1e3, "fn": fn}
+    best = max(legs, key=lambda k: legs[k]["value"])
+    el = legs[best]["el"]
+    step = legs[best]["fn"]
+    ms_step = el / args.steps * 1e3
+    value = legs[best]["value"]
 
     # ---- separate profiled pass: per-kernel durations from HIP events on `sh`
     def kernel_ms(names, fn, k):
@@ -143,14 +163,24 @@ def main():
                 out[nm] = {"avg_us": tot.value * 1e3 / cnt.value, "launches": int(cnt.value)}
         return out
 
-    probe_kernels = ["k_part_probe", "k_tile_probe", "k_masks_to_hits", "k_probe_direct"]
+    probe_kernels = ["k_part_probe", "k_tile_probe", "k_masks_to_hits", "k_probe_direct",
+                     "k_set_probe"]
     kprof = kernel_ms(probe_kernels, step, args.steps)
+    kprof_alt = kernel_ms(probe_kernels, legs["tiled" if best == "filterset" else "filterset"]["fn"], args.steps)
     dominant = max(kprof, key=lambda k: kprof[k]["avg_us"]) if kprof else None
 
-    # algorithmic bytes per probe launch:
-    # F*m/8*tau (each filter streamed once) + 16*n (keys) + F*n/8 (hit bitmaps)
-    tau = 1.0 - np.exp(-n * 1.0155 / (m / 512.0))
-    alg_bytes = F * m / 8 * tau + 16 * n + F * n / 8
+    if best == "tiled":
+        # algorithmic bytes per probe launch:
+        # F*m/8*tau (each filter streamed once) + 16*n (keys) + F*n/8 (hit bitmaps)
+        tau = 1.0 - np.exp(-n * 1.0155 / (m / 512.0))
+        alg_bytes = F * m / 8 * tau + 16 * n + F * n / 8
+        alg_def = "F*m/8*tau + 16n + F*n/8 (SURVEY.md §8d C3 row)"
+    else:
+        # bit-sliced layout (SURVEY.md §8d "alternative layout"): 64 B x distinct
+        # sectors touched by the a/b word reads + 16 B/key + the hit bitmaps
+        sectors = _set_sectors(filters, look_np, m, F)
+        alg_bytes = 64 * sectors + 16 * n + F * n / 8
+        alg_def = f"64 B x {sectors} distinct sectors + 16n + F*n/8 (SURVEY.md §8d alternative layout)"
     roof = None
     if dominant:
         dur_s = kprof[dominant]["avg_us"] * 1e-6
@@ -158,8 +188,18 @@ def main():
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("k_tile_probe" if dominant == "k_tile_probe" else dominant),
                 "kernel": dominant, "kernel_avg_us": round(kprof[dominant]["avg_us"], 2),
-                "algorithmic_bytes": int(alg_bytes),
+                "algorithmic_bytes": int(alg_bytes), "algorithmic_def": alg_def,
                 "step_effective_GBps": round(alg_bytes / (el / args.steps) / 1e9, 1)}
+
+    # maintenance cost of the set on the flush path: one new filter into an
+    # empty slot (sparse OR of its set bits)
+    fset2 = lsmt_amd.FilterSet(m, width=32, device=local)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    fset2.assign(0, filters[0], stream=sh)
+    torch.cuda.synchronize(dev)
+    set_assign_ms = (time.perf_counter() - t0) * 1e3
+    del fset2
 
     # ---- C2 build: 1M keys -> one fresh 16 MiB filter (zero-fill + batched insert)
     bk = torch.from_numpy(workload.c2_build_keys(args.build_keys)).to(dev)
@@ -229,14 +269,43 @@ def main():
                        "n_keys": n, "filters_per_gpu": F, "filters_total": nf_total, "m_bits": m,
                        "keys_per_filter": kpf,
                        "parallelism": "filter-sharded" + (", RCCL all-gather of hit bitmaps" if world > 1 else "")},
-            "path": {1: "direct", 2: "tiled"}.get(path_used, str(path_used)),
+            "path": best,
             "kernels_us": {k: round(v["avg_us"], 2) for k, v in kprof.items()},
+            "alt_paths": {k: {"value": round(v["value"], 1), "ms_per_step": round(v["ms_per_step"], 4)}
+                          for k, v in legs.items() if k != best},
+            "alt_kernels_us": {k: round(v["avg_us"], 2) for k, v in kprof_alt.items()},
+            "filterset": {"build_all_ms": round(set_build_ms, 3), "assign_one_empty_slot_ms": round(set_assign_ms, 3),
+                          "bytes": m * (4 if F <= 32 else 8)},
             "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _set_sectors(filters, look_np, m, F):
+    """Distinct 64-byte sectors of the bit-sliced set that one probe batch reads:
+    set[a] for every key, set[b] only where set[a] != 0 (the short-circuit).
+    Uses the filters' packed words (any filter has bit a set <=> set[a] != 0)
+    and a numpy restatement of the hashes."""
+    anyw = np.zeros((m + 31) // 32, np.uint32)
+    for f in filters:
+        anyw |= f.packed()
+    h1 = np.full(look_np.shape[0], 5381, np.uint64)
+    h2 = np.zeros(look_np.shape[0], np.uint64)
+    with np.errstate(over="ignore"):
+        for j in range(look_np.shape[1]):
+            b = look_np[:, j].astype(np.uint64)
+            h1 = (h1 << np.uint64(5)) + h1 + b
+            h2 = h2 * np.uint64(31) + b
+    a = (h1 % np.uint64(m)).astype(np.int64)
+    bpos = (h2 % np.uint64(m)).astype(np.int64)
+    a_set = (anyw[a >> 5] >> (a & 31).astype(np.uint32)) & 1
+    word_bytes = 4 if F <= 32 else 8
+    sec_a = (a * word_bytes) >> 6
+    sec_b = (bpos[a_set.astype(bool)] * word_bytes) >> 6
+    return int(np.unique(np.concatenate([sec_a, sec_b])).size)
 
 
 def _pmc_traffic(kernel):

@@ -115,6 +115,30 @@ int cb_filter_to_bytes(const cb_filter* f, uint8_t* out, uint64_t cap, uint64_t*
  * fields skipped) into a new filter on `device`. */
 int cb_filter_from_bytes(const uint8_t* in, uint64_t len, int device, cb_filter** out);
 
+/* ---- bit-sliced filter sets (the read-path fan-out) ---- */
+/* A FilterSet holds up to `width` (32 or 64) filters of one size m in a
+ * position-major layout: word p (uint32 / uint64) has bit s = bit p of the
+ * filter in slot s. Probing it answers may_contain for every slot with two
+ * word reads per key (Database::get's per-table loop, src/lib.rs:129-134,
+ * collapsed; m is uniform across SSTables, src/sstable.rs:44,59). The set is a
+ * derived copy: the cb_filter handles stay the source of truth. */
+typedef struct cb_filterset cb_filterset;
+int cb_set_create(uint64_t m_bits, uint32_t width, int device, cb_filterset** out);
+int cb_set_destroy(cb_filterset* set);
+/* used = 1 + the highest slot assigned so far (the number of hit rows). */
+int cb_set_info(const cb_filterset* set, uint64_t* m_out, uint32_t* width_out, uint32_t* used_out);
+/* slot := f's bits (f->m must equal the set's m). O(set bits) when the slot is
+ * empty (the LSM case: a new SSTable takes a free slot), a full pass otherwise. */
+int cb_set_assign(cb_filterset* set, uint32_t slot, const cb_filter* f, void* stream);
+/* slots 0..nf-1 := filters[0..nf-1], other slots cleared; used = nf. */
+int cb_set_assign_all(cb_filterset* set, const cb_filter* const* filters, uint32_t nf, void* stream);
+int cb_set_clear_slot(cb_filterset* set, uint32_t slot, void* stream);
+/* hits: [used][ceil(n/64)] uint64, row s = slot s's may_contain bits. */
+int cb_set_probe_fixed(const cb_filterset* set, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                       uint64_t* hits, void* stream);
+int cb_set_probe_var(const cb_filterset* set, const uint8_t* bytes, const uint64_t* offsets,
+                     uint64_t n, uint64_t* hits, void* stream);
+
 /* ---- tuning / introspection (bench + tests) ---- */
 /* Path selection: 0 = auto, 1 = force direct (per-key atomics / gathers),
  * 2 = force tiled (LDS-staged filter tiles). Process-wide. */
@@ -124,7 +148,8 @@ int cb_last_path(void);
 /* Per-kernel timing with HIP events recorded on each launch's own stream
  * (off by default). Kernel names: "k_insert_direct", "k_probe_direct",
  * "k_part_build", "k_tile_build", "k_part_probe", "k_tile_probe",
- * "k_masks_to_hits". cb_profile_read waits for pending events and returns the
+ * "k_masks_to_hits", "k_set_build", "k_set_or_slot", "k_set_put_slot",
+ * "k_set_probe". cb_profile_read waits for pending events and returns the
  * accumulated milliseconds and launch count for one kernel. */
 int cb_profile_enable(int on);
 int cb_profile_reset(void);

@@ -12,6 +12,7 @@ from .bloom import (  # noqa: E402
     BloomFilter,
     BloomProto,
     DeviceKeys,
+    FilterSet,
     KeyBatch,
     device_count,
     last_path,
@@ -20,6 +21,6 @@ from .bloom import (  # noqa: E402
     unpack_hits,
 )
 
-__all__ = ["BloomFilter", "BloomProto", "DeviceKeys", "KeyBatch", "device_count", "last_path",
+__all__ = ["BloomFilter", "BloomProto", "DeviceKeys", "FilterSet", "KeyBatch", "device_count", "last_path",
            "probe", "set_path", "unpack_hits"]
 __version__ = "0.1.0"

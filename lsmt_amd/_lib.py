@@ -84,6 +84,14 @@ def load():
         "cb_filter_from_bytes": ([u8p, u64, i32, pp], i32),
         "cb_set_path": ([i32], i32),
         "cb_last_path": ([], i32),
+        "cb_set_create": ([u64, u32, i32, pp], i32),
+        "cb_set_destroy": ([P], i32),
+        "cb_set_info": ([P, pu64, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)], i32),
+        "cb_set_assign": ([P, u32, P, P], i32),
+        "cb_set_assign_all": ([P, P, u32, P], i32),
+        "cb_set_clear_slot": ([P, u32, P], i32),
+        "cb_set_probe_fixed": ([P, u8p, u32, u64, P, P], i32),
+        "cb_set_probe_var": ([P, u8p, P, u64, P, P], i32),
         "cb_profile_enable": ([i32], i32),
         "cb_profile_reset": ([], i32),
         "cb_profile_read": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), pu64], i32),

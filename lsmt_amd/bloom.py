@@ -33,8 +33,8 @@ import numpy as np
 from . import _lib
 from ._lib import CassBloomError, check
 
-__all__ = ["BloomFilter", "BloomProto", "probe", "set_path", "last_path", "device_count",
-           "DeviceKeys", "KeyBatch"]
+__all__ = ["BloomFilter", "BloomProto", "FilterSet", "probe", "set_path", "last_path",
+           "device_count", "DeviceKeys", "KeyBatch"]
 
 
 def _L():
@@ -302,6 +302,80 @@ def probe(filters: Sequence[BloomFilter], keys, out=None, stream=None) -> np.nda
         kp, k1 = _ptr_of(b.keys)
         _raise(_L().cb_probe_fixed(ctypes.cast(arr, ctypes.c_void_p), nf, kp, b.key_len, b.n, op, s))
     return result
+
+
+class FilterSet:
+    """Up to ``width`` (32 or 64) filters of one size m, bit-sliced in HBM for
+    the read-path fan-out (Database::get, src/lib.rs:129-134): one probe call
+    answers may_contain for every slot with two word reads per key. A derived
+    copy — the BloomFilter handles remain the source of truth."""
+
+    def __init__(self, m: int, width: int = 32, device: int = 0):
+        self._h = ctypes.c_void_p()
+        _raise(_L().cb_set_create(int(m), int(width), int(device), ctypes.byref(self._h)))
+        self.m, self.width, self.device = int(m), int(width), int(device)
+
+    @classmethod
+    def from_filters(cls, filters: Sequence[BloomFilter], width: int | None = None,
+                     stream=None) -> "FilterSet":
+        if not filters:
+            raise ValueError("need at least one filter")
+        width = width or (32 if len(filters) <= 32 else 64)
+        s = cls(filters[0].m, width)
+        s.assign_all(filters, stream=stream)
+        return s
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            _L().cb_set_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def used(self) -> int:
+        u = ctypes.c_uint32()
+        check(_L().cb_set_info(self._h, None, None, ctypes.byref(u)))
+        return int(u.value)
+
+    def assign(self, slot: int, f: BloomFilter, stream=None) -> None:
+        f.flush(stream)
+        _raise(_L().cb_set_assign(self._h, int(slot), f.handle, _stream(stream)))
+
+    def assign_all(self, filters: Sequence[BloomFilter], stream=None) -> None:
+        for f in filters:
+            f.flush(stream)
+        arr = (ctypes.c_void_p * max(len(filters), 1))(*[f.handle.value for f in filters])
+        _raise(_L().cb_set_assign_all(self._h, ctypes.cast(arr, ctypes.c_void_p), len(filters),
+                                      _stream(stream)))
+
+    def clear_slot(self, slot: int, stream=None) -> None:
+        _raise(_L().cb_set_clear_slot(self._h, int(slot), _stream(stream)))
+
+    def probe(self, keys, out=None, stream=None) -> np.ndarray:
+        """uint64[used, ceil(n/64)]: row s = slot s's may_contain bits."""
+        b = as_batch(keys)
+        used = self.used
+        words = (b.n + 63) // 64
+        if out is None:
+            out = np.zeros((max(used, 1), max(words, 1)), np.uint64)
+            result = out[:used, :words]
+        else:
+            result = out
+        op, keep = _ptr_of(out)
+        s = _stream(stream)
+        if b.is_var:
+            dp, k1 = _ptr_of(b.data)
+            offp, k2 = _ptr_of(b.offsets)
+            _raise(_L().cb_set_probe_var(self._h, dp, offp, b.n, op, s))
+        else:
+            kp, k1 = _ptr_of(b.keys)
+            _raise(_L().cb_set_probe_fixed(self._h, kp, b.key_len, b.n, op, s))
+        return result
 
 
 def unpack_hits(hits: np.ndarray, n: int) -> np.ndarray:

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "cassbloom.h"
+#include "filterset.hpp"
 #include "kernels.hpp"
 
 using cb::FilterPtrs;
@@ -34,6 +35,17 @@ struct cb_filter {
   // needs the words, and skipped by a fresh tiled build (which writes every
   // tile). Exchanged atomically so concurrent readers issue it once.
   std::atomic<bool> needs_zero{false};
+  int mode = 0;
+  ModP mp{};
+};
+
+struct cb_filterset {
+  uint64_t m = 0;
+  int device = 0;
+  uint32_t width = 32;
+  void* words = nullptr;  // device, m (rounded up to 32) words of width bits
+  uint32_t used = 0;      // 1 + highest assigned slot
+  uint64_t dirty = 0;     // bit s: slot s may hold set bits
   int mode = 0;
   ModP mp{};
 };
@@ -363,6 +375,38 @@ int probe_impl(const cb_filter* const* filters, uint32_t nf, const uint8_t* keys
   g_last_path = last_path;
   if (host_hits) {
     HIP_TRY(hipMemcpyAsync(hits, dhits, (size_t)nf * hwords * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  } else if (sk.staged) {
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  return CB_OK;
+}
+
+int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t* offsets,
+                   uint32_t key_len, uint64_t n, uint64_t* hits, hipStream_t s) {
+  if (!set) return fail(CB_EINVAL, "null set");
+  if (n == 0 || set->used == 0) return CB_OK;
+  if (!hits) return fail(CB_EINVAL, "null hits");
+  if (offsets == nullptr && keys == nullptr && key_len) return fail(CB_EINVAL, "null keys");
+  DeviceGuard dg(set->device);
+  Workspace& ws = workspace(set->device, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  StagedKeys sk;
+  int rc = offsets ? stage_var(ws, keys, offsets, n, s, sk)
+                   : stage_fixed(ws, keys, key_len, n, s, sk);
+  if (rc) return rc;
+  const uint64_t hwords = (n + 63) / 64;
+  uint64_t* dhits = hits;
+  const bool host_hits = !is_device_ptr(hits);
+  if (host_hits) {
+    HIP_TRY(ws.hits.reserve((size_t)set->used * hwords * 8, s));
+    dhits = (uint64_t*)ws.hits.p;
+  }
+  HIP_TRY(cb::launch_set_probe(sk.keyk, set->mode, set->width, set->words, set->used, sk.ks, n,
+                               set->mp, dhits, hwords, s));
+  g_last_path = 3;
+  if (host_hits) {
+    HIP_TRY(hipMemcpyAsync(hits, dhits, (size_t)set->used * hwords * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
   } else if (sk.staged) {
     HIP_TRY(hipStreamSynchronize(s));
@@ -744,6 +788,112 @@ int cb_filter_from_bytes(const uint8_t* in, uint64_t len, int device, cb_filter*
   }
   *out = f;
   return CB_OK;
+}
+
+
+// ---- bit-sliced filter sets ----
+
+int cb_set_create(uint64_t m_bits, uint32_t width, int device, cb_filterset** out) {
+  if (!out) return fail(CB_EINVAL, "null out");
+  *out = nullptr;
+  if (width != 32 && width != 64) return fail(CB_EINVAL, "set width must be 32 or 64");
+  if (m_bits == 0) return fail(CB_EZEROM, "attempt to calculate the remainder with a divisor of zero");
+  int rc = cb_init(device);
+  if (rc) return rc;
+  DeviceGuard dg(device);
+  std::unique_ptr<cb_filterset> set(new cb_filterset());
+  set->m = m_bits;
+  set->device = device;
+  set->width = width;
+  set->mp = cb::make_modp(m_bits, &set->mode);
+  const size_t bytes = (size_t)((m_bits + 31) / 32 * 32) * (width / 8);
+  hipError_t e = hipMalloc(&set->words, bytes);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(CB_ENOMEM, "hipMalloc failed for filter set words");
+  }
+  HIP_TRY(hipMemsetAsync(set->words, 0, bytes, nullptr));
+  HIP_TRY(hipStreamSynchronize(nullptr));
+  *out = set.release();
+  return CB_OK;
+}
+
+int cb_set_destroy(cb_filterset* set) {
+  if (!set) return CB_OK;
+  {
+    DeviceGuard dg(set->device);
+    if (set->words) (void)hipFree(set->words);
+  }
+  delete set;
+  return CB_OK;
+}
+
+int cb_set_info(const cb_filterset* set, uint64_t* m_out, uint32_t* width_out, uint32_t* used_out) {
+  if (!set) return fail(CB_EINVAL, "null set");
+  if (m_out) *m_out = set->m;
+  if (width_out) *width_out = set->width;
+  if (used_out) *used_out = set->used;
+  return CB_OK;
+}
+
+int cb_set_assign(cb_filterset* set, uint32_t slot, const cb_filter* f, void* stream) {
+  if (!set || !f) return fail(CB_EINVAL, "null argument");
+  if (slot >= set->width) return fail(CB_EINVAL, "slot out of range");
+  if (f->m != set->m) return fail(CB_EINVAL, "filter size differs from the set's m");
+  if (f->device != set->device) return fail(CB_EINVAL, "filter and set live on different devices");
+  hipStream_t s = (hipStream_t)stream;
+  DeviceGuard dg(set->device);
+  HIP_TRY(ensure_zeroed(f, s));
+  if (set->dirty >> slot & 1)
+    HIP_TRY(cb::launch_set_put_slot(f->words, set->m, slot, set->width, set->words, s));
+  else
+    HIP_TRY(cb::launch_set_or_slot(f->words, set->m, slot, set->width, set->words, s));
+  set->dirty |= 1ull << slot;
+  set->used = std::max(set->used, slot + 1);
+  return CB_OK;
+}
+
+int cb_set_assign_all(cb_filterset* set, const cb_filter* const* filters, uint32_t nf, void* stream) {
+  if (!set) return fail(CB_EINVAL, "null set");
+  if (nf > set->width) return fail(CB_EINVAL, "more filters than set slots");
+  if (nf && !filters) return fail(CB_EINVAL, "null filters");
+  hipStream_t s = (hipStream_t)stream;
+  DeviceGuard dg(set->device);
+  FilterPtrs fp{};
+  for (uint32_t i = 0; i < nf; ++i) {
+    const cb_filter* f = filters[i];
+    if (!f) return fail(CB_EINVAL, "null filter");
+    if (f->m != set->m) return fail(CB_EINVAL, "filter size differs from the set's m");
+    if (f->device != set->device) return fail(CB_EINVAL, "filter and set live on different devices");
+    HIP_TRY(ensure_zeroed(f, s));
+    fp.w[i] = f->words;
+    fp.row[i] = i;
+  }
+  HIP_TRY(cb::launch_set_build(fp, nf, set->m, set->width, set->words, s));
+  set->used = nf;
+  set->dirty = nf >= 64 ? ~0ull : ((1ull << nf) - 1);
+  return CB_OK;
+}
+
+int cb_set_clear_slot(cb_filterset* set, uint32_t slot, void* stream) {
+  if (!set) return fail(CB_EINVAL, "null set");
+  if (slot >= set->width) return fail(CB_EINVAL, "slot out of range");
+  if (!(set->dirty >> slot & 1)) return CB_OK;
+  DeviceGuard dg(set->device);
+  HIP_TRY(cb::launch_set_put_slot(nullptr, set->m, slot, set->width, set->words, (hipStream_t)stream));
+  set->dirty &= ~(1ull << slot);
+  return CB_OK;
+}
+
+int cb_set_probe_fixed(const cb_filterset* set, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                       uint64_t* hits, void* stream) {
+  return set_probe_impl(set, keys, nullptr, key_len, n, hits, (hipStream_t)stream);
+}
+
+int cb_set_probe_var(const cb_filterset* set, const uint8_t* bytes, const uint64_t* offsets,
+                     uint64_t n, uint64_t* hits, void* stream) {
+  if (!offsets) return fail(CB_EINVAL, "null offsets");
+  return set_probe_impl(set, bytes, offsets, 0, n, hits, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -1,0 +1,315 @@
+// filterset.hip — bit-sliced filter sets for the read-path fan-out.
+//
+// A FilterSet holds up to W (32 or 64) Bloom filters of one size m in a
+// position-major layout: word p (uint32 for W = 32, uint64 for W = 64) has
+// bit s = bit p of the filter in slot s. Database::get probes every SSTable
+// for each key (/root/reference/src/lib.rs:129-134); with m uniform across
+// tables (src/sstable.rs:44,59) one key's answer for ALL slots is
+//   set[a] & set[b],  (a, b) = (h1 % m, h2 % m)            (src/bloom.rs:26-51)
+// i.e. two random word reads per key instead of one per (key, filter). The
+// reference's `&&` short-circuit is kept per key: set[b] is read only when
+// set[a] has any slot bit set.
+//
+// Compulsory HBM bytes per probe batch (SURVEY.md §8d alternative layout):
+// 64 B x distinct sectors touched by the a/b reads + 16 B/key + the hit bitmap.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <type_traits>
+
+#include "filterset.hpp"
+#include "profile.hpp"
+
+namespace cb {
+namespace {
+
+typedef const __attribute__((address_space(1))) uint32_t* gsp32;
+typedef const __attribute__((address_space(1))) uint64_t* gsp64;
+
+// In-register 32x32 bit transpose: on entry a[i] bit j = element (i, j); on
+// exit a[j] bit i = element (i, j). Every index is static after unrolling.
+template <int J>
+__device__ __forceinline__ void transpose_step(uint32_t (&a)[32]) {
+  constexpr uint32_t m = J == 16 ? 0x0000FFFFu
+                         : J == 8 ? 0x00FF00FFu
+                         : J == 4 ? 0x0F0F0F0Fu
+                         : J == 2 ? 0x33333333u
+                                  : 0x55555555u;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    if ((k & J) == 0) {
+      const uint32_t t = ((a[k] >> J) ^ a[k | J]) & m;
+      a[k] ^= t << J;
+      a[k | J] ^= t;
+    }
+  }
+}
+
+__device__ __forceinline__ void transpose32(uint32_t (&a)[32]) {
+  transpose_step<16>(a);
+  transpose_step<8>(a);
+  transpose_step<4>(a);
+  transpose_step<2>(a);
+  transpose_step<1>(a);
+}
+
+// Rebuild slots 0..nf-1 from packed filters (slots >= nf become zero). One
+// thread per 32-position group g: reads word g of every filter (coalesced
+// across threads), transposes, writes the 32 set words of the group.
+template <int W>
+__global__ __launch_bounds__(256) void k_set_build(FilterPtrs fp, uint32_t nf, uint64_t ngroups,
+                                                   uint64_t m, void* __restrict__ set) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < ngroups; g += stride) {
+    uint32_t a[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) a[i] = (uint32_t)i < nf ? fp.w[i][g] : 0u;
+    transpose32(a);
+    const uint64_t p0 = g * 32;
+    const uint32_t valid = (uint32_t)min<uint64_t>(32, m - p0);
+    if constexpr (W == 32) {
+      uint32_t* out = reinterpret_cast<uint32_t*>(set) + p0;
+      if (valid == 32) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          reinterpret_cast<uint4*>(out)[q] = make_uint4(a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+          if ((uint32_t)j < valid) out[j] = a[j];
+      }
+    } else {
+      uint32_t c[32];
+#pragma unroll
+      for (int i = 0; i < 32; ++i) c[i] = (uint32_t)(32 + i) < nf ? fp.w[32 + i][g] : 0u;
+      transpose32(c);
+      uint32_t* out = reinterpret_cast<uint32_t*>(set) + 2 * p0;  // (lo, hi) per position
+      if (valid == 32) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          reinterpret_cast<uint4*>(out)[q] = make_uint4(a[2 * q], c[2 * q], a[2 * q + 1], c[2 * q + 1]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+          if ((uint32_t)j < valid) {
+            out[2 * j] = a[j];
+            out[2 * j + 1] = c[j];
+          }
+      }
+    }
+  }
+}
+
+// OR a packed filter into a slot known to be all-zero: only the set bits
+// (~1.5% at BASELINE densities) touch the set. Position p belongs to exactly
+// one thread (the one owning word p/32), so a plain read-modify-write is safe.
+template <int W>
+__global__ __launch_bounds__(256) void k_set_or_slot(const uint32_t* __restrict__ words,
+                                                     uint64_t nwords, uint32_t slot,
+                                                     void* __restrict__ set) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < nwords; w += stride) {
+    uint32_t v = words[w];
+    while (v) {
+      const uint32_t j = __builtin_ctz(v);
+      v &= v - 1;
+      const uint64_t p = w * 32 + j;
+      if constexpr (W == 32)
+        reinterpret_cast<uint32_t*>(set)[p] |= 1u << slot;
+      else
+        reinterpret_cast<uint64_t*>(set)[p] |= 1ull << slot;
+    }
+  }
+}
+
+// Replace a slot's bits wholesale (slot possibly non-zero): every position is
+// rewritten. words == nullptr clears the slot.
+template <int W>
+__global__ __launch_bounds__(256) void k_set_put_slot(const uint32_t* __restrict__ words,
+                                                      uint64_t m, uint32_t slot,
+                                                      void* __restrict__ set) {
+  const uint64_t ngroups = (m + 31) / 32;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < ngroups; g += stride) {
+    const uint32_t v = words ? words[g] : 0u;
+    const uint32_t valid = (uint32_t)min<uint64_t>(32, m - g * 32);
+    for (uint32_t j = 0; j < valid; ++j) {
+      const uint64_t p = g * 32 + j;
+      if constexpr (W == 32) {
+        uint32_t* s = reinterpret_cast<uint32_t*>(set) + p;
+        *s = (*s & ~(1u << slot)) | (((v >> j) & 1u) << slot);
+      } else {
+        uint64_t* s = reinterpret_cast<uint64_t*>(set) + p;
+        *s = (*s & ~(1ull << slot)) | ((uint64_t)((v >> j) & 1u) << slot);
+      }
+    }
+  }
+}
+
+constexpr uint32_t kSetProbeThreads = 256;  // 4 waves
+constexpr uint32_t kSetWords = 16;          // hit words (x64 keys) per block: 1024 keys
+
+// KPL keys per lane (one hit word each, KPL words per wave): all KPL set[a]
+// reads are issued before any is consumed, then the set[b] reads, so each lane
+// keeps KPL independent random reads in flight. SC = the reference's `&&`
+// short-circuit (src/bloom.rs:50): set[b] is read only when set[a] != 0
+// (fewer bytes, but b waits for a). Ballots turn each 64-key word into one
+// hit word per slot, staged in LDS so every slot row leaves as a contiguous
+// 128-byte segment.
+template <int KEYK, int MODE, int W, int KPL, bool SC>
+__global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __restrict__ set,
+                                                                uint32_t used, KeySrc ks,
+                                                                uint64_t n, ModP mp,
+                                                                uint64_t* __restrict__ hits,
+                                                                uint64_t hwords) {
+  static_assert(KPL * (kSetProbeThreads / 64) == kSetWords, "block covers kSetWords words");
+  typedef typename std::conditional<W == 32, uint32_t, uint64_t>::type word_t;
+  typedef const __attribute__((address_space(1))) word_t* gptr;
+  __shared__ uint64_t hb[64][kSetWords];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint64_t wbase = (uint64_t)blockIdx.x * kSetWords;
+  const gptr sp = (gptr)set;
+  uint64_t pa[KPL], pb[KPL];
+  bool ok[KPL];
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) {
+    const uint64_t k = (wbase + (uint64_t)(wave * KPL + i)) * 64 + lane;
+    ok[i] = k < n;
+    pa[i] = pb[i] = 0;
+    if (ok[i]) key_positions<KEYK, MODE>(ks, k, mp, pa[i], pb[i]);
+  }
+  word_t va[KPL], vb[KPL];
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) va[i] = ok[i] ? sp[pa[i]] : (word_t)0;
+  if constexpr (!SC) {
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) vb[i] = ok[i] ? sp[pb[i]] : (word_t)0;
+  } else {
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) vb[i] = va[i] ? sp[pb[i]] : (word_t)0;
+  }
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) {
+    const word_t mask = va[i] & vb[i];
+    uint64_t mine = 0;
+#pragma unroll
+    for (uint32_t f = 0; f < (uint32_t)W; ++f) {
+      if (f < used) {
+        const uint64_t bal = __ballot((mask >> f) & 1u);
+        mine = (lane == f) ? bal : mine;
+      }
+    }
+    if (lane < used) hb[lane][wave * KPL + i] = mine;
+  }
+  __syncthreads();
+  const uint64_t nw = (n + 63) / 64;
+  for (uint32_t i = threadIdx.x; i < used * kSetWords; i += kSetProbeThreads) {
+    const uint32_t f = i / kSetWords, w = i % kSetWords;
+    if (wbase + w < nw) hits[(uint64_t)f * hwords + wbase + w] = hb[f][w];
+  }
+}
+
+#define CB_SET_DISPATCH(keyk, mode, width, CALL)                                              \
+  switch (((keyk) * 3 + (mode)) * 2 + ((width) == 64)) {                                     \
+    case 0: { constexpr int KK = KEY_FIXED16, MM = MOD_POW2_32, WW = 32; CALL; } break;     \
+    case 1: { constexpr int KK = KEY_FIXED16, MM = MOD_POW2_32, WW = 64; CALL; } break;     \
+    case 2: { constexpr int KK = KEY_FIXED16, MM = MOD_POW2_64, WW = 32; CALL; } break;     \
+    case 3: { constexpr int KK = KEY_FIXED16, MM = MOD_POW2_64, WW = 64; CALL; } break;     \
+    case 4: { constexpr int KK = KEY_FIXED16, MM = MOD_GENERIC, WW = 32; CALL; } break;     \
+    case 5: { constexpr int KK = KEY_FIXED16, MM = MOD_GENERIC, WW = 64; CALL; } break;     \
+    case 6: { constexpr int KK = KEY_FIXED, MM = MOD_POW2_32, WW = 32; CALL; } break;       \
+    case 7: { constexpr int KK = KEY_FIXED, MM = MOD_POW2_32, WW = 64; CALL; } break;       \
+    case 8: { constexpr int KK = KEY_FIXED, MM = MOD_POW2_64, WW = 32; CALL; } break;       \
+    case 9: { constexpr int KK = KEY_FIXED, MM = MOD_POW2_64, WW = 64; CALL; } break;       \
+    case 10: { constexpr int KK = KEY_FIXED, MM = MOD_GENERIC, WW = 32; CALL; } break;      \
+    case 11: { constexpr int KK = KEY_FIXED, MM = MOD_GENERIC, WW = 64; CALL; } break;      \
+    case 12: { constexpr int KK = KEY_VAR, MM = MOD_POW2_32, WW = 32; CALL; } break;        \
+    case 13: { constexpr int KK = KEY_VAR, MM = MOD_POW2_32, WW = 64; CALL; } break;        \
+    case 14: { constexpr int KK = KEY_VAR, MM = MOD_POW2_64, WW = 32; CALL; } break;        \
+    case 15: { constexpr int KK = KEY_VAR, MM = MOD_POW2_64, WW = 64; CALL; } break;        \
+    case 16: { constexpr int KK = KEY_VAR, MM = MOD_GENERIC, WW = 32; CALL; } break;        \
+    case 17: { constexpr int KK = KEY_VAR, MM = MOD_GENERIC, WW = 64; CALL; } break;        \
+    default: return hipErrorInvalidValue;                                                   \
+  }
+
+inline uint32_t grid_cap(uint64_t items, uint32_t cap) {
+  uint64_t g = (items + 255) / 256;
+  if (g < 1) g = 1;
+  return (uint32_t)(g < cap ? g : cap);
+}
+
+}  // namespace
+
+hipError_t launch_set_build(const FilterPtrs& fp, uint32_t nf, uint64_t m, uint32_t width,
+                            void* set, hipStream_t s) {
+  if (!m) return hipSuccess;
+  const uint64_t ngroups = (m + 31) / 32;
+  ProfScope ps("k_set_build", s);
+  if (width == 32)
+    hipLaunchKernelGGL((k_set_build<32>), dim3(grid_cap(ngroups, 8192)), dim3(256), 0, s, fp, nf,
+                       ngroups, m, set);
+  else
+    hipLaunchKernelGGL((k_set_build<64>), dim3(grid_cap(ngroups, 8192)), dim3(256), 0, s, fp, nf,
+                       ngroups, m, set);
+  return hipGetLastError();
+}
+
+hipError_t launch_set_or_slot(const uint32_t* words, uint64_t m, uint32_t slot, uint32_t width,
+                              void* set, hipStream_t s) {
+  if (!m) return hipSuccess;
+  const uint64_t nw = (m + 31) / 32;
+  ProfScope ps("k_set_or_slot", s);
+  if (width == 32)
+    hipLaunchKernelGGL((k_set_or_slot<32>), dim3(grid_cap(nw, 8192)), dim3(256), 0, s, words, nw,
+                       slot, set);
+  else
+    hipLaunchKernelGGL((k_set_or_slot<64>), dim3(grid_cap(nw, 8192)), dim3(256), 0, s, words, nw,
+                       slot, set);
+  return hipGetLastError();
+}
+
+hipError_t launch_set_put_slot(const uint32_t* words, uint64_t m, uint32_t slot, uint32_t width,
+                               void* set, hipStream_t s) {
+  if (!m) return hipSuccess;
+  const uint64_t ng = (m + 31) / 32;
+  ProfScope ps("k_set_put_slot", s);
+  if (width == 32)
+    hipLaunchKernelGGL((k_set_put_slot<32>), dim3(grid_cap(ng, 8192)), dim3(256), 0, s, words, m,
+                       slot, set);
+  else
+    hipLaunchKernelGGL((k_set_put_slot<64>), dim3(grid_cap(ng, 8192)), dim3(256), 0, s, words, m,
+                       slot, set);
+  return hipGetLastError();
+}
+
+template <int KK, int MM, int WW>
+static void set_probe(bool sc, const void* set, uint32_t used, const KeySrc& ks, uint64_t n,
+                      const ModP& mp, uint64_t* hits, uint64_t hwords, uint32_t grid,
+                      hipStream_t s) {
+  if (sc)
+    hipLaunchKernelGGL((k_set_probe<KK, MM, WW, 4, true>), dim3(grid), dim3(kSetProbeThreads), 0,
+                       s, set, used, ks, n, mp, hits, hwords);
+  else
+    hipLaunchKernelGGL((k_set_probe<KK, MM, WW, 4, false>), dim3(grid), dim3(kSetProbeThreads),
+                       0, s, set, used, ks, n, mp, hits, hwords);
+}
+
+hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set, uint32_t used,
+                            const KeySrc& ks, uint64_t n, const ModP& mp, uint64_t* hits,
+                            uint64_t hwords, hipStream_t s) {
+  if (!n || !used) return hipSuccess;
+  // CB_SET_SC=0 reads set[b] unconditionally (one latency, more bytes);
+  // default keeps the reference's short-circuit.
+  static const bool sc = [] {
+    const char* v = getenv("CB_SET_SC");
+    return !(v && v[0] == '0');
+  }();
+  const uint64_t nw = (n + 63) / 64;
+  const uint32_t grid = (uint32_t)((nw + kSetWords - 1) / kSetWords);
+  ProfScope ps("k_set_probe", s);
+  CB_SET_DISPATCH(keyk, mode, width,
+                  (set_probe<KK, MM, WW>(sc, set, used, ks, n, mp, hits, hwords, grid, s)));
+  return hipGetLastError();
+}
+
+}  // namespace cb

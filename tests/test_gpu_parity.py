@@ -279,3 +279,64 @@ def test_device_resident_keys_and_hits(gpu):
     o.insert_fixed(keys)
     expect = oracle.probe_fixed([o], look.cpu().numpy())
     assert np.array_equal(out.cpu().numpy().view(np.uint64), expect)
+
+
+# ---- bit-sliced filter sets ----------------------------------------------------------
+
+@pytest.mark.parametrize("width", [32, 64])
+@pytest.mark.parametrize("m", [1, 1000, 100003, 1 << 20, (1 << 21) + 3])
+def test_filterset_probe_matches_oracle(gpu, width, m):
+    nf = 5 if width == 32 else 37
+    filters, refs = [], []
+    for f in range(nf):
+        g, o = build_pair(gpu, m, workload.key_range(500 + f, 4000))
+        filters.append(g)
+        refs.append(o)
+    s = gpu.FilterSet.from_filters(filters, width=width)
+    assert s.used == nf
+    look = workload.probe_lookups(50_001, nf, 4000, seed_base=500, absent_seed=997)
+    expect = oracle.probe_fixed(refs, look)
+    assert np.array_equal(s.probe(look), expect)
+    # the per-filter multi-probe agrees with the set
+    assert np.array_equal(gpu.probe(filters, look), expect)
+
+
+def test_filterset_assign_slots_and_var_keys(gpu):
+    m = (1 << 20) + 17
+    filters, refs = [], []
+    for f in range(6):
+        g, o = build_pair(gpu, m, workload.key_range(600 + f, 5000))
+        filters.append(g)
+        refs.append(o)
+    s = gpu.FilterSet(m, width=32)
+    for i in (0, 3, 1):  # sparse path: empty slots
+        s.assign(i, filters[i])
+    assert s.used == 4
+    look = workload.probe_lookups(40_000, 6, 5000, seed_base=600, absent_seed=996)
+    exp = oracle.probe_fixed([refs[0], refs[1], oracle.OracleFilter(m), refs[3]], look)
+    assert np.array_equal(s.probe(look), exp)
+    s.assign(3, filters[5])  # dense path: slot already holds bits
+    s.clear_slot(1)
+    exp = oracle.probe_fixed([refs[0], oracle.OracleFilter(m), oracle.OracleFilter(m), refs[5]], look)
+    assert np.array_equal(s.probe(look), exp)
+    rng = np.random.default_rng(11)
+    data, offs = workload.var_keys(rng, 20_000, max_len=30)
+    exp = oracle.probe_var([refs[0], oracle.OracleFilter(m), oracle.OracleFilter(m), refs[5]], data, offs)
+    assert np.array_equal(s.probe(gpu.KeyBatch(n=20_000, data=data, offsets=offs)), exp)
+
+
+def test_filterset_c3_golden(gpu, golden):
+    g = golden["c3"]
+    filters = []
+    for f in range(g["nf"]):
+        b = gpu.BloomFilter(g["m"])
+        b.insert_batch(workload.c3_filter_keys(f, g["keys_per_filter"]))
+        filters.append(b)
+    s = gpu.FilterSet.from_filters(filters)
+    look = workload.c3_lookups(g["n_lookups"], g["nf"], g["keys_per_filter"])
+    assert sha(s.probe(look).astype("<u8")) == g["hits_sha256"]
+    # incremental: the same set built slot by slot into empty slots
+    s2 = gpu.FilterSet(g["m"])
+    for i, b in enumerate(filters):
+        s2.assign(i, b)
+    assert sha(s2.probe(look).astype("<u8")) == g["hits_sha256"]

@@ -1,0 +1,61 @@
+"""Summarise tools/profile_round.sh output: per-kernel average duration
+(kernel trace) and HBM-side bytes per launch from the PMC passes.
+
+Read bytes are priced per request size (32/64/128 B request counters) because
+gfx950's FETCH_SIZE counts a 128-B request as 64 B (MI355X_MICROARCH.md §HBM);
+FETCH_SIZE is reported beside it. WRITE_SIZE is exact for 16-B/lane stores.
+Usage: python tools/pmc_summary.py gpurun_out/prof [--json out.json]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def short(name):
+    name = name.replace("(anonymous namespace)", "anon").replace("void ", "")
+    name = name.split("(")[0]
+    return name.split("<")[0].split("::")[-1]
+
+
+def main():
+    root = sys.argv[1]
+    out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
+    dur = {}
+    stats = glob.glob(os.path.join(root, "kt", "*kernel_stats.csv"))
+    if stats:
+        for r in csv.DictReader(open(stats[0])):
+            dur[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3}
+    ctr = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(root, "pmc*", "*counter_collection.csv")):
+        per = collections.defaultdict(float)
+        for r in csv.DictReader(open(f)):
+            per[(int(r["Dispatch_Id"]), short(r["Kernel_Name"]), r["Counter_Name"])] += float(r["Counter_Value"])
+        for (d, k, c), v in per.items():
+            ctr[k][c].append(v)
+    res = {}
+    for k in sorted(set(dur) | set(ctr)):
+        c = {n: sum(v) / len(v) for n, v in ctr[k].items()}
+        e = {"avg_us": round(dur.get(k, {}).get("avg_us", 0.0), 3), "calls": dur.get(k, {}).get("calls", 0)}
+        e.update({n: round(v, 1) for n, v in c.items()})
+        if all(n in c for n in ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")):
+            rd = 32 * c["TCC_EA0_RDREQ_32B_sum"] + 64 * c["TCC_EA0_RDREQ_64B_sum"] + 128 * c["TCC_EA0_RDREQ_128B_sum"]
+            e["read_bytes"] = int(rd)
+        if "WRITE_SIZE" in c:
+            e["write_bytes"] = int(c["WRITE_SIZE"] * 1024)
+        if "read_bytes" in e and "write_bytes" in e:
+            e["hbm_bytes_per_launch"] = e["read_bytes"] + e["write_bytes"]
+            if e["avg_us"]:
+                e["hbm_GBps"] = round(e["hbm_bytes_per_launch"] / (e["avg_us"] * 1e3), 1)
+        res[k] = e
+    for k, e in res.items():
+        print(k, json.dumps(e))
+    if out_json:
+        with open(out_json, "w") as fh:
+            json.dump({"source": "tools/profile_round.sh + tools/pmc_summary.py", "kernels": res}, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
