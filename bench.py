@@ -69,6 +69,7 @@ def main():
 
     import lsmt_amd
     from lsmt_amd import _lib, workload
+    from lsmt_amd.shard import gather_hits, shard_range
 
     L = _lib.load()
     lsmt_amd.set_path(args.path)
@@ -76,8 +77,9 @@ def main():
     sh = stream.cuda_stream
 
     F, n, m, kpf = args.filters, args.n_keys, args.m_bits, args.keys_per_filter
-    nf_total = F * world
-    f_lo = rank * F
+    nf_total = F * world  # weak scaling: F filters per GPU
+    f_lo, f_hi = shard_range(nf_total, world, rank)
+    assert f_hi - f_lo == F
 
     # ---- setup (untimed): build this rank's filters, stage the lookups in HBM
     t_setup = time.time()
@@ -108,12 +110,12 @@ def main():
     def step_tiled():
         lsmt_amd.probe(filters, keys_batch, out=hits, stream=sh)
         if world > 1:
-            dist.all_gather_into_tensor(hits_all, hits)
+            gather_hits(hits, nf_total, out=hits_all)
 
     def step_set():
         fset.probe(keys_batch, out=hits, stream=sh)
         if world > 1:
-            dist.all_gather_into_tensor(hits_all, hits)
+            gather_hits(hits, nf_total, out=hits_all)
 
     def timed(fn, k):
         if world > 1:

@@ -1,0 +1,80 @@
+"""World-size-2 (and 3) gloo runs of the multi-GPU logic on CPU: filters
+sharded per rank, local probes (the CPU oracle stands in for the per-rank GPU
+probe here), one all-gather of the hit bitmaps; rank 0 checks the gathered
+bitmap against the unsharded probe."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from lsmt_amd.shard import shard_range
+
+
+def test_shard_range_covers_exactly():
+    for n in (1, 7, 32, 33, 256):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [hi - lo for lo, hi in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_filters, result_q):
+    import torch
+    import torch.distributed as dist
+
+    from lsmt_amd import workload
+    from lsmt_amd.shard import gather_hits, shard_range
+    from oracle import oracle
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        m, kpf, n = 1 << 16, 800, 5000
+        lo, hi = shard_range(n_filters, world, rank)
+        local = []
+        for f in range(lo, hi):
+            o = oracle.OracleFilter(m)
+            o.insert_fixed(workload.key_range(100 + f, kpf))
+            local.append(o)
+        look = workload.probe_lookups(n, n_filters, kpf, seed_base=100, absent_seed=999)
+        words = (n + 63) // 64
+        lh = oracle.probe_fixed(local, look) if local else np.zeros((0, words), np.uint64)
+        t = torch.from_numpy(lh.view(np.int64).copy()).reshape(hi - lo, words)
+        full = gather_hits(t, n_filters)
+        if rank == 0:
+            ref = []
+            for f in range(n_filters):
+                o = oracle.OracleFilter(m)
+                o.insert_fixed(workload.key_range(100 + f, kpf))
+                ref.append(o)
+            expect = oracle.probe_fixed(ref, look)
+            result_q.put(bool(np.array_equal(full.numpy().view(np.uint64), expect)))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_filters", [(2, 6), (2, 5), (3, 7)])
+def test_sharded_probe_allgather_gloo(world, n_filters):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_filters, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5) is True
