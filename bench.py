@@ -180,7 +180,7 @@ def main():
     else:
         # bit-sliced layout (SURVEY.md §8d "alternative layout"): 64 B x distinct
         # sectors touched by the a/b word reads + 16 B/key + the hit bitmaps
-        sectors = _set_sectors(filters, look_np, m, F)
+        sectors, rand_reads = _set_sectors(filters, look_np, m, F)
         alg_bytes = 64 * sectors + 16 * n + F * n / 8
         alg_def = f"64 B x {sectors} distinct sectors + 16n + F*n/8 (SURVEY.md §8d alternative layout)"
     roof = None
@@ -192,6 +192,14 @@ def main():
                 "kernel": dominant, "kernel_avg_us": round(kprof[dominant]["avg_us"], 2),
                 "algorithmic_bytes": int(alg_bytes), "algorithmic_def": alg_def,
                 "step_effective_GBps": round(alg_bytes / (el / args.steps) / 1e9, 1)}
+        if best == "filterset":
+            rr = _random_read_roofline()
+            if rr:
+                got = rand_reads / dur_s
+                roof["random_read_roofline"] = {
+                    "reads_per_launch": rand_reads, "achieved_reads_per_s": round(got, 1),
+                    "peak_reads_per_s": rr, "frac": round(got / rr, 4),
+                    "source": "profiles/ubench_random_r01.json (256 MiB table, hipMalloc)"}
 
     # maintenance cost of the set on the flush path: one new filter into an
     # empty slot (sparse OR of its set bits)
@@ -307,7 +315,21 @@ def _set_sectors(filters, look_np, m, F):
     word_bytes = 4 if F <= 32 else 8
     sec_a = (a * word_bytes) >> 6
     sec_b = (bpos[a_set.astype(bool)] * word_bytes) >> 6
-    return int(np.unique(np.concatenate([sec_a, sec_b])).size)
+    return int(np.unique(np.concatenate([sec_a, sec_b])).size), int(a.size + sec_b.size)
+
+
+def _random_read_roofline():
+    """Measured MI355X random 4-byte read rate on a 256 MiB table (the set's
+    size), from tools/ubench_random.hip's committed output."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "ubench_random_r01.json")) as fh:
+            d = json.load(fh)
+        for r in d["random_reads"]:
+            if r["table_MiB"] == 256 and r["mem"] == "hipMalloc":
+                return float(r["reads_per_s"])
+    except Exception:
+        return None
+    return None
 
 
 def _pmc_traffic(kernel):
