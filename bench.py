@@ -295,10 +295,11 @@ def main():
 
 
 def _set_sectors(filters, look_np, m, F):
-    """Distinct 64-byte sectors of the bit-sliced set that one probe batch reads:
-    set[a] for every key, set[b] only where set[a] != 0 (the short-circuit).
-    Uses the filters' packed words (any filter has bit a set <=> set[a] != 0)
-    and a numpy restatement of the hashes."""
+    """Compulsory reads of one FilterSet probe batch (k_set_probe): set[a] for
+    every key and set[b] where set[a] != 0 (with CB_SET_ANY=1: any[a], any[b]
+    for every key and set[a], set[b] for keys passing the union test).
+    Returns (distinct 64-B sectors touched, number of random set-word reads),
+    from the filters' packed words and a numpy restatement of the hashes."""
     anyw = np.zeros((m + 31) // 32, np.uint32)
     for f in filters:
         anyw |= f.packed()
@@ -311,11 +312,16 @@ def _set_sectors(filters, look_np, m, F):
             h2 = h2 * np.uint64(31) + b
     a = (h1 % np.uint64(m)).astype(np.int64)
     bpos = (h2 % np.uint64(m)).astype(np.int64)
-    a_set = (anyw[a >> 5] >> (a & 31).astype(np.uint32)) & 1
+    bit = lambda p: ((anyw[p >> 5] >> (p & 31).astype(np.uint32)) & 1).astype(bool)
     word_bytes = 4 if F <= 32 else 8
-    sec_a = (a * word_bytes) >> 6
-    sec_b = (bpos[a_set.astype(bool)] * word_bytes) >> 6
-    return int(np.unique(np.concatenate([sec_a, sec_b])).size), int(a.size + sec_b.size)
+    if os.environ.get("CB_SET_ANY") == "1":  # union pre-test mode
+        passed = bit(a) & bit(bpos)
+        set_sec = np.concatenate([(a[passed] * word_bytes) >> 6, (bpos[passed] * word_bytes) >> 6])
+        any_sec = np.concatenate([a >> 9, bpos >> 9])  # 512 positions per 64-B sector of any[]
+        return int(np.unique(set_sec).size) + int(np.unique(any_sec).size), int(set_sec.size)
+    # default: set[a] for every key, set[b] only where set[a] != 0 (short-circuit)
+    set_sec = np.concatenate([(a * word_bytes) >> 6, (bpos[bit(a)] * word_bytes) >> 6])
+    return int(np.unique(set_sec).size), int(set_sec.size)
 
 
 def _random_read_roofline():

@@ -44,6 +44,7 @@ struct cb_filterset {
   int device = 0;
   uint32_t width = 32;
   void* words = nullptr;  // device, m (rounded up to 32) words of width bits
+  uint32_t* any = nullptr;  // device, ceil(m/32) words: bit p = (words[p] != 0)
   uint32_t used = 0;      // 1 + highest assigned slot
   uint64_t dirty = 0;     // bit s: slot s may hold set bits
   int mode = 0;
@@ -402,8 +403,8 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
     HIP_TRY(ws.hits.reserve((size_t)set->used * hwords * 8, s));
     dhits = (uint64_t*)ws.hits.p;
   }
-  HIP_TRY(cb::launch_set_probe(sk.keyk, set->mode, set->width, set->words, set->used, sk.ks, n,
-                               set->mp, dhits, hwords, s));
+  HIP_TRY(cb::launch_set_probe(sk.keyk, set->mode, set->width, set->words, set->any, set->used,
+                               sk.ks, n, set->mp, dhits, hwords, s));
   g_last_path = 3;
   if (host_hits) {
     HIP_TRY(hipMemcpyAsync(hits, dhits, (size_t)set->used * hwords * 8, hipMemcpyDeviceToHost, s));
@@ -813,6 +814,14 @@ int cb_set_create(uint64_t m_bits, uint32_t width, int device, cb_filterset** ou
     return fail(CB_ENOMEM, "hipMalloc failed for filter set words");
   }
   HIP_TRY(hipMemsetAsync(set->words, 0, bytes, nullptr));
+  const size_t any_bytes = (size_t)((m_bits + 31) / 32) * 4;
+  e = hipMalloc(&set->any, any_bytes);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(set->words);
+    return fail(CB_ENOMEM, "hipMalloc failed for filter set union words");
+  }
+  HIP_TRY(hipMemsetAsync(set->any, 0, any_bytes, nullptr));
   HIP_TRY(hipStreamSynchronize(nullptr));
   *out = set.release();
   return CB_OK;
@@ -823,6 +832,7 @@ int cb_set_destroy(cb_filterset* set) {
   {
     DeviceGuard dg(set->device);
     if (set->words) (void)hipFree(set->words);
+    if (set->any) (void)hipFree(set->any);
   }
   delete set;
   return CB_OK;
@@ -845,9 +855,9 @@ int cb_set_assign(cb_filterset* set, uint32_t slot, const cb_filter* f, void* st
   DeviceGuard dg(set->device);
   HIP_TRY(ensure_zeroed(f, s));
   if (set->dirty >> slot & 1)
-    HIP_TRY(cb::launch_set_put_slot(f->words, set->m, slot, set->width, set->words, s));
+    HIP_TRY(cb::launch_set_put_slot(f->words, set->m, slot, set->width, set->words, set->any, s));
   else
-    HIP_TRY(cb::launch_set_or_slot(f->words, set->m, slot, set->width, set->words, s));
+    HIP_TRY(cb::launch_set_or_slot(f->words, set->m, slot, set->width, set->words, set->any, s));
   set->dirty |= 1ull << slot;
   set->used = std::max(set->used, slot + 1);
   return CB_OK;
@@ -869,7 +879,7 @@ int cb_set_assign_all(cb_filterset* set, const cb_filter* const* filters, uint32
     fp.w[i] = f->words;
     fp.row[i] = i;
   }
-  HIP_TRY(cb::launch_set_build(fp, nf, set->m, set->width, set->words, s));
+  HIP_TRY(cb::launch_set_build(fp, nf, set->m, set->width, set->words, set->any, s));
   set->used = nf;
   set->dirty = nf >= 64 ? ~0ull : ((1ull << nf) - 1);
   return CB_OK;
@@ -880,7 +890,8 @@ int cb_set_clear_slot(cb_filterset* set, uint32_t slot, void* stream) {
   if (slot >= set->width) return fail(CB_EINVAL, "slot out of range");
   if (!(set->dirty >> slot & 1)) return CB_OK;
   DeviceGuard dg(set->device);
-  HIP_TRY(cb::launch_set_put_slot(nullptr, set->m, slot, set->width, set->words, (hipStream_t)stream));
+  HIP_TRY(cb::launch_set_put_slot(nullptr, set->m, slot, set->width, set->words, set->any,
+                                  (hipStream_t)stream));
   set->dirty &= ~(1ull << slot);
   return CB_OK;
 }

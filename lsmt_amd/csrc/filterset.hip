@@ -58,12 +58,16 @@ __device__ __forceinline__ void transpose32(uint32_t (&a)[32]) {
 // across threads), transposes, writes the 32 set words of the group.
 template <int W>
 __global__ __launch_bounds__(256) void k_set_build(FilterPtrs fp, uint32_t nf, uint64_t ngroups,
-                                                   uint64_t m, void* __restrict__ set) {
+                                                   uint64_t m, void* __restrict__ set,
+                                                   uint32_t* __restrict__ any) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < ngroups; g += stride) {
-    uint32_t a[32];
+    uint32_t a[32], u = 0;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) a[i] = (uint32_t)i < nf ? fp.w[i][g] : 0u;
+    for (int i = 0; i < 32; ++i) {
+      a[i] = (uint32_t)i < nf ? fp.w[i][g] : 0u;
+      u |= a[i];
+    }
     transpose32(a);
     const uint64_t p0 = g * 32;
     const uint32_t valid = (uint32_t)min<uint64_t>(32, m - p0);
@@ -81,7 +85,10 @@ __global__ __launch_bounds__(256) void k_set_build(FilterPtrs fp, uint32_t nf, u
     } else {
       uint32_t c[32];
 #pragma unroll
-      for (int i = 0; i < 32; ++i) c[i] = (uint32_t)(32 + i) < nf ? fp.w[32 + i][g] : 0u;
+      for (int i = 0; i < 32; ++i) {
+        c[i] = (uint32_t)(32 + i) < nf ? fp.w[32 + i][g] : 0u;
+        u |= c[i];
+      }
       transpose32(c);
       uint32_t* out = reinterpret_cast<uint32_t*>(set) + 2 * p0;  // (lo, hi) per position
       if (valid == 32) {
@@ -97,6 +104,7 @@ __global__ __launch_bounds__(256) void k_set_build(FilterPtrs fp, uint32_t nf, u
           }
       }
     }
+    any[g] = u;
   }
 }
 
@@ -106,10 +114,12 @@ __global__ __launch_bounds__(256) void k_set_build(FilterPtrs fp, uint32_t nf, u
 template <int W>
 __global__ __launch_bounds__(256) void k_set_or_slot(const uint32_t* __restrict__ words,
                                                      uint64_t nwords, uint32_t slot,
-                                                     void* __restrict__ set) {
+                                                     void* __restrict__ set,
+                                                     uint32_t* __restrict__ any) {
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < nwords; w += stride) {
     uint32_t v = words[w];
+    if (v) any[w] |= v;
     while (v) {
       const uint32_t j = __builtin_ctz(v);
       v &= v - 1;
@@ -127,27 +137,33 @@ __global__ __launch_bounds__(256) void k_set_or_slot(const uint32_t* __restrict_
 template <int W>
 __global__ __launch_bounds__(256) void k_set_put_slot(const uint32_t* __restrict__ words,
                                                       uint64_t m, uint32_t slot,
-                                                      void* __restrict__ set) {
+                                                      void* __restrict__ set,
+                                                      uint32_t* __restrict__ any) {
   const uint64_t ngroups = (m + 31) / 32;
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < ngroups; g += stride) {
     const uint32_t v = words ? words[g] : 0u;
     const uint32_t valid = (uint32_t)min<uint64_t>(32, m - g * 32);
+    uint32_t u = 0;
     for (uint32_t j = 0; j < valid; ++j) {
       const uint64_t p = g * 32 + j;
       if constexpr (W == 32) {
         uint32_t* s = reinterpret_cast<uint32_t*>(set) + p;
-        *s = (*s & ~(1u << slot)) | (((v >> j) & 1u) << slot);
+        const uint32_t nv = (*s & ~(1u << slot)) | (((v >> j) & 1u) << slot);
+        *s = nv;
+        u |= (uint32_t)(nv != 0) << j;
       } else {
         uint64_t* s = reinterpret_cast<uint64_t*>(set) + p;
-        *s = (*s & ~(1ull << slot)) | ((uint64_t)((v >> j) & 1u) << slot);
+        const uint64_t nv = (*s & ~(1ull << slot)) | ((uint64_t)((v >> j) & 1u) << slot);
+        *s = nv;
+        u |= (uint32_t)(nv != 0) << j;
       }
     }
+    any[g] = u;
   }
 }
 
-constexpr uint32_t kSetProbeThreads = 256;  // 4 waves
-constexpr uint32_t kSetWords = 16;          // hit words (x64 keys) per block: 1024 keys
+constexpr uint32_t kSetWords = 16;  // hit words (x64 keys) per block: 1024 keys
 
 // KPL keys per lane (one hit word each, KPL words per wave): all KPL set[a]
 // reads are issued before any is consumed, then the set[b] reads, so each lane
@@ -157,12 +173,13 @@ constexpr uint32_t kSetWords = 16;          // hit words (x64 keys) per block: 1
 // hit word per slot, staged in LDS so every slot row leaves as a contiguous
 // 128-byte segment.
 template <int KEYK, int MODE, int W, int KPL, bool SC>
-__global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __restrict__ set,
+__global__ __launch_bounds__(64 * kSetWords / KPL) void k_set_probe(const void* __restrict__ set,
+                                                                const uint32_t* __restrict__ any,
                                                                 uint32_t used, KeySrc ks,
                                                                 uint64_t n, ModP mp,
                                                                 uint64_t* __restrict__ hits,
                                                                 uint64_t hwords) {
-  static_assert(KPL * (kSetProbeThreads / 64) == kSetWords, "block covers kSetWords words");
+  constexpr uint32_t kSetProbeThreads = 64 * kSetWords / KPL;  // KPL words per wave
   typedef typename std::conditional<W == 32, uint32_t, uint64_t>::type word_t;
   typedef const __attribute__((address_space(1))) word_t* gptr;
   __shared__ uint64_t hb[64][kSetWords];
@@ -177,6 +194,21 @@ __global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __re
     ok[i] = k < n;
     pa[i] = pb[i] = 0;
     if (ok[i]) key_positions<KEYK, MODE>(ks, k, mp, pa[i], pb[i]);
+  }
+  // Union pre-test: any[p] = (set[p] != 0) is the Bloom filter of every
+  // slot's keys (m bits, L2/MALL-resident). A key whose a or b bit is clear
+  // there is absent from every slot and skips both set reads.
+  if (any) {
+    const gsp32 ap = (gsp32)any;
+    uint32_t ua[KPL], ub[KPL];
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      ua[i] = ok[i] ? ap[pa[i] >> 5] : 0u;
+      ub[i] = ok[i] ? ap[pb[i] >> 5] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < KPL; ++i)
+      ok[i] = ok[i] && ((ua[i] >> (pa[i] & 31)) & (ub[i] >> (pb[i] & 31)) & 1u);
   }
   word_t va[KPL], vb[KPL];
 #pragma unroll
@@ -241,62 +273,75 @@ inline uint32_t grid_cap(uint64_t items, uint32_t cap) {
 }  // namespace
 
 hipError_t launch_set_build(const FilterPtrs& fp, uint32_t nf, uint64_t m, uint32_t width,
-                            void* set, hipStream_t s) {
+                            void* set, uint32_t* any, hipStream_t s) {
   if (!m) return hipSuccess;
   const uint64_t ngroups = (m + 31) / 32;
   ProfScope ps("k_set_build", s);
   if (width == 32)
     hipLaunchKernelGGL((k_set_build<32>), dim3(grid_cap(ngroups, 8192)), dim3(256), 0, s, fp, nf,
-                       ngroups, m, set);
+                       ngroups, m, set, any);
   else
     hipLaunchKernelGGL((k_set_build<64>), dim3(grid_cap(ngroups, 8192)), dim3(256), 0, s, fp, nf,
-                       ngroups, m, set);
+                       ngroups, m, set, any);
   return hipGetLastError();
 }
 
 hipError_t launch_set_or_slot(const uint32_t* words, uint64_t m, uint32_t slot, uint32_t width,
-                              void* set, hipStream_t s) {
+                              void* set, uint32_t* any, hipStream_t s) {
   if (!m) return hipSuccess;
   const uint64_t nw = (m + 31) / 32;
   ProfScope ps("k_set_or_slot", s);
   if (width == 32)
     hipLaunchKernelGGL((k_set_or_slot<32>), dim3(grid_cap(nw, 8192)), dim3(256), 0, s, words, nw,
-                       slot, set);
+                       slot, set, any);
   else
     hipLaunchKernelGGL((k_set_or_slot<64>), dim3(grid_cap(nw, 8192)), dim3(256), 0, s, words, nw,
-                       slot, set);
+                       slot, set, any);
   return hipGetLastError();
 }
 
 hipError_t launch_set_put_slot(const uint32_t* words, uint64_t m, uint32_t slot, uint32_t width,
-                               void* set, hipStream_t s) {
+                               void* set, uint32_t* any, hipStream_t s) {
   if (!m) return hipSuccess;
   const uint64_t ng = (m + 31) / 32;
   ProfScope ps("k_set_put_slot", s);
   if (width == 32)
     hipLaunchKernelGGL((k_set_put_slot<32>), dim3(grid_cap(ng, 8192)), dim3(256), 0, s, words, m,
-                       slot, set);
+                       slot, set, any);
   else
     hipLaunchKernelGGL((k_set_put_slot<64>), dim3(grid_cap(ng, 8192)), dim3(256), 0, s, words, m,
-                       slot, set);
+                       slot, set, any);
   return hipGetLastError();
 }
 
-template <int KK, int MM, int WW>
-static void set_probe(bool sc, const void* set, uint32_t used, const KeySrc& ks, uint64_t n,
-                      const ModP& mp, uint64_t* hits, uint64_t hwords, uint32_t grid,
-                      hipStream_t s) {
+template <int KK, int MM, int WW, int KPL>
+static void set_probe_k(bool sc, const void* set, const uint32_t* any, uint32_t used,
+                        const KeySrc& ks, uint64_t n, const ModP& mp, uint64_t* hits,
+                        uint64_t hwords, uint32_t grid, hipStream_t s) {
+  constexpr uint32_t nt = 64 * kSetWords / KPL;
   if (sc)
-    hipLaunchKernelGGL((k_set_probe<KK, MM, WW, 4, true>), dim3(grid), dim3(kSetProbeThreads), 0,
-                       s, set, used, ks, n, mp, hits, hwords);
+    hipLaunchKernelGGL((k_set_probe<KK, MM, WW, KPL, true>), dim3(grid), dim3(nt), 0, s, set, any,
+                       used, ks, n, mp, hits, hwords);
   else
-    hipLaunchKernelGGL((k_set_probe<KK, MM, WW, 4, false>), dim3(grid), dim3(kSetProbeThreads),
-                       0, s, set, used, ks, n, mp, hits, hwords);
+    hipLaunchKernelGGL((k_set_probe<KK, MM, WW, KPL, false>), dim3(grid), dim3(nt), 0, s, set,
+                       any, used, ks, n, mp, hits, hwords);
 }
 
-hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set, uint32_t used,
-                            const KeySrc& ks, uint64_t n, const ModP& mp, uint64_t* hits,
-                            uint64_t hwords, hipStream_t s) {
+template <int KK, int MM, int WW>
+static void set_probe(int kpl, bool sc, const void* set, const uint32_t* any, uint32_t used,
+                      const KeySrc& ks, uint64_t n, const ModP& mp, uint64_t* hits,
+                      uint64_t hwords, uint32_t grid, hipStream_t s) {
+  if (kpl == 4)
+    set_probe_k<KK, MM, WW, 4>(sc, set, any, used, ks, n, mp, hits, hwords, grid, s);
+  else if (kpl == 2)
+    set_probe_k<KK, MM, WW, 2>(sc, set, any, used, ks, n, mp, hits, hwords, grid, s);
+  else
+    set_probe_k<KK, MM, WW, 1>(sc, set, any, used, ks, n, mp, hits, hwords, grid, s);
+}
+
+hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
+                            const uint32_t* any, uint32_t used, const KeySrc& ks, uint64_t n,
+                            const ModP& mp, uint64_t* hits, uint64_t hwords, hipStream_t s) {
   if (!n || !used) return hipSuccess;
   // CB_SET_SC=0 reads set[b] unconditionally (one latency, more bytes);
   // default keeps the reference's short-circuit.
@@ -304,11 +349,27 @@ hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
     const char* v = getenv("CB_SET_SC");
     return !(v && v[0] == '0');
   }();
+  // CB_SET_KPL: keys per lane (1, 2 or 4); tuning knob, default 1.
+  static const int kpl = [] {
+    const char* v = getenv("CB_SET_KPL");
+    const int k = v ? atoi(v) : 1;
+    return (k == 2 || k == 4) ? k : 1;
+  }();
+  // CB_SET_ANY=1 enables the union pre-test. Off by default: measured on C3
+  // it costs more than it saves (52.8 vs 40.0 us), because the 2 extra random
+  // reads per key into any[] cost as much random-read throughput as the set
+  // reads they avoid, and half of C3's keys are present in some slot. It pays
+  // only when most lookups miss every table.
+  static const bool use_any = [] {
+    const char* v = getenv("CB_SET_ANY");
+    return v && v[0] == '1';
+  }();
   const uint64_t nw = (n + 63) / 64;
   const uint32_t grid = (uint32_t)((nw + kSetWords - 1) / kSetWords);
   ProfScope ps("k_set_probe", s);
   CB_SET_DISPATCH(keyk, mode, width,
-                  (set_probe<KK, MM, WW>(sc, set, used, ks, n, mp, hits, hwords, grid, s)));
+                  (set_probe<KK, MM, WW>(kpl, sc, set, use_any ? any : nullptr, used, ks, n, mp,
+                                         hits, hwords, grid, s)));
   return hipGetLastError();
 }
 

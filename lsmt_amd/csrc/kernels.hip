@@ -89,6 +89,16 @@ __device__ uint32_t block_sum(const uint32_t* arr, uint32_t len, uint32_t* wsum)
   return total;
 }
 
+// XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md, "Workgroup dispatch"), so blocks b and b+8 share an
+// L2. Giving each XCD a contiguous range of tiles lets the 128-B lines that
+// adjacent tiles' runs and run-table entries share be fetched once per XCD
+// instead of once per tile. Placement only affects speed, never results.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t bid, uint32_t T) {
+  if (T & 7u) return bid;
+  return (bid & 7u) * (T >> 3) + (bid >> 3);
+}
+
 // Last b with P[b] <= j (P: exclusive prefix of the runs' lengths, P[0] = 0).
 __device__ __forceinline__ uint32_t seg_find(const uint32_t* P, uint32_t nblk, uint32_t j) {
   uint32_t lo = 0, hi = nblk;
@@ -238,7 +248,7 @@ __global__ __launch_bounds__(kTileBuildThreads) void k_tile_build(
   uint32_t* S = P + nbp;
   uint32_t* wsum = S + nbp;
   const uint32_t tid = threadIdx.x;
-  const uint32_t t = blockIdx.x;
+  const uint32_t t = xcd_tile(blockIdx.x, T);
 
   uint4* gt = reinterpret_cast<uint4*>(words + (size_t)t * tw);
   uint4* lt = reinterpret_cast<uint4*>(tile);
@@ -363,7 +373,7 @@ __global__ __launch_bounds__(kTileProbeThreads) void k_tile_probe(
   uint32_t* wsum = S + nbp;                                                  // NT/64 words
   const uint32_t** fw = reinterpret_cast<const uint32_t**>(wsum + NT / 64);  // 32 pointers
   const uint32_t tid = threadIdx.x;
-  const uint32_t t = blockIdx.x, g = blockIdx.y;
+  const uint32_t t = xcd_tile(blockIdx.x, T), g = blockIdx.y;
   const uint32_t f0 = g * kFiltersPerGroup;
   const uint32_t nfg = min(kFiltersPerGroup, nf - f0);
   const uint32_t tmask = (1u << tb) - 1u;
@@ -634,24 +644,30 @@ static uint32_t fit_tiles(uint64_t m, int64_t tb, int64_t hi) {
   return (uint32_t)tb;
 }
 
+// Tuning overrides for experiments (unset in production): CB_PROBE_TB / CB_BUILD_TB
+// fix the tile bits, CB_PROBE_KPT / CB_BUILD_KPT the partition keys per thread.
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
 TilePlan plan_build(uint64_t m, uint64_t n) {
   TilePlan p{};
   // ~512 tiles (2 workgroups per CU), tiles within [2^12, 2^18] bits.
   int64_t tb = clamp64((int64_t)ilog2_floor(m > 512 ? m / 512 : 1), kMinTileBits, kMaxTileBits);
+  static const int env_tb = env_int("CB_BUILD_TB", 0);
+  if (env_tb) tb = clamp64(env_tb, kMinTileBits, kMaxTileBits);
   p.tb = fit_tiles(m, tb, kMaxTileBits);
   p.T = (uint32_t)((m + (1ull << p.tb) - 1) >> p.tb);
-  p.kpt = 4;
-  while (p.kpt < 16 && (n + 256ull * p.kpt - 1) / (256ull * p.kpt) > 2048) p.kpt *= 2;
+  // 2048-key partition blocks from 512K keys up (longer runs per tile; 4096
+  // blocks at most), 1024 below so small builds still fill the chip.
+  p.kpt = n >= (1ull << 19) ? 8 : 4;
+  while (p.kpt < 16 && (n + 256ull * p.kpt - 1) / (256ull * p.kpt) > 4096) p.kpt *= 2;
+  static const int env_kpt = env_int("CB_BUILD_KPT", 0);
+  if (env_kpt == 4 || env_kpt == 8 || env_kpt == 16) p.kpt = env_kpt;
   p.C = kPartThreads * p.kpt;
   p.nblk = (uint32_t)((n + p.C - 1) / p.C);
   return p;
-}
-
-// Tuning overrides for experiments (unset in production): CB_PROBE_TB fixes
-// the probe tile bits, CB_PROBE_KPT the partition keys per thread (4 or 8).
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : dflt;
 }
 
 TilePlan plan_probe(uint64_t m, uint64_t n) {
