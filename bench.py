@@ -49,11 +49,23 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--check", action="store_true", help="verify hits against the oracle (slow)")
+    p.add_argument("--overlap", action="store_true",
+                   help="N>1: run each step's all-gather on a side stream, overlapped with the next "
+                        "step's probe (measured slower on one GPU: the streams share one hardware "
+                        "queue and each cross-stream event adds 10-15 us; profiles/ r01 notes)")
+    p.add_argument("--force-dist", action="store_true",
+                   help="initialise the process group and run the exchange path even at N=1")
     return p.parse_args()
 
 
 def main():
     args = parse()
+    # The contract is ONE JSON line on stdout. Libraries (RCCL's banner, ...)
+    # write to fd 1 directly, so fd 1 is pointed at stderr for the whole run
+    # and the result line goes to a saved copy of the original stdout.
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
+    result = os.fdopen(out_fd, "w")
     import torch
     import torch.distributed as dist
 
@@ -64,7 +76,12 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
+        if "MASTER_ADDR" not in os.environ:
+            os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", "29533"
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
 
     import lsmt_amd
@@ -92,8 +109,15 @@ def main():
     look_np = workload.probe_lookups(n, nf_total, kpf, seed_base=100, absent_seed=999)
     look = torch.from_numpy(look_np).to(dev)
     words = (n + 63) // 64
-    hits = torch.zeros((F, words), dtype=torch.int64, device=dev)
-    hits_all = torch.zeros((nf_total, words), dtype=torch.int64, device=dev) if world > 1 else hits
+    # Two hit buffers: with the exchange overlapped, step i's all-gather reads
+    # hits[i % 2] on the comm stream while step i+1 probes into the other one.
+    hits_bufs = [torch.zeros((F, words), dtype=torch.int64, device=dev) for _ in range(2)]
+    hits = hits_bufs[0]
+    hits_all_bufs = [torch.zeros((nf_total, words), dtype=torch.int64, device=dev) for _ in range(2)] \
+        if use_dist else hits_bufs
+    comm = torch.cuda.Stream(device=dev) if use_dist else None
+    gather_done = [None, None]
+    step_no = [0]
     torch.cuda.synchronize(dev)
     log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: {F} filters m={m} built, {n} lookups in HBM")
     keys_batch = lsmt_amd.DeviceKeys(look)
@@ -107,28 +131,55 @@ def main():
     torch.cuda.synchronize(dev)
     set_build_ms = (time.perf_counter() - t0) * 1e3
 
+    def exchange(buf):
+        """The real exchange step: all-gather this step's hit rows from every
+        rank (filter-major -> plain concatenation) over RCCL/xGMI, right after
+        the probe. With --overlap it runs on the comm stream after the probe's
+        event while the next step probes into the other buffer; a buffer is
+        reused only after its gather has finished (gather_done)."""
+        if not use_dist:
+            return
+        if not args.overlap:
+            gather_hits(hits_bufs[buf], nf_total, out=hits_all_bufs[buf])
+            return
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        with torch.cuda.stream(comm):
+            comm.wait_event(ev)
+            gather_hits(hits_bufs[buf], nf_total, out=hits_all_bufs[buf])
+            done = torch.cuda.Event()
+            done.record(comm)
+        gather_done[buf] = done
+
+    def claim():
+        buf = step_no[0] % 2
+        step_no[0] += 1
+        if gather_done[buf] is not None:
+            stream.wait_event(gather_done[buf])
+        return buf
+
     def step_tiled():
-        lsmt_amd.probe(filters, keys_batch, out=hits, stream=sh)
-        if world > 1:
-            gather_hits(hits, nf_total, out=hits_all)
+        buf = claim()
+        lsmt_amd.probe(filters, keys_batch, out=hits_bufs[buf], stream=sh)
+        exchange(buf)
 
     def step_set():
-        fset.probe(keys_batch, out=hits, stream=sh)
-        if world > 1:
-            gather_hits(hits, nf_total, out=hits_all)
+        buf = claim()
+        fset.probe(keys_batch, out=hits_bufs[buf], stream=sh)
+        exchange(buf)
 
     def timed(fn, k):
-        if world > 1:
+        if use_dist:
             dist.barrier()
-        torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)  # all streams: every exchange of the K steps is inside
         t0 = time.perf_counter()
         for _ in range(k):
             fn()
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if use_dist:
             dist.barrier()
         el = time.perf_counter() - t0
-        if world > 1:
+        if use_dist:
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
@@ -259,7 +310,8 @@ def main():
             o.insert_fixed(workload.key_range(100 + f, kpf))
             refs.append(o)
         expect = oracle.probe_fixed(refs, look_np, threads=8)
-        got = hits.cpu().numpy().view(np.uint64)
+        torch.cuda.synchronize(dev)
+        got = hits_bufs[(step_no[0] - 1) % 2].cpu().numpy().view(np.uint64)
         assert np.array_equal(got, expect), "bench hits differ from the oracle"
         log("[check] hits bit-exact vs oracle")
 
@@ -278,7 +330,10 @@ def main():
                                    f"(m=2^{m.bit_length() - 1}), filters built from {kpf} keys each",
                        "n_keys": n, "filters_per_gpu": F, "filters_total": nf_total, "m_bits": m,
                        "keys_per_filter": kpf,
-                       "parallelism": "filter-sharded" + (", RCCL all-gather of hit bitmaps" if world > 1 else "")},
+                       "parallelism": "filter-sharded" + (
+                           ", RCCL all-gather of hit bitmaps" + (" overlapped with the next step's probe"
+                                                                 if args.overlap else " after each probe")
+                           if use_dist else "")},
             "path": best,
             "kernels_us": {k: round(v["avg_us"], 2) for k, v in kprof.items()},
             "alt_paths": {k: {"value": round(v["value"], 1), "ms_per_step": round(v["ms_per_step"], 4)}
@@ -288,8 +343,8 @@ def main():
                           "bytes": m * (4 if F <= 32 else 8)},
             "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e,
         }
-        print(json.dumps(line), flush=True)
-    if world > 1:
+        print(json.dumps(line), file=result, flush=True)
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -340,3 +340,39 @@ def test_filterset_c3_golden(gpu, golden):
     for i, b in enumerate(filters):
         s2.assign(i, b)
     assert sha(s2.probe(look).astype("<u8")) == g["hits_sha256"]
+
+
+_UNION_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import lsmt_amd
+from lsmt_amd import workload
+from oracle import oracle
+m = (1 << 20) + 9
+fs, rs = [], []
+for f in range(5):
+    k = workload.key_range(700 + f, 6000)
+    g = lsmt_amd.BloomFilter(m); g.insert_batch(k); fs.append(g)
+    o = oracle.OracleFilter(m); o.insert_fixed(k); rs.append(o)
+look = workload.probe_lookups(30000, 5, 6000, seed_base=700, absent_seed=995)
+s = lsmt_amd.FilterSet.from_filters(fs[:3])          # union built by the transpose
+assert np.array_equal(s.probe(look), oracle.probe_fixed(rs[:3], look))
+s.assign(3, fs[3]); s.assign(4, fs[4])              # union kept by the sparse OR
+assert np.array_equal(s.probe(look), oracle.probe_fixed(rs, look))
+s.clear_slot(0); s.assign(1, fs[4])                  # union recomputed by the dense rewrite
+z = oracle.OracleFilter(m)
+assert np.array_equal(s.probe(look), oracle.probe_fixed([z, rs[4], rs[2], rs[3], rs[4]], look))
+print("union ok")
+"""
+
+
+def test_filterset_union_mode(gpu):
+    # CB_SET_ANY=1 (opt-in union pre-test) is read once per process
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CB_SET_ANY="1")
+    r = subprocess.run([sys.executable, "-c", _UNION_SCRIPT, root], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "union ok" in r.stdout, r.stdout + r.stderr
