@@ -37,6 +37,10 @@ def log(*a):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--workload", choices=["c3", "c4", "c5"], default="c3",
+                   help="c3: 1M keys x 32 filters/GPU probe (default, the BASELINE metric); "
+                        "c5: 10M keys x 32 filters/GPU probe; c4: 64 concurrent builds of 256K keys "
+                        "(m=2^25) split over the GPUs")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--n-keys", type=int, default=1 << 20)
@@ -93,6 +97,11 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
 
+    if args.workload == "c4":
+        return run_c4(args, torch, dist, world, rank, local, dev, use_dist, result)
+    seed_base, absent_seed = 100, 999
+    if args.workload == "c5":  # key(1000+f, i), absent key(9999, i)
+        args.n_keys, seed_base, absent_seed = 10_000_000, 1000, 9999
     F, n, m, kpf = args.filters, args.n_keys, args.m_bits, args.keys_per_filter
     nf_total = F * world  # weak scaling: F filters per GPU
     f_lo, f_hi = shard_range(nf_total, world, rank)
@@ -102,11 +111,11 @@ def main():
     t_setup = time.time()
     filters = []
     for f in range(f_lo, f_lo + F):
-        keys = torch.from_numpy(workload.key_range(100 + f, kpf)).to(dev)
+        keys = torch.from_numpy(workload.key_range(seed_base + f, kpf)).to(dev)
         b = lsmt_amd.BloomFilter(m, device=local)
         b.insert_batch(lsmt_amd.DeviceKeys(keys), stream=sh)
         filters.append(b)
-    look_np = workload.probe_lookups(n, nf_total, kpf, seed_base=100, absent_seed=999)
+    look_np = workload.probe_lookups(n, nf_total, kpf, seed_base=seed_base, absent_seed=absent_seed)
     look = torch.from_numpy(look_np).to(dev)
     words = (n + 63) // 64
     # Two hit buffers: with the exchange overlapped, step i's all-gather reads
@@ -307,7 +316,7 @@ def main():
         refs = []
         for f in range(f_lo, f_lo + F):
             o = oracle.OracleFilter(m)
-            o.insert_fixed(workload.key_range(100 + f, kpf))
+            o.insert_fixed(workload.key_range(seed_base + f, kpf))
             refs.append(o)
         expect = oracle.probe_fixed(refs, look_np, threads=8)
         torch.cuda.synchronize(dev)
@@ -316,7 +325,7 @@ def main():
         log("[check] hits bit-exact vs oracle")
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and args.workload == "c3":
         cpu = cpu_baseline(look_np, F, m, kpf, args.build_keys, args.build_m_bits)
         log(f"[cpu] {cpu}")
 
@@ -326,7 +335,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 hex keys, SURVEY.md §8d)",
-            "config": {"workload": f"C3 probe: {n} 16-B keys x {F} filters/GPU x {m // 8 // 2**20} MiB "
+            "config": {"workload": f"{args.workload.upper()} probe: {n} 16-B keys x {F} filters/GPU x {m // 8 // 2**20} MiB "
                                    f"(m=2^{m.bit_length() - 1}), filters built from {kpf} keys each",
                        "n_keys": n, "filters_per_gpu": F, "filters_total": nf_total, "m_bits": m,
                        "keys_per_filter": kpf,
@@ -343,6 +352,65 @@ def main():
                           "bytes": m * (4 if F <= 32 else 8)},
             "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e,
         }
+        print(json.dumps(line), file=result, flush=True)
+    if use_dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result):
+    """C4: 64 concurrent flush builds (256K keys each, m = 2^25), filters
+    split one contiguous subset per GPU (strong scaling: total work fixed).
+    One step = zero-fill + batched build of this GPU's filters."""
+    import lsmt_amd
+    from lsmt_amd import workload
+    from lsmt_amd.shard import shard_range
+    nf_total, kpf, m = 64, 1 << 18, 1 << 25
+    lo, hi = shard_range(nf_total, world, rank)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    keys = [torch.from_numpy(workload.c4_filter_keys(f, kpf)).to(dev) for f in range(lo, hi)]
+    fs = [lsmt_amd.BloomFilter(m, device=local) for _ in range(lo, hi)]
+    batches = [lsmt_amd.DeviceKeys(k) for k in keys]
+
+    def step():
+        for f in fs:
+            f.clear(stream=sh)
+        lsmt_amd.insert_many(fs, batches, stream=sh)
+
+    for _ in range(args.warmup):
+        step()
+    if use_dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if use_dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if use_dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if args.check and rank == 0:
+        from oracle import oracle
+        for i, f in enumerate(fs[:4]):
+            o = oracle.OracleFilter(m)
+            o.insert_fixed(workload.c4_filter_keys(lo + i, kpf))
+            assert np.array_equal(f.bools(), o.bools()), "C4 build differs from the oracle"
+        log("[check] C4 filters bit-exact vs oracle")
+    if rank == 0:
+        alg = nf_total * (16 * kpf + m / 8)
+        line = {"metric": "build keys/s (C4: 64 concurrent flush builds x 256K keys, m=2^25)",
+                "value": round(nf_total * kpf / (el / args.steps), 1), "unit": "keys/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+                "data": "synthetic (splitmix64 hex keys, SURVEY.md §8d)",
+                "config": {"workload": "C4: 64 filters x 2^18 keys -> m=2^25 each, one subset per GPU",
+                           "parallelism": "filter-sharded, no collective"},
+                "algorithmic_bytes_total": int(alg),
+                "step_effective_GBps_all_gpus": round(alg / (el / args.steps) / 1e9, 1)}
         print(json.dumps(line), file=result, flush=True)
     if use_dist:
         dist.barrier()

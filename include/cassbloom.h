@@ -88,6 +88,12 @@ int cb_filter_insert_fixed(cb_filter* f, const uint8_t* keys, uint32_t key_len, 
 int cb_filter_insert_var(cb_filter* f, const uint8_t* bytes, const uint64_t* offsets,
                          uint64_t n, void* stream);
 
+/* Concurrent flush builds: filters[i] += keys[i][0 .. n[i]) (key_len bytes
+ * each), all filters of one m on one device, built together (one partition
+ * and one tile launch per 32 filters). Each keys[i] may be host or device. */
+int cb_filter_insert_fixed_many(cb_filter* const* filters, uint32_t nf, const uint8_t* const* keys,
+                                uint32_t key_len, const uint64_t* n, void* stream);
+
 /* ---- probe (BloomFilter::may_contain over many filters, batched) ---- */
 /* hits: [nf][ceil(n/64)] uint64; bit k%64 of word [f][k/64] is
  * filters[f].may_contain(key k). Tail bits of the last word are zero. Filters

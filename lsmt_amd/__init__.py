@@ -15,12 +15,13 @@ from .bloom import (  # noqa: E402
     FilterSet,
     KeyBatch,
     device_count,
+    insert_many,
     last_path,
     probe,
     set_path,
     unpack_hits,
 )
 
-__all__ = ["BloomFilter", "BloomProto", "DeviceKeys", "FilterSet", "KeyBatch", "device_count", "last_path",
+__all__ = ["BloomFilter", "BloomProto", "DeviceKeys", "FilterSet", "insert_many", "KeyBatch", "device_count", "last_path",
            "probe", "set_path", "unpack_hits"]
 __version__ = "0.1.0"

@@ -73,6 +73,7 @@ def load():
         "cb_filter_clear": ([P, P], i32),
         "cb_filter_insert_fixed": ([P, u8p, u32, u64, P], i32),
         "cb_filter_insert_var": ([P, u8p, P, u64, P], i32),
+        "cb_filter_insert_fixed_many": ([P, u32, P, u32, P, P], i32),
         "cb_probe_fixed": ([P, u32, u8p, u32, u64, P, P], i32),
         "cb_probe_var": ([P, u32, u8p, P, u64, P, P], i32),
         "cb_may_contain": ([P, u8p, u64, ctypes.POINTER(ctypes.c_int)], i32),

@@ -33,8 +33,8 @@ import numpy as np
 from . import _lib
 from ._lib import CassBloomError, check
 
-__all__ = ["BloomFilter", "BloomProto", "FilterSet", "probe", "set_path", "last_path",
-           "device_count", "DeviceKeys", "KeyBatch"]
+__all__ = ["BloomFilter", "BloomProto", "FilterSet", "probe", "insert_many", "set_path",
+           "last_path", "device_count", "DeviceKeys", "KeyBatch"]
 
 
 def _L():
@@ -273,6 +273,37 @@ class BloomFilter:
         h = ctypes.c_void_p()
         _raise(_L().cb_filter_from_bytes(buf.ctypes.data, len(data), device, ctypes.byref(h)))
         return cls(0, _handle=h.value)
+
+
+# ---- batched multi-filter build (concurrent flushes) ---------------------------------
+
+def insert_many(filters: Sequence["BloomFilter"], keys_per_filter, stream=None) -> None:
+    """filters[i].insert of every row of keys_per_filter[i] (uint8 [n_i, L]
+    arrays or device tensors, one key length L), all built together."""
+    nf = len(filters)
+    if nf == 0:
+        return
+    for f in filters:
+        f.flush(stream)
+    batches = [as_batch(k) for k in keys_per_filter]
+    if len(batches) != nf or any(b.is_var for b in batches):
+        raise ValueError("one fixed-length key array per filter")
+    kl = {b.key_len for b in batches if b.n}
+    if len(kl) > 1:
+        raise ValueError("all key arrays must share one key length")
+    key_len = kl.pop() if kl else 0
+    keep = []
+    ptrs = (ctypes.c_void_p * nf)()
+    ns = (ctypes.c_uint64 * nf)()
+    for i, b in enumerate(batches):
+        p, k = _ptr_of(b.keys) if b.n else (None, None)
+        keep.append(k)
+        ptrs[i] = p
+        ns[i] = b.n
+    hs = (ctypes.c_void_p * nf)(*[f.handle.value for f in filters])
+    _raise(_L().cb_filter_insert_fixed_many(ctypes.cast(hs, ctypes.c_void_p), nf,
+                                            ctypes.cast(ptrs, ctypes.c_void_p), key_len,
+                                            ctypes.cast(ns, ctypes.c_void_p), _stream(stream)))
 
 
 # ---- batched multi-filter probe ------------------------------------------------------

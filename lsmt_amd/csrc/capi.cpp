@@ -907,4 +907,91 @@ int cb_set_probe_var(const cb_filterset* set, const uint8_t* bytes, const uint64
   return set_probe_impl(set, bytes, offsets, 0, n, hits, (hipStream_t)stream);
 }
 
+
+int cb_filter_insert_fixed_many(cb_filter* const* filters, uint32_t nf, const uint8_t* const* keys,
+                                uint32_t key_len, const uint64_t* n, void* stream) {
+  if (nf == 0) return CB_OK;
+  if (!filters || !keys || !n) return fail(CB_EINVAL, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  const cb_filter* f0 = filters[0];
+  if (!f0) return fail(CB_EINVAL, "null filter");
+  uint64_t nmax = 0;
+  for (uint32_t i = 0; i < nf; ++i) {
+    const cb_filter* f = filters[i];
+    if (!f) return fail(CB_EINVAL, "null filter");
+    if (f->m != f0->m || f->device != f0->device)
+      return fail(CB_EINVAL, "batched builds need filters of one size on one device");
+    if (n[i] && f->m == 0) return fail(CB_EZEROM, "attempt to calculate the remainder with a divisor of zero");
+    if (n[i] && key_len && !keys[i]) return fail(CB_EINVAL, "null keys");
+    nmax = std::max(nmax, n[i]);
+  }
+  if (nmax == 0) return CB_OK;
+  const uint64_t chunk_limit = 4096ull * 256 * 16;
+  if (choose_build_path(f0->m, nmax) != PATH_TILED || nmax > chunk_limit) {
+    for (uint32_t i = 0; i < nf; ++i) {  // per-filter builds (direct path or huge batches)
+      int rc = insert_impl(filters[i], keys[i], nullptr, key_len, n[i], s);
+      if (rc) return rc;
+    }
+    return CB_OK;
+  }
+  DeviceGuard dg(f0->device);
+  Workspace& ws = workspace(f0->device, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  // Stage host key arrays into one workspace buffer (16-byte aligned slices).
+  std::vector<const uint8_t*> dkeys(nf);
+  std::vector<uint64_t> stage_off(nf, 0);
+  uint64_t stage_bytes = 0;
+  for (uint32_t i = 0; i < nf; ++i) {
+    dkeys[i] = keys[i];
+    if (n[i] && key_len && !is_device_ptr(keys[i])) {
+      stage_off[i] = stage_bytes;
+      stage_bytes += ((uint64_t)key_len * n[i] + 15) & ~15ull;
+      dkeys[i] = nullptr;
+    }
+  }
+  bool staged = false;
+  if (stage_bytes) {
+    HIP_TRY(ws.keys.reserve(stage_bytes, s));
+    for (uint32_t i = 0; i < nf; ++i)
+      if (!dkeys[i]) {
+        HIP_TRY(hipMemcpyAsync((uint8_t*)ws.keys.p + stage_off[i], keys[i], (uint64_t)key_len * n[i],
+                               hipMemcpyHostToDevice, s));
+        dkeys[i] = (const uint8_t*)ws.keys.p + stage_off[i];
+      }
+    staged = true;
+  }
+  const TilePlan p = cb::plan_build(f0->m, nmax);
+  for (uint32_t i = 0; i < nf; ++i)
+    if (!covers(filters[i], p)) return fail(CB_EINVAL, "internal: build tile plan exceeds the filter allocation");
+  bool all16 = key_len == 16;
+  for (uint32_t i = 0; i < nf; ++i) all16 = all16 && !((uintptr_t)dkeys[i] & 15);
+  const int keyk = all16 ? cb::KEY_FIXED16 : cb::KEY_FIXED;
+  for (uint32_t b0 = 0; b0 < nf; b0 += cb::kMaxBuildBatch) {
+    const uint32_t nb = std::min<uint32_t>(cb::kMaxBuildBatch, nf - b0);
+    cb::BuildBatch bb{};
+    for (uint32_t j = 0; j < nb; ++j) {
+      cb_filter* f = filters[b0 + j];
+      if (f->known_zero)
+        f->needs_zero.store(false);
+      else
+        HIP_TRY(ensure_zeroed(f, s));
+      bb.ks[j].bytes = dkeys[b0 + j];
+      bb.ks[j].offsets = nullptr;
+      bb.ks[j].key_len = key_len;
+      bb.n[j] = n[b0 + j];
+      bb.words[j] = f->words;
+      bb.fresh |= (f->known_zero ? 1u : 0u) << j;
+    }
+    HIP_TRY(ws.seg.reserve(cb::build_seg_bytes(p) * nb, s));
+    HIP_TRY(ws.ent.reserve(cb::build_ent_bytes(p) * nb, s));
+    HIP_TRY(cb::launch_build_batch(keyk, f0->mode, bb, nb, f0->mp, p, (uint32_t*)ws.seg.p,
+                                   (uint32_t*)ws.ent.p, s));
+    for (uint32_t j = 0; j < nb; ++j)
+      if (n[b0 + j]) filters[b0 + j]->known_zero = false;
+  }
+  g_last_path = PATH_TILED;
+  if (staged) HIP_TRY(hipStreamSynchronize(s));
+  return CB_OK;
+}
+
 }  // extern "C"

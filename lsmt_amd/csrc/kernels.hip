@@ -185,11 +185,16 @@ constexpr uint32_t kPartThreads = 256;
 // bucketed by its tile. Per block: LDS histogram with ranks, block scan, LDS
 // staging in tile order, coalesced writes of the block's run and run table.
 template <int KEYK, int MODE, int KPT>
-__global__ __launch_bounds__(kPartThreads) void k_part_build(KeySrc ks, uint64_t n, ModP mp,
-                                                             uint32_t tb, uint32_t T,
-                                                             uint32_t* __restrict__ seg,
-                                                             uint32_t* __restrict__ ent) {
+__global__ __launch_bounds__(kPartThreads) void k_part_build(BuildBatch bb, ModP mp, uint32_t tb,
+                                                             uint32_t T,
+                                                             uint32_t* __restrict__ seg_all,
+                                                             uint32_t* __restrict__ ent_all) {
   constexpr uint32_t C = kPartThreads * KPT;
+  // blockIdx.y = filter of the batch: its keys, its run table and entries.
+  const KeySrc ks = bb.ks[blockIdx.y];
+  const uint64_t n = bb.n[blockIdx.y];
+  uint32_t* seg = seg_all + (size_t)blockIdx.y * gridDim.x * (T + 1);
+  uint32_t* ent = ent_all + (size_t)blockIdx.y * gridDim.x * (2 * C);
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t Tp = (T + 4) & ~3u;
   uint32_t* hist = smem;
@@ -237,9 +242,13 @@ constexpr uint32_t kTileBuildThreads = 256;
 // One workgroup per tile: stage the tile in LDS (zeros if the filter is known
 // empty), OR in every entry of the tile with LDS atomics, write it back.
 __global__ __launch_bounds__(kTileBuildThreads) void k_tile_build(
-    uint32_t* __restrict__ words, uint32_t tb, uint32_t T, const uint32_t* __restrict__ seg,
-    uint32_t nblk, const uint32_t* __restrict__ ent, uint32_t estride, int fresh) {
+    BuildBatch bb, uint32_t tb, uint32_t T, const uint32_t* __restrict__ seg_all, uint32_t nblk,
+    const uint32_t* __restrict__ ent_all, uint32_t estride) {
   constexpr uint32_t NT = kTileBuildThreads;
+  uint32_t* __restrict__ words = bb.words[blockIdx.y];
+  const bool fresh = (bb.fresh >> blockIdx.y) & 1u;
+  const uint32_t* __restrict__ seg = seg_all + (size_t)blockIdx.y * nblk * (T + 1);
+  const uint32_t* __restrict__ ent = ent_all + (size_t)blockIdx.y * nblk * estride;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t tw = 1u << (tb - 5);
   const uint32_t nbp = (nblk + 3) & ~3u;
@@ -727,10 +736,10 @@ hipError_t launch_probe_direct(int keyk, int mode, const FilterPtrs& fp, uint32_
 }
 
 template <int KK, int MM, int KPT>
-static void part_build(const TilePlan& p, const KeySrc& ks, uint64_t n, const ModP& mp,
+static void part_build(const TilePlan& p, const BuildBatch& bb, uint32_t nb, const ModP& mp,
                        uint32_t* seg, uint32_t* ent, size_t lds, hipStream_t s) {
   allow_lds(k_part_build<KK, MM, KPT>, lds);
-  hipLaunchKernelGGL((k_part_build<KK, MM, KPT>), dim3(p.nblk), dim3(kPartThreads), lds, s, ks, n,
+  hipLaunchKernelGGL((k_part_build<KK, MM, KPT>), dim3(p.nblk, nb), dim3(kPartThreads), lds, s, bb,
                      mp, p.tb, p.T, seg, ent);
 }
 
@@ -742,20 +751,20 @@ static void part_probe(const TilePlan& p, const KeySrc& ks, uint64_t n, const Mo
                      mp, p.tb, p.T, seg, ent, lkey);
 }
 
-hipError_t launch_build_tiled(int keyk, int mode, uint32_t* words, bool fresh, const KeySrc& ks,
-                              uint64_t n, const ModP& mp, const TilePlan& p, uint32_t* seg,
-                              uint32_t* ent, hipStream_t s) {
-  if (!n) return hipSuccess;
-  if (!plan_ok(p)) return hipErrorInvalidValue;
+hipError_t launch_build_batch(int keyk, int mode, const BuildBatch& bb, uint32_t nb,
+                              const ModP& mp, const TilePlan& p, uint32_t* seg, uint32_t* ent,
+                              hipStream_t s) {
+  if (!nb) return hipSuccess;
+  if (!plan_ok(p) || nb > kMaxBuildBatch) return hipErrorInvalidValue;
   const size_t lds1 = ((size_t)((p.T + 4) & ~3u) + 2 * p.C + 8) * 4;
   {
     ProfScope ps("k_part_build", s);
     if (p.kpt == 4) {
-      CB_DISPATCH(keyk, mode, (part_build<KK, MM, 4>(p, ks, n, mp, seg, ent, lds1, s)));
+      CB_DISPATCH(keyk, mode, (part_build<KK, MM, 4>(p, bb, nb, mp, seg, ent, lds1, s)));
     } else if (p.kpt == 8) {
-      CB_DISPATCH(keyk, mode, (part_build<KK, MM, 8>(p, ks, n, mp, seg, ent, lds1, s)));
+      CB_DISPATCH(keyk, mode, (part_build<KK, MM, 8>(p, bb, nb, mp, seg, ent, lds1, s)));
     } else {
-      CB_DISPATCH(keyk, mode, (part_build<KK, MM, 16>(p, ks, n, mp, seg, ent, lds1, s)));
+      CB_DISPATCH(keyk, mode, (part_build<KK, MM, 16>(p, bb, nb, mp, seg, ent, lds1, s)));
     }
   }
   hipError_t e = hipGetLastError();
@@ -764,9 +773,21 @@ hipError_t launch_build_tiled(int keyk, int mode, uint32_t* words, bool fresh, c
   const size_t lds2 = ((size_t)(1u << (p.tb - 5)) + 2 * nbp + 8) * 4;
   allow_lds(k_tile_build, lds2);
   ProfScope ps("k_tile_build", s);
-  hipLaunchKernelGGL(k_tile_build, dim3(p.T), dim3(kTileBuildThreads), lds2, s, words, p.tb, p.T,
-                     seg, p.nblk, ent, 2 * p.C, fresh ? 1 : 0);
+  hipLaunchKernelGGL(k_tile_build, dim3(p.T, nb), dim3(kTileBuildThreads), lds2, s, bb, p.tb, p.T,
+                     seg, p.nblk, ent, 2 * p.C);
   return hipGetLastError();
+}
+
+hipError_t launch_build_tiled(int keyk, int mode, uint32_t* words, bool fresh, const KeySrc& ks,
+                              uint64_t n, const ModP& mp, const TilePlan& p, uint32_t* seg,
+                              uint32_t* ent, hipStream_t s) {
+  if (!n) return hipSuccess;
+  BuildBatch bb{};
+  bb.ks[0] = ks;
+  bb.n[0] = n;
+  bb.words[0] = words;
+  bb.fresh = fresh ? 1u : 0u;
+  return launch_build_batch(keyk, mode, bb, 1, mp, p, seg, ent, s);
 }
 
 hipError_t launch_probe_partition(int keyk, int mode, const KeySrc& ks, uint64_t n,

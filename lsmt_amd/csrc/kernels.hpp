@@ -24,6 +24,16 @@ struct FilterPtrs {
   uint32_t row[kMaxFiltersPerLaunch];  // hits row for filter i of this launch
 };
 
+// A batch of filters (same m) built together: one partition launch and one
+// tile launch for all of them (blockIdx.y = filter). C4's concurrent flushes.
+constexpr uint32_t kMaxBuildBatch = 32;
+struct BuildBatch {
+  KeySrc ks[kMaxBuildBatch];
+  uint64_t n[kMaxBuildBatch];
+  uint32_t* words[kMaxBuildBatch];
+  uint32_t fresh;  // bit i: filter i is known all-zero
+};
+
 // Geometry of one tiled pass (build or probe) over filters of m bits.
 struct TilePlan {
   uint32_t tb;    // log2(tile bits)
@@ -50,6 +60,11 @@ hipError_t launch_probe_direct(int keyk, int mode, const FilterPtrs& fp, uint32_
                                const KeySrc& ks, uint64_t n, const ModP& mp, uint64_t* hits,
                                uint64_t hwords, hipStream_t s);
 
+// seg / ent hold nb consecutive per-filter regions of build_seg_bytes /
+// build_ent_bytes each (p planned for the largest n of the batch).
+hipError_t launch_build_batch(int keyk, int mode, const BuildBatch& bb, uint32_t nb,
+                              const ModP& mp, const TilePlan& p, uint32_t* seg, uint32_t* ent,
+                              hipStream_t s);
 hipError_t launch_build_tiled(int keyk, int mode, uint32_t* words, bool fresh, const KeySrc& ks,
                               uint64_t n, const ModP& mp, const TilePlan& p, uint32_t* seg,
                               uint32_t* ent, hipStream_t s);

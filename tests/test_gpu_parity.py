@@ -376,3 +376,19 @@ def test_filterset_union_mode(gpu):
     r = subprocess.run([sys.executable, "-c", _UNION_SCRIPT, root], env=env, capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0 and "union ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("m", [100003, 1 << 20, 1 << 25])
+def test_insert_many_matches_oracle(gpu, path, m):
+    # concurrent flush builds (C4 shape, scaled down): 40 filters, ragged counts
+    counts = [0, 1, 5000] + [3000 + 97 * i for i in range(37)]
+    keys = [workload.key_range(800 + i, c) for i, c in enumerate(counts)]
+    fs = [gpu.BloomFilter(m) for _ in counts]
+    fs[5].insert_batch(workload.key_range(5, 100))  # one filter already holds bits
+    gpu.insert_many(fs, keys)
+    for i, (f, k) in enumerate(zip(fs, keys)):
+        o = oracle.OracleFilter(m)
+        if i == 5:
+            o.insert_fixed(workload.key_range(5, 100))
+        o.insert_fixed(k)
+        assert np.array_equal(f.bools(), o.bools()), i
