@@ -53,6 +53,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--check", action="store_true", help="verify hits against the oracle (slow)")
+    p.add_argument("--no-zone", action="store_true", help="skip the zone-map gate leg")
     p.add_argument("--overlap", action="store_true",
                    help="N>1: run each step's all-gather on a side stream, overlapped with the next "
                         "step's probe (measured slower on one GPU: the streams share one hardware "
@@ -271,6 +272,39 @@ def main():
     set_assign_ms = (time.perf_counter() - t0) * 1e3
     del fset2
 
+    # ---- zone-map gate: each slot's ZoneMap built on the
+    # device from its table's keys (the zone_map.update loop of SsTable::create),
+    # then the same probe with SsTable::get's full gate (src/sstable.rs:138).
+    zone = None
+    if not args.no_zone:
+        zkeys = [torch.from_numpy(workload.key_range(seed_base + f, kpf)).to(dev) for f in range(f_lo, f_lo + F)]
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i, zk in enumerate(zkeys):
+            fset.zone_from_keys(i, lsmt_amd.DeviceKeys(zk), stream=sh)
+        torch.cuda.synchronize(dev)
+        zone_build_s = time.perf_counter() - t0
+        del zkeys
+
+        def step_gated():
+            buf = claim()
+            fset.probe(keys_batch, out=hits_bufs[buf], stream=sh, gated=True)
+            exchange(buf)
+
+        for _ in range(args.warmup):
+            step_gated()
+        gel = timed(step_gated, args.steps)
+        gprof = kernel_ms(["k_set_probe_gated"], step_gated, args.steps)
+        gated_hits = int(np.unpackbits(hits_bufs[(step_no[0] - 1) % 2].cpu().numpy().view(np.uint8)).sum())
+        zone = {"value": round(probes_per_step / (gel / args.steps), 1), "unit": "gated probes/s",
+                "ms_per_step": round(gel / args.steps * 1e3, 4),
+                "kernels_us": {k: round(v["avg_us"], 2) for k, v in gprof.items()},
+                "zone_build_keys_per_s": round(F * kpf / zone_build_s, 1),
+                "gated_hits_last_step": gated_hits,
+                "note": "C3 tables hold random keys, so every zone spans ~the whole key space: "
+                        "this measures the gate's cost; tests/test_zone_gpu.py covers rejection"}
+        fset.assign_all(filters, stream=sh)  # zones reset; the set is unchanged otherwise
+
     # ---- C2 build: 1M keys -> one fresh 16 MiB filter (zero-fill + batched insert)
     bk = torch.from_numpy(workload.c2_build_keys(args.build_keys)).to(dev)
     bf = lsmt_amd.BloomFilter(args.build_m_bits, device=local)
@@ -319,6 +353,7 @@ def main():
             o.insert_fixed(workload.key_range(seed_base + f, kpf))
             refs.append(o)
         expect = oracle.probe_fixed(refs, look_np, threads=8)
+        step()  # the headline leg again (the zone leg ran after it)
         torch.cuda.synchronize(dev)
         got = hits_bufs[(step_no[0] - 1) % 2].cpu().numpy().view(np.uint64)
         assert np.array_equal(got, expect), "bench hits differ from the oracle"
@@ -350,7 +385,7 @@ def main():
             "alt_kernels_us": {k: round(v["avg_us"], 2) for k, v in kprof_alt.items()},
             "filterset": {"build_all_ms": round(set_build_ms, 3), "assign_one_empty_slot_ms": round(set_assign_ms, 3),
                           "bytes": m * (4 if F <= 32 else 8)},
-            "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e,
+            "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e, "zone_gate": zone,
         }
         print(json.dumps(line), file=result, flush=True)
     if use_dist:

@@ -145,6 +145,41 @@ int cb_set_probe_fixed(const cb_filterset* set, const uint8_t* keys, uint32_t ke
 int cb_set_probe_var(const cb_filterset* set, const uint8_t* bytes, const uint64_t* offsets,
                      uint64_t n, uint64_t* hits, void* stream);
 
+/* ---- zone maps and the SsTable::get gate ----
+ * Each slot may carry its table's ZoneMap (src/zonemap.rs:3-8: optional
+ * min/max key, compared byte-wise like Rust's str Ord). A slot whose zone
+ * lacks either bound accepts every key (zonemap.rs:37-42). cb_set_assign,
+ * cb_set_assign_all and cb_set_clear_slot reset the slot's zone to "none";
+ * set the zone after assigning the table's filter. Zone updates wait for
+ * `stream` (they happen once per flush). */
+/* The slot's zone := {min, max} — ZoneMap::from_proto (zonemap.rs:55-61). */
+int cb_set_zone(cb_filterset* set, uint32_t slot, const uint8_t* min, uint64_t min_len,
+                int has_min, const uint8_t* max, uint64_t max_len, int has_max, void* stream);
+/* Reads the slot's zone back (to_proto, zonemap.rs:46-52). Bytes are copied
+ * only when the buffer is large enough; lengths are always written. */
+int cb_set_zone_get(const cb_filterset* set, uint32_t slot, uint8_t* min, uint64_t min_cap,
+                    uint64_t* min_len, int* has_min, uint8_t* max, uint64_t max_cap,
+                    uint64_t* max_len, int* has_max);
+/* ZoneMap::update for every key of a batch, on the device (the zone half of
+ * SsTable::create's loop, src/sstable.rs:62-65). n == 0 leaves it as is. */
+int cb_set_zone_from_keys_fixed(cb_filterset* set, uint32_t slot, const uint8_t* keys,
+                                uint32_t key_len, uint64_t n, void* stream);
+int cb_set_zone_from_keys_var(cb_filterset* set, uint32_t slot, const uint8_t* bytes,
+                              const uint64_t* offsets, uint64_t n, void* stream);
+/* Index of the first lexicographically smallest / largest key of a batch
+ * (UINT64_MAX when n == 0). */
+int cb_zone_bounds_fixed(const uint8_t* keys, uint32_t key_len, uint64_t n, int device,
+                         uint64_t* min_idx, uint64_t* max_idx, void* stream);
+int cb_zone_bounds_var(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, int device,
+                       uint64_t* min_idx, uint64_t* max_idx, void* stream);
+/* SsTable::get's gate for every (key, slot): bit set iff
+ * zone_map.contains(key) && bloom.may_contain(key) (src/sstable.rs:138).
+ * Same hits layout as cb_set_probe_*. */
+int cb_set_probe_gated_fixed(const cb_filterset* set, const uint8_t* keys, uint32_t key_len,
+                             uint64_t n, uint64_t* hits, void* stream);
+int cb_set_probe_gated_var(const cb_filterset* set, const uint8_t* bytes, const uint64_t* offsets,
+                           uint64_t n, uint64_t* hits, void* stream);
+
 /* ---- tuning / introspection (bench + tests) ---- */
 /* Path selection: 0 = auto, 1 = force direct (per-key atomics / gathers),
  * 2 = force tiled (LDS-staged filter tiles). Process-wide. */

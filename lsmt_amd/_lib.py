@@ -93,6 +93,15 @@ def load():
         "cb_set_clear_slot": ([P, u32, P], i32),
         "cb_set_probe_fixed": ([P, u8p, u32, u64, P, P], i32),
         "cb_set_probe_var": ([P, u8p, P, u64, P, P], i32),
+        "cb_set_zone": ([P, u32, u8p, u64, i32, u8p, u64, i32, P], i32),
+        "cb_set_zone_get": ([P, u32, u8p, u64, pu64, ctypes.POINTER(i32), u8p, u64, pu64,
+                             ctypes.POINTER(i32)], i32),
+        "cb_set_zone_from_keys_fixed": ([P, u32, u8p, u32, u64, P], i32),
+        "cb_set_zone_from_keys_var": ([P, u32, u8p, P, u64, P], i32),
+        "cb_zone_bounds_fixed": ([u8p, u32, u64, i32, pu64, pu64, P], i32),
+        "cb_zone_bounds_var": ([u8p, P, u64, i32, pu64, pu64, P], i32),
+        "cb_set_probe_gated_fixed": ([P, u8p, u32, u64, P, P], i32),
+        "cb_set_probe_gated_var": ([P, u8p, P, u64, P, P], i32),
         "cb_profile_enable": ([i32], i32),
         "cb_profile_reset": ([], i32),
         "cb_profile_read": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), pu64], i32),

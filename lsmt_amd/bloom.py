@@ -34,7 +34,7 @@ from . import _lib
 from ._lib import CassBloomError, check
 
 __all__ = ["BloomFilter", "BloomProto", "FilterSet", "probe", "insert_many", "set_path",
-           "last_path", "device_count", "DeviceKeys", "KeyBatch"]
+           "last_path", "device_count", "DeviceKeys", "KeyBatch", "ZoneMap", "zone_bounds"]
 
 
 def _L():
@@ -137,6 +137,51 @@ def _stream(stream) -> int | None:
 class BloomProto:
     """Mirror of ``BloomProto { repeated bool bits = 1; }`` (src/bloom.rs:9-13)."""
     bits: np.ndarray = field(default_factory=lambda: np.zeros(0, bool))
+
+
+@dataclass
+class ZoneMap:
+    """Mirror of ``ZoneMap { min, max: Option<String> }`` (src/zonemap.rs:3-8).
+
+    Bounds are bytes, ordered as Rust orders ``str`` (byte-wise, a proper
+    prefix first). This host object only carries a table's bounds; the
+    per-key gate runs on the device (``FilterSet.probe(..., gated=True)``)."""
+    min: bytes | None = None
+    max: bytes | None = None
+
+    def update(self, key) -> None:
+        """zonemap.rs:21-32."""
+        k = key.encode() if isinstance(key, str) else bytes(key)
+        if self.min is None or k < self.min:
+            self.min = k
+        if self.max is None or k > self.max:
+            self.max = k
+
+    def contains(self, key) -> bool:
+        """zonemap.rs:37-42: min <= key <= max, true if a bound is missing."""
+        if self.min is None or self.max is None:
+            return True
+        k = key.encode() if isinstance(key, str) else bytes(key)
+        return self.min <= k <= self.max
+
+
+def zone_bounds(keys, device: int = 0, stream=None) -> tuple[int, int] | None:
+    """(index of first smallest key, index of first largest key), computed on
+    the device; None for an empty batch."""
+    b = as_batch(keys)
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    s = _stream(stream)
+    if b.is_var:
+        dp, k1 = _ptr_of(b.data)
+        offp, k2 = _ptr_of(b.offsets)
+        _raise(_L().cb_zone_bounds_var(dp, offp, b.n, int(device), ctypes.byref(lo), ctypes.byref(hi), s))
+    else:
+        kp, k1 = _ptr_of(b.keys)
+        _raise(_L().cb_zone_bounds_fixed(kp, b.key_len, b.n, int(device), ctypes.byref(lo),
+                                         ctypes.byref(hi), s))
+    if b.n == 0:
+        return None
+    return int(lo.value), int(hi.value)
 
 
 # ---- the filter --------------------------------------------------------------------
@@ -387,8 +432,46 @@ class FilterSet:
     def clear_slot(self, slot: int, stream=None) -> None:
         _raise(_L().cb_set_clear_slot(self._h, int(slot), _stream(stream)))
 
-    def probe(self, keys, out=None, stream=None) -> np.ndarray:
-        """uint64[used, ceil(n/64)]: row s = slot s's may_contain bits."""
+    def set_zone(self, slot: int, zone: "ZoneMap | tuple", stream=None) -> None:
+        """Slot's zone map := zone (ZoneMap or (min, max) bytes/str/None)."""
+        lo, hi = (zone.min, zone.max) if isinstance(zone, ZoneMap) else zone
+        lo = lo.encode() if isinstance(lo, str) else lo
+        hi = hi.encode() if isinstance(hi, str) else hi
+        lb = np.frombuffer(lo, np.uint8) if lo else np.zeros(1, np.uint8)
+        hb = np.frombuffer(hi, np.uint8) if hi else np.zeros(1, np.uint8)
+        _raise(_L().cb_set_zone(self._h, int(slot), lb.ctypes.data_as(ctypes.c_void_p), len(lo or b""),
+                                lo is not None, hb.ctypes.data_as(ctypes.c_void_p), len(hi or b""),
+                                hi is not None, _stream(stream)))
+
+    def zone(self, slot: int) -> ZoneMap:
+        ll, hl = ctypes.c_uint64(), ctypes.c_uint64()
+        hasl, hash_ = ctypes.c_int(), ctypes.c_int()
+        check(_L().cb_set_zone_get(self._h, int(slot), None, 0, ctypes.byref(ll), ctypes.byref(hasl), None, 0,
+                                   ctypes.byref(hl), ctypes.byref(hash_)))
+        lb = np.zeros(max(ll.value, 1), np.uint8)
+        hb = np.zeros(max(hl.value, 1), np.uint8)
+        check(_L().cb_set_zone_get(self._h, int(slot), lb.ctypes.data_as(ctypes.c_void_p), lb.size, ctypes.byref(ll),
+                                   ctypes.byref(hasl), hb.ctypes.data_as(ctypes.c_void_p), hb.size,
+                                   ctypes.byref(hl), ctypes.byref(hash_)))
+        return ZoneMap(lb[: ll.value].tobytes() if hasl.value else None,
+                       hb[: hl.value].tobytes() if hash_.value else None)
+
+    def zone_from_keys(self, slot: int, keys, stream=None) -> None:
+        """ZoneMap::update over a key batch, on the device (src/sstable.rs:62-65)."""
+        b = as_batch(keys)
+        s = _stream(stream)
+        if b.is_var:
+            dp, k1 = _ptr_of(b.data)
+            offp, k2 = _ptr_of(b.offsets)
+            _raise(_L().cb_set_zone_from_keys_var(self._h, int(slot), dp, offp, b.n, s))
+        else:
+            kp, k1 = _ptr_of(b.keys)
+            _raise(_L().cb_set_zone_from_keys_fixed(self._h, int(slot), kp, b.key_len, b.n, s))
+
+    def probe(self, keys, out=None, stream=None, gated: bool = False) -> np.ndarray:
+        """uint64[used, ceil(n/64)]: row s = slot s's may_contain bits; with
+        gated=True, SsTable::get's full gate zone.contains && may_contain
+        (src/sstable.rs:138)."""
         b = as_batch(keys)
         used = self.used
         words = (b.n + 63) // 64
@@ -402,10 +485,12 @@ class FilterSet:
         if b.is_var:
             dp, k1 = _ptr_of(b.data)
             offp, k2 = _ptr_of(b.offsets)
-            _raise(_L().cb_set_probe_var(self._h, dp, offp, b.n, op, s))
+            fn = _L().cb_set_probe_gated_var if gated else _L().cb_set_probe_var
+            _raise(fn(self._h, dp, offp, b.n, op, s))
         else:
             kp, k1 = _ptr_of(b.keys)
-            _raise(_L().cb_set_probe_fixed(self._h, kp, b.key_len, b.n, op, s))
+            fn = _L().cb_set_probe_gated_fixed if gated else _L().cb_set_probe_fixed
+            _raise(fn(self._h, kp, b.key_len, b.n, op, s))
         return result
 
 

@@ -19,6 +19,7 @@
 #include "cassbloom.h"
 #include "filterset.hpp"
 #include "kernels.hpp"
+#include "zone.hpp"
 
 using cb::FilterPtrs;
 using cb::KeySrc;
@@ -49,6 +50,13 @@ struct cb_filterset {
   uint64_t dirty = 0;     // bit s: slot s may hold set bits
   int mode = 0;
   ModP mp{};
+  // Per-slot ZoneMap (src/zonemap.rs): host copy, and the device table the
+  // gated probe reads (cb::ZoneView: 64 x 16-B headers, then the bytes).
+  std::vector<std::string> zlo, zhi;
+  std::vector<uint8_t> zhas_lo, zhas_hi;
+  void* zdev = nullptr;
+  size_t zcap = 0;
+  uint64_t zgated = 0;  // slots with both bounds
 };
 
 namespace {
@@ -58,6 +66,7 @@ thread_local int g_last_path = 0;
 int g_path_override = 0;  // 0 auto, 1 direct, 2 tiled
 
 constexpr int PATH_DIRECT = 1, PATH_TILED = 2;
+constexpr size_t cb_zone_hdr_bytes = 64 * 16;  // cb::ZoneView headers
 
 int fail(int code, const char* what) {
   g_err = what;
@@ -98,7 +107,7 @@ struct DevBuf {
 
 struct Workspace {
   std::mutex mu;
-  DevBuf keys, offsets, hits, seg, ent, masks, bools, lkey;
+  DevBuf keys, offsets, hits, seg, ent, masks, bools, lkey, zone;
 };
 
 std::mutex g_ws_mu;
@@ -384,7 +393,7 @@ int probe_impl(const cb_filter* const* filters, uint32_t nf, const uint8_t* keys
 }
 
 int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t* offsets,
-                   uint32_t key_len, uint64_t n, uint64_t* hits, hipStream_t s) {
+                   uint32_t key_len, uint64_t n, uint64_t* hits, hipStream_t s, bool gated) {
   if (!set) return fail(CB_EINVAL, "null set");
   if (n == 0 || set->used == 0) return CB_OK;
   if (!hits) return fail(CB_EINVAL, "null hits");
@@ -403,8 +412,11 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
     HIP_TRY(ws.hits.reserve((size_t)set->used * hwords * 8, s));
     dhits = (uint64_t*)ws.hits.p;
   }
+  const cb::ZoneView zv{(const uint32_t*)set->zdev,
+                       (const uint8_t*)set->zdev + cb_zone_hdr_bytes, set->zgated};
   HIP_TRY(cb::launch_set_probe(sk.keyk, set->mode, set->width, set->words, set->any, set->used,
-                               sk.ks, n, set->mp, dhits, hwords, s));
+                               sk.ks, n, set->mp, (gated && set->zgated) ? &zv : nullptr, dhits,
+                               hwords, s));
   g_last_path = 3;
   if (host_hits) {
     HIP_TRY(hipMemcpyAsync(hits, dhits, (size_t)set->used * hwords * 8, hipMemcpyDeviceToHost, s));
@@ -412,6 +424,100 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
   } else if (sk.staged) {
     HIP_TRY(hipStreamSynchronize(s));
   }
+  return CB_OK;
+}
+
+// Rebuild and upload the set's zone table (cb::ZoneView layout). Called on
+// zone updates, which happen once per table flush: the upload is ordered on
+// stream s and waited for, so the host staging vector can be reused.
+int upload_zones(cb_filterset* set, hipStream_t s) {
+  std::vector<uint8_t> tab(cb_zone_hdr_bytes, 0);
+  uint32_t* hdr = (uint32_t*)tab.data();
+  set->zgated = 0;
+  for (uint32_t i = 0; i < set->width; ++i) {
+    if (!(set->zhas_lo[i] && set->zhas_hi[i])) continue;
+    set->zgated |= 1ull << i;
+    hdr[4 * i + 0] = (uint32_t)(tab.size() - cb_zone_hdr_bytes);
+    hdr[4 * i + 1] = (uint32_t)set->zlo[i].size();
+    tab.insert(tab.end(), set->zlo[i].begin(), set->zlo[i].end());
+    hdr[4 * i + 2] = (uint32_t)(tab.size() - cb_zone_hdr_bytes);
+    hdr[4 * i + 3] = (uint32_t)set->zhi[i].size();
+    tab.insert(tab.end(), set->zhi[i].begin(), set->zhi[i].end());
+  }
+  if (!set->zgated) return CB_OK;
+  if (tab.size() > set->zcap) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (set->zdev) (void)hipFree(set->zdev);
+    set->zdev = nullptr;
+    set->zcap = 0;
+    const size_t want = (tab.size() * 2 + 4095) & ~size_t(4095);
+    if (hipMalloc(&set->zdev, want) != hipSuccess) {
+      (void)hipGetLastError();
+      set->zgated = 0;
+      return fail(CB_ENOMEM, "hipMalloc failed for zone table");
+    }
+    set->zcap = want;
+  }
+  HIP_TRY(hipMemcpyAsync(set->zdev, tab.data(), tab.size(), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return CB_OK;
+}
+
+// A slot that receives another table's filter starts with no zone map
+// (accept-all), so a stale zone can never hide a key. Headers of ungated
+// slots are never read, so no upload is needed.
+void reset_zone(cb_filterset* set, uint32_t slot) {
+  set->zlo[slot].clear();
+  set->zhi[slot].clear();
+  set->zhas_lo[slot] = set->zhas_hi[slot] = 0;
+  set->zgated &= ~(1ull << slot);
+}
+
+// Bytes of key i of a staged batch (device-resident) into out.
+int fetch_key(const StagedKeys& sk, uint64_t i, std::string& out, hipStream_t s) {
+  uint64_t o[2];
+  if (sk.keyk == cb::KEY_VAR) {
+    HIP_TRY(hipMemcpyAsync(o, sk.ks.offsets + i, 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  } else {
+    o[0] = i * sk.ks.key_len;
+    o[1] = o[0] + sk.ks.key_len;
+  }
+  out.assign((size_t)(o[1] - o[0]), '\0');
+  if (o[1] > o[0]) {
+    HIP_TRY(hipMemcpyAsync(&out[0], sk.ks.bytes + o[0], (size_t)(o[1] - o[0]),
+                           hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  return CB_OK;
+}
+
+int zone_bounds_impl(int device, const uint8_t* keys, const uint64_t* offsets, uint32_t key_len,
+                     uint64_t n, hipStream_t s, uint64_t* min_idx, uint64_t* max_idx,
+                     std::string* lo, std::string* hi) {
+  if (min_idx) *min_idx = ~0ull;
+  if (max_idx) *max_idx = ~0ull;
+  if (n == 0) return CB_OK;
+  if (offsets == nullptr && keys == nullptr && key_len) return fail(CB_EINVAL, "null keys");
+  int rc = cb_init(device);
+  if (rc) return rc;
+  DeviceGuard dg(device);
+  Workspace& ws = workspace(device, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  StagedKeys sk;
+  rc = offsets ? stage_var(ws, keys, offsets, n, s, sk) : stage_fixed(ws, keys, key_len, n, s, sk);
+  if (rc) return rc;
+  HIP_TRY(ws.zone.reserve((2 * 1024 + 2) * 8, s));
+  uint64_t* dtmp = (uint64_t*)ws.zone.p;
+  uint64_t* didx = dtmp + 2 * 1024;
+  HIP_TRY(cb::launch_zone_bounds(sk.keyk, sk.ks, n, dtmp, didx, s));
+  uint64_t idx[2];
+  HIP_TRY(hipMemcpyAsync(idx, didx, 16, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (min_idx) *min_idx = idx[0];
+  if (max_idx) *max_idx = idx[1];
+  if (lo && (rc = fetch_key(sk, idx[0], *lo, s))) return rc;
+  if (hi && (rc = fetch_key(sk, idx[1], *hi, s))) return rc;
   return CB_OK;
 }
 
@@ -807,6 +913,10 @@ int cb_set_create(uint64_t m_bits, uint32_t width, int device, cb_filterset** ou
   set->device = device;
   set->width = width;
   set->mp = cb::make_modp(m_bits, &set->mode);
+  set->zlo.assign(width, std::string());
+  set->zhi.assign(width, std::string());
+  set->zhas_lo.assign(width, 0);
+  set->zhas_hi.assign(width, 0);
   const size_t bytes = (size_t)((m_bits + 31) / 32 * 32) * (width / 8);
   hipError_t e = hipMalloc(&set->words, bytes);
   if (e != hipSuccess) {
@@ -833,6 +943,7 @@ int cb_set_destroy(cb_filterset* set) {
     DeviceGuard dg(set->device);
     if (set->words) (void)hipFree(set->words);
     if (set->any) (void)hipFree(set->any);
+    if (set->zdev) (void)hipFree(set->zdev);
   }
   delete set;
   return CB_OK;
@@ -860,6 +971,7 @@ int cb_set_assign(cb_filterset* set, uint32_t slot, const cb_filter* f, void* st
     HIP_TRY(cb::launch_set_or_slot(f->words, set->m, slot, set->width, set->words, set->any, s));
   set->dirty |= 1ull << slot;
   set->used = std::max(set->used, slot + 1);
+  reset_zone(set, slot);
   return CB_OK;
 }
 
@@ -882,12 +994,14 @@ int cb_set_assign_all(cb_filterset* set, const cb_filter* const* filters, uint32
   HIP_TRY(cb::launch_set_build(fp, nf, set->m, set->width, set->words, set->any, s));
   set->used = nf;
   set->dirty = nf >= 64 ? ~0ull : ((1ull << nf) - 1);
+  for (uint32_t i = 0; i < set->width; ++i) reset_zone(set, i);
   return CB_OK;
 }
 
 int cb_set_clear_slot(cb_filterset* set, uint32_t slot, void* stream) {
   if (!set) return fail(CB_EINVAL, "null set");
   if (slot >= set->width) return fail(CB_EINVAL, "slot out of range");
+  reset_zone(set, slot);
   if (!(set->dirty >> slot & 1)) return CB_OK;
   DeviceGuard dg(set->device);
   HIP_TRY(cb::launch_set_put_slot(nullptr, set->m, slot, set->width, set->words, set->any,
@@ -898,13 +1012,110 @@ int cb_set_clear_slot(cb_filterset* set, uint32_t slot, void* stream) {
 
 int cb_set_probe_fixed(const cb_filterset* set, const uint8_t* keys, uint32_t key_len, uint64_t n,
                        uint64_t* hits, void* stream) {
-  return set_probe_impl(set, keys, nullptr, key_len, n, hits, (hipStream_t)stream);
+  return set_probe_impl(set, keys, nullptr, key_len, n, hits, (hipStream_t)stream, false);
 }
 
 int cb_set_probe_var(const cb_filterset* set, const uint8_t* bytes, const uint64_t* offsets,
                      uint64_t n, uint64_t* hits, void* stream) {
   if (!offsets) return fail(CB_EINVAL, "null offsets");
-  return set_probe_impl(set, bytes, offsets, 0, n, hits, (hipStream_t)stream);
+  return set_probe_impl(set, bytes, offsets, 0, n, hits, (hipStream_t)stream, false);
+}
+
+// ---- zone maps (src/zonemap.rs) and the SsTable::get gate ----
+
+int cb_set_zone(cb_filterset* set, uint32_t slot, const uint8_t* min, uint64_t min_len,
+                int has_min, const uint8_t* max, uint64_t max_len, int has_max, void* stream) {
+  if (!set) return fail(CB_EINVAL, "null set");
+  if (slot >= set->width) return fail(CB_EINVAL, "slot out of range");
+  if ((has_min && min_len && !min) || (has_max && max_len && !max))
+    return fail(CB_EINVAL, "null zone bound");
+  if ((has_min && min_len > 0xFFFFFFFFull) || (has_max && max_len > 0xFFFFFFFFull))
+    return fail(CB_EINVAL, "zone bound longer than 4 GiB");
+  DeviceGuard dg(set->device);
+  set->zlo[slot].assign(has_min ? (const char*)min : "", has_min ? (size_t)min_len : 0);
+  set->zhi[slot].assign(has_max ? (const char*)max : "", has_max ? (size_t)max_len : 0);
+  set->zhas_lo[slot] = has_min ? 1 : 0;
+  set->zhas_hi[slot] = has_max ? 1 : 0;
+  return upload_zones(set, (hipStream_t)stream);
+}
+
+int cb_set_zone_get(const cb_filterset* set, uint32_t slot, uint8_t* min, uint64_t min_cap,
+                    uint64_t* min_len, int* has_min, uint8_t* max, uint64_t max_cap,
+                    uint64_t* max_len, int* has_max) {
+  if (!set) return fail(CB_EINVAL, "null set");
+  if (slot >= set->width) return fail(CB_EINVAL, "slot out of range");
+  const std::string &lo = set->zlo[slot], &hi = set->zhi[slot];
+  if (has_min) *has_min = set->zhas_lo[slot];
+  if (has_max) *has_max = set->zhas_hi[slot];
+  if (min_len) *min_len = lo.size();
+  if (max_len) *max_len = hi.size();
+  if (min && min_cap >= lo.size() && !lo.empty()) memcpy(min, lo.data(), lo.size());
+  if (max && max_cap >= hi.size() && !hi.empty()) memcpy(max, hi.data(), hi.size());
+  return CB_OK;
+}
+
+int cb_set_zone_from_keys_fixed(cb_filterset* set, uint32_t slot, const uint8_t* keys,
+                                uint32_t key_len, uint64_t n, void* stream) {
+  if (!set) return fail(CB_EINVAL, "null set");
+  if (slot >= set->width) return fail(CB_EINVAL, "slot out of range");
+  std::string lo, hi;
+  int rc = zone_bounds_impl(set->device, keys, nullptr, key_len, n, (hipStream_t)stream, nullptr,
+                            nullptr, &lo, &hi);
+  if (rc || n == 0) return rc;  // no keys: ZoneMap::update never ran, zone unchanged
+  // ZoneMap::update over the batch, merged with the slot's current bounds.
+  DeviceGuard dg(set->device);
+  auto less = [](const std::string& a, const std::string& b) {
+    return std::lexicographical_compare(a.begin(), a.end(), b.begin(), b.end(),
+                                        [](char x, char y) { return (uint8_t)x < (uint8_t)y; });
+  };
+  if (!set->zhas_lo[slot] || less(lo, set->zlo[slot])) set->zlo[slot] = lo;
+  if (!set->zhas_hi[slot] || less(set->zhi[slot], hi)) set->zhi[slot] = hi;
+  set->zhas_lo[slot] = set->zhas_hi[slot] = 1;
+  return upload_zones(set, (hipStream_t)stream);
+}
+
+int cb_set_zone_from_keys_var(cb_filterset* set, uint32_t slot, const uint8_t* bytes,
+                              const uint64_t* offsets, uint64_t n, void* stream) {
+  if (!set) return fail(CB_EINVAL, "null set");
+  if (slot >= set->width) return fail(CB_EINVAL, "slot out of range");
+  if (!offsets) return fail(CB_EINVAL, "null offsets");
+  std::string lo, hi;
+  int rc = zone_bounds_impl(set->device, bytes, offsets, 0, n, (hipStream_t)stream, nullptr,
+                            nullptr, &lo, &hi);
+  if (rc || n == 0) return rc;
+  DeviceGuard dg(set->device);
+  auto less = [](const std::string& a, const std::string& b) {
+    return std::lexicographical_compare(a.begin(), a.end(), b.begin(), b.end(),
+                                        [](char x, char y) { return (uint8_t)x < (uint8_t)y; });
+  };
+  if (!set->zhas_lo[slot] || less(lo, set->zlo[slot])) set->zlo[slot] = lo;
+  if (!set->zhas_hi[slot] || less(set->zhi[slot], hi)) set->zhi[slot] = hi;
+  set->zhas_lo[slot] = set->zhas_hi[slot] = 1;
+  return upload_zones(set, (hipStream_t)stream);
+}
+
+int cb_zone_bounds_fixed(const uint8_t* keys, uint32_t key_len, uint64_t n, int device,
+                         uint64_t* min_idx, uint64_t* max_idx, void* stream) {
+  return zone_bounds_impl(device, keys, nullptr, key_len, n, (hipStream_t)stream, min_idx,
+                          max_idx, nullptr, nullptr);
+}
+
+int cb_zone_bounds_var(const uint8_t* bytes, const uint64_t* offsets, uint64_t n, int device,
+                       uint64_t* min_idx, uint64_t* max_idx, void* stream) {
+  if (!offsets) return fail(CB_EINVAL, "null offsets");
+  return zone_bounds_impl(device, bytes, offsets, 0, n, (hipStream_t)stream, min_idx, max_idx,
+                          nullptr, nullptr);
+}
+
+int cb_set_probe_gated_fixed(const cb_filterset* set, const uint8_t* keys, uint32_t key_len,
+                             uint64_t n, uint64_t* hits, void* stream) {
+  return set_probe_impl(set, keys, nullptr, key_len, n, hits, (hipStream_t)stream, true);
+}
+
+int cb_set_probe_gated_var(const cb_filterset* set, const uint8_t* bytes, const uint64_t* offsets,
+                           uint64_t n, uint64_t* hits, void* stream) {
+  if (!offsets) return fail(CB_EINVAL, "null offsets");
+  return set_probe_impl(set, bytes, offsets, 0, n, hits, (hipStream_t)stream, true);
 }
 
 

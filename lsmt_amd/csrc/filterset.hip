@@ -19,6 +19,7 @@
 
 #include "filterset.hpp"
 #include "profile.hpp"
+#include "zone.hpp"
 
 namespace cb {
 namespace {
@@ -164,75 +165,77 @@ __global__ __launch_bounds__(256) void k_set_put_slot(const uint32_t* __restrict
 }
 
 constexpr uint32_t kSetWords = 16;  // hit words (x64 keys) per block: 1024 keys
+constexpr uint32_t kSetProbeThreads = 64 * kSetWords;
 
-// KPL keys per lane (one hit word each, KPL words per wave): all KPL set[a]
-// reads are issued before any is consumed, then the set[b] reads, so each lane
-// keeps KPL independent random reads in flight. SC = the reference's `&&`
+// One key per lane, one 64-key hit word per wave. SC = the reference's `&&`
 // short-circuit (src/bloom.rs:50): set[b] is read only when set[a] != 0
 // (fewer bytes, but b waits for a). Ballots turn each 64-key word into one
 // hit word per slot, staged in LDS so every slot row leaves as a contiguous
-// 128-byte segment.
-template <int KEYK, int MODE, int W, int KPL, bool SC>
-__global__ __launch_bounds__(64 * kSetWords / KPL) void k_set_probe(const void* __restrict__ set,
+// 128-byte segment. (Two or four keys per lane, to keep more independent
+// reads in flight, measured no faster: the wave count already saturates the
+// memory pipeline.)
+//
+// Zone gate (SsTable::get, src/sstable.rs:138): when zv.gated != 0 each
+// surviving candidate slot s of a gated slot is re-checked with
+// ZoneMap::contains and dropped if the key is outside [min, max]. The
+// reference tests the zone first; the conjunction is the same either way and
+// testing it only for Bloom candidates costs ~0.5 compare pairs per key
+// instead of one per (key, table).
+template <int KEYK, int MODE, int W, bool SC>
+__global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __restrict__ set,
                                                                 const uint32_t* __restrict__ any,
                                                                 uint32_t used, KeySrc ks,
-                                                                uint64_t n, ModP mp,
+                                                                uint64_t n, ModP mp, ZoneView zv,
                                                                 uint64_t* __restrict__ hits,
                                                                 uint64_t hwords) {
-  constexpr uint32_t kSetProbeThreads = 64 * kSetWords / KPL;  // KPL words per wave
   typedef typename std::conditional<W == 32, uint32_t, uint64_t>::type word_t;
   typedef const __attribute__((address_space(1))) word_t* gptr;
   __shared__ uint64_t hb[64][kSetWords];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint64_t wbase = (uint64_t)blockIdx.x * kSetWords;
   const gptr sp = (gptr)set;
-  uint64_t pa[KPL], pb[KPL];
-  bool ok[KPL];
-#pragma unroll
-  for (int i = 0; i < KPL; ++i) {
-    const uint64_t k = (wbase + (uint64_t)(wave * KPL + i)) * 64 + lane;
-    ok[i] = k < n;
-    pa[i] = pb[i] = 0;
-    if (ok[i]) key_positions<KEYK, MODE>(ks, k, mp, pa[i], pb[i]);
-  }
+  const uint64_t k = (wbase + wave) * 64 + lane;
+  bool ok = k < n;
+  uint64_t pa = 0, pb = 0;
+  if (ok) key_positions<KEYK, MODE>(ks, k, mp, pa, pb);
   // Union pre-test: any[p] = (set[p] != 0) is the Bloom filter of every
   // slot's keys (m bits, L2/MALL-resident). A key whose a or b bit is clear
   // there is absent from every slot and skips both set reads.
   if (any) {
     const gsp32 ap = (gsp32)any;
-    uint32_t ua[KPL], ub[KPL];
-#pragma unroll
-    for (int i = 0; i < KPL; ++i) {
-      ua[i] = ok[i] ? ap[pa[i] >> 5] : 0u;
-      ub[i] = ok[i] ? ap[pb[i] >> 5] : 0u;
-    }
-#pragma unroll
-    for (int i = 0; i < KPL; ++i)
-      ok[i] = ok[i] && ((ua[i] >> (pa[i] & 31)) & (ub[i] >> (pb[i] & 31)) & 1u);
+    const uint32_t ua = ok ? ap[pa >> 5] : 0u;
+    const uint32_t ub = ok ? ap[pb >> 5] : 0u;
+    ok = ok && ((ua >> (pa & 31)) & (ub >> (pb & 31)) & 1u);
   }
-  word_t va[KPL], vb[KPL];
-#pragma unroll
-  for (int i = 0; i < KPL; ++i) va[i] = ok[i] ? sp[pa[i]] : (word_t)0;
-  if constexpr (!SC) {
-#pragma unroll
-    for (int i = 0; i < KPL; ++i) vb[i] = ok[i] ? sp[pb[i]] : (word_t)0;
-  } else {
-#pragma unroll
-    for (int i = 0; i < KPL; ++i) vb[i] = va[i] ? sp[pb[i]] : (word_t)0;
-  }
-#pragma unroll
-  for (int i = 0; i < KPL; ++i) {
-    const word_t mask = va[i] & vb[i];
-    uint64_t mine = 0;
-#pragma unroll
-    for (uint32_t f = 0; f < (uint32_t)W; ++f) {
-      if (f < used) {
-        const uint64_t bal = __ballot((mask >> f) & 1u);
-        mine = (lane == f) ? bal : mine;
+  const word_t va = ok ? sp[pa] : (word_t)0;
+  word_t vb;
+  if constexpr (!SC)
+    vb = ok ? sp[pb] : (word_t)0;
+  else
+    vb = va ? sp[pb] : (word_t)0;
+  word_t mask = va & vb;
+  if (zv.gated) {
+    word_t c = mask & (word_t)zv.gated;
+    if (c) {
+      const uint8_t* kp;
+      uint64_t kl;
+      key_span<KEYK>(ks, k, kp, kl);
+      while (c) {
+        const uint32_t s = (uint32_t)__builtin_ctzll((uint64_t)c);
+        c &= c - 1;
+        if (!zone_contains(zv, s, kp, kl)) mask &= ~((word_t)1 << s);
       }
     }
-    if (lane < used) hb[lane][wave * KPL + i] = mine;
   }
+  uint64_t mine = 0;
+#pragma unroll
+  for (uint32_t f = 0; f < (uint32_t)W; ++f) {
+    if (f < used) {
+      const uint64_t bal = __ballot((mask >> f) & 1u);
+      mine = (lane == f) ? bal : mine;
+    }
+  }
+  if (lane < used) hb[lane][wave] = mine;
   __syncthreads();
   const uint64_t nw = (n + 63) / 64;
   for (uint32_t i = threadIdx.x; i < used * kSetWords; i += kSetProbeThreads) {
@@ -314,46 +317,28 @@ hipError_t launch_set_put_slot(const uint32_t* words, uint64_t m, uint32_t slot,
   return hipGetLastError();
 }
 
-template <int KK, int MM, int WW, int KPL>
-static void set_probe_k(bool sc, const void* set, const uint32_t* any, uint32_t used,
-                        const KeySrc& ks, uint64_t n, const ModP& mp, uint64_t* hits,
-                        uint64_t hwords, uint32_t grid, hipStream_t s) {
-  constexpr uint32_t nt = 64 * kSetWords / KPL;
-  if (sc)
-    hipLaunchKernelGGL((k_set_probe<KK, MM, WW, KPL, true>), dim3(grid), dim3(nt), 0, s, set, any,
-                       used, ks, n, mp, hits, hwords);
-  else
-    hipLaunchKernelGGL((k_set_probe<KK, MM, WW, KPL, false>), dim3(grid), dim3(nt), 0, s, set,
-                       any, used, ks, n, mp, hits, hwords);
-}
-
 template <int KK, int MM, int WW>
-static void set_probe(int kpl, bool sc, const void* set, const uint32_t* any, uint32_t used,
-                      const KeySrc& ks, uint64_t n, const ModP& mp, uint64_t* hits,
-                      uint64_t hwords, uint32_t grid, hipStream_t s) {
-  if (kpl == 4)
-    set_probe_k<KK, MM, WW, 4>(sc, set, any, used, ks, n, mp, hits, hwords, grid, s);
-  else if (kpl == 2)
-    set_probe_k<KK, MM, WW, 2>(sc, set, any, used, ks, n, mp, hits, hwords, grid, s);
+static void set_probe(bool sc, const void* set, const uint32_t* any, uint32_t used,
+                      const KeySrc& ks, uint64_t n, const ModP& mp, const ZoneView& zv,
+                      uint64_t* hits, uint64_t hwords, uint32_t grid, hipStream_t s) {
+  if (sc)
+    hipLaunchKernelGGL((k_set_probe<KK, MM, WW, true>), dim3(grid), dim3(kSetProbeThreads), 0, s,
+                       set, any, used, ks, n, mp, zv, hits, hwords);
   else
-    set_probe_k<KK, MM, WW, 1>(sc, set, any, used, ks, n, mp, hits, hwords, grid, s);
+    hipLaunchKernelGGL((k_set_probe<KK, MM, WW, false>), dim3(grid), dim3(kSetProbeThreads), 0, s,
+                       set, any, used, ks, n, mp, zv, hits, hwords);
 }
 
 hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
                             const uint32_t* any, uint32_t used, const KeySrc& ks, uint64_t n,
-                            const ModP& mp, uint64_t* hits, uint64_t hwords, hipStream_t s) {
+                            const ModP& mp, const ZoneView* zones, uint64_t* hits,
+                            uint64_t hwords, hipStream_t s) {
   if (!n || !used) return hipSuccess;
   // CB_SET_SC=0 reads set[b] unconditionally (one latency, more bytes);
   // default keeps the reference's short-circuit.
   static const bool sc = [] {
     const char* v = getenv("CB_SET_SC");
     return !(v && v[0] == '0');
-  }();
-  // CB_SET_KPL: keys per lane (1, 2 or 4); tuning knob, default 1.
-  static const int kpl = [] {
-    const char* v = getenv("CB_SET_KPL");
-    const int k = v ? atoi(v) : 1;
-    return (k == 2 || k == 4) ? k : 1;
   }();
   // CB_SET_ANY=1 enables the union pre-test. Off by default: measured on C3
   // it costs more than it saves (52.8 vs 40.0 us), because the 2 extra random
@@ -364,11 +349,12 @@ hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
     const char* v = getenv("CB_SET_ANY");
     return v && v[0] == '1';
   }();
+  const ZoneView zv = zones ? *zones : ZoneView{nullptr, nullptr, 0};
   const uint64_t nw = (n + 63) / 64;
   const uint32_t grid = (uint32_t)((nw + kSetWords - 1) / kSetWords);
-  ProfScope ps("k_set_probe", s);
+  ProfScope ps(zv.gated ? "k_set_probe_gated" : "k_set_probe", s);
   CB_SET_DISPATCH(keyk, mode, width,
-                  (set_probe<KK, MM, WW>(kpl, sc, set, use_any ? any : nullptr, used, ks, n, mp,
+                  (set_probe<KK, MM, WW>(sc, set, use_any ? any : nullptr, used, ks, n, mp, zv,
                                          hits, hwords, grid, s)));
   return hipGetLastError();
 }

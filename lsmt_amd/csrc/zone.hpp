@@ -1,0 +1,72 @@
+// zone.hpp — device restatement of ZoneMap (/root/reference/src/zonemap.rs)
+// and the per-table gate of SsTable::get (src/sstable.rs:138):
+//
+//   if !zone_map.contains(key) || !bloom.may_contain(key) { return None }
+//
+// ZoneMap keeps the lexicographically smallest and largest key a table holds
+// (update, zonemap.rs:21-32; Rust's `str` order = byte-wise, a proper prefix
+// sorts first). contains(key) is min <= key <= max, and true when either
+// bound is missing (zonemap.rs:37-42).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hash.hpp"
+
+namespace cb {
+
+// Per-slot bounds of a FilterSet, resident in HBM (a few KB, L2-resident
+// during a probe). hdr[4*s .. 4*s+3] = (lo_off, lo_len, hi_off, hi_len) into
+// blob. `gated` has bit s set iff slot s has both bounds: only those slots
+// can reject a key (a half-open zone map accepts everything).
+struct ZoneView {
+  const uint32_t* hdr;
+  const uint8_t* blob;
+  uint64_t gated;
+};
+
+// Rust `Ord for str`: byte-wise, then length. Returns <0, 0, >0.
+__device__ __forceinline__ int bytes_cmp(const uint8_t* a, uint64_t al, const uint8_t* b,
+                                         uint64_t bl) {
+  const uint64_t n = al < bl ? al : bl;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint32_t x = a[i], y = b[i];
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return al < bl ? -1 : (al > bl ? 1 : 0);
+}
+
+// Byte span of key k in a key batch.
+template <int KEYK>
+__device__ __forceinline__ void key_span(const KeySrc& ks, uint64_t k, const uint8_t*& p,
+                                         uint64_t& len) {
+  if constexpr (KEYK == KEY_FIXED16) {
+    p = ks.bytes + k * 16;
+    len = 16;
+  } else if constexpr (KEYK == KEY_FIXED) {
+    p = ks.bytes + k * ks.key_len;
+    len = ks.key_len;
+  } else {
+    const uint64_t o0 = ks.offsets[k];
+    p = ks.bytes + o0;
+    len = ks.offsets[k + 1] - o0;
+  }
+}
+
+// ZoneMap::contains for slot s (whose bit is set in zv.gated).
+__device__ __forceinline__ bool zone_contains(const ZoneView& zv, uint32_t s, const uint8_t* key,
+                                              uint64_t len) {
+  const uint4 h = reinterpret_cast<const uint4*>(zv.hdr)[s];
+  return bytes_cmp(key, len, zv.blob + h.x, h.y) >= 0 &&
+         bytes_cmp(key, len, zv.blob + h.z, h.w) <= 0;
+}
+
+// Lexicographic min / max index of a key batch (the ZoneMap::update loop of
+// SsTable::create, src/sstable.rs:62-65, over a whole batch). idx[0] = index
+// of the first smallest key, idx[1] = index of the first largest key (ties
+// keep the earliest, as `key < min` / `key > max` do). idx is device memory;
+// tmp holds 2 * 1024 uint64 partials.
+hipError_t launch_zone_bounds(int keyk, const KeySrc& ks, uint64_t n, uint64_t* tmp,
+                              uint64_t* idx, hipStream_t s);
+
+}  // namespace cb

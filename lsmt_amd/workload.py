@@ -98,3 +98,32 @@ def var_keys(rng: np.random.Generator, n: int, max_len: int = 48):
     np.cumsum(lens, out=offsets[1:])
     data = rng.integers(0x20, 0x7F, size=int(offsets[-1]), dtype=np.uint8)
     return data, offsets
+
+
+# ---- range-partitioned tables (zone-map gate) -------------
+
+_HEX_DIGITS = b"0123456789abcdef"
+
+
+def zone_tables(nt: int = 8, seed_base: int = 300, per_seed: int = 40_000) -> list[np.ndarray]:
+    """nt tables whose key ranges are disjoint, as after range compaction: table
+    f keeps the keys of key(seed_base + f, i < per_seed) whose first hex digit
+    is one of its 16/nt digits. Each table's zone map is then a narrow slice of
+    the key space, so SsTable::get's zone gate rejects most other-range keys."""
+    span = 16 // nt
+    out = []
+    for f in range(nt):
+        ks = key_range(seed_base + f, per_seed)
+        digits = np.frombuffer(_HEX_DIGITS[span * f: span * (f + 1)], np.uint8)
+        out.append(np.ascontiguousarray(ks[np.isin(ks[:, 0], digits)]))
+    return out
+
+
+def zone_lookups(tables: list[np.ndarray], n: int, absent_seed: int = 998, rng_seed: int = 5) -> np.ndarray:
+    """Even i: a key drawn from the union of the tables; odd i: key(absent_seed, i/2)."""
+    present = np.concatenate(tables)
+    pick = np.random.default_rng(rng_seed).integers(0, len(present), n // 2)
+    out = np.empty((n, 16), np.uint8)
+    out[0::2] = present[pick]
+    out[1::2] = key_range(absent_seed, n - n // 2)[: len(out[1::2])]
+    return out

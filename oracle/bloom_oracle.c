@@ -319,6 +319,81 @@ nomem:
   return OB_ENOMEM;
 }
 
+/* ---- ZoneMap and the SsTable::get gate ---- */
+
+int ob_bytes_cmp(const uint8_t* a, uint64_t alen, const uint8_t* b, uint64_t blen) {
+  uint64_t n = alen < blen ? alen : blen;
+  int c = n ? memcmp(a, b, (size_t)n) : 0;
+  if (c) return c < 0 ? -1 : 1;
+  return alen < blen ? -1 : (alen > blen ? 1 : 0);
+}
+
+void ob_zone_init(ob_zone* z) { memset(z, 0, sizeof(*z)); }
+
+void ob_zone_free(ob_zone* z) {
+  free(z->min);
+  free(z->max);
+  ob_zone_init(z);
+}
+
+static int copy_bytes(uint8_t** dst, uint64_t* dlen, const uint8_t* src, uint64_t len) {
+  uint8_t* p = (uint8_t*)malloc(len ? (size_t)len : 1);
+  if (!p) return OB_ENOMEM;
+  if (len) memcpy(p, src, (size_t)len);
+  free(*dst);
+  *dst = p;
+  *dlen = len;
+  return OB_OK;
+}
+
+int ob_zone_set(ob_zone* z, const uint8_t* min, uint64_t min_len, int has_min, const uint8_t* max,
+                uint64_t max_len, int has_max) {
+  ob_zone_free(z);
+  if (has_min && copy_bytes(&z->min, &z->min_len, min, min_len)) return OB_ENOMEM;
+  if (has_max && copy_bytes(&z->max, &z->max_len, max, max_len)) return OB_ENOMEM;
+  z->has_min = has_min;
+  z->has_max = has_max;
+  return OB_OK;
+}
+
+int ob_zone_update(ob_zone* z, const uint8_t* key, uint64_t len) {
+  /* zonemap.rs:22-26: min = key if none or key < min */
+  if (!z->has_min || ob_bytes_cmp(key, len, z->min, z->min_len) < 0) {
+    if (copy_bytes(&z->min, &z->min_len, key, len)) return OB_ENOMEM;
+    z->has_min = 1;
+  }
+  /* zonemap.rs:27-31: max = key if none or key > max */
+  if (!z->has_max || ob_bytes_cmp(key, len, z->max, z->max_len) > 0) {
+    if (copy_bytes(&z->max, &z->max_len, key, len)) return OB_ENOMEM;
+    z->has_max = 1;
+  }
+  return OB_OK;
+}
+
+int ob_zone_contains(const ob_zone* z, const uint8_t* key, uint64_t len) {
+  if (!z || !z->has_min || !z->has_max) return 1; /* zonemap.rs:40 */
+  return ob_bytes_cmp(key, len, z->min, z->min_len) >= 0 &&
+         ob_bytes_cmp(key, len, z->max, z->max_len) <= 0; /* zonemap.rs:39 */
+}
+
+int ob_probe_gated_var(const ob_filter* const* fs, const ob_zone* const* zones, uint32_t nf,
+                       const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint64_t* hits) {
+  uint64_t words = (n + 63) / 64;
+  for (uint32_t f = 0; f < nf; ++f)
+    if (n && fs[f]->m == 0) return OB_EZEROM;
+  memset(hits, 0, (size_t)(words * nf * sizeof(uint64_t)));
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint8_t* key = bytes + offsets[k];
+    uint64_t len = offsets[k + 1] - offsets[k];
+    for (uint32_t f = 0; f < nf; ++f) {
+      /* src/sstable.rs:138: `!zone_map.contains(key) || !bloom.may_contain(key)` */
+      if (ob_zone_contains(zones ? zones[f] : NULL, key, len) && ob_may_contain(fs[f], key, len) == 1)
+        hits[(uint64_t)f * words + (k >> 6)] |= (uint64_t)1 << (k & 63);
+    }
+  }
+  return OB_OK;
+}
+
 /* ---- synthetic workload ---- */
 
 uint64_t ob_splitmix64(uint64_t x) {

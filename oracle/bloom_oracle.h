@@ -75,6 +75,30 @@ uint64_t ob_encode(const ob_filter* f, uint8_t* out, uint64_t cap);
  * unpacked field-1 elements, skips unknown fields; OB_EDECODE on malformed. */
 int ob_decode(const uint8_t* in, uint64_t len, ob_filter* out);
 
+/* ZoneMap (/root/reference/src/zonemap.rs:3-42): min/max key seen, compared
+ * as Rust compares &str — byte-wise lexicographic, a proper prefix is smaller.
+ * contains() is true when either bound is missing (zonemap.rs:37-42). */
+typedef struct ob_zone {
+  uint8_t* min;
+  uint64_t min_len;
+  int has_min;
+  uint8_t* max;
+  uint64_t max_len;
+  int has_max;
+} ob_zone;
+void ob_zone_init(ob_zone* z);
+void ob_zone_free(ob_zone* z);
+int ob_zone_set(ob_zone* z, const uint8_t* min, uint64_t min_len, int has_min, const uint8_t* max,
+                uint64_t max_len, int has_max);
+int ob_zone_update(ob_zone* z, const uint8_t* key, uint64_t len);   /* zonemap.rs:21-32 */
+int ob_zone_contains(const ob_zone* z, const uint8_t* key, uint64_t len); /* zonemap.rs:37-42 */
+int ob_bytes_cmp(const uint8_t* a, uint64_t alen, const uint8_t* b, uint64_t blen);
+/* SsTable::get's gate (src/sstable.rs:138) for every (key, table):
+ * zone_map.contains(key) && bloom.may_contain(key); zones may be NULL
+ * entries (no zone map = accept). Same hits layout as ob_probe_*. */
+int ob_probe_gated_var(const ob_filter* const* fs, const ob_zone* const* zones, uint32_t nf,
+                       const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint64_t* hits);
+
 /* Synthetic workload keys: 16 lowercase hex chars, MSB
  * nibble first, of splitmix64(seed * 2^32 + i). out is n*16 bytes. */
 void ob_gen_keys(uint64_t seed, uint64_t first, uint64_t n, uint8_t* out);

@@ -30,6 +30,11 @@ class _Filter(ctypes.Structure):
     _fields_ = [("bits", ctypes.POINTER(ctypes.c_uint8)), ("m", ctypes.c_uint64)]
 
 
+class _Zone(ctypes.Structure):
+    _fields_ = [("min", ctypes.POINTER(ctypes.c_uint8)), ("min_len", ctypes.c_uint64), ("has_min", ctypes.c_int),
+                ("max", ctypes.POINTER(ctypes.c_uint8)), ("max_len", ctypes.c_uint64), ("has_max", ctypes.c_int)]
+
+
 def build() -> str:
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
@@ -58,6 +63,15 @@ def lib():
         L.ob_encode.argtypes = [FP, P, u64]
         L.ob_encode.restype = u64
         L.ob_decode.argtypes = [P, u64, FP]
+        ZP = ctypes.POINTER(_Zone)
+        L.ob_zone_init.argtypes = [ZP]
+        L.ob_zone_init.restype = None
+        L.ob_zone_free.argtypes = [ZP]
+        L.ob_zone_free.restype = None
+        L.ob_zone_set.argtypes = [ZP, P, u64, i32, P, u64, i32]
+        L.ob_zone_update.argtypes = [ZP, P, u64]
+        L.ob_zone_contains.argtypes = [ZP, P, u64]
+        L.ob_probe_gated_var.argtypes = [P, P, u32, P, P, u64, P]
         L.ob_gen_keys.argtypes = [u64, u64, u64, P]
         L.ob_gen_keys.restype = None
         L.ob_splitmix64.argtypes = [u64]
@@ -173,6 +187,56 @@ def probe_var(filters, data: np.ndarray, offsets: np.ndarray, threads: int = 1) 
                             _ptr(offsets), n, _ptr(hits), threads)
     if rc:
         raise RuntimeError(f"ob_probe_var rc={rc}")
+    return hits
+
+
+class OracleZone:
+    """ZoneMap (src/zonemap.rs) on the CPU."""
+
+    def __init__(self, lo: bytes | None = None, hi: bytes | None = None):
+        self._z = _Zone()
+        lib().ob_zone_init(ctypes.byref(self._z))
+        if lo is not None or hi is not None:
+            lb = ctypes.create_string_buffer(lo or b"", max(len(lo or b""), 1))
+            hb = ctypes.create_string_buffer(hi or b"", max(len(hi or b""), 1))
+            lib().ob_zone_set(ctypes.byref(self._z), lb, len(lo or b""), lo is not None, hb, len(hi or b""),
+                              hi is not None)
+
+    def __del__(self):
+        try:
+            lib().ob_zone_free(ctypes.byref(self._z))
+        except Exception:
+            pass
+
+    def update(self, key: bytes) -> None:
+        buf = ctypes.create_string_buffer(key, max(len(key), 1))
+        lib().ob_zone_update(ctypes.byref(self._z), buf, len(key))
+
+    def contains(self, key: bytes) -> bool:
+        buf = ctypes.create_string_buffer(key, max(len(key), 1))
+        return bool(lib().ob_zone_contains(ctypes.byref(self._z), buf, len(key)))
+
+    @property
+    def bounds(self):
+        z = self._z
+        lo = bytes(z.min[: z.min_len]) if z.has_min else None
+        hi = bytes(z.max[: z.max_len]) if z.has_max else None
+        return lo, hi
+
+
+def probe_gated(filters, zones, data: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+    """SsTable::get's gate for every (key, table): zone.contains && may_contain."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offsets) - 1
+    nf = len(filters)
+    hits = np.zeros((nf, (n + 63) // 64), np.uint64)
+    fa = (ctypes.POINTER(_Filter) * max(nf, 1))(*[ctypes.pointer(f._f) for f in filters])
+    za = (ctypes.POINTER(_Zone) * max(nf, 1))(*[ctypes.pointer(z._z) if z is not None else None for z in zones])
+    rc = lib().ob_probe_gated_var(ctypes.cast(fa, ctypes.c_void_p), ctypes.cast(za, ctypes.c_void_p), nf,
+                                  _ptr(data if len(data) else np.zeros(1, np.uint8)), _ptr(offsets), n, _ptr(hits))
+    if rc:
+        raise RuntimeError(f"ob_probe_gated_var rc={rc}")
     return hits
 
 

@@ -216,6 +216,72 @@ def main() -> None:
                "hits_sha256": sha(hits.astype("<u8")), "hits_popcount": int(sum(int(r.sum()) for r in rows)),
                "hits_per_filter": [int(r.sum()) for r in rows]}
 
+    # 7. zone maps (src/zonemap.rs:21-42) and the SsTable::get gate (src/sstable.rs:138).
+    #    Python's bytes order is Rust's str order (byte-wise, a prefix sorts first).
+    def zone_of(keys):
+        lo = hi = None
+        for k in keys:  # zonemap.rs:21-32
+            if lo is None or k < lo:
+                lo = k
+            if hi is None or k > hi:
+                hi = k
+        return lo, hi
+
+    def zone_has(z, k):  # zonemap.rs:37-42
+        return z[0] is None or z[1] is None or z[0] <= k <= z[1]
+
+    zsc = {}
+    for name, m, ins, probes in [
+        ("sstable_test", 1024, [b"a", b"b", b"c"], [b"a", b"b", b"c", b"d", b"", b"ab", b"c\x00"]),
+        ("lsm_flush_test", 1024, [b"k1", b"k2"], [b"k1", b"k2", b"missing", b"k", b"k10", b"k3", b"j"]),
+        ("sstable_local_test", 1024, [b"k"], [b"k", b"v", b"j", b"k\x00", b""]),
+        ("utf8", 1024, ["é".encode(), "z".encode(), "✓".encode()],
+         ["é".encode(), "e".encode(), "ê".encode(), "✓".encode(), "✔".encode(), b"\xff"]),
+    ]:
+        bits = build_py(ins, m)
+        z = zone_of(ins)
+        zsc[name] = {"m": m, "insert_hex": [k.hex() for k in ins], "min_hex": z[0].hex(), "max_hex": z[1].hex(),
+                     "probe_hex": [k.hex() for k in probes],
+                     "zone": [zone_has(z, k) for k in probes],
+                     "gate": [zone_has(z, k) and may_py(bits, k) for k in probes]}
+    assert zsc["sstable_local_test"]["gate"][0] is True          # tests/sstable_local_test.rs:14-15
+    assert zsc["lsm_flush_test"]["gate"][2] is False             # tests/lsm_flush_test.rs:23
+    assert zsc["sstable_test"]["gate"][:3] == [True, True, True]  # tests/sstable_test.rs:13-14
+
+    # range-partitioned tables: table f keeps the keys of key(300+f, i<40000)
+    # whose first hex digit is in {2f, 2f+1}; its zone is the min/max of those.
+    nt, mz = 8, 50021  # small generic-mode m: Bloom FPs common, so the gate matters
+    tables, zones = [], []
+    for f in range(nt):
+        ks = np_keys(300 + f, np.arange(40_000, dtype=np.uint64))
+        first = ks[:, 0]
+        keep = (first == ord("0123456789abcdef"[2 * f])) | (first == ord("0123456789abcdef"[2 * f + 1]))
+        ks = ks[keep]
+        tables.append(ks)
+        zones.append(zone_of([bytes(r) for r in ks]))
+    nlz = 100_000
+    present = np.concatenate(tables)
+    pick = np.random.default_rng(5).integers(0, len(present), nlz // 2)
+    lkz = np.empty((nlz, 16), np.uint8)
+    lkz[0::2] = present[pick]
+    lkz[1::2] = np_keys(998, np.arange(nlz // 2, dtype=np.uint64))
+    lk_bytes = [bytes(r) for r in lkz]
+    ungated, gated = [], []
+    for f in range(nt):
+        b = np_build(tables[f], mz)
+        bloom = np_probe(b, lkz)
+        zmask = np.array([zone_has(zones[f], k) for k in lk_bytes])
+        ungated.append(_pack64(bloom))
+        gated.append(_pack64(bloom & zmask))
+    g["zone"] = {"scenarios": zsc, "tables": nt, "m": mz, "seed_base": 300, "keys_per_seed": 40_000,
+                 "n_lookups": nlz, "lookups_sha256": sha(lkz),
+                 "table_sizes": [int(len(t)) for t in tables],
+                 "zones_hex": [[z[0].hex(), z[1].hex()] for z in zones],
+                 "hits_sha256": sha(np.stack(ungated).astype("<u8")),
+                 "gated_sha256": sha(np.stack(gated).astype("<u8")),
+                 "hits_popcount": int(sum(np.unpackbits(r.view(np.uint8)).sum() for r in ungated)),
+                 "gated_popcount": int(sum(np.unpackbits(r.view(np.uint8)).sum() for r in gated))}
+
     with open(os.path.join(HERE, "golden.json"), "w") as fh:
         json.dump(g, fh, indent=1, sort_keys=True)
     print("wrote", os.path.join(HERE, "golden.json"))
