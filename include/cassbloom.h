@@ -59,6 +59,7 @@ extern "C" {
 #define CB_ENODEV (-6)  /* no usable gfx950 device */
 
 typedef struct cb_filter cb_filter;
+typedef struct cb_filterset cb_filterset; /* bit-sliced filter sets, see below */
 
 /* ---- device / library ---- */
 int cb_init(int device);
@@ -121,6 +122,43 @@ int cb_filter_to_bytes(const cb_filter* f, uint8_t* out, uint64_t cap, uint64_t*
  * fields skipped) into a new filter on `device`. */
 int cb_filter_from_bytes(const uint8_t* in, uint64_t len, int device, cb_filter** out);
 
+/* ---- TableMeta: the SSTable `.meta` file ----
+ *   message TableMeta { optional BloomProto bloom = 1;          src/sstable.rs:31-37
+ *                       optional ZoneMapProto zone_map = 2; }
+ *   message ZoneMapProto { optional string min = 1; optional string max = 2; }
+ *                                                               src/zonemap.rs:11-17 */
+typedef struct cb_zone_bounds {
+  const uint8_t* min;
+  uint64_t min_len;
+  int has_min; /* 0: None */
+  const uint8_t* max;
+  uint64_t max_len;
+  int has_max;
+} cb_zone_bounds;
+typedef struct cb_meta_info {
+  int has_bloom; /* 0: no bloom field; the returned filter is BloomFilter::new(1024) */
+  int has_zone;  /* 0: no zone_map field (ZoneMap::default()) */
+  cb_zone_bounds zone; /* min/max point INTO the decoded input buffer */
+} cb_meta_info;
+/* TableMeta{bloom, zone_map}.encode (SsTable::create, src/sstable.rs:74-81).
+ * bloom NULL / zone NULL omit that field. The filter's bits are expanded to
+ * the prost 0/1 bytes on the device. out may be host or device memory;
+ * *len_out is always the encoded length, bytes are written only if cap
+ * suffices. CB_EINVAL if a zone bound is not UTF-8. */
+int cb_meta_encode(const cb_filter* bloom, const cb_zone_bounds* zone, uint8_t* out, uint64_t cap,
+                   uint64_t* len_out);
+/* TableMeta::decode + the map()s of SsTable::load (src/sstable.rs:96-108):
+ * prost merge semantics (repeated bloom fields append bits, zone strings are
+ * last-wins, unknown fields skipped, strings must be UTF-8). CB_EDECODE on a
+ * malformed message — the reference then rebuilds from the data file
+ * (src/sstable.rs:109-120). The new filter lives on `device`. */
+int cb_meta_decode(const uint8_t* in, uint64_t len, int device, cb_filter** bloom_out,
+                   cb_meta_info* info);
+/* Restart path for a set: decode one table's `.meta` straight into `slot`
+ * (filter bits and zone map). The table's m must equal the set's m. */
+int cb_set_load_meta(cb_filterset* set, uint32_t slot, const uint8_t* in, uint64_t len,
+                     void* stream);
+
 /* ---- bit-sliced filter sets (the read-path fan-out) ---- */
 /* A FilterSet holds up to `width` (32 or 64) filters of one size m in a
  * position-major layout: word p (uint32 / uint64) has bit s = bit p of the
@@ -128,7 +166,6 @@ int cb_filter_from_bytes(const uint8_t* in, uint64_t len, int device, cb_filter*
  * word reads per key (Database::get's per-table loop, src/lib.rs:129-134,
  * collapsed; m is uniform across SSTables, src/sstable.rs:44,59). The set is a
  * derived copy: the cb_filter handles stay the source of truth. */
-typedef struct cb_filterset cb_filterset;
 int cb_set_create(uint64_t m_bits, uint32_t width, int device, cb_filterset** out);
 int cb_set_destroy(cb_filterset* set);
 /* used = 1 + the highest slot assigned so far (the number of hit rows). */

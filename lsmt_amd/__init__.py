@@ -20,10 +20,11 @@ from .bloom import (  # noqa: E402
     probe,
     set_path,
     unpack_hits,
+    TableMeta,
     zone_bounds,
     ZoneMap,
 )
 
 __all__ = ["BloomFilter", "BloomProto", "DeviceKeys", "FilterSet", "insert_many", "KeyBatch", "device_count", "last_path",
-           "probe", "set_path", "unpack_hits", "zone_bounds", "ZoneMap"]
+           "probe", "set_path", "unpack_hits", "zone_bounds", "ZoneMap", "TableMeta"]
 __version__ = "0.1.0"

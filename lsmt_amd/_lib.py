@@ -38,6 +38,17 @@ class ExtensionMissing(ImportError):
     pass
 
 
+class ZoneBounds(ctypes.Structure):
+    """struct cb_zone_bounds (include/cassbloom.h)."""
+    _fields_ = [("min", ctypes.c_void_p), ("min_len", ctypes.c_uint64), ("has_min", ctypes.c_int),
+                ("max", ctypes.c_void_p), ("max_len", ctypes.c_uint64), ("has_max", ctypes.c_int)]
+
+
+class MetaInfo(ctypes.Structure):
+    """struct cb_meta_info (include/cassbloom.h)."""
+    _fields_ = [("has_bloom", ctypes.c_int), ("has_zone", ctypes.c_int), ("zone", ZoneBounds)]
+
+
 def load():
     """Load and prototype the C ABI. Raises ExtensionMissing if not built."""
     global _lib
@@ -100,6 +111,9 @@ def load():
         "cb_set_zone_from_keys_var": ([P, u32, u8p, P, u64, P], i32),
         "cb_zone_bounds_fixed": ([u8p, u32, u64, i32, pu64, pu64, P], i32),
         "cb_zone_bounds_var": ([u8p, P, u64, i32, pu64, pu64, P], i32),
+        "cb_meta_encode": ([P, ctypes.POINTER(ZoneBounds), u8p, u64, pu64], i32),
+        "cb_meta_decode": ([u8p, u64, i32, pp, ctypes.POINTER(MetaInfo)], i32),
+        "cb_set_load_meta": ([P, u32, u8p, u64, P], i32),
         "cb_set_probe_gated_fixed": ([P, u8p, u32, u64, P, P], i32),
         "cb_set_probe_gated_var": ([P, u8p, P, u64, P, P], i32),
         "cb_profile_enable": ([i32], i32),

@@ -34,7 +34,7 @@ from . import _lib
 from ._lib import CassBloomError, check
 
 __all__ = ["BloomFilter", "BloomProto", "FilterSet", "probe", "insert_many", "set_path",
-           "last_path", "device_count", "DeviceKeys", "KeyBatch", "ZoneMap", "zone_bounds"]
+           "last_path", "device_count", "DeviceKeys", "KeyBatch", "ZoneMap", "zone_bounds", "TableMeta"]
 
 
 def _L():
@@ -163,6 +163,74 @@ class ZoneMap:
             return True
         k = key.encode() if isinstance(key, str) else bytes(key)
         return self.min <= k <= self.max
+
+
+@dataclass
+class TableMeta:
+    """Mirror of ``TableMeta { bloom: Option<BloomProto>, zone_map:
+    Option<ZoneMapProto> }`` (src/sstable.rs:31-37), the SSTable ``.meta``
+    file. Encoding and decoding run through the C ABI; the filter's bits are
+    expanded / packed on the device."""
+    bloom: "BloomFilter | None" = None
+    zone_map: ZoneMap | None = None
+
+    def encode(self) -> bytes:
+        """TableMeta.encode (SsTable::create, src/sstable.rs:74-81)."""
+        zb, keep = _zone_struct(self.zone_map)
+        fh = self.bloom.handle if self.bloom is not None else None
+        if self.bloom is not None:
+            self.bloom.flush()
+        n = ctypes.c_uint64()
+        zp = ctypes.byref(zb) if zb is not None else None
+        _raise(_L().cb_meta_encode(fh, zp, None, 0, ctypes.byref(n)))
+        out = np.zeros(max(n.value, 1), np.uint8)
+        _raise(_L().cb_meta_encode(fh, zp, out.ctypes.data, n.value, ctypes.byref(n)))
+        return out[: n.value].tobytes()
+
+    @classmethod
+    def decode(cls, data: bytes, device: int = 0) -> "TableMeta":
+        """TableMeta::decode; raises ValueError (CB_EDECODE) on malformed bytes.
+        A missing field decodes to None, as in the proto."""
+        bloom, info, buf = _meta_decode(data, device)
+        return cls(bloom if info.has_bloom else None, _zone_from_info(info, buf) if info.has_zone else None)
+
+    @staticmethod
+    def load(data: bytes, device: int = 0) -> "tuple[BloomFilter, ZoneMap]":
+        """The metadata half of SsTable::load (src/sstable.rs:96-108): a missing
+        bloom is BloomFilter::new(1024), a missing zone map ZoneMap::default()."""
+        bloom, info, buf = _meta_decode(data, device)
+        return bloom, (_zone_from_info(info, buf) if info.has_zone else ZoneMap())
+
+
+def _zone_struct(z: "ZoneMap | None"):
+    if z is None:
+        return None, None
+    lo = z.min.encode() if isinstance(z.min, str) else z.min
+    hi = z.max.encode() if isinstance(z.max, str) else z.max
+    lb = ctypes.create_string_buffer(lo or b"", max(len(lo or b""), 1))
+    hb = ctypes.create_string_buffer(hi or b"", max(len(hi or b""), 1))
+    zb = _lib.ZoneBounds(ctypes.cast(lb, ctypes.c_void_p), len(lo or b""), lo is not None,
+                         ctypes.cast(hb, ctypes.c_void_p), len(hi or b""), hi is not None)
+    return zb, (lb, hb)
+
+
+def _meta_decode(data: bytes, device: int):
+    buf = np.frombuffer(bytes(data), np.uint8).copy() if data else np.zeros(1, np.uint8)
+    h = ctypes.c_void_p()
+    info = _lib.MetaInfo()
+    _raise(_L().cb_meta_decode(buf.ctypes.data, len(data), int(device), ctypes.byref(h), ctypes.byref(info)))
+    return BloomFilter(0, device=device, _handle=h.value), info, buf
+
+
+def _zone_from_info(info, buf: np.ndarray) -> ZoneMap:
+    base = buf.ctypes.data
+    z = info.zone
+
+    def span(p, n, has):
+        if not has:
+            return None
+        return buf[p - base: p - base + n].tobytes() if n else b""
+    return ZoneMap(span(z.min or 0, z.min_len, z.has_min), span(z.max or 0, z.max_len, z.has_max))
 
 
 def zone_bounds(keys, device: int = 0, stream=None) -> tuple[int, int] | None:
@@ -455,6 +523,12 @@ class FilterSet:
                                    ctypes.byref(hl), ctypes.byref(hash_)))
         return ZoneMap(lb[: ll.value].tobytes() if hasl.value else None,
                        hb[: hl.value].tobytes() if hash_.value else None)
+
+    def load_meta(self, slot: int, data: bytes, stream=None) -> None:
+        """Decode one table's ``.meta`` (TableMeta) straight into ``slot``:
+        filter bits and zone map (the restart path, src/sstable.rs:96-108)."""
+        buf = np.frombuffer(bytes(data), np.uint8).copy() if data else np.zeros(1, np.uint8)
+        _raise(_L().cb_set_load_meta(self._h, int(slot), buf.ctypes.data, len(data), _stream(stream)))
 
     def zone_from_keys(self, slot: int, keys, stream=None) -> None:
         """ZoneMap::update over a key batch, on the device (src/sstable.rs:62-65)."""

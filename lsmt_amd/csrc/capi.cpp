@@ -431,19 +431,23 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
 // zone updates, which happen once per table flush: the upload is ordered on
 // stream s and waited for, so the host staging vector can be reused.
 int upload_zones(cb_filterset* set, hipStream_t s) {
-  std::vector<uint8_t> tab(cb_zone_hdr_bytes, 0);
-  uint32_t* hdr = (uint32_t*)tab.data();
+  uint32_t hdr[64 * 4] = {};
+  std::vector<uint8_t> blob;
   set->zgated = 0;
   for (uint32_t i = 0; i < set->width; ++i) {
     if (!(set->zhas_lo[i] && set->zhas_hi[i])) continue;
     set->zgated |= 1ull << i;
-    hdr[4 * i + 0] = (uint32_t)(tab.size() - cb_zone_hdr_bytes);
+    hdr[4 * i + 0] = (uint32_t)blob.size();
     hdr[4 * i + 1] = (uint32_t)set->zlo[i].size();
-    tab.insert(tab.end(), set->zlo[i].begin(), set->zlo[i].end());
-    hdr[4 * i + 2] = (uint32_t)(tab.size() - cb_zone_hdr_bytes);
+    blob.insert(blob.end(), set->zlo[i].begin(), set->zlo[i].end());
+    hdr[4 * i + 2] = (uint32_t)blob.size();
     hdr[4 * i + 3] = (uint32_t)set->zhi[i].size();
-    tab.insert(tab.end(), set->zhi[i].begin(), set->zhi[i].end());
+    blob.insert(blob.end(), set->zhi[i].begin(), set->zhi[i].end());
   }
+  static_assert(sizeof(hdr) == cb_zone_hdr_bytes, "ZoneView header size");
+  std::vector<uint8_t> tab(cb_zone_hdr_bytes + blob.size());
+  memcpy(tab.data(), hdr, cb_zone_hdr_bytes);
+  if (!blob.empty()) memcpy(tab.data() + cb_zone_hdr_bytes, blob.data(), blob.size());
   if (!set->zgated) return CB_OK;
   if (tab.size() > set->zcap) {
     HIP_TRY(hipStreamSynchronize(s));
@@ -581,6 +585,153 @@ bool skip_field(const uint8_t*& p, const uint8_t* end, uint32_t wt, uint64_t fie
       return true;
     default: return false;
   }
+}
+
+// 0x0A varint(m): the BloomProto header written before m 0/1 bytes.
+size_t put_bloom_header(uint8_t* p, uint64_t m) {
+  size_t n = 0;
+  p[n++] = 0x0A;  // field 1 (bits), wire type 2 (packed)
+  while (m >= 0x80) {
+    p[n++] = (uint8_t)(m | 0x80);
+    m >>= 7;
+  }
+  p[n++] = (uint8_t)m;
+  return n;
+}
+
+size_t put_varint_buf(uint8_t* p, uint64_t v) {
+  size_t n = 0;
+  while (v >= 0x80) {
+    p[n++] = (uint8_t)(v | 0x80);
+    v >>= 7;
+  }
+  p[n++] = (uint8_t)v;
+  return n;
+}
+
+// Host bytes into an output buffer that may be host or device memory.
+int put_bytes(uint8_t* dst, const void* src, size_t n) {
+  if (!n) return CB_OK;
+  if (is_device_ptr(dst)) {
+    HIP_TRY(hipMemcpy(dst, src, n, hipMemcpyHostToDevice));
+  } else {
+    memcpy(dst, src, n);
+  }
+  return CB_OK;
+}
+
+// Rust's str::from_utf8 acceptance (prost rejects a `string` field that is
+// not well-formed UTF-8). Classifies each lead byte by its range and checks
+// the tightened second-byte window that rules out overlongs, surrogates and
+// code points above U+10FFFF.
+bool utf8_ok(const uint8_t* p, uint64_t n) {
+  const uint8_t* end = p + n;
+  while (p < end) {
+    const uint8_t c = *p;
+    if (c < 0x80) {
+      ++p;
+      continue;
+    }
+    int need;
+    uint8_t lo = 0x80, hi = 0xBF;
+    switch (c >> 4) {
+      case 0xC:
+      case 0xD:
+        if (c < 0xC2) return false;
+        need = 1;
+        break;
+      case 0xE:
+        need = 2;
+        if (c == 0xE0) lo = 0xA0;
+        if (c == 0xED) hi = 0x9F;
+        break;
+      case 0xF:
+        if (c > 0xF4) return false;
+        need = 3;
+        if (c == 0xF0) lo = 0x90;
+        if (c == 0xF4) hi = 0x8F;
+        break;
+      default:
+        return false;  // stray continuation byte
+    }
+    if (end - p <= need) return false;
+    if (p[1] < lo || p[1] > hi) return false;
+    for (int k = 2; k <= need; ++k)
+      if ((p[k] & 0xC0) != 0x80) return false;
+    p += need + 1;
+  }
+  return true;
+}
+
+// One pass over a TableMeta message: the spans of every `bloom` (field 1)
+// occurrence, and the last `min` / `max` of every `zone_map` (field 2)
+// occurrence — prost's merge of a repeated singular message field is the
+// decode of the concatenated payloads, so bloom spans are concatenated and
+// zone strings are last-wins.
+struct MetaScan {
+  std::vector<std::pair<const uint8_t*, uint64_t>> bloom;
+  bool has_zone = false, has_min = false, has_max = false;
+  const uint8_t *min = nullptr, *max = nullptr;
+  uint64_t min_len = 0, max_len = 0;
+};
+
+int scan_zone(const uint8_t* p, const uint8_t* end, MetaScan& ms) {
+  while (p < end) {
+    uint64_t key, l;
+    if (!get_varint(p, end, key) || key > 0xFFFFFFFFull)
+      return fail(CB_EDECODE, "ZoneMapProto decode: invalid key");
+    const uint32_t wt = (uint32_t)(key & 7);
+    const uint64_t fn = key >> 3;
+    if (fn == 0) return fail(CB_EDECODE, "ZoneMapProto decode: invalid tag value 0");
+    if (fn == 1 || fn == 2) {
+      if (wt != 2) return fail(CB_EDECODE, "ZoneMapProto decode: invalid wire type");
+      if (!get_varint(p, end, l) || l > (uint64_t)(end - p))
+        return fail(CB_EDECODE, "ZoneMapProto decode: bad length");
+      if (!utf8_ok(p, l)) return fail(CB_EDECODE, "ZoneMapProto decode: invalid string value: data is not UTF-8 encoded");
+      if (fn == 1) {
+        ms.min = p;
+        ms.min_len = l;
+        ms.has_min = true;
+      } else {
+        ms.max = p;
+        ms.max_len = l;
+        ms.has_max = true;
+      }
+      p += l;
+    } else if (!skip_field(p, end, wt, fn, 0)) {
+      return fail(CB_EDECODE, "ZoneMapProto decode: malformed unknown field");
+    }
+  }
+  return CB_OK;
+}
+
+int scan_meta(const uint8_t* in, uint64_t len, MetaScan& ms) {
+  const uint8_t* p = in;
+  const uint8_t* end = in + len;
+  while (p < end) {
+    uint64_t key, l;
+    if (!get_varint(p, end, key) || key > 0xFFFFFFFFull)
+      return fail(CB_EDECODE, "TableMeta decode: invalid key");
+    const uint32_t wt = (uint32_t)(key & 7);
+    const uint64_t fn = key >> 3;
+    if (fn == 0) return fail(CB_EDECODE, "TableMeta decode: invalid tag value 0");
+    if (fn == 1 || fn == 2) {
+      if (wt != 2) return fail(CB_EDECODE, "TableMeta decode: invalid wire type");
+      if (!get_varint(p, end, l) || l > (uint64_t)(end - p))
+        return fail(CB_EDECODE, "TableMeta decode: bad length");
+      if (fn == 1) {
+        ms.bloom.emplace_back(p, l);
+      } else {
+        ms.has_zone = true;
+        int rc = scan_zone(p, p + l, ms);
+        if (rc) return rc;
+      }
+      p += l;
+    } else if (!skip_field(p, end, wt, fn, 0)) {
+      return fail(CB_EDECODE, "TableMeta decode: malformed unknown field");
+    }
+  }
+  return CB_OK;
 }
 
 }  // namespace
@@ -809,15 +960,11 @@ int cb_filter_to_bytes(const cb_filter* f, uint8_t* out, uint64_t cap, uint64_t*
   const uint64_t total = f->m ? 1 + varint_len(f->m) + f->m : 0;
   *len_out = total;
   if (!out || cap < total || !total) return CB_OK;
-  uint8_t* p = out;
-  *p++ = 0x0A;  // field 1, wire type 2
-  uint64_t v = f->m;
-  while (v >= 0x80) {
-    *p++ = (uint8_t)(v | 0x80);
-    v >>= 7;
-  }
-  *p++ = (uint8_t)v;
-  return cb_filter_export_bools(f, p, nullptr);
+  uint8_t hdr[11];
+  const size_t hl = put_bloom_header(hdr, f->m);
+  int rc = put_bytes(out, hdr, hl);
+  if (rc) return rc;
+  return cb_filter_export_bools(f, out + hl, nullptr);
 }
 
 int cb_filter_from_bytes(const uint8_t* in, uint64_t len, int device, cb_filter** out) {
@@ -897,6 +1044,118 @@ int cb_filter_from_bytes(const uint8_t* in, uint64_t len, int device, cb_filter*
   return CB_OK;
 }
 
+
+// ---- TableMeta, the SSTable `.meta` file (src/sstable.rs:31-37) ----
+
+int cb_meta_encode(const cb_filter* bloom, const cb_zone_bounds* zone, uint8_t* out, uint64_t cap,
+                   uint64_t* len_out) {
+  if (!len_out) return fail(CB_EINVAL, "null len_out");
+  if (zone && ((zone->has_min && zone->min_len && !zone->min) ||
+               (zone->has_max && zone->max_len && !zone->max)))
+    return fail(CB_EINVAL, "null zone bound");
+  if (zone && ((zone->has_min && !utf8_ok(zone->min, zone->min_len)) ||
+               (zone->has_max && !utf8_ok(zone->max, zone->max_len))))
+    return fail(CB_EINVAL, "zone bound is not UTF-8 (ZoneMapProto strings are Rust Strings)");
+  const uint64_t bl = bloom && bloom->m ? 1 + varint_len(bloom->m) + bloom->m : 0;
+  uint64_t zl = 0, total = 0;
+  if (bloom) total += 1 + varint_len(bl) + bl;
+  if (zone) {
+    if (zone->has_min) zl += 1 + varint_len(zone->min_len) + zone->min_len;
+    if (zone->has_max) zl += 1 + varint_len(zone->max_len) + zone->max_len;
+    total += 1 + varint_len(zl) + zl;
+  }
+  *len_out = total;
+  if (!out || cap < total) return CB_OK;
+  // [0x0A len(bloom) [0x0A varint(m) m x 0/1]] [0x12 len(zone) [0x0A min] [0x12 max]]
+  uint8_t hdr[32];
+  uint64_t pos = 0;
+  int rc;
+  if (bloom) {
+    size_t h = 0;
+    hdr[h++] = 0x0A;
+    h += put_varint_buf(hdr + h, bl);
+    if (bloom->m) h += put_bloom_header(hdr + h, bloom->m);
+    if ((rc = put_bytes(out, hdr, h))) return rc;
+    pos = h;
+    if (bloom->m) {
+      if ((rc = cb_filter_export_bools(bloom, out + pos, nullptr))) return rc;
+      pos += bloom->m;
+    }
+  }
+  if (zone) {
+    std::vector<uint8_t> z;
+    z.reserve(zl + 11);
+    uint8_t v[11];
+    z.push_back(0x12);
+    z.insert(z.end(), v, v + put_varint_buf(v, zl));
+    if (zone->has_min) {
+      z.push_back(0x0A);
+      z.insert(z.end(), v, v + put_varint_buf(v, zone->min_len));
+      z.insert(z.end(), zone->min, zone->min + zone->min_len);
+    }
+    if (zone->has_max) {
+      z.push_back(0x12);
+      z.insert(z.end(), v, v + put_varint_buf(v, zone->max_len));
+      z.insert(z.end(), zone->max, zone->max + zone->max_len);
+    }
+    if ((rc = put_bytes(out + pos, z.data(), z.size()))) return rc;
+  }
+  return CB_OK;
+}
+
+int cb_meta_decode(const uint8_t* in, uint64_t len, int device, cb_filter** bloom_out,
+                   cb_meta_info* info) {
+  if (!bloom_out || !info || (!in && len)) return fail(CB_EINVAL, "null argument");
+  *bloom_out = nullptr;
+  memset(info, 0, sizeof(*info));
+  MetaScan ms;
+  int rc = scan_meta(in, len, ms);
+  if (rc) return rc;
+  cb_filter* f = nullptr;
+  if (ms.bloom.empty()) {
+    // SsTable::load: meta.bloom.map(from_proto).unwrap_or_else(|| BloomFilter::new(1024))
+    rc = cb_filter_create(1024, device, &f);
+  } else if (ms.bloom.size() == 1) {
+    rc = cb_filter_from_bytes(ms.bloom[0].first, ms.bloom[0].second, device, &f);
+  } else {
+    std::vector<uint8_t> cat;
+    for (auto& sp : ms.bloom) cat.insert(cat.end(), sp.first, sp.first + sp.second);
+    rc = cb_filter_from_bytes(cat.data(), cat.size(), device, &f);
+  }
+  if (rc) return rc == CB_EDECODE ? fail(CB_EDECODE, (std::string("TableMeta decode: ") + g_err).c_str()) : rc;
+  *bloom_out = f;
+  info->has_bloom = !ms.bloom.empty();
+  info->has_zone = ms.has_zone;
+  info->zone.min = ms.min;
+  info->zone.min_len = ms.min_len;
+  info->zone.has_min = ms.has_min;
+  info->zone.max = ms.max;
+  info->zone.max_len = ms.max_len;
+  info->zone.has_max = ms.has_max;
+  return CB_OK;
+}
+
+int cb_set_load_meta(cb_filterset* set, uint32_t slot, const uint8_t* in, uint64_t len, void* stream) {
+  if (!set) return fail(CB_EINVAL, "null set");
+  if (slot >= set->width) return fail(CB_EINVAL, "slot out of range");
+  cb_filter* f = nullptr;
+  cb_meta_info info;
+  int rc = cb_meta_decode(in, len, set->device, &f, &info);
+  if (rc) return rc;
+  if (f->m != set->m) {
+    cb_filter_destroy(f);
+    return fail(CB_EINVAL, "the table's filter size differs from the set's m");
+  }
+  rc = cb_set_assign(set, slot, f, stream);
+  if (!rc) {
+    const cb_zone_bounds& z = info.zone;
+    rc = cb_set_zone(set, slot, z.min, z.min_len, z.has_min, z.max, z.max_len, z.has_max, stream);
+  }
+  // the assign is stream-ordered: wait before the temporary filter goes away
+  if (!rc) rc = cb_stream_synchronize(stream);
+  cb_filter_destroy(f);
+  return rc;
+}
 
 // ---- bit-sliced filter sets ----
 

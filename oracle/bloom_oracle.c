@@ -394,6 +394,150 @@ int ob_probe_gated_var(const ob_filter* const* fs, const ob_zone* const* zones, 
   return OB_OK;
 }
 
+/* ---- TableMeta codec (src/sstable.rs:31-37,74-81,96-108) ---- */
+
+int ob_utf8_valid(const uint8_t* p, uint64_t n) {
+  /* Unicode 3.9 well-formed byte sequences (what Rust's from_utf8 accepts):
+   * no overlongs, no surrogates D800-DFFF, nothing above U+10FFFF. */
+  uint64_t i = 0;
+  while (i < n) {
+    uint8_t c = p[i];
+    if (c < 0x80) {
+      ++i;
+      continue;
+    }
+    int len;
+    uint8_t lo = 0x80, hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF) len = 2;
+    else if (c == 0xE0) { len = 3; lo = 0xA0; }
+    else if ((c >= 0xE1 && c <= 0xEC) || c == 0xEE || c == 0xEF) len = 3;
+    else if (c == 0xED) { len = 3; hi = 0x9F; }
+    else if (c == 0xF0) { len = 4; lo = 0x90; }
+    else if (c >= 0xF1 && c <= 0xF3) len = 4;
+    else if (c == 0xF4) { len = 4; hi = 0x8F; }
+    else return 0;
+    if (n - i < (uint64_t)len) return 0;
+    if (p[i + 1] < lo || p[i + 1] > hi) return 0;
+    for (int k = 2; k < len; ++k)
+      if (p[i + k] < 0x80 || p[i + k] > 0xBF) return 0;
+    i += (uint64_t)len;
+  }
+  return 1;
+}
+
+static uint64_t str_field_len(uint64_t l) { return 1 + varint_len(l) + l; }
+
+uint64_t ob_meta_encode(const ob_filter* bloom, const ob_zone* zone, uint8_t* out, uint64_t cap) {
+  uint64_t bl = 0, zl = 0, total = 0;
+  if (bloom) {
+    bl = ob_encode(bloom, NULL, 0);
+    total += 1 + varint_len(bl) + bl;
+  }
+  if (zone) {
+    if (zone->has_min) zl += str_field_len(zone->min_len);
+    if (zone->has_max) zl += str_field_len(zone->max_len);
+    total += 1 + varint_len(zl) + zl;
+  }
+  if (!out || cap < total) return total;
+  uint8_t* p = out;
+  if (bloom) {
+    *p++ = 0x0A; /* field 1 (bloom), length-delimited */
+    p = put_varint(p, bl);
+    p += ob_encode(bloom, p, bl);
+  }
+  if (zone) {
+    *p++ = 0x12; /* field 2 (zone_map), length-delimited */
+    p = put_varint(p, zl);
+    if (zone->has_min) {
+      *p++ = 0x0A;
+      p = put_varint(p, zone->min_len);
+      if (zone->min_len) memcpy(p, zone->min, (size_t)zone->min_len);
+      p += zone->min_len;
+    }
+    if (zone->has_max) {
+      *p++ = 0x12;
+      p = put_varint(p, zone->max_len);
+      if (zone->max_len) memcpy(p, zone->max, (size_t)zone->max_len);
+      p += zone->max_len;
+    }
+  }
+  return total;
+}
+
+void ob_meta_free(ob_meta* m) {
+  ob_free(&m->bloom);
+  ob_zone_free(&m->zone);
+  m->has_bloom = m->has_zone = 0;
+}
+
+/* ZoneMapProto::merge: each present string replaces the current value. */
+static int merge_zone(const uint8_t* p, const uint8_t* end, ob_zone* z) {
+  while (p < end) {
+    uint64_t key, l;
+    if (get_varint(&p, end, &key) || key > 0xFFFFFFFFull) return OB_EDECODE;
+    uint32_t wt = (uint32_t)(key & 7);
+    uint64_t fn = key >> 3;
+    if (fn == 0) return OB_EDECODE;
+    if (fn == 1 || fn == 2) {
+      if (wt != 2) return OB_EDECODE;
+      if (get_varint(&p, end, &l) || l > (uint64_t)(end - p)) return OB_EDECODE;
+      if (!ob_utf8_valid(p, l)) return OB_EDECODE;
+      if (fn == 1) {
+        if (copy_bytes(&z->min, &z->min_len, p, l)) return OB_ENOMEM;
+        z->has_min = 1;
+      } else {
+        if (copy_bytes(&z->max, &z->max_len, p, l)) return OB_ENOMEM;
+        z->has_max = 1;
+      }
+      p += l;
+    } else if (skip_field(&p, end, wt, fn, 0)) {
+      return OB_EDECODE;
+    }
+  }
+  return OB_OK;
+}
+
+int ob_meta_decode(const uint8_t* in, uint64_t len, ob_meta* out) {
+  const uint8_t* p = in;
+  const uint8_t* end = in + len;
+  int rc = OB_OK;
+  memset(out, 0, sizeof(*out));
+  while (p < end) {
+    uint64_t key, l;
+    if (get_varint(&p, end, &key) || key > 0xFFFFFFFFull) { rc = OB_EDECODE; break; }
+    uint32_t wt = (uint32_t)(key & 7);
+    uint64_t fn = key >> 3;
+    if (fn == 0) { rc = OB_EDECODE; break; }
+    if (fn == 1 || fn == 2) {
+      if (wt != 2) { rc = OB_EDECODE; break; }
+      if (get_varint(&p, end, &l) || l > (uint64_t)(end - p)) { rc = OB_EDECODE; break; }
+      if (fn == 1) {
+        /* BloomProto::merge: the repeated bits of this occurrence append */
+        ob_filter part = {NULL, 0};
+        if ((rc = ob_decode(p, l, &part))) break;
+        if (part.m) {
+          uint8_t* nb = (uint8_t*)realloc(out->bloom.bits, (size_t)(out->bloom.m + part.m));
+          if (!nb) { ob_free(&part); rc = OB_ENOMEM; break; }
+          memcpy(nb + out->bloom.m, part.bits, (size_t)part.m);
+          out->bloom.bits = nb;
+          out->bloom.m += part.m;
+        }
+        ob_free(&part);
+        out->has_bloom = 1;
+      } else {
+        if ((rc = merge_zone(p, p + l, &out->zone))) break;
+        out->has_zone = 1;
+      }
+      p += l;
+    } else if (skip_field(&p, end, wt, fn, 0)) {
+      rc = OB_EDECODE;
+      break;
+    }
+  }
+  if (rc) ob_meta_free(out);
+  return rc;
+}
+
 /* ---- synthetic workload ---- */
 
 uint64_t ob_splitmix64(uint64_t x) {

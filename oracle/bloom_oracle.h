@@ -99,6 +99,28 @@ int ob_bytes_cmp(const uint8_t* a, uint64_t alen, const uint8_t* b, uint64_t ble
 int ob_probe_gated_var(const ob_filter* const* fs, const ob_zone* const* zones, uint32_t nf,
                        const uint8_t* bytes, const uint64_t* offsets, uint64_t n, uint64_t* hits);
 
+/* TableMeta { optional BloomProto bloom = 1; optional ZoneMapProto zone_map = 2; }
+ * (src/sstable.rs:31-37), the `.meta` file of an SSTable, and ZoneMapProto
+ * { optional string min = 1; optional string max = 2; } (zonemap.rs:11-17).
+ * encode (src/sstable.rs:74-81): prost writes a present optional field even
+ * when empty; bloom/zone NULL = field absent, a zone bound with has_* = 0 is
+ * absent. Returns the encoded length; writes only if cap is large enough.
+ * decode (src/sstable.rs:96-108): prost merge semantics — fields in any
+ * order, a repeated singular message field merges (BloomProto bits append,
+ * ZoneMapProto strings: last wins), unknown fields skipped, strings must be
+ * UTF-8. OB_EDECODE on anything malformed (the reference then rebuilds the
+ * table's metadata from the data file, src/sstable.rs:109-120). */
+typedef struct ob_meta {
+  int has_bloom; /* 0: load() uses BloomFilter::new(1024) */
+  ob_filter bloom;
+  int has_zone; /* 0: load() uses ZoneMap::default() */
+  ob_zone zone;
+} ob_meta;
+uint64_t ob_meta_encode(const ob_filter* bloom, const ob_zone* zone, uint8_t* out, uint64_t cap);
+int ob_meta_decode(const uint8_t* in, uint64_t len, ob_meta* out);
+void ob_meta_free(ob_meta* m);
+int ob_utf8_valid(const uint8_t* p, uint64_t n); /* Rust str::from_utf8 acceptance */
+
 /* Synthetic workload keys: 16 lowercase hex chars, MSB
  * nibble first, of splitmix64(seed * 2^32 + i). out is n*16 bytes. */
 void ob_gen_keys(uint64_t seed, uint64_t first, uint64_t n, uint8_t* out);

@@ -35,6 +35,10 @@ class _Zone(ctypes.Structure):
                 ("max", ctypes.POINTER(ctypes.c_uint8)), ("max_len", ctypes.c_uint64), ("has_max", ctypes.c_int)]
 
 
+class _Meta(ctypes.Structure):
+    _fields_ = [("has_bloom", ctypes.c_int), ("bloom", _Filter), ("has_zone", ctypes.c_int), ("zone", _Zone)]
+
+
 def build() -> str:
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
@@ -72,6 +76,13 @@ def lib():
         L.ob_zone_update.argtypes = [ZP, P, u64]
         L.ob_zone_contains.argtypes = [ZP, P, u64]
         L.ob_probe_gated_var.argtypes = [P, P, u32, P, P, u64, P]
+        MP = ctypes.POINTER(_Meta)
+        L.ob_meta_encode.argtypes = [FP, ZP, P, u64]
+        L.ob_meta_encode.restype = u64
+        L.ob_meta_decode.argtypes = [P, u64, MP]
+        L.ob_meta_free.argtypes = [MP]
+        L.ob_meta_free.restype = None
+        L.ob_utf8_valid.argtypes = [P, u64]
         L.ob_gen_keys.argtypes = [u64, u64, u64, P]
         L.ob_gen_keys.restype = None
         L.ob_splitmix64.argtypes = [u64]
@@ -238,6 +249,45 @@ def probe_gated(filters, zones, data: np.ndarray, offsets: np.ndarray) -> np.nda
     if rc:
         raise RuntimeError(f"ob_probe_gated_var rc={rc}")
     return hits
+
+
+def meta_encode(bloom: "OracleFilter | None", zone: "OracleZone | None") -> bytes:
+    """TableMeta{bloom, zone_map}.encode (src/sstable.rs:74-81)."""
+    L = lib()
+    fp = ctypes.byref(bloom._f) if bloom is not None else None
+    zp = ctypes.byref(zone._z) if zone is not None else None
+    n = L.ob_meta_encode(fp, zp, None, 0)
+    out = np.zeros(max(n, 1), np.uint8)
+    L.ob_meta_encode(fp, zp, _ptr(out), n)
+    return out[:n].tobytes()
+
+
+def meta_decode(data: bytes):
+    """TableMeta::decode (src/sstable.rs:97). Returns (bloom bools | None,
+    (min, max) | None); raises ValueError on a decode error."""
+    m = _Meta()
+    buf = np.frombuffer(data, np.uint8).copy() if data else np.zeros(1, np.uint8)
+    rc = lib().ob_meta_decode(_ptr(buf), len(data), ctypes.byref(m))
+    if rc:
+        raise ValueError(f"TableMeta decode error rc={rc}")
+    try:
+        bloom = None
+        if m.has_bloom:
+            bloom = (np.ctypeslib.as_array(m.bloom.bits, shape=(m.bloom.m,)).copy() if m.bloom.m
+                     else np.zeros(0, np.uint8))
+        zone = None
+        if m.has_zone:
+            z = m.zone
+            zone = (bytes(z.min[: z.min_len]) if z.has_min else None,
+                    bytes(z.max[: z.max_len]) if z.has_max else None)
+        return bloom, zone
+    finally:
+        lib().ob_meta_free(ctypes.byref(m))
+
+
+def utf8_valid(b: bytes) -> bool:
+    buf = np.frombuffer(b, np.uint8).copy() if b else np.zeros(1, np.uint8)
+    return bool(lib().ob_utf8_valid(_ptr(buf), len(b)))
 
 
 def gen_keys(seed: int, n: int, first: int = 0) -> np.ndarray:

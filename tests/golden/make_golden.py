@@ -282,9 +282,211 @@ def main() -> None:
                  "hits_popcount": int(sum(np.unpackbits(r.view(np.uint8)).sum() for r in ungated)),
                  "gated_popcount": int(sum(np.unpackbits(r.view(np.uint8)).sum() for r in gated))}
 
+    # 8. TableMeta `.meta` codec (src/sstable.rs:31-37,74-81,96-108; zonemap.rs:11-17)
+    g["meta"] = meta_fixtures(build_py)
+
     with open(os.path.join(HERE, "golden.json"), "w") as fh:
         json.dump(g, fh, indent=1, sort_keys=True)
     print("wrote", os.path.join(HERE, "golden.json"))
+
+
+# ---- TableMeta: independent pure-Python prost restatement --------------------------
+
+def _ld(field: int, payload: bytes) -> bytes:
+    return _varint(field << 3 | 2) + _varint(len(payload)) + payload
+
+
+def meta_encode_py(bits: bytes | None, zone) -> bytes:
+    """prost: a present optional message/string is written even when empty;
+    BloomProto's repeated bool is packed and omitted when empty."""
+    out = b""
+    if bits is not None:
+        out += _ld(1, _ld(1, bits) if bits else b"")
+    if zone is not None:
+        z = b""
+        if zone[0] is not None:
+            z += _ld(1, zone[0])
+        if zone[1] is not None:
+            z += _ld(2, zone[1])
+        out += _ld(2, z)
+    return out
+
+
+class _Bad(Exception):
+    pass
+
+
+def _rd_varint(b: bytes, i: int) -> tuple[int, int]:
+    v = 0
+    for k in range(10):
+        if i >= len(b):
+            raise _Bad("eof")
+        c = b[i]
+        i += 1
+        if k == 9 and c > 1:
+            raise _Bad("varint overflow")
+        v |= (c & 0x7F) << (7 * k)
+        if not c & 0x80:
+            return v, i
+    raise _Bad("varint too long")
+
+
+def _fields(b: bytes):
+    """(field, wire_type, value) triples of one message level; fixed-width and
+    group fields are validated and skipped (value None)."""
+    i = 0
+    while i < len(b):
+        key, j = _rd_varint(b, i)
+        if key > 0xFFFFFFFF:
+            raise _Bad("key")
+        f, wt = key >> 3, key & 7
+        if f == 0:
+            raise _Bad("tag 0")
+        if wt == 0:
+            v, i = _rd_varint(b, j)
+        elif wt == 2:
+            n, j = _rd_varint(b, j)
+            if n > len(b) - j:
+                raise _Bad("eof")
+            v, i = b[j:j + n], j + n
+        elif wt in (1, 3, 5):
+            v, i = None, _skip_one(b, i, 0)
+        else:
+            raise _Bad("wire type")  # 4 (stray end-group), 6, 7
+        yield f, wt, v
+
+
+def _skip_one(b: bytes, i: int, depth: int) -> int:
+    key, j = _rd_varint(b, i)
+    if key > 0xFFFFFFFF:
+        raise _Bad("key")
+    f, wt = key >> 3, key & 7
+    if f == 0:
+        raise _Bad("tag 0")
+    if wt == 0:
+        return _rd_varint(b, j)[1]
+    if wt == 1:
+        if len(b) - j < 8:
+            raise _Bad("eof")
+        return j + 8
+    if wt == 5:
+        if len(b) - j < 4:
+            raise _Bad("eof")
+        return j + 4
+    if wt == 2:
+        n, j = _rd_varint(b, j)
+        if n > len(b) - j:
+            raise _Bad("eof")
+        return j + n
+    if wt == 3:
+        if depth > 100:
+            raise _Bad("recursion")
+        while True:
+            k2, jj = _rd_varint(b, j)
+            if k2 & 7 == 4:
+                if k2 >> 3 != f:
+                    raise _Bad("group mismatch")
+                return jj
+            j = _skip_one(b, j, depth + 1)
+    raise _Bad("wire type")
+
+
+def _bloom_bits(payload: bytes) -> list[int]:
+    bits = []
+    for f, wt, v in _fields(payload):
+        if f == 1:
+            if wt == 2:
+                j = 0
+                while j < len(v):
+                    x, j = _rd_varint(v, j)
+                    bits.append(int(x != 0))
+            elif wt == 0:
+                bits.append(int(v != 0))
+            else:
+                raise _Bad("bits wire type")
+    return bits
+
+
+def meta_decode_py(b: bytes):
+    """-> None on a decode error, else {has_bloom, m, set_bits, has_zone, min, max}."""
+    try:
+        bits, has_bloom, zone = [], False, None
+        for f, wt, v in _fields(b):
+            if f in (1, 2) and wt != 2:
+                raise _Bad("wire type")
+            if f == 1:
+                has_bloom = True
+                bits += _bloom_bits(v)  # merge: repeated bits append
+            elif f == 2:
+                zone = zone or [None, None]
+                for zf, zwt, zv in _fields(v):
+                    if zf in (1, 2):
+                        if zwt != 2:
+                            raise _Bad("wire type")
+                        zv.decode("utf-8")  # prost: string must be UTF-8
+                        zone[zf - 1] = zv  # last wins
+    except (_Bad, UnicodeDecodeError):
+        return None
+    return {"has_bloom": has_bloom, "m": len(bits), "set_bits": [i for i, x in enumerate(bits) if x],
+            "has_zone": zone is not None,
+            "min_hex": zone[0].hex() if zone and zone[0] is not None else None,
+            "max_hex": zone[1].hex() if zone and zone[1] is not None else None}
+
+
+def meta_fixtures(build_py) -> dict:
+    enc = {}
+    for name, keys in [("sstable_local_test", [b"k"]), ("sstable_test", [b"a", b"b", b"c"]),
+                       ("lsm_flush_test", [b"k1", b"k2"]), ("empty_table", [])]:
+        bits = build_py(keys, 1024)  # SsTable::create: BloomFilter::new(1024)
+        zone = (min(keys), max(keys)) if keys else (None, None)
+        b = meta_encode_py(bits, zone)
+        d = meta_decode_py(b)
+        assert d["m"] == 1024 and d["set_bits"] == [i for i, v in enumerate(bits) if v]
+        enc[name] = {"keys_hex": [k.hex() for k in keys], "len": len(b), "sha256": hashlib.sha256(b).hexdigest(),
+                     "head_hex": b[:8].hex(), "tail_hex": b[-16:].hex()}
+    assert enc["empty_table"]["tail_hex"].endswith("1200")  # zone_map: Some(ZoneMapProto{None, None})
+
+    z_az = _ld(1, b"a") + _ld(2, b"z")
+    bl3 = _ld(1, bytes([1, 0, 1]))
+    cases = {
+        "zone_then_bloom": _ld(2, z_az) + _ld(1, bl3),
+        "bloom_split": _ld(1, bl3) + _ld(1, _ld(1, bytes([0, 1]))),
+        "bloom_unpacked": _ld(1, bytes([0x08, 0x01, 0x08, 0x00, 0x08, 0x02])),
+        "bloom_packed_multibyte_varint": _ld(1, _ld(1, bytes([0x80, 0x01, 0x00, 0x01]))),
+        "zone_last_wins": _ld(2, z_az) + _ld(2, _ld(1, b"b")),
+        "zone_empty_min": _ld(2, _ld(1, b"")),
+        "zone_utf8": _ld(2, _ld(1, "é".encode()) + _ld(2, "✓".encode())),
+        "unknown_fields": (_varint(3 << 3 | 0) + _varint(300) + _varint(4 << 3 | 1) + bytes(8) +
+                           _ld(5, b"xyz") + _varint(6 << 3 | 5) + bytes(4) +
+                           _varint(7 << 3 | 3) + _varint(1 << 3 | 0) + b"\x01" + _varint(7 << 3 | 4) + bl3[:0] +
+                           _ld(1, bl3)),
+        "empty": b"",
+        "empty_bloom": _ld(1, b""),
+        "err_bloom_wire_type": _varint(1 << 3 | 0) + b"\x01",
+        "err_zone_wire_type": _ld(2, _varint(1 << 3 | 0) + b"\x01"),
+        "err_min_not_utf8": _ld(2, _ld(1, b"\xff")),
+        "err_surrogate": _ld(2, _ld(2, b"\xed\xa0\x80")),
+        "err_overlong": _ld(2, _ld(1, b"\xc0\x80")),
+        "err_truncated": _ld(1, bl3)[:-1],
+        "err_tag0": b"\x02\x00",
+        "err_bloom_inner": _ld(1, b"\x0a\x02\x80"),
+        "err_stray_end_group": _varint(9 << 3 | 4),
+        "err_varint_overflow": b"\x0a" + b"\xff" * 9 + b"\x02",
+        "err_wire_type_7": _varint(3 << 3 | 7),
+    }
+    dec = {}
+    for name, b in cases.items():
+        d = meta_decode_py(b)
+        assert (d is None) == name.startswith("err_"), name
+        dec[name] = {"hex": b.hex(), "expect": d}
+    assert dec["bloom_split"]["expect"]["set_bits"] == [0, 2, 4] and dec["bloom_split"]["expect"]["m"] == 5
+    assert dec["bloom_unpacked"]["expect"]["set_bits"] == [0, 2] and dec["bloom_unpacked"]["expect"]["m"] == 3
+    assert dec["zone_last_wins"]["expect"]["min_hex"] == b"b".hex()
+    assert dec["zone_last_wins"]["expect"]["max_hex"] == b"z".hex()
+    assert dec["empty"]["expect"] == {"has_bloom": False, "m": 0, "set_bits": [], "has_zone": False,
+                                      "min_hex": None, "max_hex": None}
+    assert dec["unknown_fields"]["expect"]["set_bits"] == [0, 2]
+    return {"encode": enc, "decode": dec}
 
 
 def _varint(v: int) -> bytes:

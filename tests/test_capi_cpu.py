@@ -3,6 +3,8 @@ public header declares. No compute calls are made here."""
 import ctypes
 import subprocess
 
+import numpy as np
+
 from lsmt_amd import _lib
 
 
@@ -41,3 +43,46 @@ def test_null_argument_errors_without_gpu():
     assert b"null" in L.cb_last_error()
     n = ctypes.c_uint64()
     assert L.cb_filter_to_bytes(None, None, 0, ctypes.byref(n)) == _lib.CB_EINVAL
+
+
+def _zone_encode(L, lo, hi):
+    from lsmt_amd import _lib
+    lb = ctypes.create_string_buffer(lo or b"", max(len(lo or b""), 1))
+    hb = ctypes.create_string_buffer(hi or b"", max(len(hi or b""), 1))
+    zb = _lib.ZoneBounds(ctypes.cast(lb, ctypes.c_void_p), len(lo or b""), lo is not None,
+                         ctypes.cast(hb, ctypes.c_void_p), len(hi or b""), hi is not None)
+    n = ctypes.c_uint64()
+    rc = L.cb_meta_encode(None, ctypes.byref(zb), None, 0, ctypes.byref(n))
+    if rc:
+        return rc, None
+    out = ctypes.create_string_buffer(max(n.value, 1))
+    rc = L.cb_meta_encode(None, ctypes.byref(zb), out, n.value, ctypes.byref(n))
+    return rc, out.raw[: n.value]
+
+
+def test_meta_zone_only_encode_matches_oracle():
+    # host-only framing of TableMeta{zone_map} (no filter: no device work)
+    from lsmt_amd import _lib
+    from oracle import oracle
+    L = _lib.load()
+    for lo, hi in [(b"k", b"k"), (None, None), (b"", None), (None, b"z"), ("é".encode(), "✓".encode()),
+                   (b"a" * 200, b"b" * 300)]:
+        rc, got = _zone_encode(L, lo, hi)
+        assert rc == 0
+        assert got == oracle.meta_encode(None, oracle.OracleZone(lo, hi)), (lo, hi)
+
+
+def test_meta_encode_rejects_non_utf8_like_rust_strings():
+    from lsmt_amd import _lib
+    L = _lib.load()
+    rng = np.random.default_rng(9)
+    samples = [b"\xff", b"\xc0\x80", b"\xed\xa0\x80", b"\xf4\x90\x80\x80", b"\xe2\x9c", "ok✓".encode()]
+    samples += [rng.integers(0x70, 0x100, rng.integers(1, 6), dtype=np.uint8).tobytes() for _ in range(500)]
+    for s in samples:
+        try:
+            s.decode("utf-8")
+            ok = True
+        except UnicodeDecodeError:
+            ok = False
+        rc, _ = _zone_encode(L, s, b"z")
+        assert (rc == 0) == ok, s
