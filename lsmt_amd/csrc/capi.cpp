@@ -67,6 +67,8 @@ int g_path_override = 0;  // 0 auto, 1 direct, 2 tiled
 
 constexpr int PATH_DIRECT = 1, PATH_TILED = 2;
 constexpr size_t cb_zone_hdr_bytes = 64 * 16;  // cb::ZoneView headers
+constexpr size_t cb_zone_pre_bytes = 64 * 2 * sizeof(cb::BoundPrefix);  // then the prefixes
+constexpr size_t cb_zone_blob_off = cb_zone_hdr_bytes + cb_zone_pre_bytes;
 
 int fail(int code, const char* what) {
   g_err = what;
@@ -413,7 +415,8 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
     dhits = (uint64_t*)ws.hits.p;
   }
   const cb::ZoneView zv{(const uint32_t*)set->zdev,
-                       (const uint8_t*)set->zdev + cb_zone_hdr_bytes, set->zgated};
+                       (const cb::BoundPrefix*)((const uint8_t*)set->zdev + cb_zone_hdr_bytes),
+                       (const uint8_t*)set->zdev + cb_zone_blob_off, set->zgated};
   HIP_TRY(cb::launch_set_probe(sk.keyk, set->mode, set->width, set->words, set->any, set->used,
                                sk.ks, n, set->mp, (gated && set->zgated) ? &zv : nullptr, dhits,
                                hwords, s));
@@ -445,9 +448,23 @@ int upload_zones(cb_filterset* set, hipStream_t s) {
     blob.insert(blob.end(), set->zhi[i].begin(), set->zhi[i].end());
   }
   static_assert(sizeof(hdr) == cb_zone_hdr_bytes, "ZoneView header size");
-  std::vector<uint8_t> tab(cb_zone_hdr_bytes + blob.size());
+  // big-endian 16-byte prefixes of every bound (cb::cmp16's operands)
+  cb::BoundPrefix pre[64 * 2] = {};
+  for (uint32_t i = 0; i < set->width; ++i) {
+    if (!((set->zgated >> i) & 1)) continue;
+    for (int j = 0; j < 2; ++j) {
+      const std::string& b = j ? set->zhi[i] : set->zlo[i];
+      cb::BoundPrefix& p = pre[2 * i + j];
+      for (size_t k = 0; k < b.size() && k < 16; ++k)
+        p.w[k >> 2] |= (uint32_t)(uint8_t)b[k] << (24 - 8 * (k & 3));
+      p.len = (uint32_t)b.size();
+    }
+  }
+  static_assert(sizeof(pre) == cb_zone_pre_bytes, "ZoneView prefix size");
+  std::vector<uint8_t> tab(cb_zone_blob_off + blob.size());
   memcpy(tab.data(), hdr, cb_zone_hdr_bytes);
-  if (!blob.empty()) memcpy(tab.data() + cb_zone_hdr_bytes, blob.data(), blob.size());
+  memcpy(tab.data() + cb_zone_hdr_bytes, pre, cb_zone_pre_bytes);
+  if (!blob.empty()) memcpy(tab.data() + cb_zone_blob_off, blob.data(), blob.size());
   if (!set->zgated) return CB_OK;
   if (tab.size() > set->zcap) {
     HIP_TRY(hipStreamSynchronize(s));

@@ -197,7 +197,15 @@ __global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __re
   const uint64_t k = (wbase + wave) * 64 + lane;
   bool ok = k < n;
   uint64_t pa = 0, pb = 0;
-  if (ok) key_positions<KEYK, MODE>(ks, k, mp, pa, pb);
+  uint4 kv = make_uint4(0, 0, 0, 0);  // KEY_FIXED16: the key, kept for the zone gate
+  if (ok) {
+    if constexpr (KEYK == KEY_FIXED16) {
+      kv = reinterpret_cast<const uint4*>(ks.bytes)[k];
+      key_positions_u4<MODE>(kv, mp, pa, pb);
+    } else {
+      key_positions<KEYK, MODE>(ks, k, mp, pa, pb);
+    }
+  }
   // Union pre-test: any[p] = (set[p] != 0) is the Bloom filter of every
   // slot's keys (m bits, L2/MALL-resident). A key whose a or b bit is clear
   // there is absent from every slot and skips both set reads.
@@ -214,9 +222,22 @@ __global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __re
   else
     vb = va ? sp[pb] : (word_t)0;
   word_t mask = va & vb;
-  if (zv.gated) {
+  if (zv.gated) {  // uniform: only gated launches pay for the zone check
     word_t c = mask & (word_t)zv.gated;
-    if (c) {
+    if constexpr (KEYK == KEY_FIXED16) {
+      // 16-byte keys: the key (still in registers from the hash) compared as
+      // 4 big-endian words against the bounds' host-computed prefixes (two
+      // 32-B loads per bound from a 4-KB L2-resident table).
+      if (c) {
+        const uint32_t kw[4] = {be32(kv.x), be32(kv.y), be32(kv.z), be32(kv.w)};
+        while (c) {
+          const uint32_t s = (uint32_t)__builtin_ctzll((uint64_t)c);
+          c &= c - 1;
+          if (cmp16(kw, zv.pre[2 * s]) < 0 || cmp16(kw, zv.pre[2 * s + 1]) > 0)
+            mask &= ~((word_t)1 << s);
+        }
+      }
+    } else if (c) {
       const uint8_t* kp;
       uint64_t kl;
       key_span<KEYK>(ks, k, kp, kl);
@@ -349,7 +370,7 @@ hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
     const char* v = getenv("CB_SET_ANY");
     return v && v[0] == '1';
   }();
-  const ZoneView zv = zones ? *zones : ZoneView{nullptr, nullptr, 0};
+  const ZoneView zv = zones ? *zones : ZoneView{nullptr, nullptr, nullptr, 0};
   const uint64_t nw = (n + 63) / 64;
   const uint32_t grid = (uint32_t)((nw + kSetWords - 1) / kSetWords);
   ProfScope ps(zv.gated ? "k_set_probe_gated" : "k_set_probe", s);

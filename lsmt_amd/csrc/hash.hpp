@@ -117,6 +117,36 @@ __device__ __forceinline__ void key_positions(const KeySrc& ks, uint64_t k, cons
   }
 }
 
+// Positions of a 16-byte key already in registers (KEY_FIXED16 callers that
+// need the key bytes again afterwards, e.g. the zone gate).
+template <int MODE>
+__device__ __forceinline__ void key_positions_u4(const uint4& v, const ModP& mp, uint64_t& a,
+                                                 uint64_t& b) {
+  if constexpr (MODE == MOD_POW2_32) {
+    H32 h;
+    h.word(v.x);
+    h.word(v.y);
+    h.word(v.z);
+    h.word(v.w);
+    const uint32_t mask = static_cast<uint32_t>(mp.mask);
+    a = h.h1 & mask;
+    b = h.h2 & mask;
+  } else {
+    H64 h;
+    h.word(v.x);
+    h.word(v.y);
+    h.word(v.z);
+    h.word(v.w);
+    if constexpr (MODE == MOD_POW2_64) {
+      a = h.h1 & mp.mask;
+      b = h.h2 & mp.mask;
+    } else {
+      a = fastmod(h.h1, mp);
+      b = fastmod(h.h2, mp);
+    }
+  }
+}
+
 inline ModP make_modp(uint64_t m, int* mode) {
   ModP mp{m, 0, 0};
   const bool pow2 = m && !(m & (m - 1));

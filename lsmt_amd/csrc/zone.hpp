@@ -15,12 +15,23 @@
 
 namespace cb {
 
+// A bound's first 16 bytes as 4 big-endian words (zero-padded) + its length:
+// enough to order any 16-byte key against it exactly. 32 B, two loads.
+struct alignas(32) BoundPrefix {
+  uint32_t w[4];
+  uint32_t len;
+  uint32_t pad[3];
+};
+
 // Per-slot bounds of a FilterSet, resident in HBM (a few KB, L2-resident
 // during a probe). hdr[4*s .. 4*s+3] = (lo_off, lo_len, hi_off, hi_len) into
-// blob. `gated` has bit s set iff slot s has both bounds: only those slots
-// can reject a key (a half-open zone map accepts everything).
+// blob; pre[2*s + j] = prefix of slot s's lower (j = 0) / upper (j = 1)
+// bound, precomputed on the host. `gated` has bit s set iff slot s has both
+// bounds: only those slots can reject a key (a half-open zone map accepts
+// everything).
 struct ZoneView {
   const uint32_t* hdr;
+  const BoundPrefix* pre;
   const uint8_t* blob;
   uint64_t gated;
 };
@@ -59,6 +70,26 @@ __device__ __forceinline__ bool zone_contains(const ZoneView& zv, uint32_t s, co
   const uint4 h = reinterpret_cast<const uint4*>(zv.hdr)[s];
   return bytes_cmp(key, len, zv.blob + h.x, h.y) >= 0 &&
          bytes_cmp(key, len, zv.blob + h.z, h.w) <= 0;
+}
+
+// Byte-swap to big-endian so an unsigned word compare is a lexicographic
+// compare of 4 bytes.
+__device__ __forceinline__ uint32_t be32(uint32_t x) { return __builtin_bswap32(x); }
+
+// Rust str order of a 16-byte key (big-endian words kw) against a bound.
+__device__ __forceinline__ int cmp16(const uint32_t kw[4], const BoundPrefix& b) {
+  // b is read field by field from global memory (L1/L2-resident table)
+  const uint32_t n = b.len < 16 ? b.len : 16;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) {
+    if (4 * i >= n) break;
+    const uint32_t nb = n - 4 * i;  // bytes of this word inside the bound
+    const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (8 * nb));
+    const uint32_t x = kw[i] & m, y = b.w[i];
+    if (x != y) return x < y ? -1 : 1;
+  }
+  // the first min(16, len) bytes agree: the shorter string sorts first
+  return b.len > 16 ? -1 : (b.len < 16 ? 1 : 0);
 }
 
 // Lexicographic min / max index of a key batch (the ZoneMap::update loop of

@@ -209,3 +209,42 @@ def test_zone_gate_device_resident(gpu):
     d = np.ascontiguousarray(lk.reshape(-1))
     offs = np.arange(0, 16 * (len(lk) + 1), 16, dtype=np.uint64)
     assert np.array_equal(host, oracle.probe_gated(refs, zs, d, offs))
+
+
+@pytest.mark.parametrize("width", [32, 64])
+def test_zone_gate_fixed16_bound_lengths(gpu, width):
+    # 16-byte keys take the LDS word-compare path: bounds of every length
+    # class (empty, inside one word, word-aligned, 16, longer than the key),
+    # cut from the keys themselves so equal prefixes are common
+    rng = np.random.default_rng(17)
+    alpha = np.frombuffer(b"ab", np.uint8)
+    m = 4099
+    nt = width
+    keys = [alpha[rng.integers(0, 2, (3000, 16))] for _ in range(nt)]
+    filters, refs, zones = [], [], []
+    lens = [0, 1, 3, 4, 5, 8, 11, 15, 16, 17, 20]
+    for f in range(nt):
+        b = gpu.BloomFilter(m)
+        b.insert_batch(keys[f])
+        o = oracle.OracleFilter(m)
+        o.insert_fixed(keys[f])
+        filters.append(b)
+        refs.append(o)
+        r = [bytes(x) for x in keys[f][:2]]
+        lo = r[0][: lens[f % len(lens)]]
+        hi = (r[1] + b"ab")[: lens[(f * 7 + 3) % len(lens)]]
+        if lo > hi:
+            lo, hi = hi, lo
+        zones.append((lo, hi))
+    s = gpu.FilterSet(m, width=width)
+    s.assign_all(filters)
+    for i, z in enumerate(zones):
+        s.set_zone(i, z)
+    look = alpha[rng.integers(0, 2, (50_000, 16))]
+    look[: len(zones)] = [np.frombuffer((z[0] + b"a" * 16)[:16], np.uint8) for z in zones]
+    got = s.probe(look, gated=True)
+    d = np.ascontiguousarray(look.reshape(-1))
+    offs = np.arange(0, 16 * (len(look) + 1), 16, dtype=np.uint64)
+    exp = oracle.probe_gated(refs, [oracle.OracleZone(lo, hi) for lo, hi in zones], d, offs)
+    assert np.array_equal(got, exp)
+    assert int(np.unpackbits(exp.view(np.uint8)).sum()) > 0
