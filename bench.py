@@ -53,7 +53,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU oracle baseline")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--check", action="store_true", help="verify hits against the oracle (slow)")
-    p.add_argument("--no-zone", action="store_true", help="skip the zone-map gate leg")
+    p.add_argument("--no-zone", action="store_true", help="skip the zone-map gate leg (and the read path)")
+    p.add_argument("--no-read", action="store_true", help="skip the SSTable read-path leg")
     p.add_argument("--overlap", action="store_true",
                    help="N>1: run each step's all-gather on a side stream, overlapped with the next "
                         "step's probe (measured slower on one GPU: the streams share one hardware "
@@ -303,6 +304,66 @@ def main():
                 "gated_hits_last_step": gated_hits,
                 "note": "C3 tables hold random keys, so every zone spans ~the whole key space: "
                         "this measures the gate's cost; tests/test_zone_gpu.py covers rejection"}
+
+    # ---- read path: the C3 tables as real SSTable data
+    # files in HBM; one step = gated probe + Database::get's newest-first walk
+    # (binary search of the candidates, base64 decode of the found values)
+    read = None
+    if not args.no_read and not args.no_zone:
+        t0 = time.perf_counter()
+        files = [torch.from_numpy(workload.sstable_bytes(k, workload.table_value(k, f)))
+                 for f, k in ((f, workload.key_range(seed_base + f, kpf)) for f in range(f_lo, f_lo + F))]
+        gen_s = time.perf_counter() - t0
+        dfiles = [f.to(dev) for f in files]
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        tables = [lsmt_amd.Table(f, device=local, stream=sh) for f in dfiles]
+        torch.cuda.synchronize(dev)
+        index_s = time.perf_counter() - t0
+        file_bytes = sum(int(f.numel()) for f in files)
+        del files
+        newest_first = tables[::-1]  # Database::get: tables.iter().rev()
+        rows = np.arange(F)[::-1].copy()
+        which_d = torch.empty(n, dtype=torch.int32, device=dev)
+        voff_d = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        vals_d = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+        hits_r = torch.empty((F, words), dtype=torch.int64, device=dev)
+        got = [0]
+
+        def step_read():
+            fset.probe(keys_batch, out=hits_r, stream=sh, gated=True)
+            got[0] = lsmt_amd.get_many(newest_first, keys_batch, hits=hits_r, hit_rows=rows,
+                                       out=(which_d, voff_d, vals_d), stream=sh)[2]
+
+        for _ in range(args.warmup):
+            step_read()
+        rel = timed(step_read, args.steps)
+        rprof = kernel_ms(["k_set_probe_gated", "k_get_many", "k_scan_u64", "k_b64_decode"], step_read, args.steps)
+        found = int((which_d >= 0).sum().item())
+        read = {"metric": "gets/s: 1M keys through zone+Bloom gate, binary search and base64 decode over "
+                          f"{F} SSTable data files ({kpf} lines each) in HBM",
+                "value": round(n / (rel / args.steps), 1), "unit": "keys/s",
+                "ms_per_step": round(rel / args.steps * 1e3, 4),
+                "kernels_us": {k: round(v["avg_us"], 2) for k, v in rprof.items()},
+                "found": found, "value_bytes": got[0],
+                "files_bytes": file_bytes, "index_build_GBps": round(file_bytes / index_s / 1e9, 2),
+                "file_generation_s": round(gen_s, 2)}
+        if rank == 0 and world == 1 and not args.no_cpu:
+            from oracle import oracle
+            sample = 1 << 15
+            ot = [oracle.OracleTable(workload.sstable_bytes(k, workload.table_value(k, f)))
+                  for f, k in ((f, workload.key_range(seed_base + f, kpf)) for f in range(f_lo, f_lo + F))][::-1]
+            hs = hits_r.cpu().numpy().view(np.uint64)[rows]
+            hs = np.ascontiguousarray(hs[:, : sample // 64])
+            t0 = time.perf_counter()
+            oracle.get_many(ot, hs, np.ascontiguousarray(look_np[:sample].reshape(-1)),
+                            np.arange(0, 16 * (sample + 1), 16, dtype=np.uint64))
+            read["cpu_baseline"] = {"value": round(sample / (time.perf_counter() - t0), 1), "unit": "keys/s",
+                                    "cores": 1, "kind": "port",
+                                    "sample": f"oracle get_many over the first {sample} keys with the same gate bits"}
+            del ot
+        del tables, dfiles
+    if zone is not None:
         fset.assign_all(filters, stream=sh)  # zones reset; the set is unchanged otherwise
 
     # ---- C2 build: 1M keys -> one fresh 16 MiB filter (zero-fill + batched insert)
@@ -385,7 +446,7 @@ def main():
             "alt_kernels_us": {k: round(v["avg_us"], 2) for k, v in kprof_alt.items()},
             "filterset": {"build_all_ms": round(set_build_ms, 3), "assign_one_empty_slot_ms": round(set_assign_ms, 3),
                           "bytes": m * (4 if F <= 32 else 8)},
-            "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e, "zone_gate": zone,
+            "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e, "zone_gate": zone, "read_path": read,
         }
         print(json.dumps(line), file=result, flush=True)
     if use_dist:

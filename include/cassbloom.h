@@ -60,6 +60,7 @@ extern "C" {
 
 typedef struct cb_filter cb_filter;
 typedef struct cb_filterset cb_filterset; /* bit-sliced filter sets, see below */
+typedef struct cb_table cb_table;         /* an SSTable data file in HBM, see below */
 
 /* ---- device / library ---- */
 int cb_init(int device);
@@ -216,6 +217,41 @@ int cb_set_probe_gated_fixed(const cb_filterset* set, const uint8_t* keys, uint3
                              uint64_t n, uint64_t* hits, void* stream);
 int cb_set_probe_gated_var(const cb_filterset* set, const uint8_t* bytes, const uint64_t* offsets,
                            uint64_t n, uint64_t* hits, void* stream);
+
+/* ---- SSTable data files and the batched read path ----
+ * A data file is SsTable::create's output (src/sstable.rs:57-72): lines
+ * `key \t base64(value) \n` sorted by key. cb_table_create uploads one (host
+ * or device bytes) and indexes its lines on the device exactly as SsTable::get
+ * splits them (raw.split('\n') minus empty lines, src/sstable.rs:142-146). */
+int cb_table_create(const uint8_t* data, uint64_t len, int device, void* stream, cb_table** out);
+int cb_table_destroy(cb_table* t);
+int cb_table_info(const cb_table* t, uint64_t* nlines, uint64_t* bytes);
+/* The line index: start offset, key length (bytes before the first TAB, or
+ * UINT32_MAX when the line has none) and line length; host or device out. */
+int cb_table_lines(const cb_table* t, uint64_t* start, uint32_t* key_len, uint32_t* line_len);
+/* SsTable::binary_search (src/sstable.rs:161-179) for a key batch, same
+ * (lo+hi)/2 trajectory: line_out[k] = matching line index or -1. */
+int cb_table_search_fixed(const cb_table* t, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                          int64_t* line_out, void* stream);
+int cb_table_search_var(const cb_table* t, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                        int64_t* line_out, void* stream);
+/* Database::get's table walk (src/lib.rs:128-134) for a key batch.
+ * tables[0] is the NEWEST table. hits (nullable): the per-table gate from a
+ * (gated) probe, [rows][ceil(n/64)] with table t in row hit_rows[t] (hit_rows
+ * NULL = row t); a table is searched for key k only where its bit is set.
+ * which[k] = index of the first table whose SsTable::get returns Ok(Some) —
+ * line found AND value decodes as base64 (base64 0.21.7 STANDARD; an Err
+ * falls through to older tables) — or -1. val_off[n+1] = offsets of the
+ * decoded values; *total = their byte count; the values are written to vals
+ * only if cap >= *total (call with vals = NULL to size). */
+int cb_get_many_fixed(const cb_table* const* tables, uint32_t nt, const uint64_t* hits,
+                      const uint32_t* hit_rows, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                      int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap,
+                      uint64_t* total, void* stream);
+int cb_get_many_var(const cb_table* const* tables, uint32_t nt, const uint64_t* hits,
+                    const uint32_t* hit_rows, const uint8_t* bytes, const uint64_t* offsets,
+                    uint64_t n, int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap,
+                    uint64_t* total, void* stream);
 
 /* ---- tuning / introspection (bench + tests) ---- */
 /* Path selection: 0 = auto, 1 = force direct (per-key atomics / gathers),

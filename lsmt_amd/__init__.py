@@ -20,11 +20,13 @@ from .bloom import (  # noqa: E402
     probe,
     set_path,
     unpack_hits,
+    Table,
     TableMeta,
+    get_many,
     zone_bounds,
     ZoneMap,
 )
 
 __all__ = ["BloomFilter", "BloomProto", "DeviceKeys", "FilterSet", "insert_many", "KeyBatch", "device_count", "last_path",
-           "probe", "set_path", "unpack_hits", "zone_bounds", "ZoneMap", "TableMeta"]
+           "probe", "set_path", "unpack_hits", "zone_bounds", "ZoneMap", "TableMeta", "Table", "get_many"]
 __version__ = "0.1.0"

@@ -114,6 +114,14 @@ def load():
         "cb_meta_encode": ([P, ctypes.POINTER(ZoneBounds), u8p, u64, pu64], i32),
         "cb_meta_decode": ([u8p, u64, i32, pp, ctypes.POINTER(MetaInfo)], i32),
         "cb_set_load_meta": ([P, u32, u8p, u64, P], i32),
+        "cb_table_create": ([u8p, u64, i32, P, pp], i32),
+        "cb_table_destroy": ([P], i32),
+        "cb_table_info": ([P, pu64, pu64], i32),
+        "cb_table_lines": ([P, P, P, P], i32),
+        "cb_table_search_fixed": ([P, u8p, u32, u64, P, P], i32),
+        "cb_table_search_var": ([P, u8p, P, u64, P, P], i32),
+        "cb_get_many_fixed": ([P, u32, P, P, u8p, u32, u64, P, P, P, u64, pu64, P], i32),
+        "cb_get_many_var": ([P, u32, P, P, u8p, P, u64, P, P, P, u64, pu64, P], i32),
         "cb_set_probe_gated_fixed": ([P, u8p, u32, u64, P, P], i32),
         "cb_set_probe_gated_var": ([P, u8p, P, u64, P, P], i32),
         "cb_profile_enable": ([i32], i32),

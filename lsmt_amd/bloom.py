@@ -34,7 +34,7 @@ from . import _lib
 from ._lib import CassBloomError, check
 
 __all__ = ["BloomFilter", "BloomProto", "FilterSet", "probe", "insert_many", "set_path",
-           "last_path", "device_count", "DeviceKeys", "KeyBatch", "ZoneMap", "zone_bounds", "TableMeta"]
+           "last_path", "device_count", "DeviceKeys", "KeyBatch", "ZoneMap", "zone_bounds", "TableMeta", "Table", "get_many"]
 
 
 def _L():
@@ -566,6 +566,122 @@ class FilterSet:
             fn = _L().cb_set_probe_gated_fixed if gated else _L().cb_set_probe_fixed
             _raise(fn(self._h, kp, b.key_len, b.n, op, s))
         return result
+
+
+# ---- SSTable data files and the batched read path (src/sstable.rs:133-179, src/lib.rs:128-134)
+
+class Table:
+    """One SSTable data file (``key \t base64(value) \n`` lines, sorted;
+    src/sstable.rs:57-72) resident in HBM with its line index, built on the
+    device. ``data``: bytes, a uint8 numpy array, or a uint8 device tensor."""
+
+    def __init__(self, data, device: int = 0, stream=None):
+        self._h = ctypes.c_void_p()
+        if isinstance(data, (bytes, bytearray, memoryview)):
+            data = np.frombuffer(bytes(data), np.uint8)
+        n = int(data.numel()) if hasattr(data, "numel") else int(len(data))
+        ptr, keep = _ptr_of(data if n else np.zeros(1, np.uint8))
+        _raise(_L().cb_table_create(ptr, n, int(device), _stream(stream), ctypes.byref(self._h)))
+        self.device = int(device)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            _L().cb_table_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    @property
+    def nlines(self) -> int:
+        n = ctypes.c_uint64()
+        check(_L().cb_table_info(self._h, ctypes.byref(n), None))
+        return int(n.value)
+
+    def lines(self):
+        """(start uint64[n], key_len uint32[n] (0xFFFFFFFF = no TAB), line_len uint32[n])."""
+        n = self.nlines
+        st = np.zeros(max(n, 1), np.uint64)
+        kl = np.zeros(max(n, 1), np.uint32)
+        ll = np.zeros(max(n, 1), np.uint32)
+        check(_L().cb_table_lines(self._h, st.ctypes.data, kl.ctypes.data, ll.ctypes.data))
+        return st[:n], kl[:n], ll[:n]
+
+    def search(self, keys, out=None, stream=None) -> np.ndarray:
+        """SsTable::binary_search per key: int64 line index or -1."""
+        b = as_batch(keys)
+        if out is None:
+            out = np.zeros(max(b.n, 1), np.int64)
+            res = out[: b.n]
+        else:
+            res = out
+        op, keep = _ptr_of(out)
+        s = _stream(stream)
+        if b.is_var:
+            dp, k1 = _ptr_of(b.data)
+            offp, k2 = _ptr_of(b.offsets)
+            _raise(_L().cb_table_search_var(self._h, dp, offp, b.n, op, s))
+        else:
+            kp, k1 = _ptr_of(b.keys)
+            _raise(_L().cb_table_search_fixed(self._h, kp, b.key_len, b.n, op, s))
+        return res
+
+
+def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=None, out=None):
+    """Database::get's newest-first walk for a key batch (tables[0] newest).
+    hits: optional per-table gate bitmaps (e.g. FilterSet.probe(gated=True));
+    table t uses row hit_rows[t] (default t). Returns (which int32[n]: table
+    index or -1, val_off uint64[n+1], vals bytes).
+
+    out=(which, val_off, vals) with preallocated (e.g. device) buffers runs
+    one pass and returns (which, val_off, total); values are written only if
+    vals is large enough for total."""
+    b = as_batch(keys)
+    nt = len(tables)
+    arr = (ctypes.c_void_p * max(nt, 1))(*[t.handle.value for t in tables])
+    hp, hk = _ptr_of(hits) if hits is not None else (None, None)
+    rows = None
+    if hit_rows is not None:
+        rows = np.ascontiguousarray(hit_rows, dtype=np.uint32)
+    rp = rows.ctypes.data if rows is not None else None
+    total = ctypes.c_uint64()
+    s = _stream(stream)
+    L = _L()
+    if out is not None:
+        which, voff, vals = out
+        cap = int(vals.numel()) if hasattr(vals, "numel") else int(vals.nbytes)
+    else:
+        which = np.zeros(max(b.n, 1), np.int32)
+        voff = np.zeros(b.n + 1, np.uint64)
+    wp, k3 = _ptr_of(which)
+    vo, k4 = _ptr_of(voff)
+    if b.is_var:
+        dp, k1 = _ptr_of(b.data)
+        offp, k2 = _ptr_of(b.offsets)
+
+        def call(vp, cap):
+            _raise(L.cb_get_many_var(ctypes.cast(arr, ctypes.c_void_p), nt, hp, rp, dp, offp, b.n,
+                                     wp, vo, vp, cap, ctypes.byref(total), s))
+    else:
+        kp, k1 = _ptr_of(b.keys)
+
+        def call(vp, cap):
+            _raise(L.cb_get_many_fixed(ctypes.cast(arr, ctypes.c_void_p), nt, hp, rp, kp, b.key_len, b.n,
+                                       wp, vo, vp, cap, ctypes.byref(total), s))
+    if out is not None:
+        call(_ptr_of(vals)[0], cap)
+        return which, voff, int(total.value)
+    call(None, 0)
+    vals = np.zeros(max(int(total.value), 1), np.uint8)
+    call(vals.ctypes.data, int(total.value))
+    return which[: b.n], voff, vals[: int(total.value)].tobytes()
 
 
 def unpack_hits(hits: np.ndarray, n: int) -> np.ndarray:

@@ -19,6 +19,7 @@
 #include "cassbloom.h"
 #include "filterset.hpp"
 #include "kernels.hpp"
+#include "sstable.hpp"
 #include "zone.hpp"
 
 using cb::FilterPtrs;
@@ -57,6 +58,17 @@ struct cb_filterset {
   void* zdev = nullptr;
   size_t zcap = 0;
   uint64_t zgated = 0;  // slots with both bounds
+};
+
+// An SSTable data file resident in HBM with its line index (sstable.hpp).
+struct cb_table {
+  int device = 0;
+  uint64_t len = 0, nlines = 0;
+  uint8_t* data = nullptr;
+  uint64_t* start = nullptr;
+  uint32_t* klen = nullptr;
+  uint32_t* llen = nullptr;
+  cb::TableView view() const { return cb::TableView{data, start, klen, llen, nlines}; }
 };
 
 namespace {
@@ -110,6 +122,7 @@ struct DevBuf {
 struct Workspace {
   std::mutex mu;
   DevBuf keys, offsets, hits, seg, ent, masks, bools, lkey, zone;
+  DevBuf t_views, t_rows, t_which, t_line, t_dlen, t_voff, t_scan, t_vals;
 };
 
 std::mutex g_ws_mu;
@@ -751,6 +764,114 @@ int scan_meta(const uint8_t* in, uint64_t len, MetaScan& ms) {
   return CB_OK;
 }
 
+// Device output: used in place when device-resident, else a workspace buffer
+// copied back at the end.
+template <class T>
+int out_buf(DevBuf& b, T* user, size_t count, hipStream_t s, T** dev) {
+  if (is_device_ptr(user)) {
+    *dev = user;
+    return CB_OK;
+  }
+  HIP_TRY(b.reserve(count * sizeof(T) + 8, s));
+  *dev = (T*)b.p;
+  return CB_OK;
+}
+
+int table_search_impl(const cb_table* t, const uint8_t* keys, const uint64_t* offsets,
+                      uint32_t key_len, uint64_t n, int64_t* line_out, hipStream_t s) {
+  if (!t || !line_out) return fail(CB_EINVAL, "null argument");
+  if (n == 0) return CB_OK;
+  if (offsets == nullptr && keys == nullptr && key_len) return fail(CB_EINVAL, "null keys");
+  DeviceGuard dg(t->device);
+  Workspace& ws = workspace(t->device, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  StagedKeys sk;
+  int rc = offsets ? stage_var(ws, keys, offsets, n, s, sk) : stage_fixed(ws, keys, key_len, n, s, sk);
+  if (rc) return rc;
+  int64_t* dl;
+  if ((rc = out_buf(ws.t_line, line_out, n, s, &dl))) return rc;
+  HIP_TRY(cb::launch_table_search(sk.keyk, t->view(), sk.ks, n, dl, s));
+  if (dl != line_out) {
+    HIP_TRY(hipMemcpyAsync(line_out, dl, n * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  } else if (sk.staged) {
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  return CB_OK;
+}
+
+int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hits,
+                  const uint32_t* hit_rows, const uint8_t* keys, const uint64_t* offsets,
+                  uint32_t key_len, uint64_t n, int32_t* which, uint64_t* val_off, uint8_t* vals,
+                  uint64_t cap, uint64_t* total, hipStream_t s) {
+  if (!which || !val_off || !total || (nt && !tables)) return fail(CB_EINVAL, "null argument");
+  *total = 0;
+  if (n == 0) {
+    const uint64_t z = 0;
+    return put_bytes((uint8_t*)val_off, &z, 8);
+  }
+  if (offsets == nullptr && keys == nullptr && key_len) return fail(CB_EINVAL, "null keys");
+  if (nt == 0) return fail(CB_EINVAL, "no tables");
+  const int dev = tables[0] ? tables[0]->device : 0;
+  std::vector<cb::TableView> views(nt);
+  uint64_t nrows = nt;
+  for (uint32_t i = 0; i < nt; ++i) {
+    if (!tables[i]) return fail(CB_EINVAL, "null table");
+    if (tables[i]->device != dev) return fail(CB_EINVAL, "tables live on different devices");
+    views[i] = tables[i]->view();
+  }
+  std::vector<uint32_t> rows;
+  if (hits && hit_rows) {
+    rows.assign(hit_rows, hit_rows + nt);
+    nrows = 0;
+    for (uint32_t r : rows) nrows = std::max<uint64_t>(nrows, (uint64_t)r + 1);
+  }
+  DeviceGuard dg(dev);
+  Workspace& ws = workspace(dev, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  StagedKeys sk;
+  int rc = offsets ? stage_var(ws, keys, offsets, n, s, sk) : stage_fixed(ws, keys, key_len, n, s, sk);
+  if (rc) return rc;
+  const uint64_t hwords = (n + 63) / 64;
+  const uint64_t* dhits = hits;
+  if (hits && !is_device_ptr(hits)) {
+    HIP_TRY(ws.hits.reserve(nrows * hwords * 8, s));
+    HIP_TRY(hipMemcpyAsync(ws.hits.p, hits, nrows * hwords * 8, hipMemcpyHostToDevice, s));
+    dhits = (const uint64_t*)ws.hits.p;
+  }
+  HIP_TRY(ws.t_views.reserve(nt * sizeof(cb::TableView), s));
+  HIP_TRY(hipMemcpyAsync(ws.t_views.p, views.data(), nt * sizeof(cb::TableView), hipMemcpyHostToDevice, s));
+  const uint32_t* drows = nullptr;
+  if (!rows.empty()) {
+    HIP_TRY(ws.t_rows.reserve(nt * 4, s));
+    HIP_TRY(hipMemcpyAsync(ws.t_rows.p, rows.data(), nt * 4, hipMemcpyHostToDevice, s));
+    drows = (const uint32_t*)ws.t_rows.p;
+  }
+  int32_t* dwhich;
+  uint64_t* dvoff;
+  if ((rc = out_buf(ws.t_which, which, n, s, &dwhich))) return rc;
+  if ((rc = out_buf(ws.t_voff, val_off, n + 1, s, &dvoff))) return rc;
+  HIP_TRY(ws.t_line.reserve(n * 8, s));
+  HIP_TRY(ws.t_dlen.reserve(n * 8, s));
+  HIP_TRY(ws.t_scan.reserve(cb::scan_tmp_words(n) * 8, s));
+  const cb::TableView* dviews = (const cb::TableView*)ws.t_views.p;
+  HIP_TRY(cb::launch_get_many(sk.keyk, dviews, nt, dhits, drows, hwords, sk.ks, n, dwhich,
+                              (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, s));
+  HIP_TRY(cb::launch_scan_u64((const uint64_t*)ws.t_dlen.p, dvoff, n, (uint64_t*)ws.t_scan.p, s));
+  HIP_TRY(hipMemcpyAsync(total, dvoff + n, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (vals && cap >= *total && *total) {
+    uint8_t* dvals;
+    if ((rc = out_buf(ws.t_vals, vals, *total, s, &dvals))) return rc;
+    HIP_TRY(cb::launch_b64_decode(dviews, dwhich, (const uint64_t*)ws.t_line.p, dvoff, n, dvals, s));
+    if (dvals != vals) HIP_TRY(hipMemcpyAsync(vals, dvals, *total, hipMemcpyDeviceToHost, s));
+  }
+  if (dwhich != which) HIP_TRY(hipMemcpyAsync(which, dwhich, n * 4, hipMemcpyDeviceToHost, s));
+  if (dvoff != val_off) HIP_TRY(hipMemcpyAsync(val_off, dvoff, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return CB_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1172,6 +1293,119 @@ int cb_set_load_meta(cb_filterset* set, uint32_t slot, const uint8_t* in, uint64
   if (!rc) rc = cb_stream_synchronize(stream);
   cb_filter_destroy(f);
   return rc;
+}
+
+// ---- SSTable data files and the batched read path ----
+
+int cb_table_destroy(cb_table* t) {
+  if (!t) return CB_OK;
+  {
+    DeviceGuard dg(t->device);
+    for (void* p : {(void*)t->data, (void*)t->start, (void*)t->klen, (void*)t->llen})
+      if (p) (void)hipFree(p);
+  }
+  delete t;
+  return CB_OK;
+}
+
+int cb_table_create(const uint8_t* data, uint64_t len, int device, void* stream, cb_table** out) {
+  if (!out || (!data && len)) return fail(CB_EINVAL, "null argument");
+  *out = nullptr;
+  int rc = cb_init(device);
+  if (rc) return rc;
+  DeviceGuard dg(device);
+  hipStream_t s = (hipStream_t)stream;
+  std::unique_ptr<cb_table, int (*)(cb_table*)> t(new cb_table(), cb_table_destroy);
+  t->device = device;
+  t->len = len;
+  auto dalloc = [](void** p, size_t bytes) {
+    if (hipMalloc(p, bytes ? bytes : 16) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(CB_ENOMEM, "hipMalloc failed for an SSTable buffer");
+    }
+    return CB_OK;
+  };
+  if ((rc = dalloc((void**)&t->data, len + 16))) return rc;
+  if (len) HIP_TRY(hipMemcpyAsync(t->data, data, len, hipMemcpyDefault, s));
+  if (len) {
+    // count -> scan -> emit -> finish (sstable.hip)
+    const uint64_t nb = cb::line_blocks(len);
+    DevBuf cnt, base, tmp, end, err;
+    HIP_TRY(cnt.reserve(nb * 8, s));
+    HIP_TRY(base.reserve((nb + 1) * 8, s));
+    HIP_TRY(tmp.reserve(cb::scan_tmp_words(nb) * 8, s));
+    HIP_TRY(cb::launch_line_count(t->data, len, (uint64_t*)cnt.p, s));
+    HIP_TRY(cb::launch_scan_u64((const uint64_t*)cnt.p, (uint64_t*)base.p, nb, (uint64_t*)tmp.p, s));
+    HIP_TRY(hipMemcpyAsync(&t->nlines, (uint64_t*)base.p + nb, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (t->nlines) {
+      if ((rc = dalloc((void**)&t->start, t->nlines * 8))) return rc;
+      if ((rc = dalloc((void**)&t->klen, t->nlines * 4))) return rc;
+      if ((rc = dalloc((void**)&t->llen, t->nlines * 4))) return rc;
+      HIP_TRY(end.reserve(t->nlines * 8, s));
+      HIP_TRY(err.reserve(4, s));
+      HIP_TRY(hipMemsetAsync(end.p, 0xFF, t->nlines * 8, s));
+      HIP_TRY(hipMemsetAsync(err.p, 0, 4, s));
+      HIP_TRY(cb::launch_line_emit(t->data, len, (const uint64_t*)base.p, t->start, (uint64_t*)end.p, s));
+      HIP_TRY(cb::launch_line_finish(t->data, len, t->nlines, t->start, (const uint64_t*)end.p, t->klen,
+                                     t->llen, (uint32_t*)err.p, s));
+      uint32_t e = 0;
+      HIP_TRY(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      if (e) return fail(CB_EINVAL, "an SSTable line is 4 GiB or longer");
+    }
+    for (DevBuf* b : {&cnt, &base, &tmp, &end, &err})
+      if (b->p) (void)hipFree(b->p);
+  } else {
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  *out = t.release();
+  return CB_OK;
+}
+
+int cb_table_info(const cb_table* t, uint64_t* nlines, uint64_t* bytes) {
+  if (!t) return fail(CB_EINVAL, "null table");
+  if (nlines) *nlines = t->nlines;
+  if (bytes) *bytes = t->len;
+  return CB_OK;
+}
+
+int cb_table_lines(const cb_table* t, uint64_t* start, uint32_t* key_len, uint32_t* line_len) {
+  if (!t) return fail(CB_EINVAL, "null table");
+  DeviceGuard dg(t->device);
+  if (!t->nlines) return CB_OK;
+  if (start) HIP_TRY(hipMemcpy(start, t->start, t->nlines * 8, hipMemcpyDefault));
+  if (key_len) HIP_TRY(hipMemcpy(key_len, t->klen, t->nlines * 4, hipMemcpyDefault));
+  if (line_len) HIP_TRY(hipMemcpy(line_len, t->llen, t->nlines * 4, hipMemcpyDefault));
+  return CB_OK;
+}
+
+int cb_table_search_fixed(const cb_table* t, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                          int64_t* line_out, void* stream) {
+  return table_search_impl(t, keys, nullptr, key_len, n, line_out, (hipStream_t)stream);
+}
+
+int cb_table_search_var(const cb_table* t, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                        int64_t* line_out, void* stream) {
+  if (!offsets) return fail(CB_EINVAL, "null offsets");
+  return table_search_impl(t, bytes, offsets, 0, n, line_out, (hipStream_t)stream);
+}
+
+int cb_get_many_fixed(const cb_table* const* tables, uint32_t nt, const uint64_t* hits,
+                      const uint32_t* hit_rows, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                      int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap,
+                      uint64_t* total, void* stream) {
+  return get_many_impl(tables, nt, hits, hit_rows, keys, nullptr, key_len, n, which, val_off, vals,
+                       cap, total, (hipStream_t)stream);
+}
+
+int cb_get_many_var(const cb_table* const* tables, uint32_t nt, const uint64_t* hits,
+                    const uint32_t* hit_rows, const uint8_t* bytes, const uint64_t* offsets,
+                    uint64_t n, int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap,
+                    uint64_t* total, void* stream) {
+  if (!offsets) return fail(CB_EINVAL, "null offsets");
+  return get_many_impl(tables, nt, hits, hit_rows, bytes, offsets, 0, n, which, val_off, vals, cap,
+                       total, (hipStream_t)stream);
 }
 
 // ---- bit-sliced filter sets ----

@@ -1,0 +1,400 @@
+// sstable.hip — line index, batched binary search and base64 for SSTable data
+// files in HBM (see sstable.hpp for the reference mapping).
+//
+// Index build is streaming byte work (HBM-bound): each block owns a 4 KiB
+// chunk, each thread 16 contiguous bytes read as one dwordx4. A byte i starts
+// a line iff data[i] != '\n' and (i == 0 or data[i-1] == '\n') — exactly the
+// non-empty pieces of raw.split('\n') (src/sstable.rs:142-146). Resolution is
+// latency-bound random access: one lane per key, binary search through the
+// start/klen arrays and the key bytes (upper levels stay L2-resident).
+#include <hip/hip_runtime.h>
+
+#include "profile.hpp"
+#include "sstable.hpp"
+#include "zone.hpp"
+
+namespace cb {
+namespace {
+
+constexpr uint32_t kNT = 256;
+
+// Block-wide exclusive scan of one uint64 per thread (NT threads). Returns the
+// thread's prefix; *total = block sum. Contains barriers: call uniformly.
+template <int NT>
+__device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t* total) {
+  static_assert(NT % 64 == 0 && NT <= 4096, "block size");
+  constexpr int NW = NT / 64;
+  __shared__ uint64_t ws[NW];
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long y = __shfl_up(x, d, 64);
+    if ((int)lane >= d) x += y;
+  }
+  if (lane == 63) ws[wid] = x;
+  __syncthreads();
+  if (wid == 0) {
+    unsigned long long w = lane < NW ? ws[lane] : 0ull;
+#pragma unroll
+    for (int d = 1; d < NW; d <<= 1) {
+      const unsigned long long y = __shfl_up(w, d, 64);
+      if ((int)lane >= d) w += y;
+    }
+    if (lane < NW) ws[lane] = w;
+  }
+  __syncthreads();
+  const uint64_t pre = wid ? ws[wid - 1] : 0;
+  *total = ws[NW - 1];
+  __syncthreads();  // ws is reused by the next call
+  return pre + (uint64_t)x - v;
+}
+
+// The 16 bytes of thread t's slice and the byte before it (0 = "before the
+// file", which counts as a line break).
+__device__ __forceinline__ void load_slice(const uint8_t* data, uint64_t len, uint64_t base,
+                                           uint8_t b[16], uint32_t& prev) {
+  if (base + 16 <= len) {
+    const uint4 v = *reinterpret_cast<const uint4*>(data + base);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) b[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) b[i] = base + i < len ? data[base + i] : (uint8_t)'\n';
+  }
+  prev = base ? data[base - 1] : (uint32_t)'\n';
+}
+
+__global__ __launch_bounds__(kNT) void k_line_count(const uint8_t* __restrict__ data, uint64_t len,
+                                                    uint64_t* __restrict__ cnt) {
+  const uint64_t base = (uint64_t)blockIdx.x * kLineChunk + threadIdx.x * 16;
+  uint32_t c = 0;
+  if (base < len) {
+    uint8_t b[16];
+    uint32_t prev;
+    load_slice(data, len, base, b, prev);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      c += (b[i] != '\n') & (prev == '\n');
+      prev = b[i];
+    }
+  }
+  uint64_t total;
+  block_scan<kNT>(c, &total);
+  if (threadIdx.x == 0) cnt[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kNT) void k_line_emit(const uint8_t* __restrict__ data, uint64_t len,
+                                                   const uint64_t* __restrict__ bbase,
+                                                   uint64_t* __restrict__ start,
+                                                   uint64_t* __restrict__ end) {
+  const uint64_t base = (uint64_t)blockIdx.x * kLineChunk + threadIdx.x * 16;
+  uint8_t b[16];
+  uint32_t prev = '\n', c = 0;
+  if (base < len) {
+    load_slice(data, len, base, b, prev);
+    uint32_t p = prev;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      c += (b[i] != '\n') & (p == '\n');
+      p = b[i];
+    }
+  }
+  uint64_t total;
+  uint64_t idx = bbase[blockIdx.x] + block_scan<kNT>(c, &total);
+  if (base >= len) return;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint64_t pos = base + i;
+    if (pos < len) {
+      if (b[i] != '\n' && prev == '\n') start[idx++] = pos;
+      else if (b[i] == '\n' && prev != '\n') end[idx - 1] = pos;  // idx >= 1 here
+    }
+    prev = b[i];
+  }
+}
+
+__global__ __launch_bounds__(kNT) void k_line_finish(const uint8_t* __restrict__ data, uint64_t len,
+                                                     uint64_t nlines,
+                                                     const uint64_t* __restrict__ start,
+                                                     const uint64_t* __restrict__ end,
+                                                     uint32_t* __restrict__ klen,
+                                                     uint32_t* __restrict__ llen, uint32_t* err) {
+  const uint64_t l = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  if (l >= nlines) return;
+  const uint64_t s = start[l];
+  const uint64_t e = end[l] == ~0ull ? len : end[l];
+  const uint64_t n = e - s;
+  if (n >= kNoSep) {
+    atomicOr(err, 1u);
+    return;
+  }
+  uint32_t k = kNoSep;
+  for (uint32_t i = 0; i < (uint32_t)n; ++i)
+    if (data[s + i] == '\t') {
+      k = i;
+      break;
+    }
+  klen[l] = k;
+  llen[l] = (uint32_t)n;
+}
+
+// ---- exclusive scan of uint64 (tiles of 1024 = 256 threads x 4) ----
+constexpr uint32_t kScanTile = 1024;
+
+__global__ __launch_bounds__(kNT) void k_scan_tiles(const uint64_t* __restrict__ in,
+                                                    uint64_t* __restrict__ out, uint64_t n,
+                                                    uint64_t* __restrict__ sums) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 4;
+  uint64_t v[4], s = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = i0 + j < n ? in[i0 + j] : 0;
+    s += v[j];
+  }
+  uint64_t total;
+  uint64_t p = block_scan<kNT>(s, &total);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (i0 + j < n) out[i0 + j] = p;
+    p += v[j];
+  }
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+// One block: exclusive scan of the tile sums in place (carry across chunks);
+// out[n] = grand total.
+__global__ __launch_bounds__(1024) void k_scan_sums(uint64_t* __restrict__ sums, uint64_t nt,
+                                                    uint64_t* __restrict__ out, uint64_t n) {
+  uint64_t carry = 0;
+  for (uint64_t c0 = 0; c0 < nt; c0 += 1024) {
+    const uint64_t i = c0 + threadIdx.x;
+    const uint64_t v = i < nt ? sums[i] : 0;
+    uint64_t total;
+    const uint64_t p = block_scan<1024>(v, &total);
+    if (i < nt) sums[i] = carry + p;
+    carry += total;
+  }
+  if (threadIdx.x == 0) out[n] = carry;
+}
+
+__global__ __launch_bounds__(kNT) void k_scan_add(uint64_t* __restrict__ out, uint64_t n,
+                                                  const uint64_t* __restrict__ sums) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 4;
+  const uint64_t add = sums[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (i0 + j < n) out[i0 + j] += add;
+}
+
+// ---- binary search and base64 ----
+
+// SsTable::binary_search (src/sstable.rs:161-179), same mid sequence.
+__device__ __forceinline__ int64_t search_one(const TableView& t, const uint8_t* kp, uint64_t kl) {
+  uint64_t lo = 0, hi = t.nlines;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    const uint32_t klm = t.klen[mid];
+    if (klm == kNoSep) break;
+    const int c = bytes_cmp(t.data + t.start[mid], klm, kp, kl);
+    if (c < 0)
+      lo = mid + 1;
+    else if (c > 0)
+      hi = mid;
+    else
+      return (int64_t)mid;
+  }
+  return -1;
+}
+
+// Standard-alphabet value of a byte, -1 if outside it.
+__device__ __forceinline__ int b64v(uint32_t c) {
+  int v = -1;
+  v = (c - 'A' < 26u) ? (int)(c - 'A') : v;
+  v = (c - 'a' < 26u) ? (int)(c - 'a') + 26 : v;
+  v = (c - '0' < 10u) ? (int)(c - '0') + 52 : v;
+  v = c == '+' ? 62 : v;
+  v = c == '/' ? 63 : v;
+  return v;
+}
+
+// base64 0.21.7 STANDARD (canonical padding, zero trailing bits): decoded
+// length of p[0..len), or -1 if STANDARD.decode would fail.
+__device__ __forceinline__ int64_t b64_len(const uint8_t* p, uint64_t len) {
+  if (len & 3) return -1;
+  if (!len) return 0;
+  const uint32_t pad = p[len - 1] == '=' ? (p[len - 2] == '=' ? 2 : 1) : 0;
+  const uint64_t body = len - pad;
+  int last = 0;
+  for (uint64_t i = 0; i < body; ++i) {
+    last = b64v(p[i]);
+    if (last < 0) return -1;
+  }
+  if (pad == 2 && (last & 0x0F)) return -1;
+  if (pad == 1 && (last & 0x03)) return -1;
+  return (int64_t)(len / 4 * 3 - pad);
+}
+
+template <int KEYK>
+__global__ __launch_bounds__(kNT) void k_table_search(TableView t, KeySrc ks, uint64_t n,
+                                                      int64_t* __restrict__ line) {
+  const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  if (k >= n) return;
+  const uint8_t* kp;
+  uint64_t kl;
+  key_span<KEYK>(ks, k, kp, kl);
+  line[k] = search_one(t, kp, kl);
+}
+
+template <int KEYK>
+__global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ tv, uint32_t nt,
+                                                  const uint64_t* __restrict__ hits,
+                                                  const uint32_t* __restrict__ rows,
+                                                  uint64_t hwords, KeySrc ks, uint64_t n,
+                                                  int32_t* __restrict__ which,
+                                                  uint64_t* __restrict__ line,
+                                                  uint64_t* __restrict__ dlen) {
+  const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  if (k >= n) return;
+  const uint8_t* kp;
+  uint64_t kl;
+  key_span<KEYK>(ks, k, kp, kl);
+  int32_t w = -1;
+  uint64_t ln = 0, d = 0;
+  for (uint32_t t = 0; t < nt; ++t) {  // tables.iter().rev(): newest first
+    if (hits) {
+      const uint64_t row = rows ? rows[t] : t;
+      if (!((hits[row * hwords + (k >> 6)] >> (k & 63)) & 1)) continue;  // gate said no
+    }
+    const TableView v = tv[t];
+    const int64_t r = search_one(v, kp, kl);
+    if (r < 0) continue;  // Ok(None)
+    const uint32_t kk = v.klen[r];
+    const int64_t dl = b64_len(v.data + v.start[r] + kk + 1, v.llen[r] - kk - 1);
+    if (dl < 0) continue;  // Err(..) is skipped by `if let Ok(Some(v))`
+    w = (int32_t)t;
+    ln = (uint64_t)r;
+    d = (uint64_t)dl;
+    break;
+  }
+  which[k] = w;
+  line[k] = ln;
+  dlen[k] = d;
+}
+
+__global__ __launch_bounds__(kNT) void k_b64_decode(const TableView* __restrict__ tv,
+                                                    const int32_t* __restrict__ which,
+                                                    const uint64_t* __restrict__ line,
+                                                    const uint64_t* __restrict__ voff, uint64_t n,
+                                                    uint8_t* __restrict__ out) {
+  const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  if (k >= n || which[k] < 0) return;
+  const TableView v = tv[which[k]];
+  const uint64_t r = line[k];
+  const uint32_t kk = v.klen[r];
+  const uint8_t* p = v.data + v.start[r] + kk + 1;
+  const uint64_t len = v.llen[r] - kk - 1;
+  uint8_t* o = out + voff[k];
+  const uint64_t dl = voff[k + 1] - voff[k];
+  uint64_t j = 0;
+  for (uint64_t q = 0; q < len; q += 4) {
+    const uint32_t w = (uint32_t)(b64v(p[q]) & 63) << 18 | (uint32_t)(b64v(p[q + 1]) & 63) << 12 |
+                       (uint32_t)(b64v(p[q + 2]) & 63) << 6 | (uint32_t)(b64v(p[q + 3]) & 63);
+    if (j < dl) o[j++] = (uint8_t)(w >> 16);
+    if (j < dl) o[j++] = (uint8_t)(w >> 8);
+    if (j < dl) o[j++] = (uint8_t)w;
+  }
+}
+
+inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
+
+}  // namespace
+
+hipError_t launch_line_count(const uint8_t* data, uint64_t len, uint64_t* cnt, hipStream_t s) {
+  if (!len) return hipSuccess;
+  ProfScope ps("k_line_count", s);
+  hipLaunchKernelGGL(k_line_count, dim3((uint32_t)line_blocks(len)), dim3(kNT), 0, s, data, len,
+                     cnt);
+  return hipGetLastError();
+}
+
+hipError_t launch_line_emit(const uint8_t* data, uint64_t len, const uint64_t* base,
+                            uint64_t* start, uint64_t* end, hipStream_t s) {
+  if (!len) return hipSuccess;
+  ProfScope ps("k_line_emit", s);
+  hipLaunchKernelGGL(k_line_emit, dim3((uint32_t)line_blocks(len)), dim3(kNT), 0, s, data, len,
+                     base, start, end);
+  return hipGetLastError();
+}
+
+hipError_t launch_line_finish(const uint8_t* data, uint64_t len, uint64_t nlines,
+                              const uint64_t* start, const uint64_t* end, uint32_t* klen,
+                              uint32_t* llen, uint32_t* err, hipStream_t s) {
+  if (!nlines) return hipSuccess;
+  ProfScope ps("k_line_finish", s);
+  hipLaunchKernelGGL(k_line_finish, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, data, len,
+                     nlines, start, end, klen, llen, err);
+  return hipGetLastError();
+}
+
+uint64_t scan_tmp_words(uint64_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+
+hipError_t launch_scan_u64(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tmp,
+                           hipStream_t s) {
+  const uint64_t nt = (n + kScanTile - 1) / kScanTile;
+  ProfScope ps("k_scan_u64", s);
+  if (nt) hipLaunchKernelGGL(k_scan_tiles, dim3((uint32_t)nt), dim3(kNT), 0, s, in, out, n, tmp);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, s, tmp, nt, out, n);
+  if (nt > 1) hipLaunchKernelGGL(k_scan_add, dim3((uint32_t)nt), dim3(kNT), 0, s, out, n, tmp);
+  return hipGetLastError();
+}
+
+hipError_t launch_table_search(int keyk, const TableView& t, const KeySrc& ks, uint64_t n,
+                               int64_t* line, hipStream_t s) {
+  if (!n) return hipSuccess;
+  ProfScope ps("k_table_search", s);
+  const dim3 g(blocks_for(n, kNT));
+  switch (keyk) {
+    case KEY_FIXED16: hipLaunchKernelGGL(k_table_search<KEY_FIXED16>, g, dim3(kNT), 0, s, t, ks, n, line); break;
+    case KEY_FIXED: hipLaunchKernelGGL(k_table_search<KEY_FIXED>, g, dim3(kNT), 0, s, t, ks, n, line); break;
+    case KEY_VAR: hipLaunchKernelGGL(k_table_search<KEY_VAR>, g, dim3(kNT), 0, s, t, ks, n, line); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uint64_t* hits,
+                           const uint32_t* rows, uint64_t hwords, const KeySrc& ks, uint64_t n,
+                           int32_t* which, uint64_t* line, uint64_t* dlen, hipStream_t s) {
+  if (!n) return hipSuccess;
+  ProfScope ps("k_get_many", s);
+  const dim3 g(blocks_for(n, kNT));
+  switch (keyk) {
+    case KEY_FIXED16:
+      hipLaunchKernelGGL(k_get_many<KEY_FIXED16>, g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks,
+                         n, which, line, dlen);
+      break;
+    case KEY_FIXED:
+      hipLaunchKernelGGL(k_get_many<KEY_FIXED>, g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n,
+                         which, line, dlen);
+      break;
+    case KEY_VAR:
+      hipLaunchKernelGGL(k_get_many<KEY_VAR>, g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n,
+                         which, line, dlen);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_b64_decode(const TableView* tv, const int32_t* which, const uint64_t* line,
+                             const uint64_t* voff, uint64_t n, uint8_t* out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  ProfScope ps("k_b64_decode", s);
+  hipLaunchKernelGGL(k_b64_decode, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, tv, which, line, voff,
+                     n, out);
+  return hipGetLastError();
+}
+
+}  // namespace cb

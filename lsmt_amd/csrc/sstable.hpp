@@ -1,0 +1,63 @@
+// sstable.hpp — SSTable data files resident in HBM and the batched read-path
+// resolution after the Bloom/zone gate.
+//
+// A data file is SsTable::create's output (/root/reference/src/sstable.rs:
+// 57-72): lines `key \t base64(value) \n` sorted by key. SsTable::get
+// (src/sstable.rs:133-153) splits it on '\n', drops empty lines, binary-
+// searches the lines (161-179) and base64-decodes the hit (148). Database::get
+// (src/lib.rs:128-134) asks the tables newest-first and keeps the first
+// Ok(Some). Here one lane resolves one key across all its candidate tables.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hash.hpp"
+
+namespace cb {
+
+constexpr uint32_t kNoSep = 0xFFFFFFFFu;  // line without a TAB: ends a search
+
+// One data file and its line index (SoA, one entry per non-empty line).
+struct TableView {
+  const uint8_t* data;
+  const uint64_t* start;  // line start offset
+  const uint32_t* klen;   // bytes before the first TAB, or kNoSep
+  const uint32_t* llen;   // line length (without the '\n')
+  uint64_t nlines;
+};
+
+// ---- line index build: count -> scan -> emit -> finish ----
+constexpr uint32_t kLineChunk = 4096;  // bytes per block (256 threads x 16 B)
+inline uint64_t line_blocks(uint64_t len) { return (len + kLineChunk - 1) / kLineChunk; }
+// cnt[b] = non-empty line starts in chunk b
+hipError_t launch_line_count(const uint8_t* data, uint64_t len, uint64_t* cnt, hipStream_t s);
+// start[base[b] + j] = j-th line start of chunk b; end[l] = its '\n' (ends of
+// the last line at EOF stay ~0: finish fills them with len)
+hipError_t launch_line_emit(const uint8_t* data, uint64_t len, const uint64_t* base,
+                            uint64_t* start, uint64_t* end, hipStream_t s);
+// klen / llen per line; *err |= 1 if a line is 4 GiB or longer
+hipError_t launch_line_finish(const uint8_t* data, uint64_t len, uint64_t nlines,
+                              const uint64_t* start, const uint64_t* end, uint32_t* klen,
+                              uint32_t* llen, uint32_t* err, hipStream_t s);
+
+// Exclusive scan of n uint64 (out[n] = total). tmp: scan_tmp_words(n) words.
+uint64_t scan_tmp_words(uint64_t n);
+hipError_t launch_scan_u64(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tmp,
+                           hipStream_t s);
+
+// ---- resolution ----
+// line[k] = SsTable::binary_search(key k) over one table, or -1.
+hipError_t launch_table_search(int keyk, const TableView& t, const KeySrc& ks, uint64_t n,
+                               int64_t* line, hipStream_t s);
+// Database::get's walk over tv[0..nt) (tv[0] newest). Table t is asked only
+// where hits (nullable, [rows][hwords]) has bit k of row rows[t] (rows
+// nullable = identity). which[k] = first t whose line decodes as base64,
+// else -1; line[k] its line; dlen[k] the decoded length (0 if none).
+hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uint64_t* hits,
+                           const uint32_t* rows, uint64_t hwords, const KeySrc& ks, uint64_t n,
+                           int32_t* which, uint64_t* line, uint64_t* dlen, hipStream_t s);
+// Decoded values of the found keys into out + voff[k].
+hipError_t launch_b64_decode(const TableView* tv, const int32_t* which, const uint64_t* line,
+                             const uint64_t* voff, uint64_t n, uint8_t* out, hipStream_t s);
+
+}  // namespace cb

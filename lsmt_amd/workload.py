@@ -127,3 +127,45 @@ def zone_lookups(tables: list[np.ndarray], n: int, absent_seed: int = 998, rng_s
     out[0::2] = present[pick]
     out[1::2] = key_range(absent_seed, n - n // 2)[: len(out[1::2])]
     return out
+
+
+# ---- SSTable data files ------------------------------------
+
+_B64 = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/", np.uint8)
+
+
+def b64_rows(v: np.ndarray) -> np.ndarray:
+    """Standard padded base64 of each row of a uint8 [n, L] array -> [n, 4*ceil(L/3)]."""
+    n, L = v.shape
+    pad = (-L) % 3
+    x = np.concatenate([v, np.zeros((n, pad), np.uint8)], axis=1).reshape(n, -1, 3).astype(np.uint32)
+    w = x[..., 0] << 16 | x[..., 1] << 8 | x[..., 2]
+    out = np.stack([_B64[(w >> s) & 63] for s in (18, 12, 6, 0)], axis=-1).reshape(n, -1)
+    if pad:
+        out[:, out.shape[1] - pad:] = ord("=")
+    return out
+
+
+def sort_keys16(keys: np.ndarray) -> np.ndarray:
+    """Rows of a uint8 [n, 16] array in Rust str order (byte-wise)."""
+    w = keys.view(">u8").reshape(len(keys), 2)
+    return keys[np.lexsort((w[:, 1], w[:, 0]))]
+
+
+def table_value(keys: np.ndarray, table_id: int) -> np.ndarray:
+    """The stored value of each key in table `table_id`: an 8-byte big-endian
+    timestamp (insert_ts layout, src/lib.rs:111-115) then the key's first 8 bytes."""
+    ts = np.frombuffer(np.array([table_id], dtype=">u8").tobytes(), np.uint8)
+    return np.concatenate([np.broadcast_to(ts, (len(keys), 8)), keys[:, :8]], axis=1)
+
+
+def sstable_bytes(keys: np.ndarray, values: np.ndarray) -> np.ndarray:
+    """SsTable::create's data file (src/sstable.rs:57-72) for 16-byte keys:
+    lines `key \\t base64(value) \\n` sorted by key."""
+    order = np.lexsort(tuple(keys.view(">u8").reshape(len(keys), 2)[:, ::-1].T)) if len(keys) else []
+    k = keys[order]
+    v = b64_rows(values[order])
+    n = len(k)
+    tab = np.full((n, 1), ord("\t"), np.uint8)
+    nl = np.full((n, 1), ord("\n"), np.uint8)
+    return np.ascontiguousarray(np.concatenate([k, tab, v, nl], axis=1).reshape(-1))

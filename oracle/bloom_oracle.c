@@ -538,6 +538,162 @@ int ob_meta_decode(const uint8_t* in, uint64_t len, ob_meta* out) {
   return rc;
 }
 
+/* ---- SSTable data file: split, binary search, base64, get ---- */
+
+int ob_table_index(const uint8_t* data, uint64_t len, ob_table* t) {
+  memset(t, 0, sizeof(*t));
+  t->data = data;
+  t->len = len;
+  uint64_t cap = 0;
+  uint64_t i = 0;
+  while (i < len) {
+    uint64_t j = i;
+    while (j < len && data[j] != '\n') ++j;
+    if (j > i) { /* .filter(|line| !line.is_empty()) */
+      if (t->nlines == cap) {
+        cap = cap ? 2 * cap : 64;
+        uint64_t* ns = (uint64_t*)realloc(t->start, cap * 8);
+        if (!ns) return OB_ENOMEM;
+        t->start = ns;
+        uint64_t* ne = (uint64_t*)realloc(t->end, cap * 8);
+        if (!ne) return OB_ENOMEM;
+        t->end = ne;
+      }
+      t->start[t->nlines] = i;
+      t->end[t->nlines] = j;
+      ++t->nlines;
+    }
+    i = j + 1;
+  }
+  return OB_OK;
+}
+
+void ob_table_free(ob_table* t) {
+  free(t->start);
+  free(t->end);
+  memset(t, 0, sizeof(*t));
+}
+
+int64_t ob_table_search(const ob_table* t, const uint8_t* key, uint64_t klen, uint64_t* val,
+                        uint64_t* val_len) {
+  uint64_t lo = 0, hi = t->nlines;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) / 2;
+    const uint8_t* line = t->data + t->start[mid];
+    uint64_t ll = t->end[mid] - t->start[mid];
+    const uint8_t* tab = (const uint8_t*)memchr(line, '\t', (size_t)ll);
+    if (!tab) break; /* no SEP: `else { break; }` */
+    uint64_t pos = (uint64_t)(tab - line);
+    int c = ob_bytes_cmp(line, pos, key, klen);
+    if (c < 0) lo = mid + 1;
+    else if (c > 0) hi = mid;
+    else {
+      if (val) *val = t->start[mid] + pos + 1;
+      if (val_len) *val_len = ll - pos - 1;
+      return (int64_t)mid;
+    }
+  }
+  return -1;
+}
+
+static int b64_sym(uint8_t c) {
+  if (c >= 'A' && c <= 'Z') return c - 'A';
+  if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+  if (c >= '0' && c <= '9') return c - '0' + 52;
+  if (c == '+') return 62;
+  if (c == '/') return 63;
+  return -1;
+}
+
+int64_t ob_b64_decode(const uint8_t* in, uint64_t len, uint8_t* out) {
+  if (len % 4) return -1; /* canonical padding: whole quads only */
+  uint64_t pad = 0;
+  if (len && in[len - 1] == '=') pad = (len >= 2 && in[len - 2] == '=') ? 2 : 1;
+  uint64_t o = 0;
+  for (uint64_t q = 0; q < len; q += 4) {
+    int last = q + 4 == len;
+    int v[4];
+    for (int k = 0; k < 4; ++k) {
+      if (last && k >= 4 - (int)pad) {
+        v[k] = 0; /* '=' only at the tail */
+        continue;
+      }
+      v[k] = b64_sym(in[q + k]);
+      if (v[k] < 0) return -1;
+    }
+    uint32_t w = (uint32_t)v[0] << 18 | (uint32_t)v[1] << 12 | (uint32_t)v[2] << 6 | (uint32_t)v[3];
+    int nout = last ? 3 - (int)pad : 3;
+    if (last && pad == 2 && (v[1] & 0x0F)) return -1; /* trailing bits must be zero */
+    if (last && pad == 1 && (v[2] & 0x03)) return -1;
+    if (out) {
+      out[o] = (uint8_t)(w >> 16);
+      if (nout > 1) out[o + 1] = (uint8_t)(w >> 8);
+      if (nout > 2) out[o + 2] = (uint8_t)w;
+    }
+    o += (uint64_t)nout;
+  }
+  return (int64_t)o;
+}
+
+uint64_t ob_b64_encode(const uint8_t* in, uint64_t len, uint8_t* out) {
+  static const char A[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  uint64_t o = 0;
+  for (uint64_t i = 0; i < len; i += 3) {
+    uint64_t r = len - i;
+    uint32_t w = (uint32_t)in[i] << 16 | (r > 1 ? (uint32_t)in[i + 1] << 8 : 0) | (r > 2 ? in[i + 2] : 0);
+    if (out) {
+      out[o] = (uint8_t)A[w >> 18];
+      out[o + 1] = (uint8_t)A[(w >> 12) & 63];
+      out[o + 2] = r > 1 ? (uint8_t)A[(w >> 6) & 63] : '=';
+      out[o + 3] = r > 2 ? (uint8_t)A[w & 63] : '=';
+    }
+    o += 4;
+  }
+  return o;
+}
+
+int ob_get_many(const ob_table* const* tables, uint32_t nt, const uint64_t* hits,
+                const uint8_t* bytes, const uint64_t* offsets, uint64_t n, int32_t* which,
+                uint64_t* val_off, uint8_t* vals, uint64_t cap, uint64_t* total) {
+  uint64_t words = (n + 63) / 64, acc = 0;
+  int64_t* got_line = (int64_t*)malloc((n ? n : 1) * 8);
+  uint64_t* vstart = (uint64_t*)malloc((n ? n : 1) * 8);
+  uint64_t* vlen = (uint64_t*)malloc((n ? n : 1) * 8);
+  if (!got_line || !vstart || !vlen) {
+    free(got_line);
+    free(vstart);
+    free(vlen);
+    return OB_ENOMEM;
+  }
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint8_t* key = bytes + offsets[k];
+    uint64_t klen = offsets[k + 1] - offsets[k];
+    which[k] = -1;
+    val_off[k] = acc;
+    for (uint32_t t = 0; t < nt; ++t) { /* tables.iter().rev(): newest first */
+      if (hits && !((hits[(uint64_t)t * words + (k >> 6)] >> (k & 63)) & 1)) continue;
+      uint64_t vs, vl;
+      if (ob_table_search(tables[t], key, klen, &vs, &vl) < 0) continue; /* Ok(None) */
+      int64_t d = ob_b64_decode(tables[t]->data + vs, vl, NULL);
+      if (d < 0) continue; /* Err(..): `if let Ok(Some(v))` skips it */
+      which[k] = (int32_t)t;
+      vstart[k] = vs;
+      vlen[k] = vl;
+      acc += (uint64_t)d;
+      break;
+    }
+  }
+  val_off[n] = acc;
+  *total = acc;
+  if (vals && cap >= acc)
+    for (uint64_t k = 0; k < n; ++k)
+      if (which[k] >= 0) ob_b64_decode(tables[which[k]]->data + vstart[k], vlen[k], vals + val_off[k]);
+  free(got_line);
+  free(vstart);
+  free(vlen);
+  return OB_OK;
+}
+
 /* ---- synthetic workload ---- */
 
 uint64_t ob_splitmix64(uint64_t x) {

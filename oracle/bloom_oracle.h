@@ -121,6 +121,40 @@ int ob_meta_decode(const uint8_t* in, uint64_t len, ob_meta* out);
 void ob_meta_free(ob_meta* m);
 int ob_utf8_valid(const uint8_t* p, uint64_t n); /* Rust str::from_utf8 acceptance */
 
+/* SSTable data file (SsTable::create, src/sstable.rs:57-72): sorted lines
+ * `key \t base64(value) \n`. ob_table_index restates SsTable::get's
+ * raw.split(NL).filter(non-empty) (src/sstable.rs:142-146): line i is
+ * data[start[i] .. end[i]). */
+typedef struct ob_table {
+  const uint8_t* data; /* not owned */
+  uint64_t len, nlines;
+  uint64_t* start;
+  uint64_t* end;
+} ob_table;
+int ob_table_index(const uint8_t* data, uint64_t len, ob_table* t);
+void ob_table_free(ob_table* t);
+/* SsTable::binary_search (src/sstable.rs:161-179), same (lo+hi)/2 trajectory:
+ * the matching line's index, or -1 (also when the probed line has no TAB,
+ * which ends the search). *val / *val_len: the bytes after the TAB. */
+int64_t ob_table_search(const ob_table* t, const uint8_t* key, uint64_t klen, uint64_t* val,
+                        uint64_t* val_len);
+/* base64 0.21.7 STANDARD engine (the reference's `STANDARD.decode`,
+ * src/sstable.rs:148): alphabet A-Z a-z 0-9 + /, canonical '=' padding
+ * required (length % 4 == 0), non-zero trailing bits rejected. Returns the
+ * decoded length, or -1 on any decode error; out may be NULL. */
+int64_t ob_b64_decode(const uint8_t* in, uint64_t len, uint8_t* out);
+/* STANDARD.encode (src/sstable.rs:69): returns the encoded length. */
+uint64_t ob_b64_encode(const uint8_t* in, uint64_t len, uint8_t* out);
+/* Database::get's table walk (src/lib.rs:128-134) for a key batch: tables[0]
+ * is the NEWEST; hits (nullable, [nt][ceil(n/64)]) is each table's gate
+ * (zone && bloom, src/sstable.rs:138). which[k] = first table whose get
+ * returns Ok(Some) (found and base64-decodable; a decode Err falls through
+ * to older tables), or -1. val_off[n+1] = prefix offsets of the decoded
+ * values in vals; vals written only if cap >= *total. */
+int ob_get_many(const ob_table* const* tables, uint32_t nt, const uint64_t* hits,
+                const uint8_t* bytes, const uint64_t* offsets, uint64_t n, int32_t* which,
+                uint64_t* val_off, uint8_t* vals, uint64_t cap, uint64_t* total);
+
 /* Synthetic workload keys: 16 lowercase hex chars, MSB
  * nibble first, of splitmix64(seed * 2^32 + i). out is n*16 bytes. */
 void ob_gen_keys(uint64_t seed, uint64_t first, uint64_t n, uint8_t* out);

@@ -39,6 +39,11 @@ class _Meta(ctypes.Structure):
     _fields_ = [("has_bloom", ctypes.c_int), ("bloom", _Filter), ("has_zone", ctypes.c_int), ("zone", _Zone)]
 
 
+class _Table(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_uint64), ("nlines", ctypes.c_uint64),
+                ("start", ctypes.POINTER(ctypes.c_uint64)), ("end", ctypes.POINTER(ctypes.c_uint64))]
+
+
 def build() -> str:
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
@@ -83,6 +88,17 @@ def lib():
         L.ob_meta_free.argtypes = [MP]
         L.ob_meta_free.restype = None
         L.ob_utf8_valid.argtypes = [P, u64]
+        TP = ctypes.POINTER(_Table)
+        L.ob_table_index.argtypes = [P, u64, TP]
+        L.ob_table_free.argtypes = [TP]
+        L.ob_table_free.restype = None
+        L.ob_table_search.argtypes = [TP, P, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+        L.ob_table_search.restype = ctypes.c_int64
+        L.ob_b64_decode.argtypes = [P, u64, P]
+        L.ob_b64_decode.restype = ctypes.c_int64
+        L.ob_b64_encode.argtypes = [P, u64, P]
+        L.ob_b64_encode.restype = u64
+        L.ob_get_many.argtypes = [P, u32, P, P, P, u64, P, P, P, u64, ctypes.POINTER(u64)]
         L.ob_gen_keys.argtypes = [u64, u64, u64, P]
         L.ob_gen_keys.restype = None
         L.ob_splitmix64.argtypes = [u64]
@@ -288,6 +304,84 @@ def meta_decode(data: bytes):
 def utf8_valid(b: bytes) -> bool:
     buf = np.frombuffer(b, np.uint8).copy() if b else np.zeros(1, np.uint8)
     return bool(lib().ob_utf8_valid(_ptr(buf), len(b)))
+
+
+def _buf(b: bytes) -> np.ndarray:
+    return np.frombuffer(b, np.uint8).copy() if b else np.zeros(1, np.uint8)
+
+
+class OracleTable:
+    """An SSTable data file split into lines as SsTable::get does (src/sstable.rs:142-146)."""
+
+    def __init__(self, data):
+        self.data = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray)
+                                         else data, dtype=np.uint8)
+        self._keep = self.data if len(self.data) else np.zeros(1, np.uint8)
+        self._t = _Table()
+        rc = lib().ob_table_index(_ptr(self._keep), len(self.data), ctypes.byref(self._t))
+        if rc:
+            raise MemoryError(rc)
+
+    def __del__(self):
+        try:
+            lib().ob_table_free(ctypes.byref(self._t))
+        except Exception:
+            pass
+
+    @property
+    def nlines(self) -> int:
+        return int(self._t.nlines)
+
+    def search(self, key: bytes):
+        """SsTable::binary_search: (line index, encoded value bytes) or (-1, None)."""
+        vs, vl = ctypes.c_uint64(), ctypes.c_uint64()
+        kb = _buf(key)
+        r = lib().ob_table_search(ctypes.byref(self._t), _ptr(kb), len(key), ctypes.byref(vs), ctypes.byref(vl))
+        if r < 0:
+            return -1, None
+        return int(r), self.data[vs.value: vs.value + vl.value].tobytes()
+
+
+def b64_decode(data: bytes) -> bytes | None:
+    b = _buf(data)
+    out = np.zeros(max(len(data), 1), np.uint8)
+    r = lib().ob_b64_decode(_ptr(b), len(data), _ptr(out))
+    return None if r < 0 else out[:r].tobytes()
+
+
+def b64_encode(data: bytes) -> bytes:
+    b = _buf(data)
+    out = np.zeros(max(4 * ((len(data) + 2) // 3), 1), np.uint8)
+    r = lib().ob_b64_encode(_ptr(b), len(data), _ptr(out))
+    return out[:r].tobytes()
+
+
+def get_many(tables, hits, data: np.ndarray, offsets: np.ndarray):
+    """Database::get's newest-first walk (tables[0] newest) for a key batch.
+    Returns (which int32[n], val_off uint64[n+1], vals bytes)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offsets) - 1
+    nt = len(tables)
+    which = np.zeros(max(n, 1), np.int32)
+    voff = np.zeros(n + 1, np.uint64)
+    tarr = (ctypes.POINTER(_Table) * max(nt, 1))(*[ctypes.pointer(t._t) for t in tables])
+    hp = None
+    if hits is not None:
+        hits = np.ascontiguousarray(hits, dtype=np.uint64)
+        hp = _ptr(hits)
+    total = ctypes.c_uint64()
+    L = lib()
+    args = [ctypes.cast(tarr, ctypes.c_void_p), nt, hp, _ptr(data if len(data) else np.zeros(1, np.uint8)),
+            _ptr(offsets), n, _ptr(which), _ptr(voff)]
+    rc = L.ob_get_many(*args, None, 0, ctypes.byref(total))
+    if rc:
+        raise RuntimeError(rc)
+    vals = np.zeros(max(total.value, 1), np.uint8)
+    rc = L.ob_get_many(*args, _ptr(vals), total.value, ctypes.byref(total))
+    if rc:
+        raise RuntimeError(rc)
+    return which[:n], voff, vals[: total.value].tobytes()
 
 
 def gen_keys(seed: int, n: int, first: int = 0) -> np.ndarray:

@@ -285,6 +285,10 @@ def main() -> None:
     # 8. TableMeta `.meta` codec (src/sstable.rs:31-37,74-81,96-108; zonemap.rs:11-17)
     g["meta"] = meta_fixtures(build_py)
 
+    # 9. SSTable data files: split, binary search, base64, newest-first get
+    #    (src/sstable.rs:57-72,133-179; src/lib.rs:128-134)
+    g["sstable"] = sstable_fixtures()
+
     with open(os.path.join(HERE, "golden.json"), "w") as fh:
         json.dump(g, fh, indent=1, sort_keys=True)
     print("wrote", os.path.join(HERE, "golden.json"))
@@ -487,6 +491,104 @@ def meta_fixtures(build_py) -> dict:
                                       "min_hex": None, "max_hex": None}
     assert dec["unknown_fields"]["expect"]["set_bits"] == [0, 2]
     return {"encode": enc, "decode": dec}
+
+
+# ---- SSTable data files: independent Python restatement ---------------------------
+
+def b64_std_decode(v: bytes):
+    """base64 0.21.7 STANDARD.decode: canonical padded base64 only. Python's
+    strict decoder plus a re-encode check is an independent statement of
+    "canonical": it rejects missing padding and non-zero trailing bits."""
+    import base64
+    import binascii
+    try:
+        d = base64.b64decode(v, validate=True)
+    except (binascii.Error, ValueError):
+        return None
+    return d if base64.b64encode(d) == v else None
+
+
+def table_get_py(data: bytes, key: bytes):
+    lines = [ln for ln in data.split(b"\n") if ln]
+    lo, hi = 0, len(lines)
+    while lo < hi:
+        mid = (lo + hi) // 2
+        line = lines[mid]
+        pos = line.find(b"\t")
+        if pos < 0:
+            break
+        k = line[:pos]
+        if k < key:
+            lo = mid + 1
+        elif k > key:
+            hi = mid
+        else:
+            return mid, line[pos + 1:]
+    return -1, None
+
+
+def db_get_py(tables_newest_first, key: bytes):
+    for t, data in enumerate(tables_newest_first):
+        ln, enc = table_get_py(data, key)
+        if ln < 0:
+            continue
+        v = b64_std_decode(enc)
+        if v is None:
+            continue  # Err(..) is skipped
+        return t, v
+    return -1, None
+
+
+def sstable_fixtures() -> dict:
+    import base64
+
+    def file_of(entries):  # SsTable::create (stable sort by key)
+        return b"".join(k + b"\t" + base64.b64encode(v) + b"\n" for k, v in sorted(entries, key=lambda e: e[0]))
+
+    ts0 = (0).to_bytes(8, "big")
+    files = {
+        "sstable_test": file_of([(b"b", b"2"), (b"a", b"1"), (b"c", b"3")]),
+        "lsm_flush_test": file_of([(b"k1", ts0 + b"v1"), (b"k2", ts0 + b"v2")]),
+        "sstable_local_test": file_of([(b"k", b"v")]),
+        "empty": b"",
+        "only_newlines": b"\n\n\n",
+        "empty_lines": b"\n\na\tMQ==\n\n\nb\tMg==\n\n",
+        "no_trailing_newline": b"a\tMQ==\nb\tMg==",
+        "line_without_tab": b"a\tMQ==\nbroken\nc\tMw==\n",
+        "unsorted": b"b\tMg==\na\tMQ==\n",
+        "bad_base64": b"a\tM===\nb\tMR==\nc\tMw\nd\tQUJD\ne\t\nf\t====\n",
+        "empty_key_and_tabs": b"\tMQ==\na\tMg==\tx\n",
+        "duplicates": b"a\tMQ==\na\tMg==\na\tMw==\n",
+        "utf8": "é\tMQ==\n✓\tMg==\n".encode(),
+    }
+    probes = [b"", b"a", b"b", b"c", b"d", b"e", b"f", b"k", b"k1", b"k2", b"missing", b"broken",
+              "é".encode(), "✓".encode()]
+    out = {"files_hex": {k: v.hex() for k, v in files.items()}, "probes_hex": [p.hex() for p in probes],
+           "search": {}}
+    for name, data in files.items():
+        res = []
+        for p in probes:
+            ln, enc = table_get_py(data, p)
+            dec = b64_std_decode(enc) if enc is not None else None
+            res.append({"line": ln, "value_hex": None if enc is None else enc.hex(),
+                        "decoded_hex": None if dec is None else dec.hex()})
+        out["search"][name] = res
+    s = out["search"]
+    assert s["sstable_test"][1]["decoded_hex"] == b"1".hex()          # tests/sstable_test.rs:13
+    assert s["sstable_test"][2]["decoded_hex"] == b"2".hex()          # tests/sstable_test.rs:14
+    assert s["lsm_flush_test"][8]["decoded_hex"] == (ts0 + b"v1").hex()
+    assert s["lsm_flush_test"][10]["line"] == -1                     # tests/lsm_flush_test.rs:23
+    assert s["line_without_tab"][3]["line"] == -1                    # mid hits "broken": search ends
+    assert s["unsorted"][2]["line"] == -1 and s["unsorted"][1]["line"] == 1
+    assert s["bad_base64"][1]["line"] == 0 and s["bad_base64"][1]["decoded_hex"] is None
+    # newest-first walk over 4 tables with overlaps and a bad newest value
+    stack = [b"a\tM===\nb\tYg==\n", files["sstable_test"], b"a\tb2xk\nz\tZW5k\n", files["empty_lines"]]
+    out["get_tables_hex"] = [t.hex() for t in stack]
+    out["get"] = [{"which": w, "value_hex": None if v is None else v.hex()}
+                  for w, v in (db_get_py(stack, p) for p in probes)]
+    assert out["get"][1] == {"which": 1, "value_hex": b"1".hex()}   # newest has bad base64 for "a"
+    assert out["get"][2] == {"which": 0, "value_hex": b"b".hex()}
+    return out
 
 
 def _varint(v: int) -> bytes:

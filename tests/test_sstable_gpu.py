@@ -1,0 +1,157 @@
+"""GPU parity for SURVEY.md §8f row 3: SSTable data files in HBM — the line
+index, SsTable::binary_search for key batches, base64 decoding, and
+Database::get's newest-first walk gated by the FilterSet probe. Exact against
+the golden fixtures and the C oracle.
+
+Reference: src/sstable.rs:57-72 (file format), 133-153 (get), 161-179
+(binary_search), src/lib.rs:128-134 (newest-first walk).
+"""
+import numpy as np
+import pytest
+
+from lsmt_amd import workload
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def var(keys):
+    offs = np.zeros(len(keys) + 1, np.uint64)
+    np.cumsum([len(k) for k in keys], out=offs[1:])
+    data = np.frombuffer(b"".join(keys), np.uint8).copy() if offs[-1] else np.zeros(1, np.uint8)
+    return data, offs
+
+
+def oracle_lines(data: bytes):
+    t = oracle.OracleTable(data)
+    n = t.nlines
+    st = np.ctypeslib.as_array(t._t.start, shape=(n,)).copy() if n else np.zeros(0, np.uint64)
+    en = np.ctypeslib.as_array(t._t.end, shape=(n,)).copy() if n else np.zeros(0, np.uint64)
+    return t, st, en
+
+
+def check_index(gpu, data: bytes):
+    t = gpu.Table(data)
+    ot, st, en = oracle_lines(data)
+    assert t.nlines == ot.nlines
+    s, kl, ll = t.lines()
+    assert np.array_equal(s, st)
+    assert np.array_equal(ll.astype(np.uint64), en - st)
+    raw = np.frombuffer(data, np.uint8)
+    for i in range(0, ot.nlines, max(1, ot.nlines // 500)):
+        line = raw[st[i]:en[i]]
+        tabs = np.flatnonzero(line == 9)
+        assert kl[i] == (tabs[0] if len(tabs) else 0xFFFFFFFF)
+    return t, ot
+
+
+def test_search_golden(gpu, golden):
+    g = golden["sstable"]
+    probes = [bytes.fromhex(p) for p in g["probes_hex"]]
+    d, o = var(probes)
+    kb = gpu.KeyBatch(n=len(probes), data=d, offsets=o)
+    for name, hexdata in g["files_hex"].items():
+        t, _ = check_index(gpu, bytes.fromhex(hexdata))
+        lines = t.search(kb)
+        assert list(lines) == [e["line"] for e in g["search"][name]], name
+
+
+def test_get_many_golden(gpu, golden):
+    g = golden["sstable"]
+    probes = [bytes.fromhex(p) for p in g["probes_hex"]]
+    d, o = var(probes)
+    tables = [gpu.Table(bytes.fromhex(h)) for h in g["get_tables_hex"]]
+    which, voff, vals = gpu.get_many(tables, gpu.KeyBatch(n=len(probes), data=d, offsets=o))
+    for k, exp in enumerate(g["get"]):
+        assert which[k] == exp["which"], probes[k]
+        if exp["which"] >= 0:
+            assert vals[voff[k]:voff[k + 1]].hex() == exp["value_hex"], probes[k]
+        else:
+            assert voff[k] == voff[k + 1]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_index_random_bytes(gpu, seed):
+    # dense '\n' / '\t' noise: empty lines, lines without TABs, chunk and
+    # slice boundaries everywhere; also a file without a final newline
+    rng = np.random.default_rng(seed)
+    alpha = np.frombuffer(b"\n\n\t abc", np.uint8)
+    for n in (1, 15, 16, 17, 4095, 4096, 4097, 300_001):
+        data = rng.choice(alpha, n).tobytes()
+        check_index(gpu, data)
+    long_line = b"x" * 100_000 + b"\tQQ==\n" + b"y\n"
+    check_index(gpu, long_line)
+
+
+def test_search_random_files_vs_oracle(gpu):
+    rng = np.random.default_rng(5)
+    for n in (1, 2, 3, 1000, 70_001):
+        keys = workload.key_range(900 + n, n)
+        data = workload.sstable_bytes(keys, workload.table_value(keys, 3)).tobytes()
+        t = gpu.Table(data)
+        ot = oracle.OracleTable(data)
+        look = np.concatenate([keys[rng.integers(0, n, 2000)], workload.key_range(77, 2000)])
+        got = t.search(look)
+        exp = [ot.search(bytes(k))[0] for k in look]
+        assert list(got) == exp
+        assert (got[:2000] >= 0).all() and (got[2000:] < 0).all()
+    # ragged keys against a file with unsorted and TAB-less lines
+    vk = [bytes(rng.integers(97, 100, rng.integers(0, 4), dtype=np.uint8)) for _ in range(3000)]
+    lines = b"".join(k + (b"\tQQ==\n" if i % 7 else b"\n") for i, k in enumerate(sorted(set(vk))))
+    t, ot = gpu.Table(lines), oracle.OracleTable(lines)
+    d, o = var(vk)
+    got = t.search(gpu.KeyBatch(n=len(vk), data=d, offsets=o))
+    assert list(got) == [ot.search(k)[0] for k in vk]
+
+
+def test_get_many_gated_vs_oracle(gpu):
+    # 8 tables (newest first) over one key space; overlapping keys get newer
+    # values; the FilterSet's gated probe decides which tables are searched
+    m = 1 << 20
+    nt = 8
+    per = [workload.key_range(1200 + (t % 5), 40_000 + 1000 * t) for t in range(nt)]
+    files = [workload.sstable_bytes(k, workload.table_value(k, 100 + t)) for t, k in enumerate(per)]
+    tables = [gpu.Table(f) for f in files]
+    otables = [oracle.OracleTable(f.tobytes()) for f in files]
+    filters = []
+    for k in per:
+        b = gpu.BloomFilter(m)
+        b.insert_batch(k)
+        filters.append(b)
+    s = gpu.FilterSet.from_filters(filters)
+    for i, k in enumerate(per):
+        s.zone_from_keys(i, k)
+    look = np.concatenate([per[3][:30_000], per[7][-20_000:], workload.key_range(4321, 50_000)])
+    look = look[np.random.default_rng(2).permutation(len(look))]
+    hits = s.probe(look, gated=True)
+    which, voff, vals = gpu.get_many(tables, look, hits=hits)
+    d = np.ascontiguousarray(look.reshape(-1))
+    offs = np.arange(0, 16 * (len(look) + 1), 16, dtype=np.uint64)
+    ow, ovoff, ovals = oracle.get_many(otables, hits, d, offs)
+    assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals
+    # ungated = the same answers (the gate has no false negatives)
+    w2, v2, vals2 = gpu.get_many(tables, look)
+    assert np.array_equal(w2, ow) and vals2 == ovals
+    # the value of a found key is table_value(key, 100 + table)
+    k0 = int(np.flatnonzero(which >= 0)[0])
+    t0 = int(which[k0])
+    assert vals[voff[k0]:voff[k0 + 1]] == workload.table_value(look[k0:k0 + 1], 100 + t0).tobytes()
+    # hit rows permuted: table t reads row rows[t]
+    rows = np.arange(nt)[::-1].copy()
+    w3, _, vals3 = gpu.get_many(tables, look, hits=hits[rows].copy(), hit_rows=rows)
+    assert np.array_equal(w3, ow) and vals3 == ovals
+
+
+def test_search_device_resident(gpu):
+    import torch
+    keys = workload.key_range(31, 50_000)
+    data = workload.sstable_bytes(keys, workload.table_value(keys, 1))
+    t = gpu.Table(torch.from_numpy(data).cuda())  # data already in HBM
+    dk = torch.from_numpy(keys[::-1].copy()).cuda()
+    out = torch.zeros(len(keys), dtype=torch.int64, device="cuda")
+    t.search(gpu.DeviceKeys(dk), out=out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    assert (got >= 0).all()
+    srt = workload.sort_keys16(keys)
+    assert np.array_equal(srt[got], keys[::-1])
