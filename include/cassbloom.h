@@ -226,6 +226,13 @@ int cb_set_probe_gated_var(const cb_filterset* set, const uint8_t* bytes, const 
 int cb_table_create(const uint8_t* data, uint64_t len, int device, void* stream, cb_table** out);
 int cb_table_destroy(cb_table* t);
 int cb_table_info(const cb_table* t, uint64_t* nlines, uint64_t* bytes);
+/* *out = 1 when the file is well-formed (a TAB on every line, keys strictly
+ * increasing — what SsTable::create writes): then any correct search gives
+ * the reference's answer and the prefix/fence index is used; otherwise the
+ * exact (lo+hi)/2 trajectory of src/sstable.rs:163-177 is replayed. */
+int cb_table_well_formed(const cb_table* t, int* out);
+/* Tests/bench: tables created while on != 0 always use the exact trajectory. */
+int cb_table_force_exact(int on);
 /* The line index: start offset, key length (bytes before the first TAB, or
  * UINT32_MAX when the line has none) and line length; host or device out. */
 int cb_table_lines(const cb_table* t, uint64_t* start, uint32_t* key_len, uint32_t* line_len);

@@ -605,6 +605,20 @@ class Table:
         check(_L().cb_table_info(self._h, ctypes.byref(n), None))
         return int(n.value)
 
+    @property
+    def well_formed(self) -> bool:
+        """A TAB on every line and strictly increasing keys (what SsTable::create
+        writes): searched through the prefix/fence index."""
+        v = ctypes.c_int()
+        check(_L().cb_table_well_formed(self._h, ctypes.byref(v)))
+        return bool(v.value)
+
+    @staticmethod
+    def force_exact(on: bool) -> None:
+        """Tables created while on always replay the reference's exact
+        (lo+hi)/2 search trajectory (tests / bench)."""
+        check(_L().cb_table_force_exact(int(bool(on))))
+
     def lines(self):
         """(start uint64[n], key_len uint32[n] (0xFFFFFFFF = no TAB), line_len uint32[n])."""
         n = self.nlines

@@ -68,7 +68,13 @@ struct cb_table {
   uint64_t* start = nullptr;
   uint32_t* klen = nullptr;
   uint32_t* llen = nullptr;
-  cb::TableView view() const { return cb::TableView{data, start, klen, llen, nlines}; }
+  uint64_t* pfx = nullptr;
+  uint64_t* fence = nullptr;
+  uint64_t nfence = 0;
+  bool fast = false;  // well-formed: TAB on every line, keys strictly increasing
+  cb::TableView view() const {
+    return cb::TableView{data, start, klen, llen, pfx, fence, nlines, nfence, fast ? 1u : 0u};
+  }
 };
 
 namespace {
@@ -76,6 +82,7 @@ namespace {
 thread_local std::string g_err;
 thread_local int g_last_path = 0;
 int g_path_override = 0;  // 0 auto, 1 direct, 2 tiled
+bool g_table_exact = false;  // cb_table_force_exact: index files for the exact-trajectory search only
 
 constexpr int PATH_DIRECT = 1, PATH_TILED = 2;
 constexpr size_t cb_zone_hdr_bytes = 64 * 16;  // cb::ZoneView headers
@@ -863,7 +870,7 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
   if (vals && cap >= *total && *total) {
     uint8_t* dvals;
     if ((rc = out_buf(ws.t_vals, vals, *total, s, &dvals))) return rc;
-    HIP_TRY(cb::launch_b64_decode(dviews, dwhich, (const uint64_t*)ws.t_line.p, dvoff, n, dvals, s));
+    HIP_TRY(cb::launch_b64_decode((const uint64_t*)ws.t_line.p, dvoff, n, dvals, s));
     if (dvals != vals) HIP_TRY(hipMemcpyAsync(vals, dvals, *total, hipMemcpyDeviceToHost, s));
   }
   if (dwhich != which) HIP_TRY(hipMemcpyAsync(which, dwhich, n * 4, hipMemcpyDeviceToHost, s));
@@ -1301,7 +1308,8 @@ int cb_table_destroy(cb_table* t) {
   if (!t) return CB_OK;
   {
     DeviceGuard dg(t->device);
-    for (void* p : {(void*)t->data, (void*)t->start, (void*)t->klen, (void*)t->llen})
+    for (void* p : {(void*)t->data, (void*)t->start, (void*)t->klen, (void*)t->llen, (void*)t->pfx,
+                    (void*)t->fence})
       if (p) (void)hipFree(p);
   }
   delete t;
@@ -1353,6 +1361,17 @@ int cb_table_create(const uint8_t* data, uint64_t len, int device, void* stream,
       HIP_TRY(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
       if (e) return fail(CB_EINVAL, "an SSTable line is 4 GiB or longer");
+      // prefix + fence index and the well-formed check (sstable.hpp)
+      t->nfence = (t->nlines + cb::kFenceStride - 1) / cb::kFenceStride;
+      if ((rc = dalloc((void**)&t->pfx, t->nlines * 8))) return rc;
+      if ((rc = dalloc((void**)&t->fence, t->nfence * 8))) return rc;
+      const uint32_t one = 1;
+      HIP_TRY(hipMemcpyAsync(err.p, &one, 4, hipMemcpyHostToDevice, s));
+      HIP_TRY(cb::launch_line_keys(t->data, t->nlines, t->start, t->klen, t->pfx, t->fence,
+                                   (uint32_t*)err.p, s));
+      HIP_TRY(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      t->fast = e != 0 && !g_table_exact;
     }
     for (DevBuf* b : {&cnt, &base, &tmp, &end, &err})
       if (b->p) (void)hipFree(b->p);
@@ -1367,6 +1386,17 @@ int cb_table_info(const cb_table* t, uint64_t* nlines, uint64_t* bytes) {
   if (!t) return fail(CB_EINVAL, "null table");
   if (nlines) *nlines = t->nlines;
   if (bytes) *bytes = t->len;
+  return CB_OK;
+}
+
+int cb_table_well_formed(const cb_table* t, int* out) {
+  if (!t || !out) return fail(CB_EINVAL, "null argument");
+  *out = t->fast ? 1 : 0;
+  return CB_OK;
+}
+
+int cb_table_force_exact(int on) {
+  g_table_exact = on != 0;
   return CB_OK;
 }
 

@@ -140,6 +140,67 @@ __global__ __launch_bounds__(kNT) void k_line_finish(const uint8_t* __restrict__
   llen[l] = (uint32_t)n;
 }
 
+// 8 bytes at any address p of a table's data buffer (allocated with 16 bytes
+// of slack past the file), little-endian: three aligned dword loads and two
+// byte-aligns instead of eight byte loads.
+__device__ __forceinline__ uint64_t ld8(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t x = w[0], y = w[1], z = w[2];
+  const uint32_t lo = __builtin_amdgcn_alignbyte(y, x, sh);
+  const uint32_t hi = __builtin_amdgcn_alignbyte(z, y, sh);
+  return (uint64_t)hi << 32 | lo;
+}
+
+// Up to 8 data bytes as a big-endian word, zero-padded past m.
+__device__ __forceinline__ uint64_t ld8_be(const uint8_t* p, uint64_t m) {
+  const uint64_t v = __builtin_bswap64(ld8(p));
+  return m >= 8 ? v : (m ? v & ~(~0ull >> (8 * m)) : 0);
+}
+
+// Rust str order of a line key (table data) against a query key: 8 bytes per
+// step, the data side through ld8.
+__device__ __forceinline__ int line_cmp(const uint8_t* a, uint64_t al, const uint8_t* b,
+                                        uint64_t bl) {
+  const uint64_t n = al < bl ? al : bl;
+  for (uint64_t i = 0; i < n; i += 8) {
+    const uint64_t m = n - i < 8 ? n - i : 8;
+    const uint64_t x = ld8_be(a + i, m), y = be_chunk(b + i, m);
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return al < bl ? -1 : (al > bl ? 1 : 0);
+}
+
+// First 8 bytes of a string, big-endian, zero-padded (monotone in Rust's
+// str order: x < y implies pfx8(x) <= pfx8(y)).
+__device__ __forceinline__ uint64_t pfx8(const uint8_t* p, uint64_t len) {
+  uint64_t v = 0;
+  const uint32_t n = len < 8 ? (uint32_t)len : 8u;
+  for (uint32_t i = 0; i < n; ++i) v |= (uint64_t)p[i] << (56 - 8 * i);
+  return v;
+}
+
+__global__ __launch_bounds__(kNT) void k_line_keys(const uint8_t* __restrict__ data, uint64_t nlines,
+                                                   const uint64_t* __restrict__ start,
+                                                   const uint32_t* __restrict__ klen,
+                                                   uint64_t* __restrict__ pfx,
+                                                   uint64_t* __restrict__ fence, uint32_t* ok) {
+  const uint64_t l = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  if (l >= nlines) return;
+  const uint32_t k = klen[l];
+  bool good = k != kNoSep;
+  const uint8_t* p = data + start[l];
+  const uint64_t v = good ? pfx8(p, k) : 0;
+  pfx[l] = v;
+  if (l % kFenceStride == 0) fence[l / kFenceStride] = v;
+  if (good && l > 0) {
+    const uint32_t kp = klen[l - 1];
+    good = kp != kNoSep && bytes_cmp(data + start[l - 1], kp, p, k) < 0;
+  }
+  if (!good) atomicAnd(ok, 0u);
+}
+
 // ---- exclusive scan of uint64 (tiles of 1024 = 256 threads x 4) ----
 constexpr uint32_t kScanTile = 1024;
 
@@ -197,7 +258,7 @@ __device__ __forceinline__ int64_t search_one(const TableView& t, const uint8_t*
     const uint64_t mid = (lo + hi) >> 1;
     const uint32_t klm = t.klen[mid];
     if (klm == kNoSep) break;
-    const int c = bytes_cmp(t.data + t.start[mid], klm, kp, kl);
+    const int c = line_cmp(t.data + t.start[mid], klm, kp, kl);
     if (c < 0)
       lo = mid + 1;
     else if (c > 0)
@@ -206,6 +267,48 @@ __device__ __forceinline__ int64_t search_one(const TableView& t, const uint8_t*
       return (int64_t)mid;
   }
   return -1;
+}
+
+// Well-formed files: lower bound of the key's prefix through the fences (an
+// L2-resident array), then inside one 64-line block of pfx, then full
+// compares only across lines that share the 8-byte prefix.
+__device__ __forceinline__ int64_t search_fast(const TableView& t, const uint8_t* kp, uint64_t kl,
+                                               uint64_t kpfx) {
+  uint64_t lo = 0, hi = t.nfence;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (t.fence[mid] < kpfx)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  // fence[lo-1] < kpfx <= fence[lo]: the lower bound is in ((lo-1)*64, lo*64]
+  uint64_t b = lo ? (lo - 1) * kFenceStride + 1 : 0;
+  uint64_t e = lo * kFenceStride < t.nlines ? lo * kFenceStride : t.nlines;
+  while (b < e) {
+    const uint64_t mid = (b + e) >> 1;
+    if (t.pfx[mid] < kpfx)
+      b = mid + 1;
+    else
+      e = mid;
+  }
+  for (uint64_t l = b; l < t.nlines && t.pfx[l] == kpfx; ++l) {
+    const int c = line_cmp(t.data + t.start[l], t.klen[l], kp, kl);
+    if (c == 0) return (int64_t)l;
+    if (c > 0) break;
+  }
+  return -1;
+}
+
+template <int KEYK>
+__device__ __forceinline__ uint64_t key_pfx(const KeySrc& ks, uint64_t k, const uint8_t* kp,
+                                            uint64_t kl) {
+  if constexpr (KEYK == KEY_FIXED16) {
+    const uint2 v = reinterpret_cast<const uint2*>(ks.bytes)[2 * k];  // first 8 bytes
+    return (uint64_t)__builtin_bswap32(v.x) << 32 | __builtin_bswap32(v.y);
+  } else {
+    return pfx8(kp, kl);
+  }
 }
 
 // Standard-alphabet value of a byte, -1 if outside it.
@@ -220,16 +323,24 @@ __device__ __forceinline__ int b64v(uint32_t c) {
 }
 
 // base64 0.21.7 STANDARD (canonical padding, zero trailing bits): decoded
-// length of p[0..len), or -1 if STANDARD.decode would fail.
+// length of p[0..len), or -1 if STANDARD.decode would fail. 8 bytes per step
+// (independent loads), validity accumulated without per-byte exits.
 __device__ __forceinline__ int64_t b64_len(const uint8_t* p, uint64_t len) {
   if (len & 3) return -1;
   if (!len) return 0;
   const uint32_t pad = p[len - 1] == '=' ? (p[len - 2] == '=' ? 2 : 1) : 0;
   const uint64_t body = len - pad;
   int last = 0;
-  for (uint64_t i = 0; i < body; ++i) {
-    last = b64v(p[i]);
-    if (last < 0) return -1;
+  for (uint64_t i = 0; i < body; i += 8) {
+    const uint64_t w = ld8(p + i);
+    int bad = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      const int v = i + j < body ? b64v((uint32_t)(w >> (8 * j)) & 0xFF) : 0;
+      bad |= v;  // negative iff some v < 0
+      if (i + j == body - 1) last = v;
+    }
+    if (bad < 0) return -1;
   }
   if (pad == 2 && (last & 0x0F)) return -1;
   if (pad == 1 && (last & 0x03)) return -1;
@@ -244,7 +355,7 @@ __global__ __launch_bounds__(kNT) void k_table_search(TableView t, KeySrc ks, ui
   const uint8_t* kp;
   uint64_t kl;
   key_span<KEYK>(ks, k, kp, kl);
-  line[k] = search_one(t, kp, kl);
+  line[k] = t.fast ? search_fast(t, kp, kl, key_pfx<KEYK>(ks, k, kp, kl)) : search_one(t, kp, kl);
 }
 
 template <int KEYK>
@@ -253,58 +364,119 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
                                                   const uint32_t* __restrict__ rows,
                                                   uint64_t hwords, KeySrc ks, uint64_t n,
                                                   int32_t* __restrict__ which,
-                                                  uint64_t* __restrict__ line,
+                                                  uint64_t* __restrict__ vsrc,
                                                   uint64_t* __restrict__ dlen) {
   const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   if (k >= n) return;
   const uint8_t* kp;
   uint64_t kl;
   key_span<KEYK>(ks, k, kp, kl);
+  const uint64_t kpfx = key_pfx<KEYK>(ks, k, kp, kl);
   int32_t w = -1;
   uint64_t ln = 0, d = 0;
-  for (uint32_t t = 0; t < nt; ++t) {  // tables.iter().rev(): newest first
+  // Tables in groups of 64, newest first (tables.iter().rev()). Each lane
+  // first collects its candidate tables of the group as a bit mask (one
+  // broadcast load per table: a wave's 64 keys share a hit word), then every
+  // lane searches its OWN next candidate in the same iteration, so lanes
+  // whose keys live in different tables search concurrently instead of the
+  // wave stepping through the tables one by one.
+  for (uint32_t t0 = 0; t0 < nt && w < 0; t0 += 64) {
+    const uint32_t gn = nt - t0 < 64 ? nt - t0 : 64;
+    uint64_t cand = gn == 64 ? ~0ull : ((1ull << gn) - 1);
     if (hits) {
-      const uint64_t row = rows ? rows[t] : t;
-      if (!((hits[row * hwords + (k >> 6)] >> (k & 63)) & 1)) continue;  // gate said no
+      cand = 0;
+      for (uint32_t i = 0; i < gn; ++i) {
+        const uint64_t row = rows ? rows[t0 + i] : t0 + i;
+        cand |= ((hits[row * hwords + (k >> 6)] >> (k & 63)) & 1) << i;  // the gate
+      }
     }
-    const TableView v = tv[t];
-    const int64_t r = search_one(v, kp, kl);
-    if (r < 0) continue;  // Ok(None)
-    const uint32_t kk = v.klen[r];
-    const int64_t dl = b64_len(v.data + v.start[r] + kk + 1, v.llen[r] - kk - 1);
-    if (dl < 0) continue;  // Err(..) is skipped by `if let Ok(Some(v))`
-    w = (int32_t)t;
-    ln = (uint64_t)r;
-    d = (uint64_t)dl;
-    break;
+    while (cand) {
+      const uint32_t t = t0 + (uint32_t)__builtin_ctzll(cand);
+      cand &= cand - 1;
+      const TableView v = tv[t];
+      const int64_t r = v.fast ? search_fast(v, kp, kl, kpfx) : search_one(v, kp, kl);
+      if (r < 0) continue;  // Ok(None)
+      const uint32_t kk = v.klen[r];
+      const uint8_t* src = v.data + v.start[r] + kk + 1;
+      const int64_t dl = b64_len(src, v.llen[r] - kk - 1);
+      if (dl < 0) continue;  // Err(..) is skipped by `if let Ok(Some(v))`
+      w = (int32_t)t;
+      ln = (uint64_t)(uintptr_t)src;
+      d = (uint64_t)dl;
+      break;
+    }
   }
   which[k] = w;
-  line[k] = ln;
+  vsrc[k] = ln;
   dlen[k] = d;
 }
 
-__global__ __launch_bounds__(kNT) void k_b64_decode(const TableView* __restrict__ tv,
-                                                    const int32_t* __restrict__ which,
-                                                    const uint64_t* __restrict__ line,
+// Decode 4 base64 chars (canonical, validated by b64_len) to 3 bytes.
+__device__ __forceinline__ uint32_t b64_quad(const uint8_t c[4]) {
+  return (uint32_t)(b64v(c[0]) & 63) << 18 | (uint32_t)(b64v(c[1]) & 63) << 12 |
+         (uint32_t)(b64v(c[2]) & 63) << 6 | (uint32_t)(b64v(c[3]) & 63);
+}
+
+// Lane k's value: dl bytes decoded from src (4*ceil(dl/3) canonical chars),
+// written through put(j, byte).
+template <class Put>
+__device__ __forceinline__ void b64_decode_into(const uint8_t* src, uint64_t dl, Put put) {
+  const uint64_t len = (dl + 2) / 3 * 4;
+  uint64_t j = 0;
+  for (uint64_t q = 0; q < len; q += 8) {  // two quads per step
+    const uint64_t x = ld8(src + q);
+    uint8_t c[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) c[i] = (uint8_t)(x >> (8 * i));
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+      const uint32_t w = b64_quad(c + 4 * h);
+      if (j < dl) put(j++, (uint8_t)(w >> 16));
+      if (j < dl) put(j++, (uint8_t)(w >> 8));
+      if (j < dl) put(j++, (uint8_t)w);
+    }
+  }
+}
+
+constexpr uint32_t kDecodeLds = 16384;  // staged output bytes per block
+
+// The block's values are one contiguous output range [voff[b0], voff[b0+256]).
+// When it fits in LDS, lanes decode into LDS and the block writes the range
+// with aligned dword stores; otherwise lanes write their bytes directly.
+__global__ __launch_bounds__(kNT) void k_b64_decode(const uint64_t* __restrict__ vsrc,
                                                     const uint64_t* __restrict__ voff, uint64_t n,
                                                     uint8_t* __restrict__ out) {
-  const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
-  if (k >= n || which[k] < 0) return;
-  const TableView v = tv[which[k]];
-  const uint64_t r = line[k];
-  const uint32_t kk = v.klen[r];
-  const uint8_t* p = v.data + v.start[r] + kk + 1;
-  const uint64_t len = v.llen[r] - kk - 1;
-  uint8_t* o = out + voff[k];
-  const uint64_t dl = voff[k + 1] - voff[k];
-  uint64_t j = 0;
-  for (uint64_t q = 0; q < len; q += 4) {
-    const uint32_t w = (uint32_t)(b64v(p[q]) & 63) << 18 | (uint32_t)(b64v(p[q + 1]) & 63) << 12 |
-                       (uint32_t)(b64v(p[q + 2]) & 63) << 6 | (uint32_t)(b64v(p[q + 3]) & 63);
-    if (j < dl) o[j++] = (uint8_t)(w >> 16);
-    if (j < dl) o[j++] = (uint8_t)(w >> 8);
-    if (j < dl) o[j++] = (uint8_t)w;
+  __shared__ uint8_t stage[kDecodeLds];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kNT;
+  const uint64_t k = b0 + threadIdx.x;
+  const uint64_t bend = b0 + kNT < n ? b0 + kNT : n;
+  const uint64_t base = voff[b0], total = voff[bend] - base;
+  uint64_t o = 0, dl = 0;
+  if (k < n) {
+    o = voff[k];
+    dl = voff[k + 1] - o;
   }
+  const uint8_t* src = (const uint8_t*)(uintptr_t)(k < n ? vsrc[k] : 0);
+  if (total > kDecodeLds) {  // uniform: large values, direct byte stores
+    if (dl) b64_decode_into(src, dl, [&](uint64_t j, uint8_t v) { out[o + j] = v; });
+    return;
+  }
+  if (dl) b64_decode_into(src, dl, [&](uint64_t j, uint8_t v) { stage[o - base + j] = v; });
+  __syncthreads();
+  // out[base .. base+total): bytes before the first 4-aligned address, then
+  // aligned dwords, then the tail
+  uint8_t* g = out + base;
+  const uint64_t head = ((4 - ((uintptr_t)g & 3)) & 3) < total ? ((4 - ((uintptr_t)g & 3)) & 3) : total;
+  if (threadIdx.x < head) g[threadIdx.x] = stage[threadIdx.x];
+  const uint64_t body = (total - head) / 4;
+  uint32_t* gw = reinterpret_cast<uint32_t*>(g + head);
+  for (uint64_t i = threadIdx.x; i < body; i += kNT) {
+    const uint64_t p = head + 4 * i;
+    gw[i] = (uint32_t)stage[p] | (uint32_t)stage[p + 1] << 8 | (uint32_t)stage[p + 2] << 16 |
+            (uint32_t)stage[p + 3] << 24;
+  }
+  const uint64_t tail0 = head + 4 * body;
+  if (tail0 + threadIdx.x < total) g[tail0 + threadIdx.x] = stage[tail0 + threadIdx.x];
 }
 
 inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
@@ -338,6 +510,16 @@ hipError_t launch_line_finish(const uint8_t* data, uint64_t len, uint64_t nlines
   return hipGetLastError();
 }
 
+hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, const uint64_t* start,
+                            const uint32_t* klen, uint64_t* pfx, uint64_t* fence, uint32_t* ok,
+                            hipStream_t s) {
+  if (!nlines) return hipSuccess;
+  ProfScope ps("k_line_keys", s);
+  hipLaunchKernelGGL(k_line_keys, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, data, nlines,
+                     start, klen, pfx, fence, ok);
+  return hipGetLastError();
+}
+
 uint64_t scan_tmp_words(uint64_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
 
 hipError_t launch_scan_u64(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tmp,
@@ -366,34 +548,33 @@ hipError_t launch_table_search(int keyk, const TableView& t, const KeySrc& ks, u
 
 hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uint64_t* hits,
                            const uint32_t* rows, uint64_t hwords, const KeySrc& ks, uint64_t n,
-                           int32_t* which, uint64_t* line, uint64_t* dlen, hipStream_t s) {
+                           int32_t* which, uint64_t* vsrc, uint64_t* dlen, hipStream_t s) {
   if (!n) return hipSuccess;
   ProfScope ps("k_get_many", s);
   const dim3 g(blocks_for(n, kNT));
   switch (keyk) {
     case KEY_FIXED16:
       hipLaunchKernelGGL(k_get_many<KEY_FIXED16>, g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks,
-                         n, which, line, dlen);
+                         n, which, vsrc, dlen);
       break;
     case KEY_FIXED:
       hipLaunchKernelGGL(k_get_many<KEY_FIXED>, g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n,
-                         which, line, dlen);
+                         which, vsrc, dlen);
       break;
     case KEY_VAR:
       hipLaunchKernelGGL(k_get_many<KEY_VAR>, g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n,
-                         which, line, dlen);
+                         which, vsrc, dlen);
       break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-hipError_t launch_b64_decode(const TableView* tv, const int32_t* which, const uint64_t* line,
-                             const uint64_t* voff, uint64_t n, uint8_t* out, hipStream_t s) {
+hipError_t launch_b64_decode(const uint64_t* vsrc, const uint64_t* voff, uint64_t n, uint8_t* out,
+                             hipStream_t s) {
   if (!n) return hipSuccess;
   ProfScope ps("k_b64_decode", s);
-  hipLaunchKernelGGL(k_b64_decode, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, tv, which, line, voff,
-                     n, out);
+  hipLaunchKernelGGL(k_b64_decode, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, vsrc, voff, n, out);
   return hipGetLastError();
 }
 

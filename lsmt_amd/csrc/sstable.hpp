@@ -17,13 +17,24 @@ namespace cb {
 
 constexpr uint32_t kNoSep = 0xFFFFFFFFu;  // line without a TAB: ends a search
 
+constexpr uint32_t kFenceStride = 64;  // lines per fence entry
+
 // One data file and its line index (SoA, one entry per non-empty line).
+// When the file is well-formed — every line has a TAB and the keys are
+// strictly increasing, as SsTable::create writes it — any correct search
+// returns what the reference's binary search returns, so `fast` files are
+// searched through pfx (each key's first 8 bytes, big-endian, zero-padded:
+// monotone in the key order) and fence (every 64th pfx, L2-resident).
+// Other files take the exact (lo+hi)/2 trajectory.
 struct TableView {
   const uint8_t* data;
   const uint64_t* start;  // line start offset
   const uint32_t* klen;   // bytes before the first TAB, or kNoSep
   const uint32_t* llen;   // line length (without the '\n')
-  uint64_t nlines;
+  const uint64_t* pfx;    // nlines, valid when fast
+  const uint64_t* fence;  // nfence = ceil(nlines / 64), valid when fast
+  uint64_t nlines, nfence;
+  uint32_t fast;
 };
 
 // ---- line index build: count -> scan -> emit -> finish ----
@@ -40,6 +51,12 @@ hipError_t launch_line_finish(const uint8_t* data, uint64_t len, uint64_t nlines
                               const uint64_t* start, const uint64_t* end, uint32_t* klen,
                               uint32_t* llen, uint32_t* err, hipStream_t s);
 
+// pfx per line and the well-formed check: *ok &= (every line has a TAB and
+// key[l-1] < key[l]); fence[j] = pfx[64 j].
+hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, const uint64_t* start,
+                            const uint32_t* klen, uint64_t* pfx, uint64_t* fence, uint32_t* ok,
+                            hipStream_t s);
+
 // Exclusive scan of n uint64 (out[n] = total). tmp: scan_tmp_words(n) words.
 uint64_t scan_tmp_words(uint64_t n);
 hipError_t launch_scan_u64(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tmp,
@@ -52,12 +69,13 @@ hipError_t launch_table_search(int keyk, const TableView& t, const KeySrc& ks, u
 // Database::get's walk over tv[0..nt) (tv[0] newest). Table t is asked only
 // where hits (nullable, [rows][hwords]) has bit k of row rows[t] (rows
 // nullable = identity). which[k] = first t whose line decodes as base64,
-// else -1; line[k] its line; dlen[k] the decoded length (0 if none).
+// else -1; vsrc[k] the device address of that value's base64 bytes; dlen[k]
+// the decoded length (0 if none).
 hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uint64_t* hits,
                            const uint32_t* rows, uint64_t hwords, const KeySrc& ks, uint64_t n,
-                           int32_t* which, uint64_t* line, uint64_t* dlen, hipStream_t s);
-// Decoded values of the found keys into out + voff[k].
-hipError_t launch_b64_decode(const TableView* tv, const int32_t* which, const uint64_t* line,
-                             const uint64_t* voff, uint64_t n, uint8_t* out, hipStream_t s);
+                           int32_t* which, uint64_t* vsrc, uint64_t* dlen, hipStream_t s);
+// Decoded values (voff = exclusive scan of dlen) into out + voff[k].
+hipError_t launch_b64_decode(const uint64_t* vsrc, const uint64_t* voff, uint64_t n, uint8_t* out,
+                             hipStream_t s);
 
 }  // namespace cb

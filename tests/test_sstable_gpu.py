@@ -89,16 +89,24 @@ def test_search_random_files_vs_oracle(gpu):
         keys = workload.key_range(900 + n, n)
         data = workload.sstable_bytes(keys, workload.table_value(keys, 3)).tobytes()
         t = gpu.Table(data)
+        assert t.well_formed
         ot = oracle.OracleTable(data)
         look = np.concatenate([keys[rng.integers(0, n, 2000)], workload.key_range(77, 2000)])
         got = t.search(look)
         exp = [ot.search(bytes(k))[0] for k in look]
         assert list(got) == exp
+        gpu.Table.force_exact(True)
+        try:
+            te = gpu.Table(data)
+        finally:
+            gpu.Table.force_exact(False)
+        assert not te.well_formed and list(te.search(look)) == exp
         assert (got[:2000] >= 0).all() and (got[2000:] < 0).all()
     # ragged keys against a file with unsorted and TAB-less lines
     vk = [bytes(rng.integers(97, 100, rng.integers(0, 4), dtype=np.uint8)) for _ in range(3000)]
     lines = b"".join(k + (b"\tQQ==\n" if i % 7 else b"\n") for i, k in enumerate(sorted(set(vk))))
     t, ot = gpu.Table(lines), oracle.OracleTable(lines)
+    assert not t.well_formed  # TAB-less lines: the exact trajectory
     d, o = var(vk)
     got = t.search(gpu.KeyBatch(n=len(vk), data=d, offsets=o))
     assert list(got) == [ot.search(k)[0] for k in vk]
@@ -129,6 +137,14 @@ def test_get_many_gated_vs_oracle(gpu):
     offs = np.arange(0, 16 * (len(look) + 1), 16, dtype=np.uint64)
     ow, ovoff, ovals = oracle.get_many(otables, hits, d, offs)
     assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals
+    # the exact-trajectory search gives the same answers on these files
+    gpu.Table.force_exact(True)
+    try:
+        exact = [gpu.Table(f) for f in files]
+    finally:
+        gpu.Table.force_exact(False)
+    we, voe, valse = gpu.get_many(exact, look, hits=hits)
+    assert np.array_equal(we, ow) and valse == ovals
     # ungated = the same answers (the gate has no false negatives)
     w2, v2, vals2 = gpu.get_many(tables, look)
     assert np.array_equal(w2, ow) and vals2 == ovals
@@ -140,6 +156,23 @@ def test_get_many_gated_vs_oracle(gpu):
     rows = np.arange(nt)[::-1].copy()
     w3, _, vals3 = gpu.get_many(tables, look, hits=hits[rows].copy(), hit_rows=rows)
     assert np.array_equal(w3, ow) and vals3 == ovals
+
+
+def test_well_formed_detection(gpu):
+    # prefix-sharing keys (equal 8-byte prefixes, keys shorter than 8 bytes,
+    # embedded NULs) in a well-formed file take the fast path and must agree
+    # with the oracle
+    keys = sorted({b"", b"a", b"a\x00", b"a\x00\x00", b"abcdefgh", b"abcdefgh\x00", b"abcdefghA",
+                   b"abcdefghB", b"abcdefgi", b"b" * 20, b"b" * 21, b"\xff" * 9})
+    data = b"".join(k + b"\tQQ==\n" for k in keys)
+    t, ot = gpu.Table(data), oracle.OracleTable(data)
+    assert t.well_formed
+    probes = keys + [b"a\x00\x01", b"abcdefgh\x01", b"abcdefg", b"b" * 22, b"\xff" * 8, b"\xff" * 10, b"c"]
+    d, o = var(probes)
+    assert list(t.search(gpu.KeyBatch(n=len(probes), data=d, offsets=o))) == [ot.search(k)[0] for k in probes]
+    # duplicates / unsorted / TAB-less are not well-formed
+    for bad in (b"a\tQQ==\na\tQQ==\n", b"b\tQQ==\na\tQQ==\n", b"a\tQQ==\nb\n"):
+        assert not gpu.Table(bad).well_formed
 
 
 def test_search_device_resident(gpu):
