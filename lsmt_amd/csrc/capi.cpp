@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -64,16 +65,14 @@ struct cb_filterset {
 struct cb_table {
   int device = 0;
   uint64_t len = 0, nlines = 0;
-  uint8_t* data = nullptr;
-  uint64_t* start = nullptr;
-  uint32_t* klen = nullptr;
-  uint32_t* llen = nullptr;
-  uint64_t* pfx = nullptr;
-  uint64_t* fence = nullptr;
+  uint8_t* data = nullptr;      // the file + 16 bytes of slack
+  cb::LineRec* rec = nullptr;   // per-line index record
+  uint64_t* pfx = nullptr;      // per-line 8-byte key prefix
+  uint64_t* fence = nullptr;    // every 64th prefix
   uint64_t nfence = 0;
   bool fast = false;  // well-formed: TAB on every line, keys strictly increasing
   cb::TableView view() const {
-    return cb::TableView{data, start, klen, llen, pfx, fence, nlines, nfence, fast ? 1u : 0u};
+    return cb::TableView{data, rec, pfx, fence, nlines, nfence, fast ? 1u : 0u};
   }
 };
 
@@ -1308,8 +1307,7 @@ int cb_table_destroy(cb_table* t) {
   if (!t) return CB_OK;
   {
     DeviceGuard dg(t->device);
-    for (void* p : {(void*)t->data, (void*)t->start, (void*)t->klen, (void*)t->llen, (void*)t->pfx,
-                    (void*)t->fence})
+    for (void* p : {(void*)t->data, (void*)t->rec, (void*)t->pfx, (void*)t->fence})
       if (p) (void)hipFree(p);
   }
   delete t;
@@ -1347,28 +1345,30 @@ int cb_table_create(const uint8_t* data, uint64_t len, int device, void* stream,
     HIP_TRY(hipMemcpyAsync(&t->nlines, (uint64_t*)base.p + nb, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (t->nlines) {
-      if ((rc = dalloc((void**)&t->start, t->nlines * 8))) return rc;
-      if ((rc = dalloc((void**)&t->klen, t->nlines * 4))) return rc;
-      if ((rc = dalloc((void**)&t->llen, t->nlines * 4))) return rc;
+      DevBuf start;
+      if ((rc = dalloc((void**)&t->rec, t->nlines * sizeof(cb::LineRec)))) return rc;
+      HIP_TRY(start.reserve(t->nlines * 8, s));
       HIP_TRY(end.reserve(t->nlines * 8, s));
       HIP_TRY(err.reserve(4, s));
       HIP_TRY(hipMemsetAsync(end.p, 0xFF, t->nlines * 8, s));
       HIP_TRY(hipMemsetAsync(err.p, 0, 4, s));
-      HIP_TRY(cb::launch_line_emit(t->data, len, (const uint64_t*)base.p, t->start, (uint64_t*)end.p, s));
-      HIP_TRY(cb::launch_line_finish(t->data, len, t->nlines, t->start, (const uint64_t*)end.p, t->klen,
-                                     t->llen, (uint32_t*)err.p, s));
+      HIP_TRY(cb::launch_line_emit(t->data, len, (const uint64_t*)base.p, (uint64_t*)start.p,
+                                   (uint64_t*)end.p, s));
+      HIP_TRY(cb::launch_line_finish(t->data, len, t->nlines, (const uint64_t*)start.p,
+                                     (const uint64_t*)end.p, t->rec, (uint32_t*)err.p, s));
       uint32_t e = 0;
       HIP_TRY(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
+      (void)hipFree(start.p);
+      start.p = nullptr;
       if (e) return fail(CB_EINVAL, "an SSTable line is 4 GiB or longer");
-      // prefix + fence index and the well-formed check (sstable.hpp)
+      // prefix + fence index, value validity and the well-formed check (sstable.hpp)
       t->nfence = (t->nlines + cb::kFenceStride - 1) / cb::kFenceStride;
       if ((rc = dalloc((void**)&t->pfx, t->nlines * 8))) return rc;
       if ((rc = dalloc((void**)&t->fence, t->nfence * 8))) return rc;
       const uint32_t one = 1;
       HIP_TRY(hipMemcpyAsync(err.p, &one, 4, hipMemcpyHostToDevice, s));
-      HIP_TRY(cb::launch_line_keys(t->data, t->nlines, t->start, t->klen, t->pfx, t->fence,
-                                   (uint32_t*)err.p, s));
+      HIP_TRY(cb::launch_line_keys(t->data, t->nlines, t->rec, t->pfx, t->fence, (uint32_t*)err.p, s));
       HIP_TRY(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
       t->fast = e != 0 && !g_table_exact;
@@ -1404,9 +1404,15 @@ int cb_table_lines(const cb_table* t, uint64_t* start, uint32_t* key_len, uint32
   if (!t) return fail(CB_EINVAL, "null table");
   DeviceGuard dg(t->device);
   if (!t->nlines) return CB_OK;
-  if (start) HIP_TRY(hipMemcpy(start, t->start, t->nlines * 8, hipMemcpyDefault));
-  if (key_len) HIP_TRY(hipMemcpy(key_len, t->klen, t->nlines * 4, hipMemcpyDefault));
-  if (line_len) HIP_TRY(hipMemcpy(line_len, t->llen, t->nlines * 4, hipMemcpyDefault));
+  // strided copies out of the 32-byte records
+  const size_t pitch = sizeof(cb::LineRec);
+  const uint8_t* r = (const uint8_t*)t->rec;
+  if (start)
+    HIP_TRY(hipMemcpy2D(start, 8, r + offsetof(cb::LineRec, start), pitch, 8, t->nlines, hipMemcpyDefault));
+  if (key_len)
+    HIP_TRY(hipMemcpy2D(key_len, 4, r + offsetof(cb::LineRec, klen), pitch, 4, t->nlines, hipMemcpyDefault));
+  if (line_len)
+    HIP_TRY(hipMemcpy2D(line_len, 4, r + offsetof(cb::LineRec, llen), pitch, 4, t->nlines, hipMemcpyDefault));
   return CB_OK;
 }
 

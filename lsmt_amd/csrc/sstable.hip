@@ -4,9 +4,13 @@
 // Index build is streaming byte work (HBM-bound): each block owns a 4 KiB
 // chunk, each thread 16 contiguous bytes read as one dwordx4. A byte i starts
 // a line iff data[i] != '\n' and (i == 0 or data[i-1] == '\n') — exactly the
-// non-empty pieces of raw.split('\n') (src/sstable.rs:142-146). Resolution is
-// latency-bound random access: one lane per key, binary search through the
-// start/klen arrays and the key bytes (upper levels stay L2-resident).
+// non-empty pieces of raw.split('\n') (src/sstable.rs:142-146). Per-line work
+// (TAB position, key prefixes, base64 validity of the value) is done once
+// here, so the read path only touches the index and, at the end, the value.
+//
+// Resolution is latency-bound random access: one lane per key. Each lane
+// gathers its candidate tables first and then searches its own next
+// candidate, so a wave's lanes search different tables concurrently.
 #include <hip/hip_runtime.h>
 
 #include "profile.hpp"
@@ -50,8 +54,78 @@ __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t* total) {
   return pre + (uint64_t)x - v;
 }
 
-// The 16 bytes of thread t's slice and the byte before it (0 = "before the
-// file", which counts as a line break).
+// ---- byte access helpers ----
+
+// 8 bytes at any address p of a table's data buffer (allocated with 16 bytes
+// of slack past the file), little-endian: three aligned dword loads and two
+// byte-aligns instead of eight byte loads.
+__device__ __forceinline__ uint64_t ld8(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t x = w[0], y = w[1], z = w[2];
+  const uint32_t lo = __builtin_amdgcn_alignbyte(y, x, sh);
+  const uint32_t hi = __builtin_amdgcn_alignbyte(z, y, sh);
+  return (uint64_t)hi << 32 | lo;
+}
+
+// Up to 8 data bytes as a big-endian word, zero-padded past m.
+__device__ __forceinline__ uint64_t ld8_be(const uint8_t* p, uint64_t m) {
+  const uint64_t v = __builtin_bswap64(ld8(p));
+  return m >= 8 ? v : (m ? v & ~(~0ull >> (8 * m)) : 0);
+}
+
+// Rust str order of a line key (table data, side a) against a query key.
+__device__ __forceinline__ int line_cmp(const uint8_t* a, uint64_t al, const uint8_t* b,
+                                        uint64_t bl) {
+  const uint64_t n = al < bl ? al : bl;
+  for (uint64_t i = 0; i < n; i += 8) {
+    const uint64_t m = n - i < 8 ? n - i : 8;
+    const uint64_t x = ld8_be(a + i, m), y = be_chunk(b + i, m);
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return al < bl ? -1 : (al > bl ? 1 : 0);
+}
+
+// Standard-alphabet value of a byte, -1 if outside it.
+__device__ __forceinline__ int b64v(uint32_t c) {
+  int v = -1;
+  v = (c - 'A' < 26u) ? (int)(c - 'A') : v;
+  v = (c - 'a' < 26u) ? (int)(c - 'a') + 26 : v;
+  v = (c - '0' < 10u) ? (int)(c - '0') + 52 : v;
+  v = c == '+' ? 62 : v;
+  v = c == '/' ? 63 : v;
+  return v;
+}
+
+// base64 0.21.7 STANDARD (canonical padding, zero trailing bits): decoded
+// length of p[0..len) (table data), or -1 if STANDARD.decode would fail.
+__device__ __forceinline__ int64_t b64_len(const uint8_t* p, uint64_t len) {
+  if (len & 3) return -1;
+  if (!len) return 0;
+  const uint32_t pad = p[len - 1] == '=' ? (p[len - 2] == '=' ? 2 : 1) : 0;
+  const uint64_t body = len - pad;
+  int last = 0;
+  for (uint64_t i = 0; i < body; i += 8) {
+    const uint64_t w = ld8(p + i);
+    int bad = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      const int v = i + j < body ? b64v((uint32_t)(w >> (8 * j)) & 0xFF) : 0;
+      bad |= v;  // negative iff some v < 0
+      if (i + j == body - 1) last = v;
+    }
+    if (bad < 0) return -1;
+  }
+  if (pad == 2 && (last & 0x0F)) return -1;
+  if (pad == 1 && (last & 0x03)) return -1;
+  return (int64_t)(len / 4 * 3 - pad);
+}
+
+// ---- line index ----
+
+// The 16 bytes of a thread's slice and the byte before it ('\n' before the
+// file: the first byte can start a line).
 __device__ __forceinline__ void load_slice(const uint8_t* data, uint64_t len, uint64_t base,
                                            uint8_t b[16], uint32_t& prev) {
   if (base + 16 <= len) {
@@ -119,8 +193,7 @@ __global__ __launch_bounds__(kNT) void k_line_finish(const uint8_t* __restrict__
                                                      uint64_t nlines,
                                                      const uint64_t* __restrict__ start,
                                                      const uint64_t* __restrict__ end,
-                                                     uint32_t* __restrict__ klen,
-                                                     uint32_t* __restrict__ llen, uint32_t* err) {
+                                                     LineRec* __restrict__ rec, uint32_t* err) {
   const uint64_t l = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   if (l >= nlines) return;
   const uint64_t s = start[l];
@@ -131,73 +204,52 @@ __global__ __launch_bounds__(kNT) void k_line_finish(const uint8_t* __restrict__
     return;
   }
   uint32_t k = kNoSep;
-  for (uint32_t i = 0; i < (uint32_t)n; ++i)
-    if (data[s + i] == '\t') {
-      k = i;
+  for (uint32_t i = 0; i < (uint32_t)n; i += 8) {  // first TAB, 8 bytes per step
+    const uint64_t w = ld8(data + s + i);
+    uint32_t hit = 8;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j)
+      if (hit == 8 && i + j < n && ((w >> (8 * j)) & 0xFF) == '\t') hit = j;
+    if (hit < 8) {
+      k = i + hit;
       break;
     }
-  klen[l] = k;
-  llen[l] = (uint32_t)n;
-}
-
-// 8 bytes at any address p of a table's data buffer (allocated with 16 bytes
-// of slack past the file), little-endian: three aligned dword loads and two
-// byte-aligns instead of eight byte loads.
-__device__ __forceinline__ uint64_t ld8(const uint8_t* p) {
-  const uintptr_t a = (uintptr_t)p;
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-  const uint32_t sh = (uint32_t)(a & 3);
-  const uint32_t x = w[0], y = w[1], z = w[2];
-  const uint32_t lo = __builtin_amdgcn_alignbyte(y, x, sh);
-  const uint32_t hi = __builtin_amdgcn_alignbyte(z, y, sh);
-  return (uint64_t)hi << 32 | lo;
-}
-
-// Up to 8 data bytes as a big-endian word, zero-padded past m.
-__device__ __forceinline__ uint64_t ld8_be(const uint8_t* p, uint64_t m) {
-  const uint64_t v = __builtin_bswap64(ld8(p));
-  return m >= 8 ? v : (m ? v & ~(~0ull >> (8 * m)) : 0);
-}
-
-// Rust str order of a line key (table data) against a query key: 8 bytes per
-// step, the data side through ld8.
-__device__ __forceinline__ int line_cmp(const uint8_t* a, uint64_t al, const uint8_t* b,
-                                        uint64_t bl) {
-  const uint64_t n = al < bl ? al : bl;
-  for (uint64_t i = 0; i < n; i += 8) {
-    const uint64_t m = n - i < 8 ? n - i : 8;
-    const uint64_t x = ld8_be(a + i, m), y = be_chunk(b + i, m);
-    if (x != y) return x < y ? -1 : 1;
   }
-  return al < bl ? -1 : (al > bl ? 1 : 0);
-}
-
-// First 8 bytes of a string, big-endian, zero-padded (monotone in Rust's
-// str order: x < y implies pfx8(x) <= pfx8(y)).
-__device__ __forceinline__ uint64_t pfx8(const uint8_t* p, uint64_t len) {
-  uint64_t v = 0;
-  const uint32_t n = len < 8 ? (uint32_t)len : 8u;
-  for (uint32_t i = 0; i < n; ++i) v |= (uint64_t)p[i] << (56 - 8 * i);
-  return v;
+  LineRec r;
+  r.start = s;
+  r.pfx2 = 0;
+  r.klen = k;
+  r.llen = (uint32_t)n;
+  r.vdl = kBadValue;
+  r.pad = 0;
+  rec[l] = r;
 }
 
 __global__ __launch_bounds__(kNT) void k_line_keys(const uint8_t* __restrict__ data, uint64_t nlines,
-                                                   const uint64_t* __restrict__ start,
-                                                   const uint32_t* __restrict__ klen,
+                                                   LineRec* __restrict__ rec,
                                                    uint64_t* __restrict__ pfx,
                                                    uint64_t* __restrict__ fence, uint32_t* ok) {
   const uint64_t l = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   if (l >= nlines) return;
-  const uint32_t k = klen[l];
-  bool good = k != kNoSep;
-  const uint8_t* p = data + start[l];
-  const uint64_t v = good ? pfx8(p, k) : 0;
+  LineRec r = rec[l];
+  bool good = r.klen != kNoSep;
+  const uint8_t* p = data + r.start;
+  uint64_t v = 0;
+  if (good) {
+    v = ld8_be(p, r.klen < 8 ? r.klen : 8);
+    r.pfx2 = r.klen > 8 ? ld8_be(p + 8, r.klen - 8 < 8 ? r.klen - 8 : 8) : 0;
+    const int64_t d = b64_len(p + r.klen + 1, r.llen - r.klen - 1);
+    r.vdl = d < 0 ? kBadValue : (uint32_t)d;
+  }
   pfx[l] = v;
   if (l % kFenceStride == 0) fence[l / kFenceStride] = v;
   if (good && l > 0) {
-    const uint32_t kp = klen[l - 1];
-    good = kp != kNoSep && bytes_cmp(data + start[l - 1], kp, p, k) < 0;
+    const LineRec q = rec[l - 1];  // start/klen only: written by k_line_finish
+    good = q.klen != kNoSep && bytes_cmp(data + q.start, q.klen, p, r.klen) < 0;
   }
+  // pfx2 and vdl go to separate words so the neighbour read above stays race-free
+  rec[l].pfx2 = r.pfx2;
+  rec[l].vdl = r.vdl;
   if (!good) atomicAnd(ok, 0u);
 }
 
@@ -249,102 +301,96 @@ __global__ __launch_bounds__(kNT) void k_scan_add(uint64_t* __restrict__ out, ui
     if (i0 + j < n) out[i0 + j] += add;
 }
 
-// ---- binary search and base64 ----
+// ---- search ----
+
+// A query key with its first 16 bytes as big-endian words.
+struct Query {
+  const uint8_t* p;
+  uint64_t len, w0, w1;
+};
+
+template <int KEYK>
+__device__ __forceinline__ Query make_query(const KeySrc& ks, uint64_t k) {
+  Query q;
+  key_span<KEYK>(ks, k, q.p, q.len);
+  if constexpr (KEYK == KEY_FIXED16) {
+    const uint4 v = reinterpret_cast<const uint4*>(ks.bytes)[k];
+    q.w0 = (uint64_t)__builtin_bswap32(v.x) << 32 | __builtin_bswap32(v.y);
+    q.w1 = (uint64_t)__builtin_bswap32(v.z) << 32 | __builtin_bswap32(v.w);
+  } else {
+    q.w0 = be_chunk(q.p, q.len < 8 ? q.len : 8);
+    q.w1 = q.len > 8 ? be_chunk(q.p + 8, q.len - 8 < 8 ? q.len - 8 : 8) : 0;
+  }
+  return q;
+}
+
+// Line key (pfx already known equal to q.w0) against the query. Keys of at
+// most 16 bytes compare from the index alone: zero-padded 16-byte forms
+// first, then length — the same order as Rust's str order for such keys.
+__device__ __forceinline__ int rec_cmp(const TableView& t, const LineRec& r, const Query& q) {
+  if (r.klen <= 16 && q.len <= 16) {
+    if (r.pfx2 != q.w1) return r.pfx2 < q.w1 ? -1 : 1;
+    return r.klen < q.len ? -1 : (r.klen > q.len ? 1 : 0);
+  }
+  return line_cmp(t.data + r.start, r.klen, q.p, q.len);
+}
 
 // SsTable::binary_search (src/sstable.rs:161-179), same mid sequence.
-__device__ __forceinline__ int64_t search_one(const TableView& t, const uint8_t* kp, uint64_t kl) {
+__device__ __forceinline__ int64_t search_exact(const TableView& t, const Query& q, LineRec& hit) {
   uint64_t lo = 0, hi = t.nlines;
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
-    const uint32_t klm = t.klen[mid];
-    if (klm == kNoSep) break;
-    const int c = line_cmp(t.data + t.start[mid], klm, kp, kl);
+    const LineRec r = t.rec[mid];
+    if (r.klen == kNoSep) break;
+    const int c = line_cmp(t.data + r.start, r.klen, q.p, q.len);
     if (c < 0)
       lo = mid + 1;
     else if (c > 0)
       hi = mid;
-    else
+    else {
+      hit = r;
       return (int64_t)mid;
+    }
   }
   return -1;
 }
 
 // Well-formed files: lower bound of the key's prefix through the fences (an
-// L2-resident array), then inside one 64-line block of pfx, then full
+// L2-resident array), then inside one 64-line block of pfx, then record
 // compares only across lines that share the 8-byte prefix.
-__device__ __forceinline__ int64_t search_fast(const TableView& t, const uint8_t* kp, uint64_t kl,
-                                               uint64_t kpfx) {
+__device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& q, LineRec& hit) {
   uint64_t lo = 0, hi = t.nfence;
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
-    if (t.fence[mid] < kpfx)
+    if (t.fence[mid] < q.w0)
       lo = mid + 1;
     else
       hi = mid;
   }
-  // fence[lo-1] < kpfx <= fence[lo]: the lower bound is in ((lo-1)*64, lo*64]
+  // fence[lo-1] < w0 <= fence[lo]: the lower bound is in ((lo-1)*64, lo*64]
   uint64_t b = lo ? (lo - 1) * kFenceStride + 1 : 0;
   uint64_t e = lo * kFenceStride < t.nlines ? lo * kFenceStride : t.nlines;
   while (b < e) {
     const uint64_t mid = (b + e) >> 1;
-    if (t.pfx[mid] < kpfx)
+    if (t.pfx[mid] < q.w0)
       b = mid + 1;
     else
       e = mid;
   }
-  for (uint64_t l = b; l < t.nlines && t.pfx[l] == kpfx; ++l) {
-    const int c = line_cmp(t.data + t.start[l], t.klen[l], kp, kl);
-    if (c == 0) return (int64_t)l;
+  for (uint64_t l = b; l < t.nlines && t.pfx[l] == q.w0; ++l) {
+    const LineRec r = t.rec[l];
+    const int c = rec_cmp(t, r, q);
+    if (c == 0) {
+      hit = r;
+      return (int64_t)l;
+    }
     if (c > 0) break;
   }
   return -1;
 }
 
-template <int KEYK>
-__device__ __forceinline__ uint64_t key_pfx(const KeySrc& ks, uint64_t k, const uint8_t* kp,
-                                            uint64_t kl) {
-  if constexpr (KEYK == KEY_FIXED16) {
-    const uint2 v = reinterpret_cast<const uint2*>(ks.bytes)[2 * k];  // first 8 bytes
-    return (uint64_t)__builtin_bswap32(v.x) << 32 | __builtin_bswap32(v.y);
-  } else {
-    return pfx8(kp, kl);
-  }
-}
-
-// Standard-alphabet value of a byte, -1 if outside it.
-__device__ __forceinline__ int b64v(uint32_t c) {
-  int v = -1;
-  v = (c - 'A' < 26u) ? (int)(c - 'A') : v;
-  v = (c - 'a' < 26u) ? (int)(c - 'a') + 26 : v;
-  v = (c - '0' < 10u) ? (int)(c - '0') + 52 : v;
-  v = c == '+' ? 62 : v;
-  v = c == '/' ? 63 : v;
-  return v;
-}
-
-// base64 0.21.7 STANDARD (canonical padding, zero trailing bits): decoded
-// length of p[0..len), or -1 if STANDARD.decode would fail. 8 bytes per step
-// (independent loads), validity accumulated without per-byte exits.
-__device__ __forceinline__ int64_t b64_len(const uint8_t* p, uint64_t len) {
-  if (len & 3) return -1;
-  if (!len) return 0;
-  const uint32_t pad = p[len - 1] == '=' ? (p[len - 2] == '=' ? 2 : 1) : 0;
-  const uint64_t body = len - pad;
-  int last = 0;
-  for (uint64_t i = 0; i < body; i += 8) {
-    const uint64_t w = ld8(p + i);
-    int bad = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) {
-      const int v = i + j < body ? b64v((uint32_t)(w >> (8 * j)) & 0xFF) : 0;
-      bad |= v;  // negative iff some v < 0
-      if (i + j == body - 1) last = v;
-    }
-    if (bad < 0) return -1;
-  }
-  if (pad == 2 && (last & 0x0F)) return -1;
-  if (pad == 1 && (last & 0x03)) return -1;
-  return (int64_t)(len / 4 * 3 - pad);
+__device__ __forceinline__ int64_t search(const TableView& t, const Query& q, LineRec& hit) {
+  return t.fast ? search_fast(t, q, hit) : search_exact(t, q, hit);
 }
 
 template <int KEYK>
@@ -352,10 +398,9 @@ __global__ __launch_bounds__(kNT) void k_table_search(TableView t, KeySrc ks, ui
                                                       int64_t* __restrict__ line) {
   const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   if (k >= n) return;
-  const uint8_t* kp;
-  uint64_t kl;
-  key_span<KEYK>(ks, k, kp, kl);
-  line[k] = t.fast ? search_fast(t, kp, kl, key_pfx<KEYK>(ks, k, kp, kl)) : search_one(t, kp, kl);
+  const Query q = make_query<KEYK>(ks, k);
+  LineRec r;
+  line[k] = search(t, q, r);
 }
 
 template <int KEYK>
@@ -368,12 +413,9 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
                                                   uint64_t* __restrict__ dlen) {
   const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   if (k >= n) return;
-  const uint8_t* kp;
-  uint64_t kl;
-  key_span<KEYK>(ks, k, kp, kl);
-  const uint64_t kpfx = key_pfx<KEYK>(ks, k, kp, kl);
+  const Query q = make_query<KEYK>(ks, k);
   int32_t w = -1;
-  uint64_t ln = 0, d = 0;
+  uint64_t src = 0, d = 0;
   // Tables in groups of 64, newest first (tables.iter().rev()). Each lane
   // first collects its candidate tables of the group as a bit mask (one
   // broadcast load per table: a wave's 64 keys share a hit word), then every
@@ -394,31 +436,30 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
       const uint32_t t = t0 + (uint32_t)__builtin_ctzll(cand);
       cand &= cand - 1;
       const TableView v = tv[t];
-      const int64_t r = v.fast ? search_fast(v, kp, kl, kpfx) : search_one(v, kp, kl);
-      if (r < 0) continue;  // Ok(None)
-      const uint32_t kk = v.klen[r];
-      const uint8_t* src = v.data + v.start[r] + kk + 1;
-      const int64_t dl = b64_len(src, v.llen[r] - kk - 1);
-      if (dl < 0) continue;  // Err(..) is skipped by `if let Ok(Some(v))`
+      LineRec r;
+      if (search(v, q, r) < 0) continue;  // Ok(None)
+      if (r.vdl == kBadValue) continue;   // Err(..) is skipped by `if let Ok(Some(v))`
       w = (int32_t)t;
-      ln = (uint64_t)(uintptr_t)src;
-      d = (uint64_t)dl;
+      src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
+      d = r.vdl;
       break;
     }
   }
   which[k] = w;
-  vsrc[k] = ln;
+  vsrc[k] = src;
   dlen[k] = d;
 }
 
-// Decode 4 base64 chars (canonical, validated by b64_len) to 3 bytes.
+// ---- base64 decode of the found values ----
+
+// Decode 4 base64 chars (canonical, validated at index time) to 3 bytes.
 __device__ __forceinline__ uint32_t b64_quad(const uint8_t c[4]) {
   return (uint32_t)(b64v(c[0]) & 63) << 18 | (uint32_t)(b64v(c[1]) & 63) << 12 |
          (uint32_t)(b64v(c[2]) & 63) << 6 | (uint32_t)(b64v(c[3]) & 63);
 }
 
-// Lane k's value: dl bytes decoded from src (4*ceil(dl/3) canonical chars),
-// written through put(j, byte).
+// dl bytes decoded from src (4*ceil(dl/3) canonical chars), written through
+// put(j, byte).
 template <class Put>
 __device__ __forceinline__ void b64_decode_into(const uint8_t* src, uint64_t dl, Put put) {
   const uint64_t len = (dl + 2) / 3 * 4;
@@ -466,7 +507,8 @@ __global__ __launch_bounds__(kNT) void k_b64_decode(const uint64_t* __restrict__
   // out[base .. base+total): bytes before the first 4-aligned address, then
   // aligned dwords, then the tail
   uint8_t* g = out + base;
-  const uint64_t head = ((4 - ((uintptr_t)g & 3)) & 3) < total ? ((4 - ((uintptr_t)g & 3)) & 3) : total;
+  const uint64_t mis = (4 - ((uintptr_t)g & 3)) & 3;
+  const uint64_t head = mis < total ? mis : total;
   if (threadIdx.x < head) g[threadIdx.x] = stage[threadIdx.x];
   const uint64_t body = (total - head) / 4;
   uint32_t* gw = reinterpret_cast<uint32_t*>(g + head);
@@ -501,22 +543,21 @@ hipError_t launch_line_emit(const uint8_t* data, uint64_t len, const uint64_t* b
 }
 
 hipError_t launch_line_finish(const uint8_t* data, uint64_t len, uint64_t nlines,
-                              const uint64_t* start, const uint64_t* end, uint32_t* klen,
-                              uint32_t* llen, uint32_t* err, hipStream_t s) {
+                              const uint64_t* start, const uint64_t* end, LineRec* rec,
+                              uint32_t* err, hipStream_t s) {
   if (!nlines) return hipSuccess;
   ProfScope ps("k_line_finish", s);
   hipLaunchKernelGGL(k_line_finish, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, data, len,
-                     nlines, start, end, klen, llen, err);
+                     nlines, start, end, rec, err);
   return hipGetLastError();
 }
 
-hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, const uint64_t* start,
-                            const uint32_t* klen, uint64_t* pfx, uint64_t* fence, uint32_t* ok,
-                            hipStream_t s) {
+hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, LineRec* rec, uint64_t* pfx,
+                            uint64_t* fence, uint32_t* ok, hipStream_t s) {
   if (!nlines) return hipSuccess;
   ProfScope ps("k_line_keys", s);
   hipLaunchKernelGGL(k_line_keys, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, data, nlines,
-                     start, klen, pfx, fence, ok);
+                     rec, pfx, fence, ok);
   return hipGetLastError();
 }
 

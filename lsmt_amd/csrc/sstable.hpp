@@ -18,21 +18,33 @@ namespace cb {
 constexpr uint32_t kNoSep = 0xFFFFFFFFu;  // line without a TAB: ends a search
 
 constexpr uint32_t kFenceStride = 64;  // lines per fence entry
+constexpr uint32_t kBadValue = 0xFFFFFFFFu;  // value that STANDARD.decode rejects
 
-// One data file and its line index (SoA, one entry per non-empty line).
-// When the file is well-formed — every line has a TAB and the keys are
-// strictly increasing, as SsTable::create writes it — any correct search
-// returns what the reference's binary search returns, so `fast` files are
-// searched through pfx (each key's first 8 bytes, big-endian, zero-padded:
-// monotone in the key order) and fence (every 64th pfx, L2-resident).
-// Other files take the exact (lo+hi)/2 trajectory.
+// Per-line index record (32 B, one load). vdl is computed once at index
+// time: the decoded length of the line's value, or kBadValue when base64
+// 0.21.7 STANDARD.decode would fail (or the line has no TAB) — so the read
+// path never re-validates a value. pfx2 lets keys of <= 16 bytes be
+// compared from the index alone.
+struct alignas(16) LineRec {
+  uint64_t start;  // line start offset in the file
+  uint64_t pfx2;   // key bytes 8..15, big-endian, zero-padded
+  uint32_t klen;   // bytes before the first TAB, or kNoSep
+  uint32_t llen;   // line length (without the '\n')
+  uint32_t vdl;    // decoded value length, or kBadValue
+  uint32_t pad;
+};
+
+// One data file and its line index. When the file is well-formed — every
+// line has a TAB and the keys are strictly increasing, as SsTable::create
+// writes it — any correct search returns what the reference's binary search
+// returns, so `fast` files are searched through pfx (each key's first 8
+// bytes, big-endian, zero-padded: monotone in the key order) and fence (every
+// 64th pfx, L2-resident). Other files replay the exact (lo+hi)/2 trajectory.
 struct TableView {
-  const uint8_t* data;
-  const uint64_t* start;  // line start offset
-  const uint32_t* klen;   // bytes before the first TAB, or kNoSep
-  const uint32_t* llen;   // line length (without the '\n')
-  const uint64_t* pfx;    // nlines, valid when fast
-  const uint64_t* fence;  // nfence = ceil(nlines / 64), valid when fast
+  const uint8_t* data;   // the file, with 16 bytes of readable slack
+  const LineRec* rec;    // nlines
+  const uint64_t* pfx;   // nlines
+  const uint64_t* fence; // nfence = ceil(nlines / 64)
   uint64_t nlines, nfence;
   uint32_t fast;
 };
@@ -46,16 +58,14 @@ hipError_t launch_line_count(const uint8_t* data, uint64_t len, uint64_t* cnt, h
 // the last line at EOF stay ~0: finish fills them with len)
 hipError_t launch_line_emit(const uint8_t* data, uint64_t len, const uint64_t* base,
                             uint64_t* start, uint64_t* end, hipStream_t s);
-// klen / llen per line; *err |= 1 if a line is 4 GiB or longer
+// rec[l].start/klen/llen; *err |= 1 if a line is 4 GiB or longer
 hipError_t launch_line_finish(const uint8_t* data, uint64_t len, uint64_t nlines,
-                              const uint64_t* start, const uint64_t* end, uint32_t* klen,
-                              uint32_t* llen, uint32_t* err, hipStream_t s);
-
-// pfx per line and the well-formed check: *ok &= (every line has a TAB and
-// key[l-1] < key[l]); fence[j] = pfx[64 j].
-hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, const uint64_t* start,
-                            const uint32_t* klen, uint64_t* pfx, uint64_t* fence, uint32_t* ok,
-                            hipStream_t s);
+                              const uint64_t* start, const uint64_t* end, LineRec* rec,
+                              uint32_t* err, hipStream_t s);
+// pfx, rec[l].pfx2 / vdl, fence[j] = pfx[64 j], and the well-formed check:
+// *ok &= (every line has a TAB and key[l-1] < key[l]).
+hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, LineRec* rec, uint64_t* pfx,
+                            uint64_t* fence, uint32_t* ok, hipStream_t s);
 
 // Exclusive scan of n uint64 (out[n] = total). tmp: scan_tmp_words(n) words.
 uint64_t scan_tmp_words(uint64_t n);
