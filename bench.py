@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--check", action="store_true", help="verify hits against the oracle (slow)")
     p.add_argument("--no-zone", action="store_true", help="skip the zone-map gate leg (and the read path)")
     p.add_argument("--no-read", action="store_true", help="skip the SSTable read-path leg")
+    p.add_argument("--no-flush", action="store_true", help="skip the flush-producer (SsTable::create) leg")
+    p.add_argument("--flush-entries", type=int, default=1 << 20)
     p.add_argument("--overlap", action="store_true",
                    help="N>1: run each step's all-gather on a side stream, overlapped with the next "
                         "step's probe (measured slower on one GPU: the streams share one hardware "
@@ -366,6 +368,53 @@ def main():
     if zone is not None:
         fset.assign_all(filters, stream=sh)  # zones reset; the set is unchanged otherwise
 
+    # ---- flush producer: SsTable::create on the device
+    # for a 1M-entry memtable (16-B keys, 16-B insert_ts values): data file +
+    # line index + Bloom filter (m = 2^26) + zone bounds, inputs in HBM
+    flush = None
+    if not args.no_flush:
+        nf_e = args.flush_entries
+        fk = workload.key_range(7000, nf_e)
+        fv = workload.table_value(fk, 1)
+        res = {}
+        for label, keys_np in (("sorted", workload.sort_keys16(fk)), ("unsorted", fk)):
+            kd = torch.from_numpy(np.ascontiguousarray(keys_np.reshape(-1))).to(dev)
+            vd = torch.from_numpy(np.ascontiguousarray(fv.reshape(-1))).to(dev)
+            ko = torch.from_numpy(np.arange(0, 16 * (nf_e + 1), 16, dtype=np.int64)).to(dev)
+            kbatch = lsmt_amd.KeyBatch(n=nf_e, data=kd, offsets=ko)
+            vbatch = lsmt_amd.KeyBatch(n=nf_e, data=vd, offsets=ko)
+            made = []
+
+            def step_flush():
+                made.append(lsmt_amd.sstable_create((kbatch, vbatch), m=1 << 26, device=local, stream=sh))
+                if len(made) > 2:
+                    made.pop(0)
+
+            for _ in range(max(1, args.warmup)):
+                step_flush()
+            k_fl = max(3, args.steps // 4)
+            fel = timed(step_flush, k_fl)
+            fprof = kernel_ms(["k_sorted_check", "k_sort_keys", "rocprim_merge_sort", "k_line_lens", "k_scan_u64",
+                               "k_format", "k_line_count", "k_line_emit", "k_line_finish", "k_line_keys",
+                               "k_part_build", "k_tile_build", "k_insert_direct"], step_flush, k_fl)
+            out_bytes = made[-1][0].nbytes
+            res[label] = {"entries_per_s": round(nf_e / (fel / k_fl), 1), "ms_per_flush": round(fel / k_fl * 1e3, 3),
+                          "file_bytes": out_bytes, "file_GBps": round(out_bytes / (fel / k_fl) / 1e9, 2),
+                          "kernels_us": {k: round(v["avg_us"], 2) for k, v in fprof.items()}}
+            del made, kd, vd, ko
+        flush = {"metric": f"SsTable::create entries/s ({nf_e} entries, 16-B keys, 16-B values, m=2^26), "
+                           "data file + index + Bloom filter + zone, inputs in HBM",
+                 "sorted_input": res["sorted"], "unsorted_input": res["unsorted"]}
+        if rank == 0 and world == 1 and not args.no_cpu:
+            from oracle import oracle
+            sample = 1 << 17
+            ents = [(bytes(fk[i]), bytes(fv[i])) for i in range(sample)]
+            t0 = time.perf_counter()
+            oracle.sstable_create(ents)
+            flush["cpu_baseline"] = {"value": round(sample / (time.perf_counter() - t0), 1), "unit": "entries/s",
+                                     "cores": 1, "kind": "port",
+                                     "sample": f"oracle sstable_create on {sample} unsorted entries (file only)"}
+
     # ---- C2 build: 1M keys -> one fresh 16 MiB filter (zero-fill + batched insert)
     bk = torch.from_numpy(workload.c2_build_keys(args.build_keys)).to(dev)
     bf = lsmt_amd.BloomFilter(args.build_m_bits, device=local)
@@ -446,7 +495,7 @@ def main():
             "alt_kernels_us": {k: round(v["avg_us"], 2) for k, v in kprof_alt.items()},
             "filterset": {"build_all_ms": round(set_build_ms, 3), "assign_one_empty_slot_ms": round(set_assign_ms, 3),
                           "bytes": m * (4 if F <= 32 else 8)},
-            "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e, "zone_gate": zone, "read_path": read,
+            "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e, "zone_gate": zone, "read_path": read, "flush": flush,
         }
         print(json.dumps(line), file=result, flush=True)
     if use_dist:

@@ -225,6 +225,22 @@ int cb_set_probe_gated_var(const cb_filterset* set, const uint8_t* bytes, const 
  * splits them (raw.split('\n') minus empty lines, src/sstable.rs:142-146). */
 int cb_table_create(const uint8_t* data, uint64_t len, int device, void* stream, cb_table** out);
 int cb_table_destroy(cb_table* t);
+/* Device pointer to the file bytes (valid until cb_table_destroy) and length. */
+int cb_table_data(const cb_table* t, const uint8_t** data, uint64_t* len);
+/* Copies file bytes [offset, offset+len) to out (host or device), synchronous:
+ * what storage.put(&path, data) writes (src/sstable.rs:73). */
+int cb_table_copy(const cb_table* t, uint64_t offset, uint64_t len, uint8_t* out);
+/* SsTable::create (src/sstable.rs:51-87) on the device, for n entries given as
+ * ragged key and value arrays (host or device): stable sort by key (skipped
+ * when already sorted, as memtable flushes are), the data file `key \t
+ * STANDARD.encode(value) \n` (*table_out, indexed and searchable), the
+ * table's Bloom filter of m_bits (*bloom_out, nullable: BloomFilter::new(1024)
+ * + insert per key in the reference) and its zone map as the input indices of
+ * a smallest and a largest key (UINT64_MAX when n == 0). */
+int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_t* vals,
+                      const uint64_t* val_off, uint64_t n, uint64_t m_bits, int device, void* stream,
+                      cb_table** table_out, cb_filter** bloom_out, uint64_t* zone_min_idx,
+                      uint64_t* zone_max_idx);
 int cb_table_info(const cb_table* t, uint64_t* nlines, uint64_t* bytes);
 /* *out = 1 when the file is well-formed (a TAB on every line, keys strictly
  * increasing — what SsTable::create writes): then any correct search gives

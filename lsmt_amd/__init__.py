@@ -23,10 +23,11 @@ from .bloom import (  # noqa: E402
     Table,
     TableMeta,
     get_many,
+    sstable_create,
     zone_bounds,
     ZoneMap,
 )
 
 __all__ = ["BloomFilter", "BloomProto", "DeviceKeys", "FilterSet", "insert_many", "KeyBatch", "device_count", "last_path",
-           "probe", "set_path", "unpack_hits", "zone_bounds", "ZoneMap", "TableMeta", "Table", "get_many"]
+           "probe", "set_path", "unpack_hits", "zone_bounds", "ZoneMap", "TableMeta", "Table", "get_many", "sstable_create"]
 __version__ = "0.1.0"

@@ -34,7 +34,7 @@ from . import _lib
 from ._lib import CassBloomError, check
 
 __all__ = ["BloomFilter", "BloomProto", "FilterSet", "probe", "insert_many", "set_path",
-           "last_path", "device_count", "DeviceKeys", "KeyBatch", "ZoneMap", "zone_bounds", "TableMeta", "Table", "get_many"]
+           "last_path", "device_count", "DeviceKeys", "KeyBatch", "ZoneMap", "zone_bounds", "TableMeta", "Table", "get_many", "sstable_create"]
 
 
 def _L():
@@ -606,6 +606,26 @@ class Table:
         return int(n.value)
 
     @property
+    def nbytes(self) -> int:
+        n = ctypes.c_uint64()
+        check(_L().cb_table_info(self._h, None, ctypes.byref(n)))
+        return int(n.value)
+
+    def data(self) -> bytes:
+        """The data file's bytes (what storage.put writes, src/sstable.rs:73)."""
+        n = self.nbytes
+        out = np.zeros(max(n, 1), np.uint8)
+        check(_L().cb_table_copy(self._h, 0, n, out.ctypes.data))
+        return out[:n].tobytes()
+
+    @classmethod
+    def _adopt(cls, handle: int, device: int) -> "Table":
+        t = cls.__new__(cls)
+        t._h = ctypes.c_void_p(handle)
+        t.device = device
+        return t
+
+    @property
     def well_formed(self) -> bool:
         """A TAB on every line and strictly increasing keys (what SsTable::create
         writes): searched through the prefix/fence index."""
@@ -646,6 +666,52 @@ class Table:
             kp, k1 = _ptr_of(b.keys)
             _raise(_L().cb_table_search_fixed(self._h, kp, b.key_len, b.n, op, s))
         return res
+
+
+def sstable_create(entries, m: int = 1024, device: int = 0, stream=None):
+    """SsTable::create (src/sstable.rs:51-87) on the device. entries: a list of
+    (key, value) pairs (str/bytes), or a (keys, values) pair of ragged
+    KeyBatches. Returns (Table, BloomFilter of m bits, ZoneMap)."""
+    if isinstance(entries, tuple) and len(entries) == 2 and isinstance(entries[0], KeyBatch):
+        kb, vb = entries
+    else:
+        kb = as_batch([k for k, _ in entries])
+        vb = as_batch([v for _, v in entries])
+    if not kb.is_var:
+        kb = _to_var(kb)
+    if not vb.is_var:
+        vb = _to_var(vb)
+    if kb.n != vb.n:
+        raise ValueError("keys and values differ in count")
+    th, fh = ctypes.c_void_p(), ctypes.c_void_p()
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    kd, k1 = _ptr_of(kb.data)
+    ko, k2 = _ptr_of(kb.offsets)
+    vd, k3 = _ptr_of(vb.data)
+    vo, k4 = _ptr_of(vb.offsets)
+    _raise(_L().cb_sstable_create(kd, ko, vd, vo, kb.n, int(m), int(device), _stream(stream), ctypes.byref(th),
+                                  ctypes.byref(fh), ctypes.byref(lo), ctypes.byref(hi)))
+    table = Table._adopt(th.value, device)
+    bloom = BloomFilter(0, device=device, _handle=fh.value)
+    zone = ZoneMap()
+    if kb.n:
+        zone = ZoneMap(_key_bytes(kb, lo.value), _key_bytes(kb, hi.value))
+    return table, bloom, zone
+
+
+def _to_var(b: KeyBatch) -> KeyBatch:
+    keys = np.ascontiguousarray(b.keys)
+    offs = (np.arange(0, b.key_len * (b.n + 1), b.key_len, dtype=np.uint64) if b.key_len
+            else np.zeros(b.n + 1, np.uint64))
+    data = keys.reshape(-1) if keys.size else np.zeros(1, np.uint8)
+    return KeyBatch(n=b.n, data=data, offsets=offs)
+
+
+def _key_bytes(b: KeyBatch, i: int) -> bytes:
+    o0, o1 = int(b.offsets[i]), int(b.offsets[i + 1])
+    if hasattr(b.data, "cpu"):
+        return bytes(b.data[o0:o1].cpu().numpy())
+    return np.asarray(b.data)[o0:o1].tobytes()
 
 
 def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=None, out=None):

@@ -19,6 +19,7 @@
 
 #include "cassbloom.h"
 #include "filterset.hpp"
+#include "flush.hpp"
 #include "kernels.hpp"
 #include "sstable.hpp"
 #include "zone.hpp"
@@ -33,11 +34,15 @@ struct cb_filter {
   int device = 0;
   uint32_t* words = nullptr;  // device, nwords_alloc words
   uint64_t nwords_alloc = 0;
+  size_t words_cap = 0;  // pool block size
   bool known_zero = true;  // logically all-zero (lets the tiled build skip the read)
   // cb_filter_clear is lazy: the memset is issued by the next operation that
   // needs the words, and skipped by a fresh tiled build (which writes every
   // tile). Exchanged atomically so concurrent readers issue it once.
   std::atomic<bool> needs_zero{false};
+  // Pool blocks are reused, so the padding words past ceil(m/32) are cleared
+  // once (lazily, on the caller's stream) by paths that skip the full fill.
+  std::atomic<bool> needs_pad_zero{false};
   int mode = 0;
   ModP mp{};
 };
@@ -66,6 +71,7 @@ struct cb_table {
   int device = 0;
   uint64_t len = 0, nlines = 0;
   uint8_t* data = nullptr;      // the file + 16 bytes of slack
+  size_t data_cap = 0, rec_cap = 0;  // pool block sizes
   cb::LineRec* rec = nullptr;   // per-line index record
   uint64_t* pfx = nullptr;      // per-line 8-byte key prefix
   uint64_t* fence = nullptr;    // every 64th prefix
@@ -125,10 +131,77 @@ struct DevBuf {
   }
 };
 
+// Device block pool for table and filter storage. hipMalloc of tens of MB
+// costs ~0.1 ms, which dominates a 1M-entry flush; released blocks are kept
+// per device (up to kPoolCap bytes) and handed to the next request they fit
+// (blocks are rounded to 2 MiB; a block is reused for requests of at least
+// half its size). Release synchronises the device first, exactly as hipFree
+// would, so no queued kernel can still be using a block when it is reused.
+constexpr size_t kPoolGrain = 2u << 20;
+constexpr size_t kPoolCap = size_t(16) << 30;
+
+struct BlockPool {
+  std::mutex mu;
+  std::map<int, std::multimap<size_t, void*>> free;
+  std::map<int, size_t> cached;
+};
+BlockPool g_pool;
+
+size_t pool_round(size_t bytes) { return (std::max<size_t>(bytes, 1) + kPoolGrain - 1) / kPoolGrain * kPoolGrain; }
+
+// *cap receives the block's size (pass it back to pool_release).
+hipError_t pool_alloc(int device, size_t bytes, void** p, size_t* cap) {
+  const size_t want = pool_round(bytes);
+  {
+    std::lock_guard<std::mutex> lk(g_pool.mu);
+    auto& fl = g_pool.free[device];
+    auto it = fl.lower_bound(want);
+    if (it != fl.end() && it->first <= 2 * want) {
+      *p = it->second;
+      *cap = it->first;
+      g_pool.cached[device] -= it->first;
+      fl.erase(it);
+      return hipSuccess;
+    }
+  }
+  hipError_t e = hipMalloc(p, want);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    // release the cached blocks and retry once
+    std::multimap<size_t, void*> drop;
+    {
+      std::lock_guard<std::mutex> lk(g_pool.mu);
+      drop.swap(g_pool.free[device]);
+      g_pool.cached[device] = 0;
+    }
+    for (auto& b : drop) (void)hipFree(b.second);
+    e = hipMalloc(p, want);
+    if (e != hipSuccess) return e;
+  }
+  *cap = want;
+  return hipSuccess;
+}
+
+void pool_release(int device, void* p, size_t cap) {
+  if (!p) return;
+  (void)hipDeviceSynchronize();  // what hipFree implies
+  {
+    std::lock_guard<std::mutex> lk(g_pool.mu);
+    if (g_pool.cached[device] + cap <= kPoolCap) {
+      g_pool.free[device].emplace(cap, p);
+      g_pool.cached[device] += cap;
+      return;
+    }
+  }
+  (void)hipFree(p);
+}
+
 struct Workspace {
   std::mutex mu;
   DevBuf keys, offsets, hits, seg, ent, masks, bools, lkey, zone;
   DevBuf t_views, t_rows, t_which, t_line, t_dlen, t_voff, t_scan, t_vals;
+  DevBuf i_cnt, i_base, i_tmp, i_end, i_err, i_start;                 // line indexing
+  DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_lens, f_loff, f_scan, f_flag;  // SsTable::create
 };
 
 std::mutex g_ws_mu;
@@ -175,9 +248,20 @@ uint64_t alloc_words_for(uint64_t m) {
   return bits / 32;
 }
 
+hipError_t ensure_pad_zeroed(const cb_filter* cf, hipStream_t s) {
+  cb_filter* f = const_cast<cb_filter*>(cf);
+  const uint64_t nw = (f->m + 31) / 32;
+  if (f->needs_pad_zero.exchange(false) && f->nwords_alloc > nw)
+    return hipMemsetAsync(f->words + nw, 0, (f->nwords_alloc - nw) * 4, s);
+  return hipSuccess;
+}
+
 hipError_t ensure_zeroed(const cb_filter* cf, hipStream_t s) {
   cb_filter* f = const_cast<cb_filter*>(cf);
-  if (f->needs_zero.exchange(false)) return hipMemsetAsync(f->words, 0, f->nwords_alloc * 4, s);
+  if (f->needs_zero.exchange(false)) {
+    f->needs_pad_zero.store(false);
+    return hipMemsetAsync(f->words, 0, f->nwords_alloc * 4, s);
+  }
   return hipSuccess;
 }
 
@@ -284,10 +368,12 @@ int insert_impl(cb_filter* f, const uint8_t* keys, const uint64_t* offsets, uint
   } else {
     // a fresh tiled build writes every tile of [0, T * 2^tb): the words past
     // it are padding that no insert ever sets, so a pending clear is moot.
-    if (f->known_zero)
-      f->needs_zero.store(false);
-    else
+    if (f->known_zero) {
+      if (f->needs_zero.exchange(false)) f->needs_pad_zero.store(true);
+      HIP_TRY(ensure_pad_zeroed(f, s));  // tiles past ceil(m/32) may not all be rewritten
+    } else {
       HIP_TRY(ensure_zeroed(f, s));
+    }
     // chunks of at most 4096 partition blocks of the largest block size
     const uint64_t chunk = 4096ull * 256 * 16;
     for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
@@ -878,6 +964,56 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
   return CB_OK;
 }
 
+// Line index of t->data[0..t->len) (count -> scan -> emit -> finish -> keys).
+// Temporaries come from the stream's workspace (taken here: callers must not
+// hold its lock); the index itself is one allocation: rec | pfx | fence.
+int index_table(cb_table* t, hipStream_t s) {
+  const uint64_t len = t->len;
+  if (!len) return CB_OK;
+  Workspace& ws = workspace(t->device, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  const uint64_t nb = cb::line_blocks(len);
+  HIP_TRY(ws.i_cnt.reserve(nb * 8, s));
+  HIP_TRY(ws.i_base.reserve((nb + 1) * 8, s));
+  HIP_TRY(ws.i_tmp.reserve(cb::scan_tmp_words(nb) * 8, s));
+  HIP_TRY(ws.i_err.reserve(8, s));
+  uint64_t* cnt = (uint64_t*)ws.i_cnt.p;
+  uint64_t* base = (uint64_t*)ws.i_base.p;
+  uint32_t* err = (uint32_t*)ws.i_err.p;
+  HIP_TRY(cb::launch_line_count(t->data, len, cnt, s));
+  HIP_TRY(cb::launch_scan_u64(cnt, base, nb, (uint64_t*)ws.i_tmp.p, s));
+  HIP_TRY(hipMemcpyAsync(&t->nlines, base + nb, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (!t->nlines) return CB_OK;
+  const uint64_t nl = t->nlines;
+  t->nfence = (nl + cb::kFenceStride - 1) / cb::kFenceStride;
+  const size_t bytes = nl * sizeof(cb::LineRec) + nl * 8 + t->nfence * 8;
+  if (pool_alloc(t->device, bytes, (void**)&t->rec, &t->rec_cap) != hipSuccess) {
+    t->rec = nullptr;
+    return fail(CB_ENOMEM, "device allocation failed for an SSTable index");
+  }
+  t->pfx = (uint64_t*)(t->rec + nl);
+  t->fence = t->pfx + nl;
+  HIP_TRY(ws.i_start.reserve(nl * 8, s));
+  HIP_TRY(ws.i_end.reserve(nl * 8, s));
+  uint64_t* start = (uint64_t*)ws.i_start.p;
+  uint64_t* end = (uint64_t*)ws.i_end.p;
+  HIP_TRY(hipMemsetAsync(end, 0xFF, nl * 8, s));
+  HIP_TRY(hipMemsetAsync(err, 0, 4, s));
+  const uint32_t one = 1;
+  HIP_TRY(hipMemcpyAsync(err + 1, &one, 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(cb::launch_line_emit(t->data, len, base, start, end, s));
+  HIP_TRY(cb::launch_line_finish(t->data, len, nl, start, end, t->rec, err, s));
+  // prefix + fence index, value validity and the well-formed check (sstable.hpp)
+  HIP_TRY(cb::launch_line_keys(t->data, nl, t->rec, t->pfx, t->fence, err + 1, s));
+  uint32_t e[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(e, err, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (e[0]) return fail(CB_EINVAL, "an SSTable line is 4 GiB or longer");
+  t->fast = e[1] != 0 && !g_table_exact;
+  return CB_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -935,13 +1071,11 @@ int cb_filter_create(uint64_t m_bits, int device, cb_filter** out) {
   f->device = device;
   f->nwords_alloc = alloc_words_for(m_bits);
   if (m_bits) f->mp = cb::make_modp(m_bits, &f->mode);
-  hipError_t e = hipMalloc(&f->words, f->nwords_alloc * 4);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    return fail(CB_ENOMEM, "hipMalloc failed for filter words");
-  }
-  HIP_TRY(hipMemsetAsync(f->words, 0, f->nwords_alloc * 4, nullptr));
-  HIP_TRY(hipStreamSynchronize(nullptr));
+  if (pool_alloc(device, f->nwords_alloc * 4, (void**)&f->words, &f->words_cap) != hipSuccess)
+    return fail(CB_ENOMEM, "device allocation failed for filter words");
+  // zero-filled lazily by the first operation that reads the words; a fresh
+  // tiled build writes every tile and skips the fill (see ensure_zeroed)
+  f->needs_zero.store(true);
   f->known_zero = true;
   *out = f.release();
   return CB_OK;
@@ -951,7 +1085,7 @@ int cb_filter_destroy(cb_filter* f) {
   if (!f) return CB_OK;
   {
     DeviceGuard dg(f->device);
-    if (f->words) (void)hipFree(f->words);
+    pool_release(f->device, f->words, f->words_cap);
   }
   delete f;
   return CB_OK;
@@ -1060,7 +1194,8 @@ int cb_filter_import_bools(cb_filter* f, const uint8_t* in, uint64_t m, void* st
     HIP_TRY(cb::launch_import_bools(f->words, m, (const uint8_t*)ws.bools.p, s));
     HIP_TRY(hipStreamSynchronize(s));
   }
-  f->needs_zero.store(false);  // every word < ceil(m/32) was rewritten; padding is never set
+  if (f->needs_zero.exchange(false)) f->needs_pad_zero.store(true);
+  HIP_TRY(ensure_pad_zeroed(f, s));  // every word < ceil(m/32) was rewritten
   f->known_zero = false;
   return CB_OK;
 }
@@ -1092,8 +1227,9 @@ int cb_filter_import_packed(cb_filter* f, const uint32_t* in, uint64_t nwords, v
   HIP_TRY(hipMemcpyAsync(f->words, in, nw * 4, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                          s));
   HIP_TRY(cb::launch_mask_tail(f->words, f->m, s));
+  if (f->needs_zero.exchange(false)) f->needs_pad_zero.store(true);
+  HIP_TRY(ensure_pad_zeroed(f, s));
   if (!dev) HIP_TRY(hipStreamSynchronize(s));
-  f->needs_zero.store(false);
   f->known_zero = false;
   return CB_OK;
 }
@@ -1307,8 +1443,8 @@ int cb_table_destroy(cb_table* t) {
   if (!t) return CB_OK;
   {
     DeviceGuard dg(t->device);
-    for (void* p : {(void*)t->data, (void*)t->rec, (void*)t->pfx, (void*)t->fence})
-      if (p) (void)hipFree(p);
+    pool_release(t->device, t->data, t->data_cap);
+    pool_release(t->device, t->rec, t->rec_cap);  // rec heads the one index allocation
   }
   delete t;
   return CB_OK;
@@ -1324,61 +1460,144 @@ int cb_table_create(const uint8_t* data, uint64_t len, int device, void* stream,
   std::unique_ptr<cb_table, int (*)(cb_table*)> t(new cb_table(), cb_table_destroy);
   t->device = device;
   t->len = len;
-  auto dalloc = [](void** p, size_t bytes) {
-    if (hipMalloc(p, bytes ? bytes : 16) != hipSuccess) {
-      (void)hipGetLastError();
-      return fail(CB_ENOMEM, "hipMalloc failed for an SSTable buffer");
-    }
-    return CB_OK;
-  };
-  if ((rc = dalloc((void**)&t->data, len + 16))) return rc;
-  if (len) HIP_TRY(hipMemcpyAsync(t->data, data, len, hipMemcpyDefault, s));
-  if (len) {
-    // count -> scan -> emit -> finish (sstable.hip)
-    const uint64_t nb = cb::line_blocks(len);
-    DevBuf cnt, base, tmp, end, err;
-    HIP_TRY(cnt.reserve(nb * 8, s));
-    HIP_TRY(base.reserve((nb + 1) * 8, s));
-    HIP_TRY(tmp.reserve(cb::scan_tmp_words(nb) * 8, s));
-    HIP_TRY(cb::launch_line_count(t->data, len, (uint64_t*)cnt.p, s));
-    HIP_TRY(cb::launch_scan_u64((const uint64_t*)cnt.p, (uint64_t*)base.p, nb, (uint64_t*)tmp.p, s));
-    HIP_TRY(hipMemcpyAsync(&t->nlines, (uint64_t*)base.p + nb, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    if (t->nlines) {
-      DevBuf start;
-      if ((rc = dalloc((void**)&t->rec, t->nlines * sizeof(cb::LineRec)))) return rc;
-      HIP_TRY(start.reserve(t->nlines * 8, s));
-      HIP_TRY(end.reserve(t->nlines * 8, s));
-      HIP_TRY(err.reserve(4, s));
-      HIP_TRY(hipMemsetAsync(end.p, 0xFF, t->nlines * 8, s));
-      HIP_TRY(hipMemsetAsync(err.p, 0, 4, s));
-      HIP_TRY(cb::launch_line_emit(t->data, len, (const uint64_t*)base.p, (uint64_t*)start.p,
-                                   (uint64_t*)end.p, s));
-      HIP_TRY(cb::launch_line_finish(t->data, len, t->nlines, (const uint64_t*)start.p,
-                                     (const uint64_t*)end.p, t->rec, (uint32_t*)err.p, s));
-      uint32_t e = 0;
-      HIP_TRY(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipStreamSynchronize(s));
-      (void)hipFree(start.p);
-      start.p = nullptr;
-      if (e) return fail(CB_EINVAL, "an SSTable line is 4 GiB or longer");
-      // prefix + fence index, value validity and the well-formed check (sstable.hpp)
-      t->nfence = (t->nlines + cb::kFenceStride - 1) / cb::kFenceStride;
-      if ((rc = dalloc((void**)&t->pfx, t->nlines * 8))) return rc;
-      if ((rc = dalloc((void**)&t->fence, t->nfence * 8))) return rc;
-      const uint32_t one = 1;
-      HIP_TRY(hipMemcpyAsync(err.p, &one, 4, hipMemcpyHostToDevice, s));
-      HIP_TRY(cb::launch_line_keys(t->data, t->nlines, t->rec, t->pfx, t->fence, (uint32_t*)err.p, s));
-      HIP_TRY(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipStreamSynchronize(s));
-      t->fast = e != 0 && !g_table_exact;
-    }
-    for (DevBuf* b : {&cnt, &base, &tmp, &end, &err})
-      if (b->p) (void)hipFree(b->p);
-  } else {
-    HIP_TRY(hipStreamSynchronize(s));
+  if (pool_alloc(device, len + 16, (void**)&t->data, &t->data_cap) != hipSuccess) {
+    t->data = nullptr;
+    return fail(CB_ENOMEM, "device allocation failed for an SSTable buffer");
   }
+  HIP_TRY(hipMemsetAsync(t->data + len, 0, 16, s));
+  if (len) HIP_TRY(hipMemcpyAsync(t->data, data, len, hipMemcpyDefault, s));
+  if ((rc = index_table(t.get(), s))) return rc;
+  HIP_TRY(hipStreamSynchronize(s));
   *out = t.release();
+  return CB_OK;
+}
+
+int cb_table_data(const cb_table* t, const uint8_t** data, uint64_t* len) {
+  if (!t) return fail(CB_EINVAL, "null table");
+  if (data) *data = t->data;
+  if (len) *len = t->len;
+  return CB_OK;
+}
+
+int cb_table_copy(const cb_table* t, uint64_t offset, uint64_t len, uint8_t* out) {
+  if (!t || (!out && len)) return fail(CB_EINVAL, "null argument");
+  if (offset > t->len || len > t->len - offset) return fail(CB_EINVAL, "range outside the file");
+  if (!len) return CB_OK;
+  DeviceGuard dg(t->device);
+  HIP_TRY(hipMemcpy(out, t->data + offset, len, hipMemcpyDefault));
+  return CB_OK;
+}
+
+int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_t* vals,
+                      const uint64_t* val_off, uint64_t n, uint64_t m_bits, int device, void* stream,
+                      cb_table** table_out, cb_filter** bloom_out, uint64_t* zone_min_idx,
+                      uint64_t* zone_max_idx) {
+  if (!table_out || !key_off || !val_off) return fail(CB_EINVAL, "null argument");
+  if (n >= 0xFFFFFFFFull) return fail(CB_EINVAL, "too many entries for one table");
+  *table_out = nullptr;
+  if (bloom_out) *bloom_out = nullptr;
+  if (zone_min_idx) *zone_min_idx = ~0ull;
+  if (zone_max_idx) *zone_max_idx = ~0ull;
+  int rc = cb_init(device);
+  if (rc) return rc;
+  DeviceGuard dg(device);
+  hipStream_t s = (hipStream_t)stream;
+  // entries into the stream workspace (host or device inputs)
+  std::unique_ptr<cb_table, int (*)(cb_table*)> t(new cb_table(), cb_table_destroy);
+  t->device = device;
+  const uint8_t *dk = nullptr, *dv = nullptr;
+  const uint64_t *dko = nullptr, *dvo = nullptr;
+  const cb::SortKey* order = nullptr;
+  cb::SortKey ends[2];
+  {
+    Workspace& ws = workspace(device, s);
+    std::lock_guard<std::mutex> lk(ws.mu);
+    auto stage = [&](DevBuf& dbytes, DevBuf& doff, const uint8_t* bytes, const uint64_t* off,
+                     const uint8_t** bp, const uint64_t** op) -> int {
+      uint64_t total = 0;
+      if (is_device_ptr(off)) {
+        HIP_TRY(hipMemcpyAsync(&total, off + n, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        *op = off;
+      } else {
+        for (uint64_t i = 0; i < n; ++i)
+          if (off[i + 1] < off[i]) return fail(CB_EINVAL, "offsets must be non-decreasing");
+        total = off[n];
+        HIP_TRY(doff.reserve((n + 1) * 8, s));
+        HIP_TRY(hipMemcpyAsync(doff.p, off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+        *op = (const uint64_t*)doff.p;
+      }
+      if (total && !bytes) return fail(CB_EINVAL, "null bytes");
+      if (!total || is_device_ptr(bytes)) {
+        *bp = bytes;
+      } else {
+        HIP_TRY(dbytes.reserve(total, s));
+        HIP_TRY(hipMemcpyAsync(dbytes.p, bytes, total, hipMemcpyHostToDevice, s));
+        *bp = (const uint8_t*)dbytes.p;
+      }
+      return CB_OK;
+    };
+    if ((rc = stage(ws.keys, ws.offsets, keys, key_off, &dk, &dko))) return rc;
+    if ((rc = stage(ws.f_vb, ws.f_vo, vals, val_off, &dv, &dvo))) return rc;
+    if (n) {
+      // stable sort by key unless already sorted (memtable flushes are)
+      uint32_t sorted = 1;
+      HIP_TRY(ws.f_flag.reserve(4, s));
+      HIP_TRY(hipMemcpyAsync(ws.f_flag.p, &sorted, 4, hipMemcpyHostToDevice, s));
+      HIP_TRY(cb::launch_sorted_check(dk, dko, n, (uint32_t*)ws.f_flag.p, s));
+      HIP_TRY(hipMemcpyAsync(&sorted, ws.f_flag.p, 4, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      if (!sorted) {
+        HIP_TRY(ws.f_sk.reserve(n * sizeof(cb::SortKey), s));
+        HIP_TRY(ws.f_sk2.reserve(n * sizeof(cb::SortKey), s));
+        cb::SortKey* a0 = (cb::SortKey*)ws.f_sk.p;
+        cb::SortKey* a1 = (cb::SortKey*)ws.f_sk2.p;
+        HIP_TRY(cb::launch_sort_keys(dk, dko, n, a0, s));
+        size_t tmp_bytes = 0;
+        HIP_TRY(cb::entry_sort(nullptr, tmp_bytes, a0, a1, n, dk, dko, s));
+        HIP_TRY(ws.f_sort.reserve(tmp_bytes + 16, s));
+        HIP_TRY(cb::entry_sort(ws.f_sort.p, tmp_bytes, a0, a1, n, dk, dko, s));
+        order = a1;
+      }
+      HIP_TRY(ws.f_lens.reserve(n * 8, s));
+      HIP_TRY(ws.f_loff.reserve((n + 1) * 8, s));
+      HIP_TRY(ws.f_scan.reserve(cb::scan_tmp_words(n) * 8, s));
+      uint64_t* loff = (uint64_t*)ws.f_loff.p;
+      HIP_TRY(cb::launch_line_lens(order, dko, dvo, n, (uint64_t*)ws.f_lens.p, s));
+      HIP_TRY(cb::launch_scan_u64((const uint64_t*)ws.f_lens.p, loff, n, (uint64_t*)ws.f_scan.p, s));
+      HIP_TRY(hipMemcpyAsync(&t->len, loff + n, 8, hipMemcpyDeviceToHost, s));
+      if (order) {
+        HIP_TRY(hipMemcpyAsync(&ends[0], order, sizeof(cb::SortKey), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&ends[1], order + n - 1, sizeof(cb::SortKey), hipMemcpyDeviceToHost, s));
+      }
+      HIP_TRY(hipStreamSynchronize(s));
+    }
+    if (pool_alloc(device, t->len + 16, (void**)&t->data, &t->data_cap) != hipSuccess) {
+      t->data = nullptr;
+      return fail(CB_ENOMEM, "device allocation failed for an SSTable buffer");
+    }
+    HIP_TRY(hipMemsetAsync(t->data + t->len, 0, 16, s));
+    if (n)
+      HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, (const uint64_t*)ws.f_loff.p, n, t->data, s));
+  }
+  if ((rc = index_table(t.get(), s))) return rc;
+  // zone map: ZoneMap::update over the sorted keys = first / last line
+  if (n) {
+    if (zone_min_idx) *zone_min_idx = order ? ends[0].idx : 0;
+    if (zone_max_idx) *zone_max_idx = order ? ends[1].idx : n - 1;
+  }
+  // the table's Bloom filter: SsTable::create's bloom.insert loop, batched
+  if (bloom_out) {
+    cb_filter* f = nullptr;
+    if ((rc = cb_filter_create(m_bits, device, &f))) return rc;
+    if (n && (rc = insert_impl(f, dk, dko, 0, n, s))) {
+      cb_filter_destroy(f);
+      return rc;
+    }
+    *bloom_out = f;
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  *table_out = t.release();
   return CB_OK;
 }
 
@@ -1728,10 +1947,12 @@ int cb_filter_insert_fixed_many(cb_filter* const* filters, uint32_t nf, const ui
     cb::BuildBatch bb{};
     for (uint32_t j = 0; j < nb; ++j) {
       cb_filter* f = filters[b0 + j];
-      if (f->known_zero)
-        f->needs_zero.store(false);
-      else
+      if (f->known_zero) {
+        if (f->needs_zero.exchange(false)) f->needs_pad_zero.store(true);
+        HIP_TRY(ensure_pad_zeroed(f, s));
+      } else {
         HIP_TRY(ensure_zeroed(f, s));
+      }
       bb.ks[j].bytes = dkeys[b0 + j];
       bb.ks[j].offsets = nullptr;
       bb.ks[j].key_len = key_len;

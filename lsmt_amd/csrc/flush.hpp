@@ -1,0 +1,33 @@
+// flush.hpp — SsTable::create's data file on the device (flush.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace cb {
+
+// Sort record of one entry: the key's first 16 bytes as big-endian words
+// (zero-padded), its length (clamped) and the entry's input index.
+struct SortKey {
+  uint64_t w0, w1;
+  uint32_t len, idx;
+};
+
+hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, SortKey* out,
+                            hipStream_t s);
+// *ok &= (keys already in non-decreasing order)
+hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, uint64_t n, uint32_t* ok,
+                               hipStream_t s);
+// Stable sort of the records by key (rocPRIM merge sort). tmp == nullptr:
+// only writes the scratch size to tmp_bytes.
+hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* out, uint64_t n,
+                      const uint8_t* kb, const uint64_t* ko, hipStream_t s);
+// lens[p] = byte length of the p-th output line (order == nullptr: input order)
+hipError_t launch_line_lens(const SortKey* order, const uint64_t* ko, const uint64_t* vo, uint64_t n,
+                            uint64_t* lens, hipStream_t s);
+// The lines into out at loff[p].
+hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
+                         const uint8_t* vb, const uint64_t* vo, const uint64_t* loff, uint64_t n,
+                         uint8_t* out, hipStream_t s);
+
+}  // namespace cb

@@ -230,27 +230,30 @@ __global__ __launch_bounds__(kNT) void k_line_keys(const uint8_t* __restrict__ d
                                                    uint64_t* __restrict__ pfx,
                                                    uint64_t* __restrict__ fence, uint32_t* ok) {
   const uint64_t l = (uint64_t)blockIdx.x * kNT + threadIdx.x;
-  if (l >= nlines) return;
-  LineRec r = rec[l];
-  bool good = r.klen != kNoSep;
+  const bool live = l < nlines;
+  LineRec r = live ? rec[l] : LineRec{};
+  bool good = !live || r.klen != kNoSep;
   const uint8_t* p = data + r.start;
   uint64_t v = 0;
-  if (good) {
+  if (live && good) {
     v = ld8_be(p, r.klen < 8 ? r.klen : 8);
     r.pfx2 = r.klen > 8 ? ld8_be(p + 8, r.klen - 8 < 8 ? r.klen - 8 : 8) : 0;
     const int64_t d = b64_len(p + r.klen + 1, r.llen - r.klen - 1);
     r.vdl = d < 0 ? kBadValue : (uint32_t)d;
   }
-  pfx[l] = v;
-  if (l % kFenceStride == 0) fence[l / kFenceStride] = v;
-  if (good && l > 0) {
-    const LineRec q = rec[l - 1];  // start/klen only: written by k_line_finish
-    good = q.klen != kNoSep && bytes_cmp(data + q.start, q.klen, p, r.klen) < 0;
+  if (live) {
+    pfx[l] = v;
+    if (l % kFenceStride == 0) fence[l / kFenceStride] = v;
+    if (good && l > 0) {
+      const LineRec q = rec[l - 1];  // start/klen only: written by k_line_finish
+      good = q.klen != kNoSep && bytes_cmp(data + q.start, q.klen, p, r.klen) < 0;
+    }
+    // pfx2 and vdl go to separate words so the neighbour read above stays race-free
+    rec[l].pfx2 = r.pfx2;
+    rec[l].vdl = r.vdl;
   }
-  // pfx2 and vdl go to separate words so the neighbour read above stays race-free
-  rec[l].pfx2 = r.pfx2;
-  rec[l].vdl = r.vdl;
-  if (!good) atomicAnd(ok, 0u);
+  // one atomic per block, none once the flag is down
+  if (__syncthreads_or(!good) && threadIdx.x == 0 && *(volatile uint32_t*)ok) atomicAnd(ok, 0u);
 }
 
 // ---- exclusive scan of uint64 (tiles of 1024 = 256 threads x 4) ----

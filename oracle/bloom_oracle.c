@@ -694,6 +694,45 @@ int ob_get_many(const ob_table* const* tables, uint32_t nt, const uint64_t* hits
   return OB_OK;
 }
 
+/* ---- SsTable::create (src/sstable.rs:56-72) ---- */
+
+static const uint8_t* g_sort_kb;
+static const uint64_t* g_sort_ko;
+
+static int entry_cmp(const void* x, const void* y) {
+  uint64_t i = *(const uint64_t*)x, j = *(const uint64_t*)y;
+  int c = ob_bytes_cmp(g_sort_kb + g_sort_ko[i], g_sort_ko[i + 1] - g_sort_ko[i], g_sort_kb + g_sort_ko[j],
+                       g_sort_ko[j + 1] - g_sort_ko[j]);
+  if (c) return c;
+  return i < j ? -1 : (i > j); /* Rust's sort_by is stable: equal keys keep input order */
+}
+
+uint64_t ob_sstable_create(const uint8_t* kbytes, const uint64_t* koff, const uint8_t* vbytes,
+                           const uint64_t* voff, uint64_t n, uint8_t* out, uint64_t cap) {
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; ++i)
+    total += (koff[i + 1] - koff[i]) + 1 + 4 * ((voff[i + 1] - voff[i] + 2) / 3) + 1;
+  if (!out || cap < total || !n) return total;
+  uint64_t* ord = (uint64_t*)malloc(n * 8);
+  if (!ord) return 0;
+  for (uint64_t i = 0; i < n; ++i) ord[i] = i;
+  g_sort_kb = kbytes;
+  g_sort_ko = koff;
+  qsort(ord, (size_t)n, 8, entry_cmp); /* not thread-safe: test infrastructure only */
+  uint8_t* p = out;
+  for (uint64_t r = 0; r < n; ++r) {
+    uint64_t i = ord[r];
+    uint64_t kl = koff[i + 1] - koff[i];
+    memcpy(p, kbytes + koff[i], (size_t)kl);
+    p += kl;
+    *p++ = '\t';                                                           /* SEP */
+    p += ob_b64_encode(vbytes + voff[i], voff[i + 1] - voff[i], p);        /* STANDARD.encode */
+    *p++ = '\n';                                                           /* NL */
+  }
+  free(ord);
+  return total;
+}
+
 /* ---- synthetic workload ---- */
 
 uint64_t ob_splitmix64(uint64_t x) {

@@ -155,6 +155,13 @@ int ob_get_many(const ob_table* const* tables, uint32_t nt, const uint64_t* hits
                 const uint8_t* bytes, const uint64_t* offsets, uint64_t n, int32_t* which,
                 uint64_t* val_off, uint8_t* vals, uint64_t cap, uint64_t* total);
 
+/* SsTable::create's data file (src/sstable.rs:56-72): entries stably sorted
+ * by key (sort_by on &str), each written as key \t STANDARD.encode(value) \n.
+ * Keys/values are ragged arrays (offsets n+1). Returns the file length;
+ * writes only if cap is large enough. */
+uint64_t ob_sstable_create(const uint8_t* kbytes, const uint64_t* koff, const uint8_t* vbytes,
+                           const uint64_t* voff, uint64_t n, uint8_t* out, uint64_t cap);
+
 /* Synthetic workload keys: 16 lowercase hex chars, MSB
  * nibble first, of splitmix64(seed * 2^32 + i). out is n*16 bytes. */
 void ob_gen_keys(uint64_t seed, uint64_t first, uint64_t n, uint8_t* out);

@@ -99,6 +99,8 @@ def lib():
         L.ob_b64_encode.argtypes = [P, u64, P]
         L.ob_b64_encode.restype = u64
         L.ob_get_many.argtypes = [P, u32, P, P, P, u64, P, P, P, u64, ctypes.POINTER(u64)]
+        L.ob_sstable_create.argtypes = [P, P, P, P, u64, P, u64]
+        L.ob_sstable_create.restype = u64
         L.ob_gen_keys.argtypes = [u64, u64, u64, P]
         L.ob_gen_keys.restype = None
         L.ob_splitmix64.argtypes = [u64]
@@ -382,6 +384,25 @@ def get_many(tables, hits, data: np.ndarray, offsets: np.ndarray):
     if rc:
         raise RuntimeError(rc)
     return which[:n], voff, vals[: total.value].tobytes()
+
+
+def _ragged(items):
+    offs = np.zeros(len(items) + 1, np.uint64)
+    np.cumsum([len(x) for x in items], out=offs[1:])
+    data = np.frombuffer(b"".join(items), np.uint8).copy() if offs[-1] else np.zeros(1, np.uint8)
+    return data, offs
+
+
+def sstable_create(entries) -> bytes:
+    """SsTable::create's data file for [(key bytes, value bytes)]."""
+    kd, ko = _ragged([k for k, _ in entries])
+    vd, vo = _ragged([v for _, v in entries])
+    L = lib()
+    n = len(entries)
+    total = L.ob_sstable_create(_ptr(kd), _ptr(ko), _ptr(vd), _ptr(vo), n, None, 0)
+    out = np.zeros(max(total, 1), np.uint8)
+    L.ob_sstable_create(_ptr(kd), _ptr(ko), _ptr(vd), _ptr(vo), n, _ptr(out), total)
+    return out[:total].tobytes()
 
 
 def gen_keys(seed: int, n: int, first: int = 0) -> np.ndarray:

@@ -289,6 +289,9 @@ def main() -> None:
     #    (src/sstable.rs:57-72,133-179; src/lib.rs:128-134)
     g["sstable"] = sstable_fixtures()
 
+    # 10. SsTable::create's data file (src/sstable.rs:56-72)
+    g["create"] = create_fixtures()
+
     with open(os.path.join(HERE, "golden.json"), "w") as fh:
         json.dump(g, fh, indent=1, sort_keys=True)
     print("wrote", os.path.join(HERE, "golden.json"))
@@ -588,6 +591,37 @@ def sstable_fixtures() -> dict:
                   for w, v in (db_get_py(stack, p) for p in probes)]
     assert out["get"][1] == {"which": 1, "value_hex": b"1".hex()}   # newest has bad base64 for "a"
     assert out["get"][2] == {"which": 0, "value_hex": b"b".hex()}
+    return out
+
+
+def create_fixtures() -> dict:
+    """Python's sorted() is stable and orders bytes as Rust orders &str."""
+    import base64
+
+    def create_py(entries):
+        return b"".join(k + b"\t" + base64.b64encode(v) + b"\n" for k, v in sorted(entries, key=lambda e: e[0]))
+
+    rng = np.random.default_rng(21)
+    cases = {
+        "sstable_test": [(b"b", b"2"), (b"a", b"1"), (b"c", b"3")],
+        "lsm_flush_test": [(b"k1", (0).to_bytes(8, "big") + b"v1"), (b"k2", (0).to_bytes(8, "big") + b"v2")],
+        "empty": [],
+        "duplicates_stable": [(b"k", b"first"), (b"a", b""), (b"k", b"second"), (b"a", b"x"), (b"k", b"third")],
+        "value_lengths": [(bytes([97 + i]), bytes(range(i))) for i in range(12)],
+        "binary_values": [(b"v%03d" % i, rng.integers(0, 256, int(rng.integers(0, 70)), dtype=np.uint8).tobytes())
+                          for i in range(40)][::-1],
+        "shared_prefixes": [(k, k[::-1]) for k in [b"abcdefghijklmnopq", b"abcdefghijklmnop", b"abcdefghijklmnopa",
+                                                   b"abcdefghijklmnoo", b"abcdefgh", b"abcdefgh\x00", b"", b"\xff",
+                                                   b"abcdefghijklmnop\x00", "é".encode()]],
+        "long_value": [(b"big", bytes(range(256)) * 8), (b"a", b"z" * 1001)],
+    }
+    out = {}
+    for name, entries in cases.items():
+        f = create_py(entries)
+        out[name] = {"keys_hex": [k.hex() for k, _ in entries], "values_hex": [v.hex() for _, v in entries],
+                     "file_hex": f.hex(), "len": len(f)}
+    assert bytes.fromhex(out["sstable_test"]["file_hex"]) == b"a\tMQ==\nb\tMg==\nc\tMw==\n"  # sstable_test.rs:20-25
+    assert bytes.fromhex(out["duplicates_stable"]["file_hex"]).startswith(b"a\t\na\teA==\nk\tZmlyc3Q=\n")
     return out
 
 
