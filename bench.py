@@ -396,7 +396,7 @@ def main():
             fel = timed(step_flush, k_fl)
             fprof = kernel_ms(["k_sorted_check", "k_sort_keys", "rocprim_merge_sort", "k_line_lens", "k_scan_u64",
                                "k_format", "k_line_count", "k_line_emit", "k_line_finish", "k_line_keys",
-                               "k_part_build", "k_tile_build", "k_insert_direct"], step_flush, k_fl)
+                               "k_build_part", "k_build_tile", "k_insert_direct"], step_flush, k_fl)
             out_bytes = made[-1][0].nbytes
             res[label] = {"entries_per_s": round(nf_e / (fel / k_fl), 1), "ms_per_flush": round(fel / k_fl * 1e3, 3),
                           "file_bytes": out_bytes, "file_GBps": round(out_bytes / (fel / k_fl) / 1e9, 2),
@@ -427,7 +427,7 @@ def main():
     for _ in range(args.warmup):
         build_step()
     bel = timed(build_step, args.steps)
-    bprof = kernel_ms(["k_part_build", "k_tile_build", "k_insert_direct"], build_step, args.steps)
+    bprof = kernel_ms(["k_build_part", "k_build_tile", "k_insert_direct"], build_step, args.steps)
     b_alg = 16 * args.build_keys + args.build_m_bits / 8
     build = {"metric": "build keys/s (C2: 1M 16-B keys -> one 16 MiB filter, m=2^27)",
              "value": round(args.build_keys * world / (bel / args.steps), 1), "unit": "keys/s",

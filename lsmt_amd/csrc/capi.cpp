@@ -1936,7 +1936,7 @@ int cb_filter_insert_fixed_many(cb_filter* const* filters, uint32_t nf, const ui
       }
     staged = true;
   }
-  const TilePlan p = cb::plan_build(f0->m, nmax);
+  const TilePlan p = cb::plan_build(f0->m, nmax, std::min<uint32_t>(nf, cb::kMaxBuildBatch));
   for (uint32_t i = 0; i < nf; ++i)
     if (!covers(filters[i], p)) return fail(CB_EINVAL, "internal: build tile plan exceeds the filter allocation");
   bool all16 = key_len == 16;

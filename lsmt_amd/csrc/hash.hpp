@@ -62,6 +62,46 @@ struct H64 {
   }
 };
 
+// 16-byte keys, 32-bit state, without the byte loop. Unrolled, the fold is
+//   h = seed*M^16 + sum_i b_i * M^(15-i)   (mod 2^32),  M = 33 or 31.
+// Splitting each coefficient c_i = M^(15-i) into its four bytes c_i[p] gives
+//   sum_i b_i c_i = sum_p 2^(8p) * sum_i b_i c_i[p],
+// and each inner sum over a key word's four bytes is one v_dot4_u32_u8 (u8 x
+// u8 products accumulated in u32; a plane's total is < 16 * 255^2, so it never
+// wraps). 16 dot4 + 4 adds per hash instead of 16 multiply-add steps plus byte
+// extraction. Exact mod 2^32, hence exact for MOD_POW2_32 (see the header).
+namespace dot16 {
+constexpr uint32_t powm(uint32_t mul, int e) {
+  uint32_t r = 1;
+  for (int i = 0; i < e; ++i) r *= mul;
+  return r;
+}
+// K(mul, w, p): byte j = byte p of mul^(15 - (4w + j))
+constexpr uint32_t K(uint32_t mul, int w, int p) {
+  uint32_t k = 0;
+  for (int j = 0; j < 4; ++j) k |= ((powm(mul, 15 - (4 * w + j)) >> (8 * p)) & 0xFFu) << (8 * j);
+  return k;
+}
+template <uint32_t MUL, uint32_t SEED>
+__device__ __forceinline__ uint32_t fold(const uint4& v) {
+  uint32_t acc[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    uint32_t a = __builtin_amdgcn_udot4(v.x, K(MUL, 0, p), 0u, false);
+    a = __builtin_amdgcn_udot4(v.y, K(MUL, 1, p), a, false);
+    a = __builtin_amdgcn_udot4(v.z, K(MUL, 2, p), a, false);
+    acc[p] = __builtin_amdgcn_udot4(v.w, K(MUL, 3, p), a, false);
+  }
+  constexpr uint32_t H0 = SEED * powm(MUL, 16);
+  return H0 + acc[0] + (acc[1] << 8) + (acc[2] << 16) + (acc[3] << 24);
+}
+}  // namespace dot16
+
+__device__ __forceinline__ void hash16_u32(const uint4& v, uint32_t& h1, uint32_t& h2) {
+  h1 = dot16::fold<33u, 5381u>(v);  // src/bloom.rs:29-31
+  h2 = dot16::fold<31u, 0u>(v);     // src/bloom.rs:32-34
+}
+
 template <class H>
 __device__ __forceinline__ void hash_range(const uint8_t* p, uint64_t len, H& h) {
   uint64_t i = 0;
@@ -98,7 +138,13 @@ __device__ __forceinline__ uint64_t fastmod(uint64_t h, const ModP& mp) {
 template <int KEYK, int MODE>
 __device__ __forceinline__ void key_positions(const KeySrc& ks, uint64_t k, const ModP& mp,
                                               uint64_t& a, uint64_t& b) {
-  if constexpr (MODE == MOD_POW2_32) {
+  if constexpr (MODE == MOD_POW2_32 && KEYK == KEY_FIXED16) {
+    uint32_t h1, h2;
+    hash16_u32(reinterpret_cast<const uint4*>(ks.bytes)[k], h1, h2);
+    const uint32_t mask = static_cast<uint32_t>(mp.mask);
+    a = h1 & mask;
+    b = h2 & mask;
+  } else if constexpr (MODE == MOD_POW2_32) {
     H32 h;
     hash_key<KEYK>(ks, k, h);
     const uint32_t mask = static_cast<uint32_t>(mp.mask);
@@ -123,14 +169,11 @@ template <int MODE>
 __device__ __forceinline__ void key_positions_u4(const uint4& v, const ModP& mp, uint64_t& a,
                                                  uint64_t& b) {
   if constexpr (MODE == MOD_POW2_32) {
-    H32 h;
-    h.word(v.x);
-    h.word(v.y);
-    h.word(v.z);
-    h.word(v.w);
+    uint32_t h1, h2;
+    hash16_u32(v, h1, h2);
     const uint32_t mask = static_cast<uint32_t>(mp.mask);
-    a = h.h1 & mask;
-    b = h.h2 & mask;
+    a = h1 & mask;
+    b = h2 & mask;
   } else {
     H64 h;
     h.word(v.x);

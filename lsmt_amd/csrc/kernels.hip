@@ -26,6 +26,23 @@
 #include "kernels.hpp"
 #include "profile.hpp"
 
+// Phase stamps for diagnostics (tools/ubench_build.hip defines CB_STAMPS and
+// provides g_stamps): wall-clock s_memrealtime at phase boundaries, one row of
+// 8 per workgroup. Compiled out of the library.
+#ifdef CB_STAMPS
+__device__ uint64_t* g_stamps;
+#define CB_STAMP(i)                                                                   \
+  do {                                                                                \
+    if (threadIdx.x == 0 && g_stamps)                                                 \
+      g_stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] =             \
+          __builtin_amdgcn_s_memrealtime();                                           \
+  } while (0)
+#else
+#define CB_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
 namespace cb {
 
 namespace {
@@ -181,115 +198,195 @@ __global__ __launch_bounds__(kBlock) void k_probe_direct(FilterPtrs fp, uint32_t
 
 constexpr uint32_t kPartThreads = 256;
 
-// Partition for build: every key contributes two entries (bit a, bit b), each
-// bucketed by its tile. Per block: LDS histogram with ranks, block scan, LDS
-// staging in tile order, coalesced writes of the block's run and run table.
+// ------------------------------------------------------- build ------------
+//
+// Two passes. Every key contributes two entries (bit a, bit b), bucketed by
+// the filter tile they fall in; then one workgroup per tile ORs its entries
+// into the tile in LDS and writes the tile back once. At C2 size a pass over
+// 16 MiB is ~3 us of bandwidth, so the dependent steps, not the bytes, set the
+// time (tools/ubench_build.hip stamps the phases):
+//   k_build_part — 1024-thread blocks of KPT keys per thread (C = 1024*KPT).
+//                  All key loads issue before any LDS work; ranks from LDS
+//                  atomics; the block's entries leave tile-sorted as one
+//                  contiguous region, its run starts as one row of seg.
+//   k_build_tile — one 1024-thread workgroup per tile of up to 2^19 bits
+//                  (64 KiB of LDS). Wave w reads whole runs (lane i = entry i
+//                  of the run, one coalesced load per run), 8 runs in flight
+//                  per wave, so the 128-B lines of a run are fetched by one
+//                  instruction instead of by 64 lanes' scattered loads.
+// Fewer, larger tiles (~256 for C2) and larger blocks make the average run
+// ~32 entries = one 128-B line.
+constexpr uint32_t kBuildNT = 1024;
+
+// Exclusive scan of arr[0..len) in LDS by wave 0 alone (the other waves wait
+// at the caller's next barrier); arr[len] receives the total. One barrier
+// fewer than block_exclusive_scan and no cross-wave partials.
+__device__ __forceinline__ void wave0_exclusive_scan(uint32_t* arr, uint32_t len) {
+  if (threadIdx.x >= 64) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t per = (len + 63) / 64;
+  const uint32_t beg = min(lane * per, len), end = min(beg + per, len);
+  uint32_t sum = 0;
+  for (uint32_t i = beg; i < end; ++i) sum += arr[i];
+  uint32_t x = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  uint32_t run = x - sum;
+  for (uint32_t i = beg; i < end; ++i) {
+    const uint32_t v = arr[i];
+    arr[i] = run;
+    run += v;
+  }
+  if (lane == 63) arr[len] = x;
+}
+
 template <int KEYK, int MODE, int KPT>
-__global__ __launch_bounds__(kPartThreads) void k_part_build(BuildBatch bb, ModP mp, uint32_t tb,
-                                                             uint32_t T,
-                                                             uint32_t* __restrict__ seg_all,
-                                                             uint32_t* __restrict__ ent_all) {
-  constexpr uint32_t C = kPartThreads * KPT;
-  // blockIdx.y = filter of the batch: its keys, its run table and entries.
+__global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp, uint32_t tb,
+                                                         uint32_t T,
+                                                         uint32_t* __restrict__ seg_all,
+                                                         uint32_t* __restrict__ ent_all) {
+  constexpr uint32_t NT = kBuildNT, C = NT * KPT;
   const KeySrc ks = bb.ks[blockIdx.y];
   const uint64_t n = bb.n[blockIdx.y];
   uint32_t* seg = seg_all + (size_t)blockIdx.y * gridDim.x * (T + 1);
   uint32_t* ent = ent_all + (size_t)blockIdx.y * gridDim.x * (2 * C);
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t Tp = (T + 4) & ~3u;
-  uint32_t* hist = smem;
+  uint32_t* hist = smem;  // T + 1 entries: counts, then run starts and the total
   uint32_t* stage = smem + Tp;
-  uint32_t* wsum = stage + 2 * C;
   const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < Tp; i += kPartThreads) hist[i] = 0;
-  __syncthreads();
-
   const uint64_t kbase = (uint64_t)blockIdx.x * C;
-  const uint32_t tmask = (1u << tb) - 1u;
-  uint32_t et[2 * KPT], er[2 * KPT], eo[2 * KPT];
+  CB_STAMP(0);
+
+  // positions first: every key load of the thread is in flight together
+  uint64_t pa[KPT], pb[KPT];
+  bool ok[KPT];
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
-    const uint64_t k = kbase + (uint64_t)j * kPartThreads + tid;
+    const uint64_t k = kbase + (uint64_t)j * NT + tid;
+    ok[j] = k < n;
+    pa[j] = pb[j] = 0;
+    if (ok[j]) key_positions<KEYK, MODE>(ks, k, mp, pa[j], pb[j]);
+  }
+  for (uint32_t i = tid; i < Tp; i += NT) hist[i] = 0;
+  __syncthreads();
+  CB_STAMP(1);
+  const uint32_t tmask = (1u << tb) - 1u;
+  uint32_t et[2 * KPT], er[2 * KPT];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
     et[2 * j] = et[2 * j + 1] = 0xFFFFFFFFu;
-    if (k < n) {
-      uint64_t a, b;
-      key_positions<KEYK, MODE>(ks, k, mp, a, b);
-      const uint32_t ta = (uint32_t)(a >> tb), tbb = (uint32_t)(b >> tb);
-      et[2 * j] = ta;
-      eo[2 * j] = (uint32_t)a & tmask;
-      er[2 * j] = atomicAdd(&hist[ta], 1u);
-      et[2 * j + 1] = tbb;
-      eo[2 * j + 1] = (uint32_t)b & tmask;
-      er[2 * j + 1] = atomicAdd(&hist[tbb], 1u);
+    if (ok[j]) {
+      et[2 * j] = (uint32_t)(pa[j] >> tb);
+      et[2 * j + 1] = (uint32_t)(pb[j] >> tb);
+      er[2 * j] = atomicAdd(&hist[et[2 * j]], 1u);
+      er[2 * j + 1] = atomicAdd(&hist[et[2 * j + 1]], 1u);
     }
   }
   __syncthreads();
-  const uint32_t total = block_exclusive_scan<kPartThreads>(hist, T, wsum);
-  if (tid == 0) hist[T] = total;
+  CB_STAMP(2);
+  wave0_exclusive_scan(hist, T);
   __syncthreads();
+  CB_STAMP(3);
+  const uint32_t total = hist[T];
   uint32_t* srow = seg + (size_t)blockIdx.x * (T + 1);
-  for (uint32_t t = tid; t <= T; t += kPartThreads) srow[t] = hist[t];
+  for (uint32_t t = tid; t <= T; t += NT) srow[t] = hist[t];
 #pragma unroll
-  for (int e = 0; e < 2 * KPT; ++e)
-    if (et[e] != 0xFFFFFFFFu) stage[hist[et[e]] + er[e]] = eo[e];
+  for (int j = 0; j < KPT; ++j) {
+    if (et[2 * j] != 0xFFFFFFFFu) {
+      stage[hist[et[2 * j]] + er[2 * j]] = (uint32_t)pa[j] & tmask;
+      stage[hist[et[2 * j + 1]] + er[2 * j + 1]] = (uint32_t)pb[j] & tmask;
+    }
+  }
   __syncthreads();
+  CB_STAMP(4);
   uint32_t* out = ent + (size_t)blockIdx.x * (2 * C);
-  for (uint32_t i = tid; i < total; i += kPartThreads) out[i] = stage[i];
+  for (uint32_t i = tid; i < total; i += NT) out[i] = stage[i];
+  CB_STAMP(5);
 }
 
-constexpr uint32_t kTileBuildThreads = 256;
-
-// One workgroup per tile: stage the tile in LDS (zeros if the filter is known
-// empty), OR in every entry of the tile with LDS atomics, write it back.
-__global__ __launch_bounds__(kTileBuildThreads) void k_tile_build(
-    BuildBatch bb, uint32_t tb, uint32_t T, const uint32_t* __restrict__ seg_all, uint32_t nblk,
-    const uint32_t* __restrict__ ent_all, uint32_t estride) {
-  constexpr uint32_t NT = kTileBuildThreads;
+// Wave w owns partition blocks b = w + NW*u. Per group of 16: lanes 0..15
+// load the 16 blocks' run bounds (seg[b][t], seg[b][t+1]), shuffles hand each
+// run's start and length to the whole wave, and the wave issues the 16 run
+// loads back to back (lane i = entry i): two dependent memory round trips per
+// group and no LDS run table or barrier before the ORs.
+template <int G>
+__global__ __launch_bounds__(kBuildNT) void k_build_tile(BuildBatch bb, uint32_t tb, uint32_t T,
+                                                         const uint32_t* __restrict__ seg_all,
+                                                         uint32_t nblk,
+                                                         const uint32_t* __restrict__ ent_all,
+                                                         uint32_t estride) {
+  constexpr uint32_t NT = kBuildNT, NW = NT / 64;
+  static_assert(G <= 64, "one lane per run bound");
   uint32_t* __restrict__ words = bb.words[blockIdx.y];
   const bool fresh = (bb.fresh >> blockIdx.y) & 1u;
   const uint32_t* __restrict__ seg = seg_all + (size_t)blockIdx.y * nblk * (T + 1);
   const uint32_t* __restrict__ ent = ent_all + (size_t)blockIdx.y * nblk * estride;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t tw = 1u << (tb - 5);
-  const uint32_t nbp = (nblk + 3) & ~3u;
   uint32_t* tile = smem;
-  uint32_t* P = tile + tw;
-  uint32_t* S = P + nbp;
-  uint32_t* wsum = S + nbp;
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const uint32_t t = xcd_tile(blockIdx.x, T);
+  CB_STAMP(0);
 
+  // first group's run bounds in flight while the tile is cleared / loaded
+  uint32_t s0 = 0, s1 = 0;
+  {
+    const uint32_t b = w + NW * lane;
+    if (lane < (uint32_t)G && b < nblk) {
+      const uint32_t* row = seg + (size_t)b * (T + 1) + t;
+      s0 = row[0];
+      s1 = row[1];
+    }
+  }
   uint4* gt = reinterpret_cast<uint4*>(words + (size_t)t * tw);
   uint4* lt = reinterpret_cast<uint4*>(tile);
   for (uint32_t i = tid; i < tw / 4; i += NT) lt[i] = fresh ? make_uint4(0, 0, 0, 0) : gt[i];
-  const uint32_t E = load_runs<NT>(seg, nblk, T, t, S, P, wsum);
-  const uint32_t per = (E + NT - 1) / NT;
-  const uint32_t j0 = min(tid * per, E), j1 = min(j0 + per, E);
-  if (j0 < j1) {
-    uint32_t b = seg_find(P, nblk, j0);
-    uint32_t pnext = (b + 1 < nblk) ? P[b + 1] : E;
-    // 8 entries per round: the 8 loads issue back to back, then 8 ds_or.
-    for (uint32_t jb = j0; jb < j1; jb += 8) {
-      uint32_t o[8];
+  __syncthreads();
+  CB_STAMP(1);
+
+  for (uint32_t g0 = 0; w + NW * g0 < nblk; g0 += G) {
+    if (g0) {
+      s0 = s1 = 0;
+      const uint32_t b = w + NW * (g0 + lane);
+      if (lane < (uint32_t)G && b < nblk) {
+        const uint32_t* row = seg + (size_t)b * (T + 1) + t;
+        s0 = row[0];
+        s1 = row[1];
+      }
+    }
+    uint32_t o[G];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t j = jb + i;
-        o[i] = 0xFFFFFFFFu;
-        if (j < j1) {
-          while (j >= pnext) {
-            ++b;
-            pnext = (b + 1 < nblk) ? P[b + 1] : E;
-          }
-          o[i] = ent[(size_t)b * estride + S[b] + (j - P[b])];
+    for (int u = 0; u < G; ++u) {
+      const uint32_t st = __shfl(s0, u, 64), len = __shfl(s1, u, 64) - st;
+      const uint32_t b = w + NW * (g0 + u);
+      o[u] = 0xFFFFFFFFu;
+      if (lane < len) o[u] = ent[(size_t)b * estride + st + lane];
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+      if (o[u] != 0xFFFFFFFFu) atomicOr(&tile[o[u] >> 5], 1u << (o[u] & 31));
+    // runs longer than one wave (skewed inputs, few partition blocks)
+    if (__ballot(lane < (uint32_t)G && s1 - s0 > 64u)) {
+#pragma unroll 1
+      for (int u = 0; u < G; ++u) {
+        const uint32_t st = __shfl(s0, u, 64), len = __shfl(s1, u, 64) - st;
+        const uint32_t* run = ent + (size_t)(w + NW * (g0 + u)) * estride + st;
+        for (uint32_t i = 64 + lane; i < len; i += 64) {
+          const uint32_t v = run[i];
+          atomicOr(&tile[v >> 5], 1u << (v & 31));
         }
       }
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (o[i] != 0xFFFFFFFFu) atomicOr(&tile[o[i] >> 5], 1u << (o[i] & 31));
     }
   }
+  CB_STAMP(2);
   __syncthreads();
+  CB_STAMP(3);
   for (uint32_t i = tid; i < tw / 4; i += NT) gt[i] = lt[i];
+  CB_STAMP(4);
 }
 
 // Partition for probe: one 8-byte entry per key, bucketed by the tile of bit
@@ -660,21 +757,25 @@ static int env_int(const char* name, int dflt) {
   return v && *v ? atoi(v) : dflt;
 }
 
-TilePlan plan_build(uint64_t m, uint64_t n) {
+TilePlan plan_build(uint64_t m, uint64_t n, uint32_t nb) {
+  // ~256 tiles per launch over the whole batch, each as large as the 64 KiB
+  // LDS tile allows (fewer tiles = longer runs per partition block);
+  // 1024-thread partition blocks of up to 4096 keys, fewer keys per thread
+  // only while that leaves under 256 blocks in the launch.
   TilePlan p{};
-  // ~512 tiles (2 workgroups per CU), tiles within [2^12, 2^18] bits.
-  int64_t tb = clamp64((int64_t)ilog2_floor(m > 512 ? m / 512 : 1), kMinTileBits, kMaxTileBits);
   static const int env_tb = env_int("CB_BUILD_TB", 0);
+  static const int env_kpt = env_int("CB_BUILD_KPT", 0);
+  if (nb < 1) nb = 1;
+  const uint64_t want_tiles = nb >= 256 ? 1 : 256 / nb;
+  int64_t tb = clamp64((int64_t)ilog2_floor(m > want_tiles ? m / want_tiles : 1), kMinTileBits,
+                       kMaxTileBits);
   if (env_tb) tb = clamp64(env_tb, kMinTileBits, kMaxTileBits);
   p.tb = fit_tiles(m, tb, kMaxTileBits);
   p.T = (uint32_t)((m + (1ull << p.tb) - 1) >> p.tb);
-  // 2048-key partition blocks from 512K keys up (longer runs per tile; 4096
-  // blocks at most), 1024 below so small builds still fill the chip.
-  p.kpt = n >= (1ull << 19) ? 8 : 4;
-  while (p.kpt < 16 && (n + 256ull * p.kpt - 1) / (256ull * p.kpt) > 4096) p.kpt *= 2;
-  static const int env_kpt = env_int("CB_BUILD_KPT", 0);
-  if (env_kpt == 4 || env_kpt == 8 || env_kpt == 16) p.kpt = env_kpt;
-  p.C = kPartThreads * p.kpt;
+  p.kpt = 4;
+  while (p.kpt > 1 && nb * ((n + kBuildNT * p.kpt - 1) / (kBuildNT * p.kpt)) < 256) p.kpt /= 2;
+  if (env_kpt == 1 || env_kpt == 2 || env_kpt == 4) p.kpt = env_kpt;
+  p.C = kBuildNT * p.kpt;
   p.nblk = (uint32_t)((n + p.C - 1) / p.C);
   return p;
 }
@@ -736,14 +837,6 @@ hipError_t launch_probe_direct(int keyk, int mode, const FilterPtrs& fp, uint32_
 }
 
 template <int KK, int MM, int KPT>
-static void part_build(const TilePlan& p, const BuildBatch& bb, uint32_t nb, const ModP& mp,
-                       uint32_t* seg, uint32_t* ent, size_t lds, hipStream_t s) {
-  allow_lds(k_part_build<KK, MM, KPT>, lds);
-  hipLaunchKernelGGL((k_part_build<KK, MM, KPT>), dim3(p.nblk, nb), dim3(kPartThreads), lds, s, bb,
-                     mp, p.tb, p.T, seg, ent);
-}
-
-template <int KK, int MM, int KPT>
 static void part_probe(const TilePlan& p, const KeySrc& ks, uint64_t n, const ModP& mp,
                        uint32_t* seg, uint2* ent, uint16_t* lkey, size_t lds, hipStream_t s) {
   allow_lds(k_part_probe<KK, MM, KPT>, lds);
@@ -751,30 +844,37 @@ static void part_probe(const TilePlan& p, const KeySrc& ks, uint64_t n, const Mo
                      mp, p.tb, p.T, seg, ent, lkey);
 }
 
+template <int KK, int MM, int KPT>
+static void build_part(const TilePlan& p, const BuildBatch& bb, uint32_t nb, const ModP& mp,
+                       uint32_t* seg, uint32_t* ent, size_t lds, hipStream_t s) {
+  allow_lds(k_build_part<KK, MM, KPT>, lds);
+  hipLaunchKernelGGL((k_build_part<KK, MM, KPT>), dim3(p.nblk, nb), dim3(kBuildNT), lds, s, bb, mp,
+                     p.tb, p.T, seg, ent);
+}
+
 hipError_t launch_build_batch(int keyk, int mode, const BuildBatch& bb, uint32_t nb,
                               const ModP& mp, const TilePlan& p, uint32_t* seg, uint32_t* ent,
                               hipStream_t s) {
   if (!nb) return hipSuccess;
-  if (!plan_ok(p) || nb > kMaxBuildBatch) return hipErrorInvalidValue;
-  const size_t lds1 = ((size_t)((p.T + 4) & ~3u) + 2 * p.C + 8) * 4;
+  if (!plan_ok(p) || nb > kMaxBuildBatch || p.nblk > kMaxBuildBlocks) return hipErrorInvalidValue;
+  const size_t lds1 = ((size_t)((p.T + 4) & ~3u) + 2 * p.C) * 4;
   {
-    ProfScope ps("k_part_build", s);
-    if (p.kpt == 4) {
-      CB_DISPATCH(keyk, mode, (part_build<KK, MM, 4>(p, bb, nb, mp, seg, ent, lds1, s)));
-    } else if (p.kpt == 8) {
-      CB_DISPATCH(keyk, mode, (part_build<KK, MM, 8>(p, bb, nb, mp, seg, ent, lds1, s)));
+    ProfScope ps("k_build_part", s);
+    if (p.kpt == 1) {
+      CB_DISPATCH(keyk, mode, (build_part<KK, MM, 1>(p, bb, nb, mp, seg, ent, lds1, s)));
+    } else if (p.kpt == 2) {
+      CB_DISPATCH(keyk, mode, (build_part<KK, MM, 2>(p, bb, nb, mp, seg, ent, lds1, s)));
     } else {
-      CB_DISPATCH(keyk, mode, (part_build<KK, MM, 16>(p, bb, nb, mp, seg, ent, lds1, s)));
+      CB_DISPATCH(keyk, mode, (build_part<KK, MM, 4>(p, bb, nb, mp, seg, ent, lds1, s)));
     }
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const uint32_t nbp = (p.nblk + 3) & ~3u;
-  const size_t lds2 = ((size_t)(1u << (p.tb - 5)) + 2 * nbp + 8) * 4;
-  allow_lds(k_tile_build, lds2);
-  ProfScope ps("k_tile_build", s);
-  hipLaunchKernelGGL(k_tile_build, dim3(p.T, nb), dim3(kTileBuildThreads), lds2, s, bb, p.tb, p.T,
-                     seg, p.nblk, ent, 2 * p.C);
+  const size_t lds2 = (size_t)(1u << (p.tb - 5)) * 4;
+  allow_lds(k_build_tile<16>, lds2);
+  ProfScope ps("k_build_tile", s);
+  hipLaunchKernelGGL(k_build_tile<16>, dim3(p.T, nb), dim3(kBuildNT), lds2, s, bb, p.tb, p.T, seg,
+                     p.nblk, ent, 2 * p.C);
   return hipGetLastError();
 }
 

@@ -10,7 +10,8 @@ namespace cb {
 constexpr uint32_t kMaxFiltersPerLaunch = 64;  // filter pointers carried in kernargs
 constexpr uint32_t kFiltersPerGroup = 32;      // one uint32 result mask per key
 constexpr uint32_t kMaxTiles = 4096;           // LDS histogram bound in the partition pass
-constexpr uint32_t kMaxTileBits = 18;          // build: 32 KiB LDS tiles at most
+constexpr uint32_t kMaxTileBits = 19;          // build: 64 KiB LDS tiles at most
+constexpr uint32_t kMaxBuildBlocks = 4096;     // partition blocks per build launch (host chunks keys)
 constexpr uint32_t kMinTileBits = 12;          // build: 512 B tiles at least
 constexpr uint32_t kMinProbeTileBits = 16;     // probe kernel instantiations: 2^16..2^18
 constexpr uint32_t kMaxProbeTileBits = 18;
@@ -39,11 +40,12 @@ struct TilePlan {
   uint32_t tb;    // log2(tile bits)
   uint32_t T;     // number of tiles = ceil(m / 2^tb)
   uint32_t kpt;   // keys per thread in the partition pass
-  uint32_t C;     // keys per partition block = 256 * kpt
+  uint32_t C;     // keys per partition block = threads * kpt
   uint32_t nblk;  // partition blocks = ceil(n / C)
 };
 
-TilePlan plan_build(uint64_t m, uint64_t n);
+// nb: filters built together in one launch pair (insert_fixed_many batches).
+TilePlan plan_build(uint64_t m, uint64_t n, uint32_t nb = 1);
 TilePlan plan_probe(uint64_t m, uint64_t n);
 bool plan_ok(const TilePlan& p);  // tile count fits the partition histogram
 

@@ -134,6 +134,17 @@ def test_build_incremental_and_idempotent(gpu, path):
     assert np.array_equal(g2.packed(), g1.packed())
 
 
+def test_build_skewed_runs(gpu, path):
+    # Duplicate keys pile every entry of a partition block into two tiles, so
+    # runs exceed one wave (64 entries) and one tile takes most of the batch.
+    base = workload.key_range(31, 3000)
+    keys = np.concatenate([np.repeat(base[:1], 200_000, axis=0), base,
+                           np.repeat(base[7:8], 70_001, axis=0)])
+    for m in (1 << 20, 1 << 27, 100003):
+        g, o = build_pair(gpu, m, keys)
+        assert np.array_equal(g.bools(), o.bools()), m
+
+
 @pytest.mark.parametrize("m", [(1 << 32) + 15, 1 << 33])
 def test_build_64bit_modes(gpu, m):
     # m > 2^32: 64-bit state (mask or exact 64-bit fastmod). Checked by set positions.
