@@ -229,9 +229,68 @@ def main():
                 out[nm] = {"avg_us": tot.value * 1e3 / cnt.value, "launches": int(cnt.value)}
         return out
 
+    def cold_run(names, fn, reps=8):
+        """SURVEY.md §8d timing protocol, cold leg: before every rep a 1 GiB
+        streaming device write evicts the L2s and the 256 MiB Infinity Cache,
+        then ONE step runs; medians over reps of the step (HIP events on the
+        kernels' stream) and of each kernel (cb_profile events)."""
+        flush = torch.empty(1 << 28, dtype=torch.int32, device=dev)
+        step_ms, kus = [], {nm: [] for nm in names}
+        for r in range(2 * reps):
+            flush.fill_(r)
+            torch.cuda.synchronize(dev)
+            if use_dist:
+                dist.barrier()
+            if r < reps:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                fn()
+                e1.record(stream)
+                torch.cuda.synchronize(dev)
+                step_ms.append(e0.elapsed_time(e1))
+            else:
+                for nm, v in kernel_ms(names, fn, 1).items():
+                    kus[nm].append(v["avg_us"])
+        del flush
+        torch.cuda.synchronize(dev)
+        return (float(np.median(step_ms)),
+                {nm: round(float(np.median(v)), 2) for nm, v in kus.items() if v})
+
     probe_kernels = ["k_part_probe", "k_tile_probe", "k_masks_to_hits", "k_probe_direct",
                      "k_set_probe"]
     kprof = kernel_ms(probe_kernels, step, args.steps)
+    cold_ms, cold_k = cold_run(probe_kernels, step)
+    cold = {"value": round(probes_per_step / (cold_ms * 1e-3), 1), "ms_per_step": round(cold_ms, 4),
+            "kernels_us": cold_k, "protocol": "1 GiB device write before each of 8 reps, median"}
+
+    # rotating batches: 4 different lookup batches over the same filters, one
+    # per step in turn, so a step cannot find the set lines of its own
+    # previous run in the Infinity Cache (warm = the same batch every step)
+    rot = None
+    if best == "filterset":
+        nrot = 4
+        shift = (n // 2 // nf_total) or 1
+        rot_keys = [keys_batch] + [
+            lsmt_amd.DeviceKeys(torch.from_numpy(workload.probe_lookups(
+                n, nf_total, kpf, seed_base=seed_base, absent_seed=absent_seed + 7919 * r,
+                shift=r * shift)).to(dev)) for r in range(1, nrot)]
+        rot_i = [0]
+
+        def step_rot():
+            buf = claim()
+            fset.probe(rot_keys[rot_i[0] % nrot], out=hits_bufs[buf], stream=sh)
+            rot_i[0] += 1
+            exchange(buf)
+
+        for _ in range(args.warmup):
+            step_rot()
+        rel = timed(step_rot, args.steps)
+        rprof = kernel_ms(probe_kernels, step_rot, args.steps)
+        rot = {"value": round(probes_per_step / (rel / args.steps), 1),
+               "ms_per_step": round(rel / args.steps * 1e3, 4),
+               "kernels_us": {k: round(v["avg_us"], 2) for k, v in rprof.items()},
+               "batches": nrot}
+        del rot_keys
     kprof_alt = kernel_ms(probe_kernels, legs["tiled" if best == "filterset" else "filterset"]["fn"], args.steps)
     dominant = max(kprof, key=lambda k: kprof[k]["avg_us"]) if kprof else None
 
@@ -251,8 +310,10 @@ def main():
     if dominant:
         dur_s = kprof[dominant]["avg_us"] * 1e-6
         ach = alg_bytes / dur_s / 1e9
+        # PMC bytes are recorded for the default C3 shape only (profiles/pmc_*.json)
+        c3_default = (args.workload == "c3" and n == 1 << 20 and F == 32 and m == 1 << 26 and kpf == 1 << 19)
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("k_tile_probe" if dominant == "k_tile_probe" else dominant),
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(dominant) if c3_default else None,
                 "kernel": dominant, "kernel_avg_us": round(kprof[dominant]["avg_us"], 2),
                 "algorithmic_bytes": int(alg_bytes), "algorithmic_def": alg_def,
                 "step_effective_GBps": round(alg_bytes / (el / args.steps) / 1e9, 1)}
@@ -428,32 +489,46 @@ def main():
         build_step()
     bel = timed(build_step, args.steps)
     bprof = kernel_ms(["k_build_part", "k_build_tile", "k_insert_direct"], build_step, args.steps)
+    bcold_ms, bcold_k = cold_run(["k_build_part", "k_build_tile", "k_insert_direct"], build_step)
     b_alg = 16 * args.build_keys + args.build_m_bits / 8
     build = {"metric": "build keys/s (C2: 1M 16-B keys -> one 16 MiB filter, m=2^27)",
              "value": round(args.build_keys * world / (bel / args.steps), 1), "unit": "keys/s",
              "ms_per_step": round(bel / args.steps * 1e3, 4), "path": int(L.cb_last_path()),
              "kernels": {k: round(v["avg_us"], 2) for k, v in bprof.items()},
              "algorithmic_bytes": int(b_alg),
-             "step_effective_GBps": round(b_alg / (bel / args.steps) / 1e9, 1)}
+             "step_effective_GBps": round(b_alg / (bel / args.steps) / 1e9, 1),
+             "cold": {"value": round(args.build_keys * world / (bcold_ms * 1e-3), 1),
+                      "ms_per_step": round(bcold_ms, 4), "kernels_us": bcold_k}}
 
     # ---- PCIe-inclusive end-to-end probe (pinned host keys -> host hits)
     e2e = None
     if not args.no_e2e and rank == 0:
+        # keys arrive in pinned host memory from the query layer and the hit
+        # bitmap returns there (SURVEY.md §8d end-to-end leg): the FilterSet
+        # probe reading keys / writing hits over PCIe from the kernel
+        # (zero-copy), and the per-filter probe with one staged H2D and one D2H
         look_pin = torch.from_numpy(look_np).pin_memory()
         hits_host = torch.zeros((F, words), dtype=torch.int64).pin_memory()
         hb = lsmt_amd.KeyBatch(n=n, key_len=16, keys=look_pin)
 
-        def e2e_step():
-            lsmt_amd.probe(filters, hb, out=hits_host, stream=sh)
+        def wall(fn, k):
+            fn()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(k):
+                fn()
+            return (time.perf_counter() - t0) / k
 
-        e2e_step()
-        t0 = time.perf_counter()
-        k_e2e = max(3, args.steps // 2)
-        for _ in range(k_e2e):
-            e2e_step()
-        t_e2e = (time.perf_counter() - t0) / k_e2e
-        e2e = {"probes_per_s": round(n * F / t_e2e, 1), "ms_per_step": round(t_e2e * 1e3, 3),
-               "h2d_bytes": 16 * n, "d2h_bytes": F * words * 8, "host_buffers": "pinned"}
+        k_e2e = max(5, args.steps // 2)
+        t_set = wall(lambda: fset.probe(hb, out=hits_host, stream=sh), k_e2e)
+        pipelined = int(L.cb_last_path()) == 4
+        t_tiled = wall(lambda: lsmt_amd.probe(filters, hb, out=hits_host, stream=sh), k_e2e)
+        e2e = {"probes_per_s": round(n * F / t_set, 1), "ms_per_step": round(t_set * 1e3, 3),
+               "path": "filterset" + (", zero-copy (kernel loads keys / stores hits over PCIe)" if pipelined else ""),
+               "h2d_bytes": 16 * n, "d2h_bytes": F * words * 8, "host_buffers": "pinned",
+               "pcie_GBps": round((16 * n + F * words * 8) / t_set / 1e9, 1),
+               "alt_per_filter_tiled": {"probes_per_s": round(n * F / t_tiled, 1),
+                                        "ms_per_step": round(t_tiled * 1e3, 3)}}
 
     if args.check and rank == 0:
         from oracle import oracle
@@ -495,7 +570,7 @@ def main():
             "alt_kernels_us": {k: round(v["avg_us"], 2) for k, v in kprof_alt.items()},
             "filterset": {"build_all_ms": round(set_build_ms, 3), "assign_one_empty_slot_ms": round(set_assign_ms, 3),
                           "bytes": m * (4 if F <= 32 else 8)},
-            "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e, "zone_gate": zone, "read_path": read, "flush": flush,
+            "cold": cold, "rotating_batches": rot, "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e, "zone_gate": zone, "read_path": read, "flush": flush,
         }
         print(json.dumps(line), file=result, flush=True)
     if use_dist:

@@ -177,7 +177,11 @@ int cb_set_assign(cb_filterset* set, uint32_t slot, const cb_filter* f, void* st
 /* slots 0..nf-1 := filters[0..nf-1], other slots cleared; used = nf. */
 int cb_set_assign_all(cb_filterset* set, const cb_filter* const* filters, uint32_t nf, void* stream);
 int cb_set_clear_slot(cb_filterset* set, uint32_t slot, void* stream);
-/* hits: [used][ceil(n/64)] uint64, row s = slot s's may_contain bits. */
+/* hits: [used][ceil(n/64)] uint64, row s = slot s's may_contain bits.
+ * Pinned host keys AND hits (hipHostMalloc / torch pin_memory) of fixed-length
+ * keys take the zero-copy path: the probe kernel loads the keys and stores the
+ * hit rows over PCIe itself (both directions and the HBM gathers overlap in one
+ * launch); the call returns when the hits are in host memory. */
 int cb_set_probe_fixed(const cb_filterset* set, const uint8_t* keys, uint32_t key_len, uint64_t n,
                        uint64_t* hits, void* stream);
 int cb_set_probe_var(const cb_filterset* set, const uint8_t* bytes, const uint64_t* offsets,
@@ -280,11 +284,12 @@ int cb_get_many_var(const cb_table* const* tables, uint32_t nt, const uint64_t* 
 /* Path selection: 0 = auto, 1 = force direct (per-key atomics / gathers),
  * 2 = force tiled (LDS-staged filter tiles). Process-wide. */
 int cb_set_path(int path);
-/* Path the last insert/probe on this thread used (1 direct, 2 tiled). */
+/* Path the last insert/probe on this thread used (1 direct, 2 tiled, 3 FilterSet,
+ * 4 FilterSet zero-copy: pinned host keys and hits read/written by the kernel). */
 int cb_last_path(void);
 /* Per-kernel timing with HIP events recorded on each launch's own stream
  * (off by default). Kernel names: "k_insert_direct", "k_probe_direct",
- * "k_part_build", "k_tile_build", "k_part_probe", "k_tile_probe",
+ * "k_build_part", "k_build_tile", "k_part_probe", "k_tile_probe",
  * "k_masks_to_hits", "k_set_build", "k_set_or_slot", "k_set_put_slot",
  * "k_set_probe". cb_profile_read waits for pending events and returns the
  * accumulated milliseconds and launch count for one kernel. */

@@ -499,6 +499,39 @@ int probe_impl(const cb_filter* const* filters, uint32_t nf, const uint8_t* keys
   return CB_OK;
 }
 
+bool is_pinned_host(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t attr;
+  hipError_t e = hipPointerGetAttributes(&attr, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost;
+}
+
+// Pinned host keys in, pinned host hits out (the query layer's buffers,
+// SURVEY.md §8d end-to-end leg): the probe kernel itself loads the keys over
+// PCIe and stores the hit rows over PCIe (zero-copy; pinned memory is mapped
+// into the device's address space), so the two PCIe directions overlap each
+// other and the HBM gathers inside ONE launch. Measured on this stack
+// (tools/ubench_pcie.hip): chunked pipelines across copy streams cost more
+// per cross-stream event than they overlap (4 chunks, 3 streams: 0.87 ms vs
+// 0.50 ms on one stream), while kernel loads from pinned memory run at
+// 43-46 GB/s and kernel stores to it at 53 GB/s, the copy engines' rates.
+int set_probe_zero_copy(const cb_filterset* set, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                        uint64_t* hits, hipStream_t s, const cb::ZoneView* zv) {
+  void *dk = nullptr, *dh = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(&dk, const_cast<uint8_t*>(keys), 0));
+  HIP_TRY(hipHostGetDevicePointer(&dh, hits, 0));
+  const int keyk = (key_len == 16 && !((uintptr_t)dk & 15)) ? cb::KEY_FIXED16 : cb::KEY_FIXED;
+  cb::KeySrc ks{(const uint8_t*)dk, nullptr, key_len};
+  HIP_TRY(cb::launch_set_probe(keyk, set->mode, set->width, set->words, set->any, set->used, ks, n,
+                               set->mp, zv, (uint64_t*)dh, (n + 63) / 64, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return CB_OK;
+}
+
 int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t* offsets,
                    uint32_t key_len, uint64_t n, uint64_t* hits, hipStream_t s, bool gated) {
   if (!set) return fail(CB_EINVAL, "null set");
@@ -508,6 +541,13 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
   DeviceGuard dg(set->device);
   Workspace& ws = workspace(set->device, s);
   std::lock_guard<std::mutex> lk(ws.mu);
+  const cb::ZoneView zv{(const uint32_t*)set->zdev,
+                       (const cb::BoundPrefix*)((const uint8_t*)set->zdev + cb_zone_hdr_bytes),
+                       (const uint8_t*)set->zdev + cb_zone_blob_off, set->zgated};
+  if (!offsets && key_len && is_pinned_host(keys) && is_pinned_host(hits)) {
+    g_last_path = 4;
+    return set_probe_zero_copy(set, keys, key_len, n, hits, s, (gated && set->zgated) ? &zv : nullptr);
+  }
   StagedKeys sk;
   int rc = offsets ? stage_var(ws, keys, offsets, n, s, sk)
                    : stage_fixed(ws, keys, key_len, n, s, sk);
@@ -519,9 +559,6 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
     HIP_TRY(ws.hits.reserve((size_t)set->used * hwords * 8, s));
     dhits = (uint64_t*)ws.hits.p;
   }
-  const cb::ZoneView zv{(const uint32_t*)set->zdev,
-                       (const cb::BoundPrefix*)((const uint8_t*)set->zdev + cb_zone_hdr_bytes),
-                       (const uint8_t*)set->zdev + cb_zone_blob_off, set->zgated};
   HIP_TRY(cb::launch_set_probe(sk.keyk, set->mode, set->width, set->words, set->any, set->used,
                                sk.ks, n, set->mp, (gated && set->zgated) ? &zv : nullptr, dhits,
                                hwords, s));

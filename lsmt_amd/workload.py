@@ -48,16 +48,19 @@ def c2_build_keys(n: int = 1 << 20) -> np.ndarray:
     return key_range(1, n)
 
 
-def probe_lookups(n: int, nf: int, keys_per_filter: int, seed_base: int, absent_seed: int) -> np.ndarray:
+def probe_lookups(n: int, nf: int, keys_per_filter: int, seed_base: int, absent_seed: int,
+                  shift: int = 0) -> np.ndarray:
     """Lookup batch of the probe configs: even i -> present key
-    key(seed_base + j mod nf, (j div nf) mod keys_per_filter) with j = i/2;
-    odd i -> absent key key(absent_seed, i)."""
+    key(seed_base + j mod nf, (j div nf + shift) mod keys_per_filter) with
+    j = i/2; odd i -> absent key key(absent_seed, i). shift = 0 is the
+    SURVEY.md §8d batch; other shifts give further batches over the same
+    filters (bench.py's rotating-batch leg)."""
     i = np.arange(n, dtype=np.uint64)
     out = np.empty((n, 16), np.uint8)
     even = i[0::2]
     j = even // np.uint64(2)
     f = (j % np.uint64(nf)).astype(np.int64)
-    kidx = (j // np.uint64(nf)) % np.uint64(keys_per_filter)
+    kidx = (j // np.uint64(nf) + np.uint64(shift)) % np.uint64(keys_per_filter)
     ev = np.empty((len(even), 16), np.uint8)
     for fs in np.unique(f):
         sel = f == fs

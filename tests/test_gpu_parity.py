@@ -312,6 +312,36 @@ def test_filterset_probe_matches_oracle(gpu, width, m):
     assert np.array_equal(gpu.probe(filters, look), expect)
 
 
+@pytest.mark.parametrize("width", [32, 64])
+def test_filterset_zero_copy_host_buffers(gpu, width):
+    # Pinned host keys and hits take the zero-copy path (the kernel reads keys
+    # and writes hit rows over PCIe); a ragged last word; plain and zone-gated
+    # answers must match the oracle / the device-resident path bit for bit.
+    import torch
+    m, nf, kpf = 1 << 20, (7 if width == 32 else 40), 3000
+    filters, refs = [], []
+    for f in range(nf):
+        g, o = build_pair(gpu, m, workload.key_range(600 + f, kpf))
+        filters.append(g)
+        refs.append(o)
+    s = gpu.FilterSet.from_filters(filters, width=width)
+    n = 4 * (1 << 18) + 12_345
+    look = workload.probe_lookups(n, nf, kpf, seed_base=600, absent_seed=996)
+    expect = oracle.probe_fixed(refs, look)
+    keys = torch.from_numpy(look).pin_memory()
+    out = torch.zeros((nf, (n + 63) // 64), dtype=torch.int64).pin_memory()
+    s.probe(gpu.KeyBatch(n=n, key_len=16, keys=keys), out=out)
+    assert gpu.last_path() == 4
+    assert np.array_equal(out.numpy().view(np.uint64), expect)
+    # gated: zones from each table's keys (every present key lies inside its zone)
+    for f in range(nf):
+        s.zone_from_keys(f, workload.key_range(600 + f, kpf))
+    out.zero_()
+    s.probe(gpu.KeyBatch(n=n, key_len=16, keys=keys), out=out, gated=True)
+    dev = s.probe(look, gated=True)
+    assert np.array_equal(out.numpy().view(np.uint64), dev)
+
+
 def test_filterset_assign_slots_and_var_keys(gpu):
     m = (1 << 20) + 17
     filters, refs = [], []

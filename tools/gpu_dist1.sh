@@ -9,6 +9,6 @@ timeout -k 10 300 python bench.py --no-cpu --no-e2e --force-dist --check > gpuru
 grep check gpurun_out/d1.err
 python -c "import json;d=json.load(open('gpurun_out/d1.json'));print('overlap',d['path'],round(d['value']/1e9,1),d['ms_per_step'],d['config']['parallelism'])"
 timeout -k 10 300 python bench.py --no-cpu --no-e2e --force-dist --overlap > gpurun_out/d2.json 2> gpurun_out/d2.err || { tail -20 gpurun_out/d2.err; exit 1; }
-python -c "import json;d=json.load(open('gpurun_out/d2.json'));print("overlap2",,d['path'],round(d['value']/1e9,1),d['ms_per_step'],d['config']['parallelism'])"
+python -c "import json;d=json.load(open('gpurun_out/d2.json'));print("overlap2",d['path'],round(d['value']/1e9,1),d['ms_per_step'],d['config']['parallelism'])"
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --no-cpu --no-e2e --force-dist > gpurun_out/d3.json 2> gpurun_out/d3.err || { tail -20 gpurun_out/d3.err; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/d3.json'));print('torchrun',d['path'],round(d['value']/1e9,1),d['ms_per_step'],d['n_gpus'])"
