@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--no-zone", action="store_true", help="skip the zone-map gate leg (and the read path)")
     p.add_argument("--no-read", action="store_true", help="skip the SSTable read-path leg")
     p.add_argument("--no-flush", action="store_true", help="skip the flush-producer (SsTable::create) leg")
+    p.add_argument("--no-cold", action="store_true",
+                   help="skip the cold-cache legs (profiles: keeps every k_set_probe launch warm, so "
+                        "rocprofv3's average matches the bench line's warm kernel time)")
     p.add_argument("--flush-entries", type=int, default=1 << 20)
     p.add_argument("--overlap", action="store_true",
                    help="N>1: run each step's all-gather on a side stream, overlapped with the next "
@@ -259,9 +262,11 @@ def main():
     probe_kernels = ["k_part_probe", "k_tile_probe", "k_masks_to_hits", "k_probe_direct",
                      "k_set_probe"]
     kprof = kernel_ms(probe_kernels, step, args.steps)
-    cold_ms, cold_k = cold_run(probe_kernels, step)
-    cold = {"value": round(probes_per_step / (cold_ms * 1e-3), 1), "ms_per_step": round(cold_ms, 4),
-            "kernels_us": cold_k, "protocol": "1 GiB device write before each of 8 reps, median"}
+    cold = None
+    if not args.no_cold:
+        cold_ms, cold_k = cold_run(probe_kernels, step)
+        cold = {"value": round(probes_per_step / (cold_ms * 1e-3), 1), "ms_per_step": round(cold_ms, 4),
+                "kernels_us": cold_k, "protocol": "1 GiB device write before each of 8 reps, median"}
 
     # rotating batches: 4 different lookup batches over the same filters, one
     # per step in turn, so a step cannot find the set lines of its own
@@ -489,7 +494,11 @@ def main():
         build_step()
     bel = timed(build_step, args.steps)
     bprof = kernel_ms(["k_build_part", "k_build_tile", "k_insert_direct"], build_step, args.steps)
-    bcold_ms, bcold_k = cold_run(["k_build_part", "k_build_tile", "k_insert_direct"], build_step)
+    bcold = None
+    if not args.no_cold:
+        bcold_ms, bcold_k = cold_run(["k_build_part", "k_build_tile", "k_insert_direct"], build_step)
+        bcold = {"value": round(args.build_keys * world / (bcold_ms * 1e-3), 1),
+                 "ms_per_step": round(bcold_ms, 4), "kernels_us": bcold_k}
     b_alg = 16 * args.build_keys + args.build_m_bits / 8
     build = {"metric": "build keys/s (C2: 1M 16-B keys -> one 16 MiB filter, m=2^27)",
              "value": round(args.build_keys * world / (bel / args.steps), 1), "unit": "keys/s",
@@ -497,8 +506,7 @@ def main():
              "kernels": {k: round(v["avg_us"], 2) for k, v in bprof.items()},
              "algorithmic_bytes": int(b_alg),
              "step_effective_GBps": round(b_alg / (bel / args.steps) / 1e9, 1),
-             "cold": {"value": round(args.build_keys * world / (bcold_ms * 1e-3), 1),
-                      "ms_per_step": round(bcold_ms, 4), "kernels_us": bcold_k}}
+             "cold": bcold}
 
     # ---- PCIe-inclusive end-to-end probe (pinned host keys -> host hits)
     e2e = None
@@ -710,19 +718,24 @@ def cpu_baseline(look_np, F, m, kpf, build_keys, build_m):
         o.insert_fixed(workload.key_range(100 + f, kpf))
         refs.append(o)
     n = look_np.shape[0]
+    reps = 3  # ~10 s of single-thread CPU work in all
     t0 = time.perf_counter()
-    oracle.probe_fixed(refs, look_np, threads=1)
-    t1 = time.perf_counter() - t0
+    for _ in range(reps):
+        oracle.probe_fixed(refs, look_np, threads=1)
+    t1 = (time.perf_counter() - t0) / reps
     cores = min(16, os.cpu_count() or 1)
     t0 = time.perf_counter()
     oracle.probe_fixed(refs, look_np, threads=cores)
     tn = time.perf_counter() - t0
     del refs
     bk = workload.c2_build_keys(build_keys)
-    o = oracle.OracleFilter(build_m)
-    t0 = time.perf_counter()
-    o.insert_fixed(bk)
-    tb = time.perf_counter() - t0
+    tb = 0.0
+    for _ in range(reps):
+        o = oracle.OracleFilter(build_m)
+        t0 = time.perf_counter()
+        o.insert_fixed(bk)
+        tb += (time.perf_counter() - t0) / reps
+        del o
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as fh:
@@ -733,10 +746,12 @@ def cpu_baseline(look_np, F, m, kpf, build_keys, build_m):
     except OSError:
         pass
     return {"value": round(n * F / t1, 1), "unit": "probes/s", "cores": 1, "kind": "port",
-            "sample": f"full C3 probe: {n} keys x {F} filters (m=2^{m.bit_length() - 1}, byte-per-bit) on 1 thread, {t1:.2f}s",
+            "sample": f"full C3 probe: {n} keys x {F} filters (m=2^{m.bit_length() - 1}, byte-per-bit) on 1 thread, "
+                      f"{reps} reps of {t1:.2f}s",
             "all_cores": {"value": round(n * F / tn, 1), "threads": cores, "seconds": round(tn, 3)},
             "build": {"value": round(build_keys / tb, 1), "unit": "keys/s", "cores": 1,
-                      "sample": f"C2 build {build_keys} keys into m=2^{build_m.bit_length() - 1} bytes, {tb:.3f}s"},
+                      "sample": f"C2 build {build_keys} keys into m=2^{build_m.bit_length() - 1} bytes, "
+                                f"{reps} reps of {tb:.3f}s"},
             "cpu_model": cpu_model, "nproc": os.cpu_count()}
 
 

@@ -7,7 +7,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-BENCH="python bench.py --no-cpu --no-e2e --steps 10 --warmup 2 $*"
+BENCH="python bench.py --no-cpu --no-e2e --no-cold --steps 10 --warmup 2 $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $BENCH > $OUT/kt_bench.json 2> $OUT/kt.err || exit 1
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum" "TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_DRAM_sum"; do
