@@ -97,7 +97,7 @@ def main():
 
     import lsmt_amd
     from lsmt_amd import _lib, workload
-    from lsmt_amd.shard import gather_hits, shard_range
+    from lsmt_amd.shard import gather_hits, gather_hits_sparse, shard_range, sparse_cap
 
     L = _lib.load()
     lsmt_amd.set_path(args.path)
@@ -147,6 +147,30 @@ def main():
     torch.cuda.synchronize(dev)
     set_build_ms = (time.perf_counter() - t0) * 1e3
 
+    # Sparse exchange (shard.gather_hits_sparse): ship set-bit positions
+    # instead of dense rows. Default from 4 ranks up, where the dense gather's
+    # (N-1) x 4 MiB per rank outweighs the pack round trip's host check;
+    # CB_SPARSE_EXCHANGE=1/0 forces it on/off.
+    sparse_env = os.environ.get("CB_SPARSE_EXCHANGE")
+    use_sparse = use_dist and (sparse_env == "1" or (sparse_env != "0" and world >= 4))
+    cap = sparse_cap(n, nf_total, world)
+    xstats = {"sparse_steps": 0}
+    # asynchronous overflow report (no host round trip per step): cleared by
+    # k_hits_expand if any rank's set bits ever exceed cap; checked below
+    # before the results are reported
+    x_ok = torch.ones(1, dtype=torch.int32, device=dev) if use_sparse else None
+
+    def gather(buf):
+        if use_sparse:
+            gather_hits_sparse(hits_bufs[buf], nf_total, cap,
+                               lambda h, p: lsmt_amd.hits_compress(h, p, stream=sh),
+                               lambda pk, w, ro, full, ok: lsmt_amd.hits_expand(pk, w, ro, full, ok=ok,
+                                                                                stream=sh),
+                               out=hits_all_bufs[buf], ok=x_ok)
+            xstats["sparse_steps"] += 1
+        else:
+            gather_hits(hits_bufs[buf], nf_total, out=hits_all_bufs[buf])
+
     def exchange(buf):
         """The real exchange step: all-gather this step's hit rows from every
         rank (filter-major -> plain concatenation) over RCCL/xGMI, right after
@@ -155,8 +179,8 @@ def main():
         reused only after its gather has finished (gather_done)."""
         if not use_dist:
             return
-        if not args.overlap:
-            gather_hits(hits_bufs[buf], nf_total, out=hits_all_bufs[buf])
+        if not args.overlap or use_sparse:
+            gather(buf)
             return
         ev = torch.cuda.Event()
         ev.record(stream)
@@ -550,12 +574,21 @@ def main():
         torch.cuda.synchronize(dev)
         got = hits_bufs[(step_no[0] - 1) % 2].cpu().numpy().view(np.uint64)
         assert np.array_equal(got, expect), "bench hits differ from the oracle"
-        log("[check] hits bit-exact vs oracle")
+        if use_dist:  # the exchanged map: this rank's rows inside the global one
+            full = hits_all_bufs[(step_no[0] - 1) % 2].cpu().numpy().view(np.uint64)
+            assert np.array_equal(full[f_lo:f_lo + F], expect), "exchanged hits differ from the oracle"
+        log("[check] hits bit-exact vs oracle" + (" (local rows and the exchanged map)" if use_dist else ""))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.workload == "c3":
         cpu = cpu_baseline(look_np, F, m, kpf, args.build_keys, args.build_m_bits)
         log(f"[cpu] {cpu}")
+
+    x_fit = None
+    if use_sparse:  # every step's packs held all set bits: every exchanged map was complete
+        x_fit = bool(int(x_ok.item()))
+        if not x_fit:
+            log(f"[rank {rank}] WARNING: a sparse exchange overflowed cap={cap}; its map was incomplete")
 
     if rank == 0:
         line = {
@@ -568,9 +601,12 @@ def main():
                        "n_keys": n, "filters_per_gpu": F, "filters_total": nf_total, "m_bits": m,
                        "keys_per_filter": kpf,
                        "parallelism": "filter-sharded" + (
-                           ", RCCL all-gather of hit bitmaps" + (" overlapped with the next step's probe"
-                                                                 if args.overlap else " after each probe")
+                           ", RCCL all-gather of hit bitmaps" + (
+                               " as set-bit positions (sparse packs)" if use_sparse else
+                               (" overlapped with the next step's probe" if args.overlap else " after each probe"))
                            if use_dist else "")},
+            "exchange": (dict(xstats, mode="sparse", cap=cap, all_fit=x_fit) if use_sparse else
+                         {"mode": "dense"} if use_dist else None),
             "path": best,
             "kernels_us": {k: round(v["avg_us"], 2) for k, v in kprof.items()},
             "alt_paths": {k: {"value": round(v["value"], 1), "ms_per_step": round(v["ms_per_step"], 4)}

@@ -68,6 +68,12 @@ int cb_device_count(int* out);
 const char* cb_last_error(void);
 const char* cb_version(void);
 int cb_stream_synchronize(void* stream);
+/* Pinned (page-locked, device-mapped) host memory for key and hit buffers:
+ * FilterSet probes whose keys AND hits live in it run zero-copy (see
+ * cb_set_probe_fixed). For callers without the HIP runtime (the Rust shim,
+ * INTEGRATION.md §4). */
+int cb_host_alloc(uint64_t bytes, void** out);
+int cb_host_free(void* p);
 
 /* ---- filter lifetime (BloomFilter::new / Drop) ---- */
 /* m_bits may be 0 (legal in the reference; inserts/probes then fail with
@@ -279,6 +285,29 @@ int cb_get_many_var(const cb_table* const* tables, uint32_t nt, const uint64_t* 
                     const uint32_t* hit_rows, const uint8_t* bytes, const uint64_t* offsets,
                     uint64_t n, int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap,
                     uint64_t* total, void* stream);
+
+/* ---- multi-GPU exchange ----
+ * Each rank holds hit rows [rows][words] (uint64) for its filter subset; the
+ * ranks all-gather them so every rank has the [total_rows][words] map that
+ * Database::get's fan-out reads (src/lib.rs:129-134). At BASELINE densities
+ * the rows are sparse, so a rank can ship the positions of its set bits:
+ *   cb_hits_compress: pack = uint32[2 + cap] = {count, 0, positions...};
+ *     position = row * words * 64 + bit, ascending; count may exceed cap (then
+ *     only the first cap positions are stored: all ranks must fall back to the
+ *     dense exchange).
+ *     Requires rows * words * 64 <= 2^32. Device pointers, async on stream.
+ *   cb_hits_expand: full := the dense map holding the positions of packs[r]
+ *     (nranks packs of 2 + cap words from cb_hits_compress, as all-gathered)
+ *     at global row row_off[r] (host array, ascending, nranks <= 64); every
+ *     word of full is written once. Bit-identical to the dense all-gather when no
+ *     rank's count exceeds cap. A rank whose count exceeds cap is skipped and
+ *     clears *ok (a device uint32, may be NULL): the overflow report is
+ *     asynchronous, so the caller checks ok before using full and redoes that
+ *     batch's exchange densely when it is 0. */
+int cb_hits_compress(const uint64_t* hits, uint64_t rows, uint64_t words, uint32_t* pack,
+                     uint64_t cap, void* stream);
+int cb_hits_expand(const uint32_t* packs, uint32_t nranks, uint64_t cap, const uint64_t* row_off,
+                   uint64_t words, uint64_t total_rows, uint64_t* full, uint32_t* ok, void* stream);
 
 /* ---- tuning / introspection (bench + tests) ---- */
 /* Path selection: 0 = auto, 1 = force direct (per-key atomics / gathers),

@@ -26,8 +26,11 @@ from .bloom import (  # noqa: E402
     sstable_create,
     zone_bounds,
     ZoneMap,
+    hits_compress,
+    hits_expand,
 )
 
 __all__ = ["BloomFilter", "BloomProto", "DeviceKeys", "FilterSet", "insert_many", "KeyBatch", "device_count", "last_path",
-           "probe", "set_path", "unpack_hits", "zone_bounds", "ZoneMap", "TableMeta", "Table", "get_many", "sstable_create"]
+           "probe", "set_path", "unpack_hits", "zone_bounds", "ZoneMap", "TableMeta", "Table", "get_many", "sstable_create",
+           "hits_compress", "hits_expand"]
 __version__ = "0.1.0"

@@ -76,6 +76,10 @@ def load():
         "cb_last_error": ([], ctypes.c_char_p),
         "cb_version": ([], ctypes.c_char_p),
         "cb_stream_synchronize": ([P], i32),
+        "cb_host_alloc": ([u64, ctypes.POINTER(P)], i32),
+        "cb_host_free": ([P], i32),
+        "cb_hits_compress": ([P, u64, u64, P, u64, P], i32),
+        "cb_hits_expand": ([P, u32, u64, pu64, u64, u64, P, P, P], i32),
         "cb_filter_create": ([u64, i32, pp], i32),
         "cb_filter_destroy": ([P], i32),
         "cb_filter_bits": ([P, pu64], i32),

@@ -769,3 +769,29 @@ def unpack_hits(hits: np.ndarray, n: int) -> np.ndarray:
     h = np.ascontiguousarray(hits, dtype="<u8")
     bits = np.unpackbits(h.view(np.uint8).reshape(h.shape[0], -1), axis=1, bitorder="little")
     return bits[:, :n].astype(bool)
+
+
+# ---- multi-GPU exchange (lsmt_amd/shard.py) ---------------------
+
+def hits_compress(hits, pack, stream=None) -> None:
+    """pack (int32 device tensor of 2 + cap) := {count, 0, set-bit positions}
+    of hits ([rows][words] int64 device tensor): cb_hits_compress."""
+    rows, words = hits.shape
+    cap = int(pack.numel()) - 2
+    hp, k1 = _ptr_of(hits)
+    pp, k2 = _ptr_of(pack)
+    _raise(_L().cb_hits_compress(hp, rows, words, pp, cap, _stream(stream)))
+
+
+def hits_expand(packs, world: int, row_off, full, ok=None, stream=None) -> None:
+    """full ([total_rows][words] int64 device tensor) := the OR of every
+    rank's positions (packs: the all-gathered int32 [world * (2 + cap)]).
+    ok: optional int32 device tensor, cleared to 0 when some rank's count
+    exceeds cap (that rank is then missing from full)."""
+    cap = int(packs.numel()) // world - 2
+    total_rows, words = full.shape
+    off = (ctypes.c_uint64 * world)(*[int(x) for x in row_off])
+    pp, k1 = _ptr_of(packs)
+    fp, k2 = _ptr_of(full)
+    op, k3 = _ptr_of(ok)
+    _raise(_L().cb_hits_expand(pp, world, cap, off, words, total_rows, fp, op, _stream(stream)))

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "cassbloom.h"
+#include "exchange.hpp"
 #include "filterset.hpp"
 #include "flush.hpp"
 #include "kernels.hpp"
@@ -202,6 +203,7 @@ struct Workspace {
   DevBuf t_views, t_rows, t_which, t_line, t_dlen, t_voff, t_scan, t_vals;
   DevBuf i_cnt, i_base, i_tmp, i_end, i_err, i_start;                 // line indexing
   DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_lens, f_loff, f_scan, f_flag;  // SsTable::create
+  DevBuf x_sums;                                                          // cb_hits_compress
 };
 
 std::mutex g_ws_mu;
@@ -1094,6 +1096,43 @@ int cb_init(int device) {
 
 int cb_stream_synchronize(void* stream) {
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return CB_OK;
+}
+
+int cb_hits_compress(const uint64_t* hits, uint64_t rows, uint64_t words, uint32_t* pack,
+                     uint64_t cap, void* stream) {
+  if (!pack || (rows * words && !hits)) return fail(CB_EINVAL, "null argument");
+  if (rows && words && rows * words > (1ull << 26)) return fail(CB_EINVAL, "rows * words * 64 exceeds 2^32");
+  hipStream_t s = (hipStream_t)stream;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  Workspace& ws = workspace(dev, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  HIP_TRY(ws.x_sums.reserve(cb::kMaxCompressBlocks * 4, s));
+  HIP_TRY(cb::launch_hits_compress(hits, rows, words, pack, cap, (uint32_t*)ws.x_sums.p, s));
+  return CB_OK;
+}
+
+int cb_hits_expand(const uint32_t* packs, uint32_t nranks, uint64_t cap, const uint64_t* row_off,
+                   uint64_t words, uint64_t total_rows, uint64_t* full, uint32_t* ok, void* stream) {
+  if (!full || (nranks && (!packs || !row_off))) return fail(CB_EINVAL, "null argument");
+  if (nranks > cb::kMaxRanks) return fail(CB_EINVAL, "more than 64 ranks");
+  cb::RankRows rr{};
+  for (uint32_t r = 0; r < nranks; ++r) rr.row_off[r] = row_off[r];
+  HIP_TRY(cb::launch_hits_expand(packs, nranks, cap, rr, words, total_rows, full, ok, (hipStream_t)stream));
+  return CB_OK;
+}
+
+int cb_host_alloc(uint64_t bytes, void** out) {
+  if (!out) return fail(CB_EINVAL, "null out");
+  *out = nullptr;
+  if (!bytes) return CB_OK;
+  HIP_TRY(hipHostMalloc(out, bytes, hipHostMallocDefault));
+  return CB_OK;
+}
+
+int cb_host_free(void* p) {
+  if (p) HIP_TRY(hipHostFree(p));
   return CB_OK;
 }
 

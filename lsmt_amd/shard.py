@@ -8,6 +8,13 @@ layout is filter-major, rank r's rows are one contiguous slice of the global
 [F][ceil(n/64)] bitmap, so the exchange is a plain concatenation:
 ``all_gather_into_tensor`` over RCCL/xGMI on GPUs (gloo on CPU in the tests).
 Uneven shards are padded to the largest shard and sliced back.
+
+The rows are sparse at BASELINE densities (one table per present key, false
+positives ~(1.55 %)^2 per (key, table)), so ``gather_hits_sparse`` ships each
+rank's set-bit positions instead (cb_hits_compress -> all-gather of fixed-size
+packs -> cb_hits_expand) and rebuilds the identical map; if any rank has more
+set bits than the pack holds, every rank sees that in the gathered counts and
+all of them take the dense path for that step.
 """
 from __future__ import annotations
 
@@ -49,4 +56,58 @@ def gather_hits(local_hits, n_total: int, group=None, out=None):
     if out is not None:
         out.copy_(full)
         return out
+    return full
+
+
+def sparse_cap(n_keys: int, f_total: int, world: int) -> int:
+    """Pack capacity for a probe batch, the same on every rank (the packs are
+    all-gathered as equal-size tensors): sized for the largest shard, with the
+    present keys whose table lives on it (half of the SURVEY.md §8d lookups,
+    spread over all tables) plus 25 % slack, one false positive per 1000
+    (key, table) pairs (the expected rate is 2.4e-4), and 4096."""
+    f_local = -(-f_total // world)
+    present = (n_keys // 2) * f_local // max(f_total, 1)
+    return int(1.25 * present + n_keys * f_local / 1000) + 4096
+
+
+def gather_hits_sparse(local_hits, n_total: int, cap: int, compress, expand, group=None, out=None,
+                       stats=None, ok=None):
+    """Same result as gather_hits; cap must be equal on every rank
+    (sparse_cap). compress(local_hits, pack) fills an int32
+    pack of 2 + cap words {count, 0, positions}; expand(packs, world, row_off,
+    full, ok) rebuilds the global map (lsmt_amd.hits_compress / hits_expand on
+    GPUs).
+
+    Synchronous (ok=None): the gathered counts are read on the host; if some
+    rank overflowed (the same decision on every rank) all ranks then run the
+    dense all-gather, so the result is always complete. stats (a dict,
+    optional) receives "sparse" (whether the packs sufficed) and "max_count".
+
+    Asynchronous (ok = an int32 device tensor holding 1): no host round trip;
+    expand clears ok if some rank overflowed, and the caller must check ok
+    before using the map and redo that batch with gather_hits if it is 0."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    words = local_hits.shape[1]
+    pack = torch.empty(2 + cap, dtype=torch.int32, device=local_hits.device)
+    compress(local_hits, pack)
+    packs = torch.empty(world * (2 + cap), dtype=torch.int32, device=local_hits.device)
+    dist.all_gather_into_tensor(packs, pack, group=group)
+    row_off = [shard_range(n_total, world, r)[0] for r in range(world)]
+    if ok is not None:
+        full = out if out is not None else torch.empty((n_total, words), dtype=local_hits.dtype,
+                                                       device=local_hits.device)
+        expand(packs, world, row_off, full, ok)
+        return full
+    counts = packs.view(world, 2 + cap)[:, 0].cpu().numpy().astype("int64") & 0xFFFFFFFF
+    if stats is not None:
+        stats["sparse"] = bool((counts <= cap).all())
+        stats["max_count"] = int(counts.max())
+    if (counts > cap).any():
+        return gather_hits(local_hits, n_total, group=group, out=out)
+    full = out if out is not None else torch.empty((n_total, words), dtype=local_hits.dtype,
+                                                   device=local_hits.device)
+    expand(packs, world, row_off, full, None)
     return full

@@ -30,7 +30,37 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_filters, result_q):
+def np_compress(h, pack):
+    """CPU stand-in for lsmt_amd.hits_compress (the kernel is covered on the
+    GPU by tests/test_gpu_parity.py::test_hits_compress_expand)."""
+    a = np.ascontiguousarray(h.numpy()).view(np.uint64).reshape(-1)
+    pos = np.flatnonzero(np.unpackbits(a.view(np.uint8), bitorder="little")).astype(np.uint32)
+    cap = pack.numel() - 2
+    pk = pack.numpy().view(np.uint32)
+    pk[:] = 0
+    pk[0] = len(pos)
+    k = min(len(pos), cap)
+    pk[2:2 + k] = pos[:k]
+
+
+def np_expand(packs, world, row_off, full, ok=None):
+    words = full.shape[1]
+    fw = full.numpy().view(np.uint64).reshape(-1)
+    fw[:] = 0
+    pk = packs.numpy().view(np.uint32).reshape(world, -1)
+    cap = pk.shape[1] - 2
+    for r in range(world):
+        if int(pk[r, 0]) > cap:  # as k_hits_expand: skip the rank, report
+            if ok is not None:
+                ok[0] = 0
+            continue
+        cnt = int(pk[r, 0])
+        pos = pk[r, 2:2 + cnt].astype(np.uint64)
+        np.bitwise_or.at(fw, row_off[r] * words + (pos >> np.uint64(6)),
+                         np.left_shift(np.uint64(1), pos & np.uint64(63)))
+
+
+def _worker(rank, world, port, n_filters, result_q, mode="dense"):
     import torch
     import torch.distributed as dist
 
@@ -51,7 +81,25 @@ def _worker(rank, world, port, n_filters, result_q):
         words = (n + 63) // 64
         lh = oracle.probe_fixed(local, look) if local else np.zeros((0, words), np.uint64)
         t = torch.from_numpy(lh.view(np.int64).copy()).reshape(hi - lo, words)
-        full = gather_hits(t, n_filters)
+        if mode == "dense":
+            full = gather_hits(t, n_filters)
+        else:
+            from lsmt_amd.shard import gather_hits_sparse, sparse_cap
+            # "overflow": a pack too small for one rank -> every rank takes the dense path
+            cap = 3 if mode == "overflow" else sparse_cap(n, n_filters, world)
+            if mode.startswith("async"):
+                # no host round trip: the overflow comes back in ok, and the
+                # caller redoes that batch with the dense exchange
+                cap = 3 if mode == "async_overflow" else cap
+                ok = torch.ones(1, dtype=torch.int32)
+                full = gather_hits_sparse(t, n_filters, cap, np_compress, np_expand, ok=ok)
+                assert int(ok[0]) == (0 if mode == "async_overflow" else 1)
+                if not int(ok[0]):
+                    full = gather_hits(t, n_filters)
+            else:
+                st = {}
+                full = gather_hits_sparse(t, n_filters, cap, np_compress, np_expand, stats=st)
+                assert st["sparse"] == (mode == "sparse")
         if rank == 0:
             ref = []
             for f in range(n_filters):
@@ -65,13 +113,15 @@ def _worker(rank, world, port, n_filters, result_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_filters", [(2, 6), (2, 5), (3, 7)])
-def test_sharded_probe_allgather_gloo(world, n_filters):
+@pytest.mark.parametrize("world,n_filters,mode", [(2, 6, "dense"), (2, 5, "dense"), (3, 7, "dense"),
+                                                  (2, 6, "sparse"), (3, 7, "sparse"), (3, 7, "overflow"),
+                                                  (3, 7, "async"), (2, 5, "async_overflow")])
+def test_sharded_probe_allgather_gloo(world, n_filters, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_filters, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_filters, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -1,0 +1,64 @@
+"""Time the pieces of the sparse hit-bitmap exchange (lsmt_amd/shard.py
+gather_hits_sparse) on one GPU at the per-rank shape of C3 on 8 GPUs: a
+[32][16384] rank slice holding ~66K set bits, 8 packs of that size to expand
+into the [256][16384] global map. Prints one JSON line of microseconds per
+piece (HIP events, median of 50). Diagnostic only."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import lsmt_amd  # noqa: E402
+from lsmt_amd.shard import sparse_cap  # noqa: E402
+
+
+def timed(fn, reps=50):
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    return round(float(np.median(ts)), 2)
+
+
+def main():
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29517")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    rows, words, world = 32, 16384, 8
+    rng = np.random.default_rng(1)
+    bits = np.zeros(rows * words * 64, np.uint8)
+    bits[rng.choice(bits.size, 66_000, replace=False)] = 1
+    h = torch.from_numpy(np.packbits(bits, bitorder="little").view(np.int64).reshape(rows, words).copy()).to(dev)
+    cap = sparse_cap(1 << 20, rows * world, world)
+    pack = torch.empty(2 + cap, dtype=torch.int32, device=dev)
+    packs = torch.empty(world * (2 + cap), dtype=torch.int32, device=dev)
+    full = torch.empty((rows * world, words), dtype=torch.int64, device=dev)
+    lsmt_amd.hits_compress(h, pack)
+    for r in range(world):
+        packs[r * (2 + cap):(r + 1) * (2 + cap)] = pack
+    row_off = [r * rows for r in range(world)]
+    out = {"cap": cap, "bits_per_rank": int(bits.sum())}
+    out["compress_us"] = timed(lambda: lsmt_amd.hits_compress(h, pack))
+    out["expand_8_ranks_us"] = timed(lambda: lsmt_amd.hits_expand(packs, world, row_off, full))
+    out["memset_full_us"] = timed(lambda: full.zero_())
+    out["counts_to_host_us"] = timed(lambda: packs.view(world, 2 + cap)[:, 0].cpu())
+    one = torch.empty(2 + cap, dtype=torch.int32, device=dev)
+    out["allgather_pack_world1_us"] = timed(lambda: dist.all_gather_into_tensor(one, pack))
+    dense = torch.empty((rows, words), dtype=torch.int64, device=dev)
+    out["allgather_dense_world1_us"] = timed(lambda: dist.all_gather_into_tensor(dense, h))
+    print(json.dumps(out))
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
