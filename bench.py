@@ -149,8 +149,8 @@ def main():
 
     # Sparse exchange (shard.gather_hits_sparse): ship set-bit positions
     # instead of dense rows. Default from 4 ranks up, where the dense gather's
-    # (N-1) x 4 MiB per rank outweighs the pack round trip's host check;
-    # CB_SPARSE_EXCHANGE=1/0 forces it on/off.
+    # (N-1) x 4 MiB per rank outweighs compress + expand (~28 us measured on
+    # one GPU, tools/xchg_parts.py); CB_SPARSE_EXCHANGE=1/0 forces it on/off.
     sparse_env = os.environ.get("CB_SPARSE_EXCHANGE")
     use_sparse = use_dist and (sparse_env == "1" or (sparse_env != "0" and world >= 4))
     cap = sparse_cap(n, nf_total, world)
@@ -485,7 +485,7 @@ def main():
             k_fl = max(3, args.steps // 4)
             fel = timed(step_flush, k_fl)
             fprof = kernel_ms(["k_sorted_check", "k_sort_keys", "rocprim_merge_sort", "k_line_lens", "k_scan_u64",
-                               "k_format", "k_line_count", "k_line_emit", "k_line_finish", "k_line_keys",
+                               "k_format", "k_format_index", "k_line_count", "k_line_emit", "k_line_finish", "k_line_keys",
                                "k_build_part", "k_build_tile", "k_insert_direct"], step_flush, k_fl)
             out_bytes = made[-1][0].nbytes
             res[label] = {"entries_per_s": round(nf_e / (fel / k_fl), 1), "ms_per_flush": round(fel / k_fl * 1e3, 3),

@@ -695,8 +695,21 @@ def sstable_create(entries, m: int = 1024, device: int = 0, stream=None):
     bloom = BloomFilter(0, device=device, _handle=fh.value)
     zone = ZoneMap()
     if kb.n:
-        zone = ZoneMap(_key_bytes(kb, lo.value), _key_bytes(kb, hi.value))
+        zone = ZoneMap(*_key_pair(kb, lo.value, hi.value))
     return table, bloom, zone
+
+
+def _key_pair(b: KeyBatch, i: int, j: int):
+    """Keys i and j of a ragged batch as bytes: two device round trips for
+    device buffers (their offsets, then both keys' bytes), none for host ones."""
+    if hasattr(b.offsets, "cpu") or hasattr(b.data, "cpu"):
+        import torch
+        offs = b.offsets if hasattr(b.offsets, "cpu") else torch.from_numpy(np.asarray(b.offsets).view(np.int64))
+        o = torch.stack([offs[i:i + 2], offs[j:j + 2]]).cpu().reshape(-1).tolist()
+        data = b.data if hasattr(b.data, "cpu") else torch.from_numpy(np.asarray(b.data))
+        both = torch.cat([data[o[0]:o[1]], data[o[2]:o[3]]]).cpu().numpy().tobytes()
+        return both[:o[1] - o[0]], both[o[1] - o[0]:]
+    return _key_bytes(b, i), _key_bytes(b, j)
 
 
 def _to_var(b: KeyBatch) -> KeyBatch:

@@ -1585,45 +1585,70 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   const uint64_t *dko = nullptr, *dvo = nullptr;
   const cb::SortKey* order = nullptr;
   cb::SortKey ends[2];
+  // flags: [0] input already sorted, [1] some key holds '\n' or '\t' (the
+  // direct line index does not apply), [2] keys strictly increasing
+  uint32_t hflags[4] = {1, 0, 1, 0};
+  uint64_t ktot = 0, vtot = 0;
   {
     Workspace& ws = workspace(device, s);
     std::lock_guard<std::mutex> lk(ws.mu);
-    auto stage = [&](DevBuf& dbytes, DevBuf& doff, const uint8_t* bytes, const uint64_t* off,
-                     const uint8_t** bp, const uint64_t** op) -> int {
-      uint64_t total = 0;
-      if (is_device_ptr(off)) {
-        HIP_TRY(hipMemcpyAsync(&total, off + n, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
+    // Offsets: host ones are validated and copied (their totals are known
+    // here); device ones are used in place, their totals read back together
+    // with the sortedness flag in ONE round trip below.
+    auto stage_off = [&](DevBuf& doff, const uint64_t* off, const uint64_t** op, uint64_t* tot,
+                         bool* on_dev) -> int {
+      *on_dev = is_device_ptr(off);
+      if (*on_dev) {
         *op = off;
-      } else {
-        for (uint64_t i = 0; i < n; ++i)
-          if (off[i + 1] < off[i]) return fail(CB_EINVAL, "offsets must be non-decreasing");
-        total = off[n];
-        HIP_TRY(doff.reserve((n + 1) * 8, s));
-        HIP_TRY(hipMemcpyAsync(doff.p, off, (n + 1) * 8, hipMemcpyHostToDevice, s));
-        *op = (const uint64_t*)doff.p;
+        return CB_OK;
       }
-      if (total && !bytes) return fail(CB_EINVAL, "null bytes");
-      if (!total || is_device_ptr(bytes)) {
-        *bp = bytes;
-      } else {
-        HIP_TRY(dbytes.reserve(total, s));
-        HIP_TRY(hipMemcpyAsync(dbytes.p, bytes, total, hipMemcpyHostToDevice, s));
-        *bp = (const uint8_t*)dbytes.p;
-      }
+      for (uint64_t i = 0; i < n; ++i)
+        if (off[i + 1] < off[i]) return fail(CB_EINVAL, "offsets must be non-decreasing");
+      *tot = off[n];
+      HIP_TRY(doff.reserve((n + 1) * 8, s));
+      HIP_TRY(hipMemcpyAsync(doff.p, off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+      *op = (const uint64_t*)doff.p;
       return CB_OK;
     };
-    if ((rc = stage(ws.keys, ws.offsets, keys, key_off, &dk, &dko))) return rc;
-    if ((rc = stage(ws.f_vb, ws.f_vo, vals, val_off, &dv, &dvo))) return rc;
+    // Bytes: device bytes in place; host bytes copied (device offsets over
+    // host bytes need the total first: one extra round trip, a rare mix).
+    auto stage_bytes = [&](DevBuf& dbytes, const uint8_t* bytes, const uint64_t* off, bool off_dev,
+                           uint64_t* tot, const uint8_t** bp) -> int {
+      if (!bytes || is_device_ptr(bytes)) {
+        *bp = bytes;
+        return CB_OK;
+      }
+      if (off_dev) {
+        HIP_TRY(hipMemcpyAsync(tot, off + n, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+      }
+      if (*tot) {
+        HIP_TRY(dbytes.reserve(*tot, s));
+        HIP_TRY(hipMemcpyAsync(dbytes.p, bytes, *tot, hipMemcpyHostToDevice, s));
+      }
+      *bp = (const uint8_t*)dbytes.p;
+      return CB_OK;
+    };
+    bool kdev = false, vdev = false;
+    if ((rc = stage_off(ws.offsets, key_off, &dko, &ktot, &kdev))) return rc;
+    if ((rc = stage_off(ws.f_vo, val_off, &dvo, &vtot, &vdev))) return rc;
+    if ((rc = stage_bytes(ws.keys, keys, key_off, kdev, &ktot, &dk))) return rc;
+    if ((rc = stage_bytes(ws.f_vb, vals, val_off, vdev, &vtot, &dv))) return rc;
+    HIP_TRY(ws.f_flag.reserve(16, s));
+    uint32_t* flags = (uint32_t*)ws.f_flag.p;
+    HIP_TRY(hipMemcpyAsync(flags, hflags, 16, hipMemcpyHostToDevice, s));
+    // stable sort by key unless already sorted (memtable flushes are)
+    if (n) HIP_TRY(cb::launch_sorted_check(dk, dko, n, flags, s));
+    HIP_TRY(hipMemcpyAsync(&hflags[0], flags, 4, hipMemcpyDeviceToHost, s));
+    if (kdev) HIP_TRY(hipMemcpyAsync(&ktot, dko + n, 8, hipMemcpyDeviceToHost, s));
+    if (vdev) HIP_TRY(hipMemcpyAsync(&vtot, dvo + n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if ((ktot && !keys) || (vtot && !vals)) return fail(CB_EINVAL, "null bytes");
+    // the file's length is read back at the end; its buffer is sized by the
+    // bound sum(k + 2 + 4 ceil(v / 3)) <= K + 2n + (4V + 8n) / 3, plus slack
+    const uint64_t cap_bytes = ktot + 2 * n + (4 * vtot + 8 * n) / 3 + 1 + 16;
     if (n) {
-      // stable sort by key unless already sorted (memtable flushes are)
-      uint32_t sorted = 1;
-      HIP_TRY(ws.f_flag.reserve(4, s));
-      HIP_TRY(hipMemcpyAsync(ws.f_flag.p, &sorted, 4, hipMemcpyHostToDevice, s));
-      HIP_TRY(cb::launch_sorted_check(dk, dko, n, (uint32_t*)ws.f_flag.p, s));
-      HIP_TRY(hipMemcpyAsync(&sorted, ws.f_flag.p, 4, hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipStreamSynchronize(s));
-      if (!sorted) {
+      if (!hflags[0]) {
         HIP_TRY(ws.f_sk.reserve(n * sizeof(cb::SortKey), s));
         HIP_TRY(ws.f_sk2.reserve(n * sizeof(cb::SortKey), s));
         cb::SortKey* a0 = (cb::SortKey*)ws.f_sk.p;
@@ -1641,38 +1666,64 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
       uint64_t* loff = (uint64_t*)ws.f_loff.p;
       HIP_TRY(cb::launch_line_lens(order, dko, dvo, n, (uint64_t*)ws.f_lens.p, s));
       HIP_TRY(cb::launch_scan_u64((const uint64_t*)ws.f_lens.p, loff, n, (uint64_t*)ws.f_scan.p, s));
-      HIP_TRY(hipMemcpyAsync(&t->len, loff + n, 8, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(&t->len, loff + n, 8, hipMemcpyDeviceToHost, s));  // read after the last sync
       if (order) {
         HIP_TRY(hipMemcpyAsync(&ends[0], order, sizeof(cb::SortKey), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(&ends[1], order + n - 1, sizeof(cb::SortKey), hipMemcpyDeviceToHost, s));
       }
-      HIP_TRY(hipStreamSynchronize(s));
     }
-    if (pool_alloc(device, t->len + 16, (void**)&t->data, &t->data_cap) != hipSuccess) {
+    if (pool_alloc(device, cap_bytes, (void**)&t->data, &t->data_cap) != hipSuccess) {
       t->data = nullptr;
       return fail(CB_ENOMEM, "device allocation failed for an SSTable buffer");
     }
-    HIP_TRY(hipMemsetAsync(t->data + t->len, 0, 16, s));
-    if (n)
-      HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, (const uint64_t*)ws.f_loff.p, n, t->data, s));
-  }
-  if ((rc = index_table(t.get(), s))) return rc;
-  // zone map: ZoneMap::update over the sorted keys = first / last line
-  if (n) {
-    if (zone_min_idx) *zone_min_idx = order ? ends[0].idx : 0;
-    if (zone_max_idx) *zone_max_idx = order ? ends[1].idx : n - 1;
+    if (!n) HIP_TRY(hipMemsetAsync(t->data, 0, 16, s));
+    if (n) {
+      const uint64_t* loff = (const uint64_t*)ws.f_loff.p;
+      HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, loff, n, t->data, s));  // + 16 B of slack
+      // the line index straight from the entries (entry p is line p), no re-read of the file
+      t->nlines = n;
+      t->nfence = (n + cb::kFenceStride - 1) / cb::kFenceStride;
+      const size_t ibytes = n * sizeof(cb::LineRec) + n * 8 + t->nfence * 8;
+      if (pool_alloc(device, ibytes, (void**)&t->rec, &t->rec_cap) != hipSuccess) {
+        t->rec = nullptr;
+        return fail(CB_ENOMEM, "device allocation failed for an SSTable index");
+      }
+      t->pfx = (uint64_t*)(t->rec + n);
+      t->fence = t->pfx + n;
+      HIP_TRY(cb::launch_format_index(order, dk, dko, dvo, loff, n, t->rec, t->pfx, t->fence, flags, s));
+      HIP_TRY(hipMemcpyAsync(&hflags[1], flags + 1, 8, hipMemcpyDeviceToHost, s));
+    }
   }
   // the table's Bloom filter: SsTable::create's bloom.insert loop, batched
+  cb_filter* f = nullptr;
   if (bloom_out) {
-    cb_filter* f = nullptr;
     if ((rc = cb_filter_create(m_bits, device, &f))) return rc;
     if (n && (rc = insert_impl(f, dk, dko, 0, n, s))) {
       cb_filter_destroy(f);
       return rc;
     }
-    *bloom_out = f;
   }
   HIP_TRY(hipStreamSynchronize(s));
+  if (n) {
+    // zone map: ZoneMap::update over the sorted keys = first / last line
+    if (zone_min_idx) *zone_min_idx = order ? ends[0].idx : 0;
+    if (zone_max_idx) *zone_max_idx = order ? ends[1].idx : n - 1;
+    if (hflags[1]) {
+      // a key holds '\n' or '\t': the file's lines are not the entries, so
+      // index it the way SsTable::get splits it (src/sstable.rs:142-146)
+      pool_release(device, t->rec, t->rec_cap);
+      t->rec = nullptr;
+      t->pfx = t->fence = nullptr;
+      t->nlines = t->nfence = 0;
+      if ((rc = index_table(t.get(), s))) {
+        if (f) cb_filter_destroy(f);
+        return rc;
+      }
+    } else {
+      t->fast = hflags[2] != 0 && !g_table_exact;
+    }
+  }
+  if (bloom_out) *bloom_out = f;
   *table_out = t.release();
   return CB_OK;
 }

@@ -43,13 +43,75 @@ __global__ __launch_bounds__(kNT) void k_sort_keys(const uint8_t* __restrict__ k
   out[i] = s;
 }
 
-// *ok &= key[i-1] <= key[i] for all i (already in stable-sorted order).
+// The first 16 bytes of key p (output order) as zero-padded big-endian words,
+// and its length. Unsorted input: the sort record already holds them. Sorted
+// input: the aligned dwords that contain the key's bytes (a dword never
+// crosses a page edge, so these loads stay inside mapped memory however the
+// key buffer is aligned), byte-aligned in registers.
+__device__ __forceinline__ void key_words(const SortKey* order, const uint8_t* kb,
+                                          const uint64_t* ko, uint64_t p, uint64_t& i,
+                                          uint64_t& kl, uint64_t& w0, uint64_t& w1) {
+  i = order ? order[p].idx : p;
+  const uint64_t o0 = ko[i];
+  kl = ko[i + 1] - o0;
+  if (order) {
+    w0 = order[p].w0;
+    w1 = order[p].w1;
+    return;
+  }
+  const uint64_t m = kl < 16 ? kl : 16;
+  uint32_t d[5] = {0, 0, 0, 0, 0};
+  const uint64_t a0 = (uint64_t)(uintptr_t)(kb + o0);
+  const uint32_t* base = reinterpret_cast<const uint32_t*>((uintptr_t)(a0 & ~3ull));
+  const uint32_t sh = (uint32_t)(a0 & 3);
+  const uint32_t nd = m ? (uint32_t)((sh + m + 3) / 4) : 0;  // dwords holding the key's first m bytes
+#pragma unroll
+  for (uint32_t j = 0; j < 5; ++j)
+    if (j < nd) d[j] = base[j];
+  uint32_t x[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) x[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+  // little-endian bytes -> big-endian words, bytes past m cleared
+  const uint64_t lo = (uint64_t)x[1] << 32 | x[0], hi = (uint64_t)x[3] << 32 | x[2];
+  const uint64_t b0 = __builtin_bswap64(lo), b1 = __builtin_bswap64(hi);
+  w0 = m >= 8 ? b0 : (m ? b0 & ~(~0ull >> (8 * m)) : 0);
+  w1 = m >= 16 ? b1 : (m > 8 ? b1 & ~(~0ull >> (8 * (m - 8))) : 0);
+}
+
+// Does a big-endian word hold byte c among its first m (<= 8) bytes?
+__device__ __forceinline__ bool has_byte(uint64_t w, uint64_t m, uint32_t c) {
+  if (!m) return false;
+  const uint64_t keep = m >= 8 ? ~0ull : ~(~0ull >> (8 * m));  // the first m bytes
+  const uint64_t x = (w ^ (0x0101010101010101ull * c)) | ~keep;  // 0x00 where byte == c
+  return ((x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull) != 0;
+}
+
+// Rust str order of keys q and p (q, p index the key batch) given their first
+// 16 bytes as words: from the words alone when both fit in 16 bytes.
+__device__ __forceinline__ int key_cmp(const uint8_t* kb, const uint64_t* ko, uint64_t q,
+                                       uint64_t ql, uint64_t qw0, uint64_t qw1, uint64_t p,
+                                       uint64_t pl, uint64_t pw0, uint64_t pw1) {
+  if (ql <= 16 && pl <= 16) {
+    if (qw0 != pw0) return qw0 < pw0 ? -1 : 1;
+    if (qw1 != pw1) return qw1 < pw1 ? -1 : 1;
+    return ql < pl ? -1 : (ql > pl ? 1 : 0);
+  }
+  return bytes_cmp(kb + ko[q], ql, kb + ko[p], pl);
+}
+
+// *ok &= key[i-1] <= key[i] for all i (already in stable-sorted order). Each
+// lane's key comes in as words; the previous one from the neighbour lane.
 __global__ __launch_bounds__(kNT) void k_sorted_check(const uint8_t* __restrict__ kb,
                                                       const uint64_t* __restrict__ ko, uint64_t n,
                                                       uint32_t* ok) {
-  const uint64_t i = (uint64_t)blockIdx.x * kNT + threadIdx.x + 1;
-  const bool bad =
-      i < n && bytes_cmp(kb + ko[i - 1], ko[i] - ko[i - 1], kb + ko[i], ko[i + 1] - ko[i]) > 0;
+  const uint64_t p = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t i = 0, kl = 0, w0 = 0, w1 = 0;
+  if (p < n) key_words(nullptr, kb, ko, p, i, kl, w0, w1);
+  uint64_t pkl = __shfl_up(kl, 1, 64), pw0 = __shfl_up(w0, 1, 64), pw1 = __shfl_up(w1, 1, 64);
+  uint64_t pi = p - 1;
+  if (p < n && lane == 0 && p > 0) key_words(nullptr, kb, ko, p - 1, pi, pkl, pw0, pw1);
+  const bool bad = p < n && p > 0 && key_cmp(kb, ko, p - 1, pkl, pw0, pw1, p, kl, w0, w1) > 0;
   // one atomic per block, and none once the flag is down: a fully unsorted
   // batch would otherwise serialise up to a million atomics on one word
   if (__syncthreads_or(bad) && threadIdx.x == 0 && *(volatile uint32_t*)ok) atomicAnd(ok, 0u);
@@ -128,6 +190,8 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   const uint8_t* v = vb + (live ? vo[i] : 0);
   const uint64_t vl = live ? vo[i + 1] - vo[i] : 0;
   const uint64_t o = live ? loff[p] : 0;
+  // 16 zero bytes after the file: the readable slack of the table's buffer
+  if (pend == n && threadIdx.x < 16) out[loff[n] + threadIdx.x] = 0;
   if (total > kFormatLds) {  // uniform: long lines, direct byte stores
     if (live) format_line(k, kl, v, vl, [&](uint64_t j, uint8_t c) { out[o + j] = c; });
     return;
@@ -149,7 +213,65 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   if (tail0 + threadIdx.x < total) g[tail0 + threadIdx.x] = stage[tail0 + threadIdx.x];
 }
 
+// One lane per entry p (= line p of the file): the LineRec, prefix and fence
+// that k_line_finish / k_line_keys would derive by re-reading the file.
+__global__ __launch_bounds__(kNT) void k_format_index(const SortKey* __restrict__ order,
+                                                      const uint8_t* __restrict__ kb,
+                                                      const uint64_t* __restrict__ ko,
+                                                      const uint64_t* __restrict__ vo,
+                                                      const uint64_t* __restrict__ loff, uint64_t n,
+                                                      LineRec* __restrict__ rec,
+                                                      uint64_t* __restrict__ pfx,
+                                                      uint64_t* __restrict__ fence, uint32_t* flags) {
+  const uint64_t p = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  bool special = false, not_inc = false;
+  uint64_t i = 0, kl = 0, w0 = 0, w1 = 0;
+  const bool live = p < n;
+  if (live) key_words(order, kb, ko, p, i, kl, w0, w1);
+  // the previous entry's key: the neighbour lane's, or loaded by lane 0
+  uint64_t pkl = __shfl_up(kl, 1, 64), pw0 = __shfl_up(w0, 1, 64), pw1 = __shfl_up(w1, 1, 64);
+  uint64_t pi = __shfl_up(i, 1, 64);
+  if (live && lane == 0 && p > 0) key_words(order, kb, ko, p - 1, pi, pkl, pw0, pw1);
+  if (live) {
+    const uint64_t vl = vo[i + 1] - vo[i];
+    const uint64_t llen = kl + 1 + (vl + 2) / 3 * 4;  // without the '\n'
+    if (kl <= 16) {
+      special = has_byte(w0, kl < 8 ? kl : 8, '\n') || has_byte(w0, kl < 8 ? kl : 8, '\t') ||
+                (kl > 8 && (has_byte(w1, kl - 8, '\n') || has_byte(w1, kl - 8, '\t')));
+    } else {
+      const uint8_t* k = kb + ko[i];
+      for (uint64_t j = 0; j < kl; ++j) special |= (k[j] == '\n') | (k[j] == '\t');
+    }
+    special |= llen >= kNoSep;  // the re-index reports it
+    LineRec r;
+    r.start = loff[p];
+    r.pfx2 = w1;  // bytes 8..15 (zero when kl <= 8)
+    r.klen = (uint32_t)kl;
+    r.llen = (uint32_t)llen;
+    r.vdl = (uint32_t)vl;  // canonical STANDARD encoding: always decodes
+    r.pad = 0;
+    rec[p] = r;
+    pfx[p] = w0;
+    if (p % kFenceStride == 0) fence[p / kFenceStride] = w0;
+    if (p > 0) not_inc = key_cmp(kb, ko, pi, pkl, pw0, pw1, i, kl, w0, w1) >= 0;
+  }
+  if (__syncthreads_or(special) && threadIdx.x == 0) atomicOr(&flags[1], 1u);
+  if (__syncthreads_or(not_inc) && threadIdx.x == 0) atomicAnd(&flags[2], 0u);
+}
+
 }  // namespace
+
+hipError_t launch_format_index(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
+                               const uint64_t* vo, const uint64_t* loff, uint64_t n,
+                               LineRec* rec, uint64_t* pfx, uint64_t* fence, uint32_t* flags,
+                               hipStream_t s) {
+  if (!n) return hipSuccess;
+  ProfScope ps("k_format_index", s);
+  hipLaunchKernelGGL(k_format_index, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, order, kb, ko, vo, loff,
+                     n, rec, pfx, fence, flags);
+  return hipGetLastError();
+}
 
 hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, SortKey* out,
                             hipStream_t s) {
@@ -163,7 +285,7 @@ hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, uint64_t n
                                hipStream_t s) {
   if (n < 2) return hipSuccess;
   ProfScope ps("k_sorted_check", s);
-  hipLaunchKernelGGL(k_sorted_check, dim3(blocks_for(n - 1, kNT)), dim3(kNT), 0, s, kb, ko, n, ok);
+  hipLaunchKernelGGL(k_sorted_check, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, kb, ko, n, ok);
   return hipGetLastError();
 }
 

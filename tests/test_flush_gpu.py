@@ -65,6 +65,47 @@ def test_create_random_vs_oracle(gpu, n, sorted_input):
         assert vals[voffs[j]:voffs[j + 1]] == vdata[voff[i]:voff[i + 1]].tobytes()
 
 
+def _same_index(gpu, t, probes):
+    # the index written straight from the entries equals the one built by
+    # re-reading the file (cb_table_create), and searches agree with the oracle
+    r = gpu.Table(t.data())
+    for a, b in zip(t.lines(), r.lines()):
+        assert np.array_equal(a, b)
+    assert t.nlines == r.nlines and t.well_formed == r.well_formed
+    ot = oracle.OracleTable(t.data())
+    d = np.frombuffer(b"".join(probes) or b"\0", np.uint8)
+    offs = np.zeros(len(probes) + 1, np.uint64)
+    np.cumsum([len(k) for k in probes], out=offs[1:])
+    kb = gpu.KeyBatch(n=len(probes), data=d, offsets=offs)
+    exp = [ot.search(k)[0] for k in probes]
+    assert list(t.search(kb)) == exp and list(r.search(kb)) == exp
+
+
+@pytest.mark.parametrize("sorted_input", [True, False])
+def test_create_direct_index(gpu, sorted_input):
+    rng = np.random.default_rng(11)
+    keys = [bytes(rng.integers(32, 127, rng.integers(0, 30), dtype=np.uint8)).replace(b"\t", b"_")
+            for _ in range(5000)]
+    keys = sorted(set(keys)) if sorted_input else list(dict.fromkeys(keys))
+    vals = [bytes(rng.integers(0, 256, rng.integers(0, 50), dtype=np.uint8)) for _ in keys]
+    t, _, _ = gpu.sstable_create(list(zip(keys, vals)))
+    assert t.data() == oracle.sstable_create(list(zip(keys, vals)))
+    assert t.well_formed and t.nlines == len(keys)
+    _same_index(gpu, t, keys[::7] + [b"zz" * 20, b"", b"\x00"])
+
+
+def test_create_keys_with_line_breaks_and_tabs(gpu):
+    # keys holding '\n' / '\t' split lines / keys differently in the file than
+    # in the entry list: the table is then indexed from the file, as
+    # SsTable::get splits it (src/sstable.rs:142-146)
+    keys = [b"a", b"b\tc", b"d\ne", b"f", b"g\n", b"\th", b"i"]
+    vals = [bytes([i]) * i for i in range(len(keys))]
+    t, _, _ = gpu.sstable_create(list(zip(keys, vals)))
+    assert t.data() == oracle.sstable_create(list(zip(keys, vals)))
+    assert t.nlines == oracle.OracleTable(t.data()).nlines != len(keys)
+    _same_index(gpu, t, keys + [b"b", b"d", b"e", b"g", b"", b"h"])
+
+
 def test_create_ragged_duplicates(gpu):
     # ragged keys with many duplicates and shared prefixes (longer than 16
     # bytes too): the rocPRIM merge sort must be stable and order by full key
