@@ -674,7 +674,8 @@ def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result):
                 "config": {"workload": "C4: 64 filters x 2^18 keys -> m=2^25 each, one subset per GPU",
                            "parallelism": "filter-sharded, no collective"},
                 "algorithmic_bytes_total": int(alg),
-                "step_effective_GBps_all_gpus": round(alg / (el / args.steps) / 1e9, 1)}
+                "step_effective_GBps_all_gpus": round(alg / (el / args.steps) / 1e9, 1),
+                "cpu_baseline": c4_cpu_baseline(nf_total, kpf, m) if world == 1 and not args.no_cpu else None}
         print(json.dumps(line), file=result, flush=True)
     if use_dist:
         dist.barrier()
@@ -740,6 +741,35 @@ def _pmc_traffic(kernel):
         return int(v) if v else None
     except Exception:
         return None
+
+
+def c4_cpu_baseline(nf, kpf, m):
+    """SURVEY.md §8d CPU baseline for C4: the C oracle (byte-per-bit
+    src/bloom.rs) building the 64 filters one after another on one thread,
+    and over 16 threads (one filter per task; ctypes releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from lsmt_amd import workload
+    from oracle import oracle
+    keys = [workload.c4_filter_keys(f, kpf) for f in range(nf)]
+
+    def build(k):
+        o = oracle.OracleFilter(m)
+        o.insert_fixed(k)
+        del o
+
+    t0 = time.perf_counter()
+    for k in keys:
+        build(k)
+    t1 = time.perf_counter() - t0
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(build, keys))
+    tn = time.perf_counter() - t0
+    return {"value": round(nf * kpf / t1, 1), "unit": "keys/s", "cores": 1, "kind": "port",
+            "sample": f"all {nf} C4 builds ({kpf} keys -> m=2^{m.bit_length() - 1} bytes each) on 1 thread, {t1:.2f}s",
+            "all_cores": {"value": round(nf * kpf / tn, 1), "threads": threads, "seconds": round(tn, 3)}}
 
 
 def cpu_baseline(look_np, F, m, kpf, build_keys, build_m):
