@@ -1653,6 +1653,8 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
         HIP_TRY(ws.f_sk2.reserve(n * sizeof(cb::SortKey), s));
         cb::SortKey* a0 = (cb::SortKey*)ws.f_sk.p;
         cb::SortKey* a1 = (cb::SortKey*)ws.f_sk2.p;
+        // (rocPRIM's radix sort in three LSD passes over (len, w1, w0) when every
+        // key is <= 16 bytes was measured no faster at 1M entries: 573 vs 577 us)
         HIP_TRY(cb::launch_sort_keys(dk, dko, n, a0, s));
         size_t tmp_bytes = 0;
         HIP_TRY(cb::entry_sort(nullptr, tmp_bytes, a0, a1, n, dk, dko, s));

@@ -24,24 +24,6 @@ constexpr uint32_t kNT = 256;
 
 inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
 
-__device__ __forceinline__ uint64_t prefix_word(const uint8_t* p, uint64_t len, uint64_t at) {
-  return at < len ? be_chunk(p + at, len - at < 8 ? len - at : 8) : 0;
-}
-
-__global__ __launch_bounds__(kNT) void k_sort_keys(const uint8_t* __restrict__ kb,
-                                                   const uint64_t* __restrict__ ko, uint64_t n,
-                                                   SortKey* __restrict__ out) {
-  const uint64_t i = (uint64_t)blockIdx.x * kNT + threadIdx.x;
-  if (i >= n) return;
-  const uint8_t* p = kb + ko[i];
-  const uint64_t len = ko[i + 1] - ko[i];
-  SortKey s;
-  s.w0 = prefix_word(p, len, 0);
-  s.w1 = prefix_word(p, len, 8);
-  s.len = len > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)len;
-  s.idx = (uint32_t)i;
-  out[i] = s;
-}
 
 // The first 16 bytes of key p (output order) as zero-padded big-endian words,
 // and its length. Unsorted input: the sort record already holds them. Sorted
@@ -84,6 +66,22 @@ __device__ __forceinline__ bool has_byte(uint64_t w, uint64_t m, uint32_t c) {
   const uint64_t keep = m >= 8 ? ~0ull : ~(~0ull >> (8 * m));  // the first m bytes
   const uint64_t x = (w ^ (0x0101010101010101ull * c)) | ~keep;  // 0x00 where byte == c
   return ((x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull) != 0;
+}
+
+// Sort records in input order (the key's first 16 bytes read as words).
+__global__ __launch_bounds__(kNT) void k_sort_keys(const uint8_t* __restrict__ kb,
+                                                   const uint64_t* __restrict__ ko, uint64_t n,
+                                                   SortKey* __restrict__ out) {
+  const uint64_t p = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  if (p >= n) return;
+  uint64_t i, kl, w0, w1;
+  key_words(nullptr, kb, ko, p, i, kl, w0, w1);
+  SortKey s;
+  s.w0 = w0;
+  s.w1 = w1;
+  s.len = kl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)kl;
+  s.idx = (uint32_t)p;
+  out[p] = s;
 }
 
 // Rust str order of keys q and p (q, p index the key batch) given their first
@@ -280,6 +278,7 @@ hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, S
   hipLaunchKernelGGL(k_sort_keys, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, kb, ko, n, out);
   return hipGetLastError();
 }
+
 
 hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, uint64_t n, uint32_t* ok,
                                hipStream_t s) {

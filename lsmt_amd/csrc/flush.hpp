@@ -15,6 +15,7 @@ struct SortKey {
   uint32_t len, idx;
 };
 
+// out[i] = the sort record of key i.
 hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, SortKey* out,
                             hipStream_t s);
 // *ok &= (keys already in non-decreasing order)

@@ -106,6 +106,21 @@ def test_create_keys_with_line_breaks_and_tabs(gpu):
     _same_index(gpu, t, keys + [b"b", b"d", b"e", b"g", b"", b"h"])
 
 
+def test_create_short_keys_stable_sort(gpu):
+    # unsorted keys of 0..16 bytes, compared from their sort records alone:
+    # duplicates keep their input order, trailing NULs order after the shorter
+    # key ("a" < "a\0"), shared 8- and 16-byte prefixes
+    rng = np.random.default_rng(13)
+    base = [b"", b"a", b"a\x00", b"a\x00\x00", b"abcdefgh", b"abcdefgh\x00", b"abcdefghA", b"\xff" * 16,
+            b"\xff" * 15, b"0123456789abcdef", b"0123456789abcdee"]
+    base += [bytes(rng.integers(0, 256, rng.integers(0, 17), dtype=np.uint8)) for _ in range(200)]
+    keys = [base[i] for i in rng.integers(0, len(base), 30_000)]
+    vals = [i.to_bytes(3, "little") for i in range(len(keys))]
+    t, bloom, zone = gpu.sstable_create(list(zip(keys, vals)))
+    assert t.data() == oracle.sstable_create(list(zip(keys, vals)))
+    assert (zone.min, zone.max) == (min(keys), max(keys))
+
+
 def test_create_ragged_duplicates(gpu):
     # ragged keys with many duplicates and shared prefixes (longer than 16
     # bytes too): the rocPRIM merge sort must be stable and order by full key
