@@ -89,23 +89,6 @@ __device__ uint32_t block_exclusive_scan(uint32_t* arr, uint32_t len, uint32_t* 
   return total;
 }
 
-// Sum of arr[0..len) in LDS by a whole NT-thread block (barriers inside).
-template <uint32_t NT>
-__device__ uint32_t block_sum(const uint32_t* arr, uint32_t len, uint32_t* wsum) {
-  uint32_t x = 0;
-  for (uint32_t i = threadIdx.x; i < len; i += NT) x += arr[i];
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-  __syncthreads();  // wsum may still be read by a preceding scan
-  if (lane_id() == 0) wsum[threadIdx.x >> 6] = x;
-  __syncthreads();
-  uint32_t total = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < NT / 64; ++w) total += wsum[w];
-  __syncthreads();
-  return total;
-}
-
 // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs
 // (MI355X_MICROARCH.md, "Workgroup dispatch"), so blocks b and b+8 share an
 // L2. Giving each XCD a contiguous range of tiles lets the 128-B lines that
