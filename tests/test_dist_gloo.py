@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from lsmt_amd.shard import shard_range
+from lsmt_amd.shard import shard_range, sparse_cap
 
 
 def test_shard_range_covers_exactly():
@@ -128,3 +128,17 @@ def test_sharded_probe_allgather_gloo(world, n_filters, mode):
         p.join(timeout=180)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5) is True
+
+
+@pytest.mark.parametrize("n_keys,f_total", [(1 << 20, 256), (10_000_000, 256), (4096, 3)])
+def test_sparse_cap_covers_every_shard(n_keys, f_total):
+    """The pack capacity covers the largest shard's present keys (half of the
+    lookups, key j = i/2 in table j mod f_total, lsmt_amd/workload.py) plus
+    four times the expected false positives (2.4e-4 per pair at 10 bits/key)."""
+    for world in range(1, 9):
+        cap = sparse_cap(n_keys, f_total, world)
+        for r in range(world):
+            lo, hi = shard_range(f_total, world, r)
+            j = np.arange(n_keys // 2)
+            present = int(((j % f_total >= lo) & (j % f_total < hi)).sum())
+            assert cap >= present + 4 * 2.4e-4 * n_keys * (hi - lo), (world, r)
