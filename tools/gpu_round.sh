@@ -12,3 +12,5 @@ timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.er
 cat gpurun_out/bench.json
 bash tools/profile_round.sh > gpurun_out/profile_round.log 2>&1 || { tail -20 gpurun_out/profile_round.log; exit 1; }
 tail -20 gpurun_out/profile_round.log | cut -c1-300
+timeout -k 10 180 python tools/xchg_parts.py > gpurun_out/xchg_parts.json 2> gpurun_out/xchg_parts.err || { tail -20 gpurun_out/xchg_parts.err; exit 1; }
+cat gpurun_out/xchg_parts.json
