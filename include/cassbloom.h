@@ -251,6 +251,12 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
                       const uint64_t* val_off, uint64_t n, uint64_t m_bits, int device, void* stream,
                       cb_table** table_out, cb_filter** bloom_out, uint64_t* zone_min_idx,
                       uint64_t* zone_max_idx);
+/* The zone map bounds of a table made by cb_sstable_create with n >= 1 (the
+ * first / last key of the file: ZoneMap::update over the sorted entries,
+ * src/sstable.rs:60-64): which = 0 min, 1 max. *len = the key's length; up to
+ * cap bytes are copied to host memory out. Host only, no device access.
+ * CB_EINVAL for other tables. */
+int cb_table_zone(const cb_table* t, int which, uint8_t* out, uint64_t cap, uint64_t* len);
 int cb_table_info(const cb_table* t, uint64_t* nlines, uint64_t* bytes);
 /* *out = 1 when the file is well-formed (a TAB on every line, keys strictly
  * increasing — what SsTable::create writes): then any correct search gives

@@ -625,6 +625,14 @@ class Table:
         t.device = device
         return t
 
+    def _zone(self, which: int) -> bytes:
+        """ZoneMap bound kept by cb_sstable_create: 0 = min, 1 = max (host copy)."""
+        n = ctypes.c_uint64()
+        check(_L().cb_table_zone(self._h, int(which), None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(max(int(n.value), 1))
+        check(_L().cb_table_zone(self._h, int(which), buf, n.value, ctypes.byref(n)))
+        return buf.raw[:n.value]
+
     @property
     def well_formed(self) -> bool:
         """A TAB on every line and strictly increasing keys (what SsTable::create
@@ -695,21 +703,8 @@ def sstable_create(entries, m: int = 1024, device: int = 0, stream=None):
     bloom = BloomFilter(0, device=device, _handle=fh.value)
     zone = ZoneMap()
     if kb.n:
-        zone = ZoneMap(*_key_pair(kb, lo.value, hi.value))
+        zone = ZoneMap(table._zone(0), table._zone(1))
     return table, bloom, zone
-
-
-def _key_pair(b: KeyBatch, i: int, j: int):
-    """Keys i and j of a ragged batch as bytes: two device round trips for
-    device buffers (their offsets, then both keys' bytes), none for host ones."""
-    if hasattr(b.offsets, "cpu") or hasattr(b.data, "cpu"):
-        import torch
-        offs = b.offsets if hasattr(b.offsets, "cpu") else torch.from_numpy(np.asarray(b.offsets).view(np.int64))
-        o = torch.stack([offs[i:i + 2], offs[j:j + 2]]).cpu().reshape(-1).tolist()
-        data = b.data if hasattr(b.data, "cpu") else torch.from_numpy(np.asarray(b.data))
-        both = torch.cat([data[o[0]:o[1]], data[o[2]:o[3]]]).cpu().numpy().tobytes()
-        return both[:o[1] - o[0]], both[o[1] - o[0]:]
-    return _key_bytes(b, i), _key_bytes(b, j)
 
 
 def _to_var(b: KeyBatch) -> KeyBatch:
@@ -718,13 +713,6 @@ def _to_var(b: KeyBatch) -> KeyBatch:
             else np.zeros(b.n + 1, np.uint64))
     data = keys.reshape(-1) if keys.size else np.zeros(1, np.uint8)
     return KeyBatch(n=b.n, data=data, offsets=offs)
-
-
-def _key_bytes(b: KeyBatch, i: int) -> bytes:
-    o0, o1 = int(b.offsets[i]), int(b.offsets[i + 1])
-    if hasattr(b.data, "cpu"):
-        return bytes(b.data[o0:o1].cpu().numpy())
-    return np.asarray(b.data)[o0:o1].tobytes()
 
 
 def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=None, out=None):

@@ -12,6 +12,9 @@
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_merge_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "flush.hpp"
 #include "profile.hpp"
@@ -100,10 +103,15 @@ __device__ __forceinline__ int key_cmp(const uint8_t* kb, const uint64_t* ko, ui
 // *ok &= key[i-1] <= key[i] for all i (already in stable-sorted order). Each
 // lane's key comes in as words; the previous one from the neighbour lane.
 __global__ __launch_bounds__(kNT) void k_sorted_check(const uint8_t* __restrict__ kb,
-                                                      const uint64_t* __restrict__ ko, uint64_t n,
-                                                      uint32_t* ok) {
+                                                      const uint64_t* __restrict__ ko,
+                                                      const uint64_t* __restrict__ vo, uint64_t n,
+                                                      CreateResult* r) {
   const uint64_t p = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
+  if (p == 0) {
+    r->ktot = ko[n];
+    r->vtot = vo[n];
+  }
   uint64_t i = 0, kl = 0, w0 = 0, w1 = 0;
   if (p < n) key_words(nullptr, kb, ko, p, i, kl, w0, w1);
   uint64_t pkl = __shfl_up(kl, 1, 64), pw0 = __shfl_up(w0, 1, 64), pw1 = __shfl_up(w1, 1, 64);
@@ -112,6 +120,7 @@ __global__ __launch_bounds__(kNT) void k_sorted_check(const uint8_t* __restrict_
   const bool bad = p < n && p > 0 && key_cmp(kb, ko, p - 1, pkl, pw0, pw1, p, kl, w0, w1) > 0;
   // one atomic per block, and none once the flag is down: a fully unsorted
   // batch would otherwise serialise up to a million atomics on one word
+  uint32_t* ok = &r->flags[0];
   if (__syncthreads_or(bad) && threadIdx.x == 0 && *(volatile uint32_t*)ok) atomicAnd(ok, 0u);
 }
 
@@ -130,15 +139,41 @@ struct KeyLess {
   }
 };
 
-__global__ __launch_bounds__(kNT) void k_line_lens(const SortKey* __restrict__ order,
-                                                   const uint64_t* __restrict__ ko,
-                                                   const uint64_t* __restrict__ vo, uint64_t n,
-                                                   uint64_t* __restrict__ lens) {
-  const uint64_t p = (uint64_t)blockIdx.x * kNT + threadIdx.x;
-  if (p >= n) return;
-  const uint64_t i = order ? order[p].idx : p;
-  const uint64_t vl = vo[i + 1] - vo[i];
-  lens[p] = (ko[i + 1] - ko[i]) + 1 + (vl + 2) / 3 * 4 + 1;
+// Line p's byte length: key, TAB, base64 of the value, newline
+// (src/sstable.rs:66-70); 0 past the last line so the scan's last output is
+// the file's length.
+struct LineLen {
+  const SortKey* order;
+  const uint64_t* ko;
+  const uint64_t* vo;
+  uint64_t n;
+  __host__ __device__ uint64_t operator()(uint64_t p) const {
+    if (p >= n) return 0;
+    const uint64_t i = order ? order[p].idx : p;
+    const uint64_t vl = vo[i + 1] - vo[i];
+    return (ko[i + 1] - ko[i]) + 1 + (vl + 2) / 3 * 4 + 1;
+  }
+};
+
+// The host's view of the new table: file length, first / last key's input
+// index and bytes (the ZoneMap bounds: the file is in key order).
+__global__ __launch_bounds__(256) void k_create_result(const SortKey* __restrict__ order,
+                                                      const uint8_t* __restrict__ kb,
+                                                      const uint64_t* __restrict__ ko,
+                                                      const uint64_t* __restrict__ loff, uint64_t n,
+                                                      CreateResult* r) {
+  const uint64_t imin = order ? order[0].idx : 0, imax = order ? order[n - 1].idx : n - 1;
+  if (threadIdx.x == 0) {
+    r->len = loff[n];
+    r->idx_min = imin;
+    r->idx_max = imax;
+  }
+  for (uint32_t w = 0; w < 2; ++w) {
+    const uint64_t i = w ? imax : imin;
+    const uint64_t o = ko[i], kl = ko[i + 1] - o;
+    if (threadIdx.x == 0) r->zlen[w] = (uint32_t)min<uint64_t>(kl, 0xFFFFFFFFull);
+    for (uint32_t b = threadIdx.x; b < kl && b < kZoneInline; b += 256) r->zkey[w][b] = kb[o + b];
+  }
 }
 
 __device__ __forceinline__ uint8_t b64c(uint32_t v) {
@@ -280,11 +315,10 @@ hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, S
 }
 
 
-hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, uint64_t n, uint32_t* ok,
-                               hipStream_t s) {
-  if (n < 2) return hipSuccess;
+hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, const uint64_t* vo, uint64_t n,
+                               CreateResult* r, hipStream_t s) {
   ProfScope ps("k_sorted_check", s);
-  hipLaunchKernelGGL(k_sorted_check, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, kb, ko, n, ok);
+  hipLaunchKernelGGL(k_sorted_check, dim3(n ? blocks_for(n, kNT) : 1), dim3(kNT), 0, s, kb, ko, vo, n, r);
   return hipGetLastError();
 }
 
@@ -295,11 +329,23 @@ hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* 
   return rocprim::merge_sort(tmp, tmp_bytes, in, out, (size_t)n, KeyLess{kb, ko}, s);
 }
 
-hipError_t launch_line_lens(const SortKey* order, const uint64_t* ko, const uint64_t* vo, uint64_t n,
-                            uint64_t* lens, hipStream_t s) {
+hipError_t line_offsets(void* tmp, size_t& tmp_bytes, const SortKey* order, const uint64_t* ko,
+                        const uint64_t* vo, uint64_t n, uint64_t* loff, hipStream_t s) {
+  auto lens = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint64_t>(0),
+                                               LineLen{order, ko, vo, n});
+  if (!tmp)
+    return rocprim::exclusive_scan(tmp, tmp_bytes, lens, loff, (uint64_t)0, (size_t)n + 1,
+                                   rocprim::plus<uint64_t>(), s);
+  ProfScope ps("rocprim_line_scan", s);
+  return rocprim::exclusive_scan(tmp, tmp_bytes, lens, loff, (uint64_t)0, (size_t)n + 1,
+                                 rocprim::plus<uint64_t>(), s);
+}
+
+hipError_t launch_create_result(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
+                                const uint64_t* loff, uint64_t n, CreateResult* r, hipStream_t s) {
   if (!n) return hipSuccess;
-  ProfScope ps("k_line_lens", s);
-  hipLaunchKernelGGL(k_line_lens, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, order, ko, vo, n, lens);
+  ProfScope ps("k_create_result", s);
+  hipLaunchKernelGGL(k_create_result, dim3(1), dim3(256), 0, s, order, kb, ko, loff, n, r);
   return hipGetLastError();
 }
 

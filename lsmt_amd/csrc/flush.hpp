@@ -15,19 +15,37 @@ struct SortKey {
   uint32_t len, idx;
 };
 
+// What SsTable::create hands back to the host, assembled on the device so that
+// each of its two host round trips is one copy into pinned memory.
+constexpr uint32_t kZoneInline = 256;  // zone bound key bytes carried inline
+struct CreateResult {
+  uint32_t flags[4];          // [0] input sorted, [1] a key holds '\n' / '\t', [2] strictly increasing
+  uint64_t ktot, vtot;        // ko[n], vo[n]
+  uint64_t len;               // the file's length
+  uint64_t idx_min, idx_max;  // input indices of the first / last key in file order
+  uint32_t zlen[2];           // their full lengths
+  uint8_t zkey[2][kZoneInline];
+};
+
 // out[i] = the sort record of key i.
 hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, SortKey* out,
                             hipStream_t s);
-// *ok &= (keys already in non-decreasing order)
-hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, uint64_t n, uint32_t* ok,
-                               hipStream_t s);
+// r->flags[0] &= (keys already in non-decreasing order); r->ktot = ko[n],
+// r->vtot = vo[n]. Launches for any n, n = 0 included.
+hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, const uint64_t* vo, uint64_t n,
+                               CreateResult* r, hipStream_t s);
+// loff[p] = start of output line p, loff[n] = the file's length: one rocPRIM
+// scan over the line lengths computed on the fly (order == nullptr: input
+// order). tmp == nullptr: only writes the scratch size to tmp_bytes.
+hipError_t line_offsets(void* tmp, size_t& tmp_bytes, const SortKey* order, const uint64_t* ko,
+                        const uint64_t* vo, uint64_t n, uint64_t* loff, hipStream_t s);
+// r's len, idx_min / idx_max and the two zone bound keys (n >= 1).
+hipError_t launch_create_result(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
+                                const uint64_t* loff, uint64_t n, CreateResult* r, hipStream_t s);
 // Stable sort of the records by key (rocPRIM merge sort). tmp == nullptr:
 // only writes the scratch size to tmp_bytes.
 hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* out, uint64_t n,
                       const uint8_t* kb, const uint64_t* ko, hipStream_t s);
-// lens[p] = byte length of the p-th output line (order == nullptr: input order)
-hipError_t launch_line_lens(const SortKey* order, const uint64_t* ko, const uint64_t* vo, uint64_t n,
-                            uint64_t* lens, hipStream_t s);
 // The lines into out at loff[p], and 16 zero bytes of slack after the last.
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* loff, uint64_t n,

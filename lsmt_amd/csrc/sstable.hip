@@ -12,6 +12,9 @@
 // gathers its candidate tables first and then searches its own next
 // candidate, so a wave's lanes search different tables concurrently.
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "profile.hpp"
 #include "sstable.hpp"
@@ -256,53 +259,13 @@ __global__ __launch_bounds__(kNT) void k_line_keys(const uint8_t* __restrict__ d
   if (__syncthreads_or(!good) && threadIdx.x == 0 && *(volatile uint32_t*)ok) atomicAnd(ok, 0u);
 }
 
-// ---- exclusive scan of uint64 (tiles of 1024 = 256 threads x 4) ----
-constexpr uint32_t kScanTile = 1024;
-
-__global__ __launch_bounds__(kNT) void k_scan_tiles(const uint64_t* __restrict__ in,
-                                                    uint64_t* __restrict__ out, uint64_t n,
-                                                    uint64_t* __restrict__ sums) {
-  const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 4;
-  uint64_t v[4], s = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    v[j] = i0 + j < n ? in[i0 + j] : 0;
-    s += v[j];
-  }
-  uint64_t total;
-  uint64_t p = block_scan<kNT>(s, &total);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (i0 + j < n) out[i0 + j] = p;
-    p += v[j];
-  }
-  if (threadIdx.x == 0) sums[blockIdx.x] = total;
-}
-
-// One block: exclusive scan of the tile sums in place (carry across chunks);
-// out[n] = grand total.
-__global__ __launch_bounds__(1024) void k_scan_sums(uint64_t* __restrict__ sums, uint64_t nt,
-                                                    uint64_t* __restrict__ out, uint64_t n) {
-  uint64_t carry = 0;
-  for (uint64_t c0 = 0; c0 < nt; c0 += 1024) {
-    const uint64_t i = c0 + threadIdx.x;
-    const uint64_t v = i < nt ? sums[i] : 0;
-    uint64_t total;
-    const uint64_t p = block_scan<1024>(v, &total);
-    if (i < nt) sums[i] = carry + p;
-    carry += total;
-  }
-  if (threadIdx.x == 0) out[n] = carry;
-}
-
-__global__ __launch_bounds__(kNT) void k_scan_add(uint64_t* __restrict__ out, uint64_t n,
-                                                  const uint64_t* __restrict__ sums) {
-  const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 4;
-  const uint64_t add = sums[blockIdx.x];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (i0 + j < n) out[i0 + j] += add;
-}
+// ---- exclusive scan of uint64: one rocPRIM look-back scan over n + 1 items
+// (the last reads as 0, so out[n] = total) ----
+struct TailZero {
+  const uint64_t* in;
+  uint64_t n;
+  __host__ __device__ uint64_t operator()(uint64_t p) const { return p < n ? in[p] : 0; }
+};
 
 // ---- search ----
 
@@ -564,16 +527,24 @@ hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, LineRec* rec, 
   return hipGetLastError();
 }
 
-uint64_t scan_tmp_words(uint64_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+static hipError_t scan_u64(void* tmp, size_t& bytes, const uint64_t* in, uint64_t* out, uint64_t n,
+                           hipStream_t s) {
+  auto it = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint64_t>(0), TailZero{in, n});
+  return rocprim::exclusive_scan(tmp, bytes, it, out, (uint64_t)0, (size_t)n + 1,
+                                 rocprim::plus<uint64_t>(), s);
+}
+
+uint64_t scan_tmp_words(uint64_t n) {
+  size_t bytes = 0;
+  (void)scan_u64(nullptr, bytes, nullptr, nullptr, n, 0);
+  return bytes / 8 + 1;
+}
 
 hipError_t launch_scan_u64(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tmp,
                            hipStream_t s) {
-  const uint64_t nt = (n + kScanTile - 1) / kScanTile;
+  size_t bytes = scan_tmp_words(n) * 8;
   ProfScope ps("k_scan_u64", s);
-  if (nt) hipLaunchKernelGGL(k_scan_tiles, dim3((uint32_t)nt), dim3(kNT), 0, s, in, out, n, tmp);
-  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, s, tmp, nt, out, n);
-  if (nt > 1) hipLaunchKernelGGL(k_scan_add, dim3((uint32_t)nt), dim3(kNT), 0, s, out, n, tmp);
-  return hipGetLastError();
+  return scan_u64(tmp, bytes, in, out, n, s);
 }
 
 hipError_t launch_table_search(int keyk, const TableView& t, const KeySrc& ks, uint64_t n,

@@ -132,3 +132,35 @@ def test_create_ragged_duplicates(gpu):
     assert t.data() == oracle.sstable_create(list(zip(keys, vals)))
     assert not t.well_formed  # duplicate keys: the exact search trajectory is used
     assert (zone.min, zone.max) == (min(keys), max(keys))
+
+
+@pytest.mark.parametrize("on_device", [False, True])
+def test_create_zone_keys_long_and_device(gpu, on_device):
+    # zone bounds come back with the table (cb_table_zone): keys longer than
+    # the 256 bytes carried inline take one extra copy; inputs on the host or
+    # in HBM give the same table, filter and bounds
+    import torch
+    rng = np.random.default_rng(21)
+    keys = [bytes(rng.integers(97, 123, int(rng.integers(1, 600)), dtype=np.uint8)) for _ in range(3000)]
+    keys = list(dict.fromkeys(keys))
+    keys[5] = b"\x00" + b"a" * 700     # smallest, longer than the inline bytes
+    keys[9] = b"\xff" * 300 + b"z"     # largest
+    vals = [bytes(rng.integers(0, 256, int(rng.integers(0, 20)), dtype=np.uint8)) for _ in keys]
+    kd = np.frombuffer(b"".join(keys), np.uint8)
+    ko = np.zeros(len(keys) + 1, np.uint64)
+    np.cumsum([len(k) for k in keys], out=ko[1:])
+    vd = np.frombuffer(b"".join(vals) + b"\0", np.uint8)
+    vo = np.zeros(len(vals) + 1, np.uint64)
+    np.cumsum([len(v) for v in vals], out=vo[1:])
+    if on_device:
+        kd, vd = torch.from_numpy(kd.copy()).cuda(), torch.from_numpy(vd.copy()).cuda()
+        ko, vo = torch.from_numpy(ko.view(np.int64)).cuda(), torch.from_numpy(vo.view(np.int64)).cuda()
+    kb = gpu.KeyBatch(n=len(keys), data=kd, offsets=ko)
+    vb = gpu.KeyBatch(n=len(vals), data=vd, offsets=vo)
+    t, bloom, zone = gpu.sstable_create((kb, vb), m=1 << 16)
+    assert t.data() == oracle.sstable_create(list(zip(keys, vals)))
+    assert (zone.min, zone.max) == (min(keys), max(keys))
+    o = oracle.OracleFilter(1 << 16)
+    for k in keys:
+        o.insert(k)
+    assert np.array_equal(bloom.bools(), o.bools())
