@@ -207,6 +207,7 @@ struct Workspace {
   DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_lens, f_loff, f_scan, f_flag;  // SsTable::create
   DevBuf x_sums;                                                          // cb_hits_compress
   cb::CreateResult* hres = nullptr;  // pinned host mirror of f_flag (SsTable::create)
+  uint64_t* htot = nullptr;          // pinned: get_many's value byte total
   hipEvent_t ev = nullptr;           // marks hres's first copy in the stream
 };
 
@@ -999,17 +1000,27 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
   HIP_TRY(cb::launch_get_many(sk.keyk, dviews, nt, dhits, drows, hwords, sk.ks, n, dwhich,
                               (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, s));
   HIP_TRY(cb::launch_scan_u64((const uint64_t*)ws.t_dlen.p, dvoff, n, (uint64_t*)ws.t_scan.p, s));
-  HIP_TRY(hipMemcpyAsync(total, dvoff + n, 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  if (vals && cap >= *total && *total) {
-    uint8_t* dvals;
-    if ((rc = out_buf(ws.t_vals, vals, *total, s, &dvals))) return rc;
-    HIP_TRY(cb::launch_b64_decode((const uint64_t*)ws.t_line.p, dvoff, n, dvals, s));
-    if (dvals != vals) HIP_TRY(hipMemcpyAsync(vals, dvals, *total, hipMemcpyDeviceToHost, s));
+  if (!ws.htot) HIP_TRY(hipHostMalloc((void**)&ws.htot, 64, hipHostMallocDefault));
+  if (vals && is_device_ptr(vals)) {
+    // device values: decoded in the same pass; the kernel itself skips the
+    // writes when the total exceeds cap, so one host round trip suffices
+    HIP_TRY(cb::launch_b64_decode((const uint64_t*)ws.t_line.p, dvoff, n, vals, cap, s));
+    HIP_TRY(hipMemcpyAsync(ws.htot, dvoff + n, 8, hipMemcpyDeviceToHost, s));
+  } else {
+    HIP_TRY(hipMemcpyAsync(ws.htot, dvoff + n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint64_t tot = *ws.htot;
+    if (vals && cap >= tot && tot) {
+      uint8_t* dvals;
+      if ((rc = out_buf(ws.t_vals, vals, tot, s, &dvals))) return rc;
+      HIP_TRY(cb::launch_b64_decode((const uint64_t*)ws.t_line.p, dvoff, n, dvals, tot, s));
+      HIP_TRY(hipMemcpyAsync(vals, dvals, tot, hipMemcpyDeviceToHost, s));
+    }
   }
   if (dwhich != which) HIP_TRY(hipMemcpyAsync(which, dwhich, n * 4, hipMemcpyDeviceToHost, s));
   if (dvoff != val_off) HIP_TRY(hipMemcpyAsync(val_off, dvoff, (n + 1) * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  *total = *ws.htot;
   return CB_OK;
 }
 

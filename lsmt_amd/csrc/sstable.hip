@@ -452,8 +452,9 @@ constexpr uint32_t kDecodeLds = 16384;  // staged output bytes per block
 // with aligned dword stores; otherwise lanes write their bytes directly.
 __global__ __launch_bounds__(kNT) void k_b64_decode(const uint64_t* __restrict__ vsrc,
                                                     const uint64_t* __restrict__ voff, uint64_t n,
-                                                    uint8_t* __restrict__ out) {
+                                                    uint8_t* __restrict__ out, uint64_t cap) {
   __shared__ uint8_t stage[kDecodeLds];
+  if (voff[n] > cap) return;  // uniform: the output does not fit
   const uint64_t b0 = (uint64_t)blockIdx.x * kNT;
   const uint64_t k = b0 + threadIdx.x;
   const uint64_t bend = b0 + kNT < n ? b0 + kNT : n;
@@ -586,10 +587,10 @@ hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uin
 }
 
 hipError_t launch_b64_decode(const uint64_t* vsrc, const uint64_t* voff, uint64_t n, uint8_t* out,
-                             hipStream_t s) {
+                             uint64_t cap, hipStream_t s) {
   if (!n) return hipSuccess;
   ProfScope ps("k_b64_decode", s);
-  hipLaunchKernelGGL(k_b64_decode, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, vsrc, voff, n, out);
+  hipLaunchKernelGGL(k_b64_decode, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, vsrc, voff, n, out, cap);
   return hipGetLastError();
 }
 

@@ -84,8 +84,9 @@ hipError_t launch_table_search(int keyk, const TableView& t, const KeySrc& ks, u
 hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uint64_t* hits,
                            const uint32_t* rows, uint64_t hwords, const KeySrc& ks, uint64_t n,
                            int32_t* which, uint64_t* vsrc, uint64_t* dlen, hipStream_t s);
-// Decoded values (voff = exclusive scan of dlen) into out + voff[k].
+// Decoded values (voff = exclusive scan of dlen) into out + voff[k]; nothing
+// is written when voff[n] > cap (the caller's buffer is too small).
 hipError_t launch_b64_decode(const uint64_t* vsrc, const uint64_t* voff, uint64_t n, uint8_t* out,
-                             hipStream_t s);
+                             uint64_t cap, hipStream_t s);
 
 }  // namespace cb

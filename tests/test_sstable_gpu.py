@@ -188,3 +188,32 @@ def test_search_device_resident(gpu):
     assert (got >= 0).all()
     srt = workload.sort_keys16(keys)
     assert np.array_equal(srt[got], keys[::-1])
+
+
+def test_get_many_device_out_cap(gpu):
+    # device output buffers: one pass; a value buffer smaller than the total is
+    # left untouched and the total is still reported (then the caller retries)
+    import torch
+    keys = [b"k%05d" % i for i in range(3000)]
+    vals = [bytes([i % 251]) * (i % 37) for i in range(3000)]
+    t, _, _ = gpu.sstable_create(list(zip(keys, vals)))
+    look = keys[::3] + [b"absent", b"k99999"]
+    d = np.frombuffer(b"".join(look), np.uint8)
+    offs = np.zeros(len(look) + 1, np.uint64)
+    np.cumsum([len(k) for k in look], out=offs[1:])
+    kb = gpu.KeyBatch(n=len(look), data=d, offsets=offs)
+    want = b"".join(vals[::3])
+    which = torch.empty(len(look), dtype=torch.int32, device="cuda")
+    voff = torch.empty(len(look) + 1, dtype=torch.int64, device="cuda")
+    small = torch.full((len(want) - 1,), 7, dtype=torch.uint8, device="cuda")
+    _, _, total = gpu.get_many([t], kb, out=(which, voff, small))
+    assert total == len(want)
+    assert bool((small == 7).all())
+    big = torch.full((len(want) + 64,), 7, dtype=torch.uint8, device="cuda")
+    _, _, total = gpu.get_many([t], kb, out=(which, voff, big))
+    assert total == len(want)
+    assert bytes(big[:total].cpu().numpy()) == want and bool((big[total:] == 7).all())
+    w = which.cpu().numpy()
+    assert (w[:-2] == 0).all() and (w[-2:] == -1).all()
+    vo = voff.cpu().numpy()
+    assert vo[-1] == total and vo[-2] == vo[-3] == total
