@@ -485,7 +485,7 @@ def main():
             k_fl = max(3, args.steps // 4)
             fel = timed(step_flush, k_fl)
             fprof = kernel_ms(["k_sorted_check", "k_sort_keys", "rocprim_merge_sort", "rocprim_line_scan",
-                               "k_format", "k_format_index", "k_create_result", "k_line_count", "k_line_emit", "k_line_finish", "k_line_keys",
+                               "k_format", "k_line_count", "k_line_emit", "k_line_finish", "k_line_keys",
                                "k_build_part", "k_build_tile", "k_insert_direct"], step_flush, k_fl)
             out_bytes = made[-1][0].nbytes
             res[label] = {"entries_per_s": round(nf_e / (fel / k_fl), 1), "ms_per_flush": round(fel / k_fl * 1e3, 3),

@@ -1725,7 +1725,6 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   HIP_TRY(cb::line_offsets(nullptr, scan_bytes, order, dko, dvo, n, loff, s));
   HIP_TRY(ws.f_scan.reserve(scan_bytes + 16, s));
   HIP_TRY(cb::line_offsets(ws.f_scan.p, scan_bytes, order, dko, dvo, n, loff, s));
-  HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, loff, n, t->data, s));  // + 16 B of slack
   // the line index straight from the entries (entry p is line p), no re-read of the file
   t->nlines = n;
   t->nfence = (n + cb::kFenceStride - 1) / cb::kFenceStride;
@@ -1736,9 +1735,8 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   }
   t->pfx = (uint64_t*)(t->rec + n);
   t->fence = t->pfx + n;
-  HIP_TRY(cb::launch_format_index(order, dk, dko, dvo, loff, n, t->rec, t->pfx, t->fence, dr->flags, s));
+  HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, loff, n, t->data, t->rec, t->pfx, t->fence, dr, s));
   // Round trip 2: flags, file length, zone bounds
-  HIP_TRY(cb::launch_create_result(order, dk, dko, loff, n, dr, s));
   HIP_TRY(hipMemcpyAsync(hr, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   t->len = hr->len;

@@ -28,28 +28,16 @@ constexpr uint32_t kNT = 256;
 inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
 
 
-// The first 16 bytes of key p (output order) as zero-padded big-endian words,
-// and its length. Unsorted input: the sort record already holds them. Sorted
-// input: the aligned dwords that contain the key's bytes (a dword never
-// crosses a page edge, so these loads stay inside mapped memory however the
-// key buffer is aligned), byte-aligned in registers.
-__device__ __forceinline__ void key_words(const SortKey* order, const uint8_t* kb,
-                                          const uint64_t* ko, uint64_t p, uint64_t& i,
-                                          uint64_t& kl, uint64_t& w0, uint64_t& w1) {
-  i = order ? order[p].idx : p;
-  const uint64_t o0 = ko[i];
-  kl = ko[i + 1] - o0;
-  if (order) {
-    w0 = order[p].w0;
-    w1 = order[p].w1;
-    return;
-  }
-  const uint64_t m = kl < 16 ? kl : 16;
+// The first min(len, 16) bytes at src as zero-padded big-endian words, from
+// the aligned dwords that contain them (a dword never crosses a page edge, so
+// these loads stay inside mapped memory however src is aligned).
+__device__ __forceinline__ void load16(const uint8_t* src, uint64_t len, uint64_t& w0, uint64_t& w1) {
+  const uint64_t m = len < 16 ? len : 16;
   uint32_t d[5] = {0, 0, 0, 0, 0};
-  const uint64_t a0 = (uint64_t)(uintptr_t)(kb + o0);
+  const uint64_t a0 = (uint64_t)(uintptr_t)src;
   const uint32_t* base = reinterpret_cast<const uint32_t*>((uintptr_t)(a0 & ~3ull));
   const uint32_t sh = (uint32_t)(a0 & 3);
-  const uint32_t nd = m ? (uint32_t)((sh + m + 3) / 4) : 0;  // dwords holding the key's first m bytes
+  const uint32_t nd = m ? (uint32_t)((sh + m + 3) / 4) : 0;  // dwords holding the first m bytes
 #pragma unroll
   for (uint32_t j = 0; j < 5; ++j)
     if (j < nd) d[j] = base[j];
@@ -61,6 +49,23 @@ __device__ __forceinline__ void key_words(const SortKey* order, const uint8_t* k
   const uint64_t b0 = __builtin_bswap64(lo), b1 = __builtin_bswap64(hi);
   w0 = m >= 8 ? b0 : (m ? b0 & ~(~0ull >> (8 * m)) : 0);
   w1 = m >= 16 ? b1 : (m > 8 ? b1 & ~(~0ull >> (8 * (m - 8))) : 0);
+}
+
+// The first 16 bytes of key p (output order) as zero-padded big-endian words,
+// and its length. Unsorted input: the sort record already holds them; sorted
+// input: load16 of the key's bytes.
+__device__ __forceinline__ void key_words(const SortKey* order, const uint8_t* kb,
+                                          const uint64_t* ko, uint64_t p, uint64_t& i,
+                                          uint64_t& kl, uint64_t& w0, uint64_t& w1) {
+  i = order ? order[p].idx : p;
+  const uint64_t o0 = ko[i];
+  kl = ko[i + 1] - o0;
+  if (order) {
+    w0 = order[p].w0;
+    w1 = order[p].w1;
+    return;
+  }
+  load16(kb + o0, kl, w0, w1);
 }
 
 // Does a big-endian word hold byte c among its first m (<= 8) bytes?
@@ -155,42 +160,38 @@ struct LineLen {
   }
 };
 
-// The host's view of the new table: file length, first / last key's input
-// index and bytes (the ZoneMap bounds: the file is in key order).
-__global__ __launch_bounds__(256) void k_create_result(const SortKey* __restrict__ order,
-                                                      const uint8_t* __restrict__ kb,
-                                                      const uint64_t* __restrict__ ko,
-                                                      const uint64_t* __restrict__ loff, uint64_t n,
-                                                      CreateResult* r) {
-  const uint64_t imin = order ? order[0].idx : 0, imax = order ? order[n - 1].idx : n - 1;
+// One bound of the ZoneMap (the file's first or last key, w = 0 / 1) into r:
+// input index, full length and up to kZoneInline bytes. Whole block.
+__device__ __forceinline__ void zone_bound(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
+                                           uint64_t p, uint32_t w, CreateResult* r) {
+  const uint64_t i = order ? order[p].idx : p;
+  const uint64_t o = ko[i], kl = ko[i + 1] - o;
   if (threadIdx.x == 0) {
-    r->len = loff[n];
-    r->idx_min = imin;
-    r->idx_max = imax;
+    (w ? r->idx_max : r->idx_min) = i;
+    r->zlen[w] = (uint32_t)min<uint64_t>(kl, 0xFFFFFFFFull);
   }
-  for (uint32_t w = 0; w < 2; ++w) {
-    const uint64_t i = w ? imax : imin;
-    const uint64_t o = ko[i], kl = ko[i + 1] - o;
-    if (threadIdx.x == 0) r->zlen[w] = (uint32_t)min<uint64_t>(kl, 0xFFFFFFFFull);
-    for (uint32_t b = threadIdx.x; b < kl && b < kZoneInline; b += 256) r->zkey[w][b] = kb[o + b];
-  }
+  for (uint32_t b = threadIdx.x; b < kl && b < kZoneInline; b += kNT) r->zkey[w][b] = kb[o + b];
 }
 
 __device__ __forceinline__ uint8_t b64c(uint32_t v) {
   return (uint8_t)(v < 26 ? 'A' + v : v < 52 ? 'a' + (v - 26) : v < 62 ? '0' + (v - 52) : v == 62 ? '+' : '/');
 }
 
-// One lane per line: key, TAB, STANDARD.encode(value), NL, through put(j, b).
-template <class Put>
-__device__ __forceinline__ void format_line(const uint8_t* k, uint64_t kl, const uint8_t* v,
-                                            uint64_t vl, Put put) {
+// Byte j (< 16) of a string held as two zero-padded big-endian words.
+__device__ __forceinline__ uint32_t be_byte(uint64_t w0, uint64_t w1, uint64_t j) {
+  return (uint32_t)((j < 8 ? w0 >> (56 - 8 * j) : w1 >> (120 - 8 * j)) & 0xFF);
+}
+
+// One lane per line: key, TAB, STANDARD.encode(value), NL, through put(j, b);
+// kb(j) / vb(j) give the key's and the value's bytes.
+template <class KB, class VB, class Put>
+__device__ __forceinline__ void format_line(uint64_t kl, KB kbyte, uint64_t vl, VB vbyte, Put put) {
   uint64_t o = 0;
-  for (uint64_t j = 0; j < kl; ++j) put(o++, k[j]);
+  for (uint64_t j = 0; j < kl; ++j) put(o++, kbyte(j));
   put(o++, '\t');
   for (uint64_t j = 0; j < vl; j += 3) {
     const uint64_t r = vl - j;
-    const uint32_t w = (uint32_t)v[j] << 16 | (r > 1 ? (uint32_t)v[j + 1] << 8 : 0u) |
-                       (r > 2 ? (uint32_t)v[j + 2] : 0u);
+    const uint32_t w = vbyte(j) << 16 | (r > 1 ? vbyte(j + 1) << 8 : 0u) | (r > 2 ? vbyte(j + 2) : 0u);
     put(o++, b64c(w >> 18));
     put(o++, b64c((w >> 12) & 63));
     put(o++, r > 1 ? b64c((w >> 6) & 63) : (uint8_t)'=');
@@ -201,73 +202,45 @@ __device__ __forceinline__ void format_line(const uint8_t* k, uint64_t kl, const
 
 constexpr uint32_t kFormatLds = 32768;  // staged output bytes per block
 
-// A block's 256 lines are one contiguous output range [loff[p0], loff[p0+256]).
-// When it fits in LDS the lanes format into LDS and the block writes the
-// range with aligned dword stores; otherwise lanes write bytes directly.
+// SsTable::create's file and everything derived from it, one lane per entry p
+// (= line p; entries in key order):
+// - the line `key \t base64(value) \n` at loff[p]. A block's 256 lines are one
+//   contiguous range; when it fits in LDS the lanes format into LDS (staged at
+//   the range's address mod 4, so LDS and global dwords line up) and the block
+//   writes it with aligned dword stores, else lanes write bytes directly.
+//   Keys and values of <= 16 bytes come in as aligned dword loads.
+// - the line index that k_line_finish / k_line_keys would derive by re-reading
+//   the file: LineRec, prefix and fence (sstable.hpp layout). flags[1] |= 1 if
+//   a key holds '\n' or '\t' (the caller then re-indexes the file the way
+//   SsTable::get splits it); flags[2] &= keys strictly increasing.
+// - r: the file length and the ZoneMap bounds (first / last key).
 __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ order,
                                                 const uint8_t* __restrict__ kb,
                                                 const uint64_t* __restrict__ ko,
                                                 const uint8_t* __restrict__ vb,
                                                 const uint64_t* __restrict__ vo,
                                                 const uint64_t* __restrict__ loff, uint64_t n,
-                                                uint8_t* __restrict__ out) {
-  __shared__ uint8_t stage[kFormatLds];
+                                                uint8_t* __restrict__ out, LineRec* __restrict__ rec,
+                                                uint64_t* __restrict__ pfx, uint64_t* __restrict__ fence,
+                                                CreateResult* r) {
+  __shared__ uint32_t stage32[kFormatLds / 4];
+  uint8_t* stage = reinterpret_cast<uint8_t*>(stage32);
   const uint64_t p0 = (uint64_t)blockIdx.x * kNT;
   const uint64_t p = p0 + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
   const uint64_t pend = p0 + kNT < n ? p0 + kNT : n;
   const uint64_t base = loff[p0], total = loff[pend] - base;
   const bool live = p < n;
-  const uint64_t i = live ? (order ? order[p].idx : p) : 0;
-  const uint8_t* k = kb + (live ? ko[i] : 0);
-  const uint64_t kl = live ? ko[i + 1] - ko[i] : 0;
-  const uint8_t* v = vb + (live ? vo[i] : 0);
-  const uint64_t vl = live ? vo[i + 1] - vo[i] : 0;
-  const uint64_t o = live ? loff[p] : 0;
-  // 16 zero bytes after the file: the readable slack of the table's buffer
-  if (pend == n && threadIdx.x < 16) out[loff[n] + threadIdx.x] = 0;
-  if (total > kFormatLds) {  // uniform: long lines, direct byte stores
-    if (live) format_line(k, kl, v, vl, [&](uint64_t j, uint8_t c) { out[o + j] = c; });
-    return;
-  }
-  if (live) format_line(k, kl, v, vl, [&](uint64_t j, uint8_t c) { stage[o - base + j] = c; });
-  __syncthreads();
-  uint8_t* g = out + base;
-  const uint64_t mis = (4 - ((uintptr_t)g & 3)) & 3;
-  const uint64_t head = mis < total ? mis : total;
-  if (threadIdx.x < head) g[threadIdx.x] = stage[threadIdx.x];
-  const uint64_t body = (total - head) / 4;
-  uint32_t* gw = reinterpret_cast<uint32_t*>(g + head);
-  for (uint64_t j = threadIdx.x; j < body; j += kNT) {
-    const uint64_t q = head + 4 * j;
-    gw[j] = (uint32_t)stage[q] | (uint32_t)stage[q + 1] << 8 | (uint32_t)stage[q + 2] << 16 |
-            (uint32_t)stage[q + 3] << 24;
-  }
-  const uint64_t tail0 = head + 4 * body;
-  if (tail0 + threadIdx.x < total) g[tail0 + threadIdx.x] = stage[tail0 + threadIdx.x];
-}
-
-// One lane per entry p (= line p of the file): the LineRec, prefix and fence
-// that k_line_finish / k_line_keys would derive by re-reading the file.
-__global__ __launch_bounds__(kNT) void k_format_index(const SortKey* __restrict__ order,
-                                                      const uint8_t* __restrict__ kb,
-                                                      const uint64_t* __restrict__ ko,
-                                                      const uint64_t* __restrict__ vo,
-                                                      const uint64_t* __restrict__ loff, uint64_t n,
-                                                      LineRec* __restrict__ rec,
-                                                      uint64_t* __restrict__ pfx,
-                                                      uint64_t* __restrict__ fence, uint32_t* flags) {
-  const uint64_t p = (uint64_t)blockIdx.x * kNT + threadIdx.x;
-  const uint32_t lane = threadIdx.x & 63u;
-  bool special = false, not_inc = false;
   uint64_t i = 0, kl = 0, w0 = 0, w1 = 0;
-  const bool live = p < n;
   if (live) key_words(order, kb, ko, p, i, kl, w0, w1);
   // the previous entry's key: the neighbour lane's, or loaded by lane 0
   uint64_t pkl = __shfl_up(kl, 1, 64), pw0 = __shfl_up(w0, 1, 64), pw1 = __shfl_up(w1, 1, 64);
   uint64_t pi = __shfl_up(i, 1, 64);
   if (live && lane == 0 && p > 0) key_words(order, kb, ko, p - 1, pi, pkl, pw0, pw1);
+  const uint64_t vo0 = live ? vo[i] : 0, vl = live ? vo[i + 1] - vo0 : 0;
+  const uint64_t o = live ? loff[p] : 0;
+  bool special = false, not_inc = false;
   if (live) {
-    const uint64_t vl = vo[i + 1] - vo[i];
     const uint64_t llen = kl + 1 + (vl + 2) / 3 * 4;  // without the '\n'
     if (kl <= 16) {
       special = has_byte(w0, kl < 8 ? kl : 8, '\n') || has_byte(w0, kl < 8 ? kl : 8, '\t') ||
@@ -277,34 +250,62 @@ __global__ __launch_bounds__(kNT) void k_format_index(const SortKey* __restrict_
       for (uint64_t j = 0; j < kl; ++j) special |= (k[j] == '\n') | (k[j] == '\t');
     }
     special |= llen >= kNoSep;  // the re-index reports it
-    LineRec r;
-    r.start = loff[p];
-    r.pfx2 = w1;  // bytes 8..15 (zero when kl <= 8)
-    r.klen = (uint32_t)kl;
-    r.llen = (uint32_t)llen;
-    r.vdl = (uint32_t)vl;  // canonical STANDARD encoding: always decodes
-    r.pad = 0;
-    rec[p] = r;
+    LineRec lr;
+    lr.start = o;
+    lr.pfx2 = w1;  // bytes 8..15 (zero when kl <= 8)
+    lr.klen = (uint32_t)kl;
+    lr.llen = (uint32_t)llen;
+    lr.vdl = (uint32_t)vl;  // canonical STANDARD encoding: always decodes
+    lr.pad = 0;
+    rec[p] = lr;
     pfx[p] = w0;
     if (p % kFenceStride == 0) fence[p / kFenceStride] = w0;
     if (p > 0) not_inc = key_cmp(kb, ko, pi, pkl, pw0, pw1, i, kl, w0, w1) >= 0;
   }
-  if (__syncthreads_or(special) && threadIdx.x == 0) atomicOr(&flags[1], 1u);
-  if (__syncthreads_or(not_inc) && threadIdx.x == 0) atomicAnd(&flags[2], 0u);
+  if (__syncthreads_or(special) && threadIdx.x == 0) atomicOr(&r->flags[1], 1u);
+  if (__syncthreads_or(not_inc) && threadIdx.x == 0) atomicAnd(&r->flags[2], 0u);
+  if (blockIdx.x == 0) zone_bound(order, kb, ko, 0, 0, r);
+  if (pend == n) {
+    zone_bound(order, kb, ko, n - 1, 1, r);
+    if (threadIdx.x == 0) r->len = loff[n];
+    // 16 zero bytes after the file: the readable slack of the table's buffer
+    if (threadIdx.x < 16) out[loff[n] + threadIdx.x] = 0;
+  }
+  const uint8_t* k = kb + (live ? ko[i] : 0);
+  const uint8_t* v = vb + vo0;
+  uint64_t v0 = 0, v1 = 0;
+  const bool words = kl <= 16 && vl <= 16;
+  if (live && words) load16(v, vl, v0, v1);
+  auto emit = [&](auto put) {
+    if (!live) return;
+    if (words)
+      format_line(kl, [&](uint64_t j) { return be_byte(w0, w1, j); }, vl,
+                  [&](uint64_t j) { return be_byte(v0, v1, j); }, put);
+    else
+      format_line(kl, [&](uint64_t j) { return (uint32_t)k[j]; }, vl,
+                  [&](uint64_t j) { return (uint32_t)v[j]; }, put);
+  };
+  const uint64_t sh0 = base & 3;
+  if (total + sh0 > kFormatLds) {  // uniform: long lines, direct byte stores
+    emit([&](uint64_t j, uint8_t c) { out[o + j] = c; });
+    return;
+  }
+  emit([&](uint64_t j, uint8_t c) { stage[o - base + sh0 + j] = c; });
+  __syncthreads();
+  // out[base .. base+total): bytes up to the first 4-aligned address, then
+  // aligned dwords (LDS dword-aligned too), then the tail
+  uint8_t* g = out + base;
+  const uint64_t head = min<uint64_t>((4 - sh0) & 3, total);
+  if (threadIdx.x < head) g[threadIdx.x] = stage[sh0 + threadIdx.x];
+  const uint64_t body = (total - head) / 4;
+  uint32_t* gw = reinterpret_cast<uint32_t*>(g + head);
+  const uint32_t* sw = stage32 + (sh0 + head) / 4;
+  for (uint64_t j = threadIdx.x; j < body; j += kNT) gw[j] = sw[j];
+  const uint64_t tail0 = head + 4 * body;
+  if (tail0 + threadIdx.x < total) g[tail0 + threadIdx.x] = stage[sh0 + tail0 + threadIdx.x];
 }
 
 }  // namespace
-
-hipError_t launch_format_index(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
-                               const uint64_t* vo, const uint64_t* loff, uint64_t n,
-                               LineRec* rec, uint64_t* pfx, uint64_t* fence, uint32_t* flags,
-                               hipStream_t s) {
-  if (!n) return hipSuccess;
-  ProfScope ps("k_format_index", s);
-  hipLaunchKernelGGL(k_format_index, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, order, kb, ko, vo, loff,
-                     n, rec, pfx, fence, flags);
-  return hipGetLastError();
-}
 
 hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, SortKey* out,
                             hipStream_t s) {
@@ -341,21 +342,15 @@ hipError_t line_offsets(void* tmp, size_t& tmp_bytes, const SortKey* order, cons
                                  rocprim::plus<uint64_t>(), s);
 }
 
-hipError_t launch_create_result(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
-                                const uint64_t* loff, uint64_t n, CreateResult* r, hipStream_t s) {
-  if (!n) return hipSuccess;
-  ProfScope ps("k_create_result", s);
-  hipLaunchKernelGGL(k_create_result, dim3(1), dim3(256), 0, s, order, kb, ko, loff, n, r);
-  return hipGetLastError();
-}
 
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* loff, uint64_t n,
-                         uint8_t* out, hipStream_t s) {
+                         uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
+                         hipStream_t s) {
   if (!n) return hipSuccess;
   ProfScope ps("k_format", s);
   hipLaunchKernelGGL(k_format, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, order, kb, ko, vb, vo, loff,
-                     n, out);
+                     n, out, rec, pfx, fence, r);
   return hipGetLastError();
 }
 

@@ -39,25 +39,20 @@ hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, const uint
 // order). tmp == nullptr: only writes the scratch size to tmp_bytes.
 hipError_t line_offsets(void* tmp, size_t& tmp_bytes, const SortKey* order, const uint64_t* ko,
                         const uint64_t* vo, uint64_t n, uint64_t* loff, hipStream_t s);
-// r's len, idx_min / idx_max and the two zone bound keys (n >= 1).
-hipError_t launch_create_result(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
-                                const uint64_t* loff, uint64_t n, CreateResult* r, hipStream_t s);
 // Stable sort of the records by key (rocPRIM merge sort). tmp == nullptr:
 // only writes the scratch size to tmp_bytes.
 hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* out, uint64_t n,
                       const uint8_t* kb, const uint64_t* ko, hipStream_t s);
-// The lines into out at loff[p], and 16 zero bytes of slack after the last.
+// The file (lines into out at loff[p], then 16 zero bytes of slack), its
+// line index without re-reading it (sstable.hpp layout: entry p is line p),
+// and r's flags[1] / flags[2], len and zone bounds, in one pass (n >= 1 for
+// r). The index is valid only when no key holds '\n' or '\t' (a key byte the
+// reference's line split or TAB search would see): flags[1] |= 1 otherwise,
+// and the caller re-indexes the file. flags[2] &= (keys strictly increasing:
+// the well-formed check).
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* loff, uint64_t n,
-                         uint8_t* out, hipStream_t s);
-// The created file's line index without re-reading it (sstable.hpp layout):
-// entry p is line p, so rec / pfx / fence follow from the entry itself. Valid
-// only when no key holds '\n' or '\t' (a key byte the reference's line split
-// or TAB search would see): flags[1] |= 1 otherwise, and the caller re-indexes
-// the file. flags[2] &= (keys strictly increasing: the well-formed check).
-hipError_t launch_format_index(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
-                               const uint64_t* vo, const uint64_t* loff, uint64_t n,
-                               LineRec* rec, uint64_t* pfx, uint64_t* fence, uint32_t* flags,
-                               hipStream_t s);
+                         uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
+                         hipStream_t s);
 
 }  // namespace cb
