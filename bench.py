@@ -430,7 +430,7 @@ def main():
         for _ in range(args.warmup):
             step_read()
         rel = timed(step_read, args.steps)
-        rprof = kernel_ms(["k_set_probe_gated", "k_get_many", "k_scan_u64", "k_b64_decode"], step_read, args.steps)
+        rprof = kernel_ms(["k_set_probe_gated", "k_get_many", "k_tile_scan", "k_b64_decode"], step_read, args.steps)
         found = int((which_d >= 0).sum().item())
         read = {"metric": "gets/s: 1M keys through zone+Bloom gate, binary search and base64 decode over "
                           f"{F} SSTable data files ({kpf} lines each) in HBM",
@@ -484,7 +484,7 @@ def main():
                 step_flush()
             k_fl = max(3, args.steps // 4)
             fel = timed(step_flush, k_fl)
-            fprof = kernel_ms(["k_sorted_check", "k_sort_keys", "rocprim_merge_sort", "rocprim_line_scan",
+            fprof = kernel_ms(["k_sorted_check", "k_sort_keys", "rocprim_merge_sort", "k_line_sums", "k_tile_scan",
                                "k_format", "k_line_count", "k_line_emit", "k_line_finish", "k_line_keys",
                                "k_build_part", "k_build_tile", "k_insert_direct"], step_flush, k_fl)
             out_bytes = made[-1][0].nbytes

@@ -1,0 +1,40 @@
+// blockscan.hpp — block-wide scans shared by the flush and read-path kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cb {
+
+// Block-wide exclusive scan of one uint64 per thread (NT threads). Returns the
+// thread's prefix; *total = block sum. Contains barriers: call uniformly.
+template <int NT>
+__device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t* total) {
+  static_assert(NT % 64 == 0 && NT <= 4096, "block size");
+  constexpr int NW = NT / 64;
+  __shared__ uint64_t ws[NW];
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long y = __shfl_up(x, d, 64);
+    if ((int)lane >= d) x += y;
+  }
+  if (lane == 63) ws[wid] = x;
+  __syncthreads();
+  if (wid == 0) {
+    unsigned long long w = lane < NW ? ws[lane] : 0ull;
+#pragma unroll
+    for (int d = 1; d < NW; d <<= 1) {
+      const unsigned long long y = __shfl_up(w, d, 64);
+      if ((int)lane >= d) w += y;
+    }
+    if (lane < NW) ws[lane] = w;
+  }
+  __syncthreads();
+  const uint64_t pre = wid ? ws[wid - 1] : 0;
+  *total = ws[NW - 1];
+  __syncthreads();  // ws is reused by the next call
+  return pre + (uint64_t)x - v;
+}
+
+}  // namespace cb

@@ -204,7 +204,7 @@ struct Workspace {
   DevBuf keys, offsets, hits, seg, ent, masks, bools, lkey, zone;
   DevBuf t_views, t_rows, t_which, t_line, t_dlen, t_voff, t_scan, t_vals;
   DevBuf i_cnt, i_base, i_tmp, i_end, i_err, i_start;                 // line indexing
-  DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_lens, f_loff, f_scan, f_flag;  // SsTable::create
+  DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_tsum, f_flag;  // SsTable::create
   DevBuf x_sums;                                                          // cb_hits_compress
   cb::CreateResult* hres = nullptr;  // pinned host mirror of f_flag (SsTable::create)
   uint64_t* htot = nullptr;          // pinned: get_many's value byte total
@@ -995,25 +995,29 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
   if ((rc = out_buf(ws.t_voff, val_off, n + 1, s, &dvoff))) return rc;
   HIP_TRY(ws.t_line.reserve(n * 8, s));
   HIP_TRY(ws.t_dlen.reserve(n * 8, s));
-  HIP_TRY(ws.t_scan.reserve(cb::scan_tmp_words(n) * 8, s));
+  HIP_TRY(ws.t_scan.reserve(cb::get_tiles(n) * 8, s));
   const cb::TableView* dviews = (const cb::TableView*)ws.t_views.p;
+  const uint64_t* vsrc = (const uint64_t*)ws.t_line.p;
+  const uint64_t* dlen = (const uint64_t*)ws.t_dlen.p;
+  uint64_t* tsum = (uint64_t*)ws.t_scan.p;
   HIP_TRY(cb::launch_get_many(sk.keyk, dviews, nt, dhits, drows, hwords, sk.ks, n, dwhich,
-                              (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, s));
-  HIP_TRY(cb::launch_scan_u64((const uint64_t*)ws.t_dlen.p, dvoff, n, (uint64_t*)ws.t_scan.p, s));
+                              (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, tsum, s));
+  HIP_TRY(cb::launch_tile_scan(tsum, cb::get_tiles(n), dvoff + n, s));
   if (!ws.htot) HIP_TRY(hipHostMalloc((void**)&ws.htot, 64, hipHostMallocDefault));
   if (vals && is_device_ptr(vals)) {
-    // device values: decoded in the same pass; the kernel itself skips the
-    // writes when the total exceeds cap, so one host round trip suffices
-    HIP_TRY(cb::launch_b64_decode((const uint64_t*)ws.t_line.p, dvoff, n, vals, cap, s));
+    // device values: offsets and values in one pass (the kernel skips the
+    // value writes when the total exceeds cap): one host round trip
+    HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, vals, cap, s));
     HIP_TRY(hipMemcpyAsync(ws.htot, dvoff + n, 8, hipMemcpyDeviceToHost, s));
   } else {
+    HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, nullptr, 0, s));  // offsets only
     HIP_TRY(hipMemcpyAsync(ws.htot, dvoff + n, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     const uint64_t tot = *ws.htot;
     if (vals && cap >= tot && tot) {
       uint8_t* dvals;
       if ((rc = out_buf(ws.t_vals, vals, tot, s, &dvals))) return rc;
-      HIP_TRY(cb::launch_b64_decode((const uint64_t*)ws.t_line.p, dvoff, n, dvals, tot, s));
+      HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, dvals, tot, s));
       HIP_TRY(hipMemcpyAsync(vals, dvals, tot, hipMemcpyDeviceToHost, s));
     }
   }
@@ -1673,7 +1677,9 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   hr->flags[2] = 1;
   hr->flags[3] = 0;
   HIP_TRY(hipMemcpyAsync(dr->flags, hr->flags, 16, hipMemcpyHostToDevice, s));
-  HIP_TRY(cb::launch_sorted_check(dk, dko, dvo, n, dr, s));
+  HIP_TRY(ws.f_tsum.reserve(cb::format_tiles(n) * 8, s));
+  uint64_t* tsum = (uint64_t*)ws.f_tsum.p;
+  HIP_TRY(cb::launch_sorted_check(dk, dko, dvo, n, dr, tsum, s));
   HIP_TRY(hipMemcpyAsync(hr, dr, offsetof(cb::CreateResult, len), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipEventRecord(ws.ev, s));
   auto build_bloom = [&]() -> int {  // (keys are non-null or all empty here)
@@ -1719,12 +1725,8 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
     HIP_TRY(cb::entry_sort(ws.f_sort.p, tmp_bytes, a0, a1, n, dk, dko, s));
     order = a1;
   }
-  HIP_TRY(ws.f_loff.reserve((n + 1) * 8, s));
-  uint64_t* loff = (uint64_t*)ws.f_loff.p;
-  size_t scan_bytes = 0;
-  HIP_TRY(cb::line_offsets(nullptr, scan_bytes, order, dko, dvo, n, loff, s));
-  HIP_TRY(ws.f_scan.reserve(scan_bytes + 16, s));
-  HIP_TRY(cb::line_offsets(ws.f_scan.p, scan_bytes, order, dko, dvo, n, loff, s));
+  if (order) HIP_TRY(cb::launch_line_sums(order, dko, dvo, n, tsum, s));
+  HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
   // the line index straight from the entries (entry p is line p), no re-read of the file
   t->nlines = n;
   t->nfence = (n + cb::kFenceStride - 1) / cb::kFenceStride;
@@ -1735,7 +1737,7 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   }
   t->pfx = (uint64_t*)(t->rec + n);
   t->fence = t->pfx + n;
-  HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, loff, n, t->data, t->rec, t->pfx, t->fence, dr, s));
+  HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, tsum, n, t->data, t->rec, t->pfx, t->fence, dr, s));
   // Round trip 2: flags, file length, zone bounds
   HIP_TRY(hipMemcpyAsync(hr, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));

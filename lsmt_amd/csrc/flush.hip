@@ -12,10 +12,8 @@
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_merge_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
 
+#include "blockscan.hpp"
 #include "flush.hpp"
 #include "profile.hpp"
 #include "zone.hpp"
@@ -23,7 +21,7 @@
 namespace cb {
 namespace {
 
-constexpr uint32_t kNT = 256;
+constexpr uint32_t kNT = 256;  // = kFormatTile
 
 inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
 
@@ -105,14 +103,41 @@ __device__ __forceinline__ int key_cmp(const uint8_t* kb, const uint64_t* ko, ui
   return bytes_cmp(kb + ko[q], ql, kb + ko[p], pl);
 }
 
+// Line p's byte length: key, TAB, base64 of the value, newline
+// (src/sstable.rs:66-70); 0 past the last line.
+__device__ __forceinline__ uint64_t line_len(uint64_t kl, uint64_t vl) { return kl + 1 + (vl + 2) / 3 * 4 + 1; }
+
+// The sum of each kFormatTile-line tile's lengths (order == nullptr: input
+// order), for k_format's offsets. Call uniformly.
+__device__ __forceinline__ void tile_sum(const SortKey* order, const uint64_t* ko, const uint64_t* vo,
+                                         uint64_t n, uint64_t* tsum) {
+  const uint64_t p = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  uint64_t len = 0;
+  if (p < n) {
+    const uint64_t i = order ? order[p].idx : p;
+    len = line_len(ko[i + 1] - ko[i], vo[i + 1] - vo[i]);
+  }
+  uint64_t total;
+  (void)block_scan<kNT>(len, &total);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kNT) void k_line_sums(const SortKey* __restrict__ order,
+                                                   const uint64_t* __restrict__ ko,
+                                                   const uint64_t* __restrict__ vo, uint64_t n,
+                                                   uint64_t* __restrict__ tsum) {
+  tile_sum(order, ko, vo, n, tsum);
+}
+
 // *ok &= key[i-1] <= key[i] for all i (already in stable-sorted order). Each
 // lane's key comes in as words; the previous one from the neighbour lane.
 __global__ __launch_bounds__(kNT) void k_sorted_check(const uint8_t* __restrict__ kb,
                                                       const uint64_t* __restrict__ ko,
                                                       const uint64_t* __restrict__ vo, uint64_t n,
-                                                      CreateResult* r) {
+                                                      CreateResult* r, uint64_t* __restrict__ tsum) {
   const uint64_t p = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
+  tile_sum(nullptr, ko, vo, n, tsum);  // the line tiles if the input is already sorted
   if (p == 0) {
     r->ktot = ko[n];
     r->vtot = vo[n];
@@ -144,21 +169,6 @@ struct KeyLess {
   }
 };
 
-// Line p's byte length: key, TAB, base64 of the value, newline
-// (src/sstable.rs:66-70); 0 past the last line so the scan's last output is
-// the file's length.
-struct LineLen {
-  const SortKey* order;
-  const uint64_t* ko;
-  const uint64_t* vo;
-  uint64_t n;
-  __host__ __device__ uint64_t operator()(uint64_t p) const {
-    if (p >= n) return 0;
-    const uint64_t i = order ? order[p].idx : p;
-    const uint64_t vl = vo[i + 1] - vo[i];
-    return (ko[i + 1] - ko[i]) + 1 + (vl + 2) / 3 * 4 + 1;
-  }
-};
 
 // One bound of the ZoneMap (the file's first or last key, w = 0 / 1) into r:
 // input index, full length and up to kZoneInline bytes. Whole block.
@@ -204,7 +214,10 @@ constexpr uint32_t kFormatLds = 32768;  // staged output bytes per block
 
 // SsTable::create's file and everything derived from it, one lane per entry p
 // (= line p; entries in key order):
-// - the line `key \t base64(value) \n` at loff[p]. A block's 256 lines are one
+// - the line `key \t base64(value) \n` at its offset: the tile sums before
+//   the block (tsum from k_sorted_check or k_line_sums, scanned by
+//   k_tile_scan) plus the scan of the block's line lengths: no full-length
+//   scan pass. A block's 256 lines are one
 //   contiguous range; when it fits in LDS the lanes format into LDS (staged at
 //   the range's address mod 4, so LDS and global dwords line up) and the block
 //   writes it with aligned dword stores, else lanes write bytes directly.
@@ -213,13 +226,13 @@ constexpr uint32_t kFormatLds = 32768;  // staged output bytes per block
 //   the file: LineRec, prefix and fence (sstable.hpp layout). flags[1] |= 1 if
 //   a key holds '\n' or '\t' (the caller then re-indexes the file the way
 //   SsTable::get splits it); flags[2] &= keys strictly increasing.
-// - r: the file length and the ZoneMap bounds (first / last key).
+// - r: the ZoneMap bounds (first / last key); k_tile_scan wrote r->len.
 __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ order,
                                                 const uint8_t* __restrict__ kb,
                                                 const uint64_t* __restrict__ ko,
                                                 const uint8_t* __restrict__ vb,
                                                 const uint64_t* __restrict__ vo,
-                                                const uint64_t* __restrict__ loff, uint64_t n,
+                                                const uint64_t* __restrict__ tsum, uint64_t n,
                                                 uint8_t* __restrict__ out, LineRec* __restrict__ rec,
                                                 uint64_t* __restrict__ pfx, uint64_t* __restrict__ fence,
                                                 CreateResult* r) {
@@ -229,7 +242,6 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   const uint64_t p = p0 + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t pend = p0 + kNT < n ? p0 + kNT : n;
-  const uint64_t base = loff[p0], total = loff[pend] - base;
   const bool live = p < n;
   uint64_t i = 0, kl = 0, w0 = 0, w1 = 0;
   if (live) key_words(order, kb, ko, p, i, kl, w0, w1);
@@ -238,7 +250,11 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   uint64_t pi = __shfl_up(i, 1, 64);
   if (live && lane == 0 && p > 0) key_words(order, kb, ko, p - 1, pi, pkl, pw0, pw1);
   const uint64_t vo0 = live ? vo[i] : 0, vl = live ? vo[i + 1] - vo0 : 0;
-  const uint64_t o = live ? loff[p] : 0;
+  // the line's offset: the tiles before this block, then the scan inside it
+  uint64_t total;
+  const uint64_t pre = block_scan<kNT>(live ? line_len(kl, vl) : 0, &total);
+  const uint64_t base = tsum[blockIdx.x];  // k_tile_scan: the tiles before
+  const uint64_t o = base + pre;
   bool special = false, not_inc = false;
   if (live) {
     const uint64_t llen = kl + 1 + (vl + 2) / 3 * 4;  // without the '\n'
@@ -267,9 +283,8 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   if (blockIdx.x == 0) zone_bound(order, kb, ko, 0, 0, r);
   if (pend == n) {
     zone_bound(order, kb, ko, n - 1, 1, r);
-    if (threadIdx.x == 0) r->len = loff[n];
     // 16 zero bytes after the file: the readable slack of the table's buffer
-    if (threadIdx.x < 16) out[loff[n] + threadIdx.x] = 0;
+    if (threadIdx.x < 16) out[base + total + threadIdx.x] = 0;
   }
   const uint8_t* k = kb + (live ? ko[i] : 0);
   const uint8_t* v = vb + vo0;
@@ -317,9 +332,18 @@ hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, S
 
 
 hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, const uint64_t* vo, uint64_t n,
-                               CreateResult* r, hipStream_t s) {
+                               CreateResult* r, uint64_t* tsum, hipStream_t s) {
   ProfScope ps("k_sorted_check", s);
-  hipLaunchKernelGGL(k_sorted_check, dim3(n ? blocks_for(n, kNT) : 1), dim3(kNT), 0, s, kb, ko, vo, n, r);
+  hipLaunchKernelGGL(k_sorted_check, dim3(n ? blocks_for(n, kNT) : 1), dim3(kNT), 0, s, kb, ko, vo, n, r,
+                     tsum);
+  return hipGetLastError();
+}
+
+hipError_t launch_line_sums(const SortKey* order, const uint64_t* ko, const uint64_t* vo, uint64_t n,
+                            uint64_t* tsum, hipStream_t s) {
+  if (!n) return hipSuccess;
+  ProfScope ps("k_line_sums", s);
+  hipLaunchKernelGGL(k_line_sums, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, order, ko, vo, n, tsum);
   return hipGetLastError();
 }
 
@@ -330,26 +354,15 @@ hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* 
   return rocprim::merge_sort(tmp, tmp_bytes, in, out, (size_t)n, KeyLess{kb, ko}, s);
 }
 
-hipError_t line_offsets(void* tmp, size_t& tmp_bytes, const SortKey* order, const uint64_t* ko,
-                        const uint64_t* vo, uint64_t n, uint64_t* loff, hipStream_t s) {
-  auto lens = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint64_t>(0),
-                                               LineLen{order, ko, vo, n});
-  if (!tmp)
-    return rocprim::exclusive_scan(tmp, tmp_bytes, lens, loff, (uint64_t)0, (size_t)n + 1,
-                                   rocprim::plus<uint64_t>(), s);
-  ProfScope ps("rocprim_line_scan", s);
-  return rocprim::exclusive_scan(tmp, tmp_bytes, lens, loff, (uint64_t)0, (size_t)n + 1,
-                                 rocprim::plus<uint64_t>(), s);
-}
 
 
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
-                         const uint8_t* vb, const uint64_t* vo, const uint64_t* loff, uint64_t n,
+                         const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
                          hipStream_t s) {
   if (!n) return hipSuccess;
   ProfScope ps("k_format", s);
-  hipLaunchKernelGGL(k_format, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, order, kb, ko, vb, vo, loff,
+  hipLaunchKernelGGL(k_format, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum,
                      n, out, rec, pfx, fence, r);
   return hipGetLastError();
 }

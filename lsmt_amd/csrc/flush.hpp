@@ -30,20 +30,24 @@ struct CreateResult {
 // out[i] = the sort record of key i.
 hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, SortKey* out,
                             hipStream_t s);
+// Lines per tile of the file's offsets: tsum holds format_tiles(n) (>= 1)
+// sums of line lengths.
+constexpr uint32_t kFormatTile = 256;
+inline uint64_t format_tiles(uint64_t n) { return n ? (n + kFormatTile - 1) / kFormatTile : 1; }
 // r->flags[0] &= (keys already in non-decreasing order); r->ktot = ko[n],
-// r->vtot = vo[n]. Launches for any n, n = 0 included.
+// r->vtot = vo[n]; tsum = the line tiles in input order (valid if sorted).
+// Launches for any n, n = 0 included.
 hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, const uint64_t* vo, uint64_t n,
-                               CreateResult* r, hipStream_t s);
-// loff[p] = start of output line p, loff[n] = the file's length: one rocPRIM
-// scan over the line lengths computed on the fly (order == nullptr: input
-// order). tmp == nullptr: only writes the scratch size to tmp_bytes.
-hipError_t line_offsets(void* tmp, size_t& tmp_bytes, const SortKey* order, const uint64_t* ko,
-                        const uint64_t* vo, uint64_t n, uint64_t* loff, hipStream_t s);
+                               CreateResult* r, uint64_t* tsum, hipStream_t s);
+// tsum = the line tiles in the order of the sort records.
+hipError_t launch_line_sums(const SortKey* order, const uint64_t* ko, const uint64_t* vo, uint64_t n,
+                            uint64_t* tsum, hipStream_t s);
 // Stable sort of the records by key (rocPRIM merge sort). tmp == nullptr:
 // only writes the scratch size to tmp_bytes.
 hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* out, uint64_t n,
                       const uint8_t* kb, const uint64_t* ko, hipStream_t s);
-// The file (lines into out at loff[p], then 16 zero bytes of slack), its
+// The file (lines at the offsets tsum and the line lengths give, then 16
+// zero bytes of slack), its
 // line index without re-reading it (sstable.hpp layout: entry p is line p),
 // and r's flags[1] / flags[2], len and zone bounds, in one pass (n >= 1 for
 // r). The index is valid only when no key holds '\n' or '\t' (a key byte the
@@ -51,7 +55,7 @@ hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* 
 // and the caller re-indexes the file. flags[2] &= (keys strictly increasing:
 // the well-formed check).
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
-                         const uint8_t* vb, const uint64_t* vo, const uint64_t* loff, uint64_t n,
+                         const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
                          hipStream_t s);
 

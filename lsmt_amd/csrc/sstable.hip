@@ -16,6 +16,7 @@
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
 
+#include "blockscan.hpp"
 #include "profile.hpp"
 #include "sstable.hpp"
 #include "zone.hpp"
@@ -25,37 +26,6 @@ namespace {
 
 constexpr uint32_t kNT = 256;
 
-// Block-wide exclusive scan of one uint64 per thread (NT threads). Returns the
-// thread's prefix; *total = block sum. Contains barriers: call uniformly.
-template <int NT>
-__device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t* total) {
-  static_assert(NT % 64 == 0 && NT <= 4096, "block size");
-  constexpr int NW = NT / 64;
-  __shared__ uint64_t ws[NW];
-  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  unsigned long long x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const unsigned long long y = __shfl_up(x, d, 64);
-    if ((int)lane >= d) x += y;
-  }
-  if (lane == 63) ws[wid] = x;
-  __syncthreads();
-  if (wid == 0) {
-    unsigned long long w = lane < NW ? ws[lane] : 0ull;
-#pragma unroll
-    for (int d = 1; d < NW; d <<= 1) {
-      const unsigned long long y = __shfl_up(w, d, 64);
-      if ((int)lane >= d) w += y;
-    }
-    if (lane < NW) ws[lane] = w;
-  }
-  __syncthreads();
-  const uint64_t pre = wid ? ws[wid - 1] : 0;
-  *total = ws[NW - 1];
-  __syncthreads();  // ws is reused by the next call
-  return pre + (uint64_t)x - v;
-}
 
 // ---- byte access helpers ----
 
@@ -259,6 +229,23 @@ __global__ __launch_bounds__(kNT) void k_line_keys(const uint8_t* __restrict__ d
   if (__syncthreads_or(!good) && threadIdx.x == 0 && *(volatile uint32_t*)ok) atomicAnd(ok, 0u);
 }
 
+// In-place exclusive scan of the nt tile sums a producer kernel left (one
+// block: a few thousand values), *total_out = their sum. The consumer kernel
+// then reads its block's base in one load; see launch_tile_scan.
+__global__ __launch_bounds__(1024) void k_tile_scan(uint64_t* __restrict__ tsum, uint64_t nt,
+                                                    uint64_t* __restrict__ total_out) {
+  uint64_t carry = 0;
+  for (uint64_t c0 = 0; c0 < nt; c0 += 1024) {
+    const uint64_t i = c0 + threadIdx.x;
+    const uint64_t v = i < nt ? tsum[i] : 0;
+    uint64_t total;
+    const uint64_t p = block_scan<1024>(v, &total);
+    if (i < nt) tsum[i] = carry + p;
+    carry += total;
+  }
+  if (threadIdx.x == 0) *total_out = carry;
+}
+
 // ---- exclusive scan of uint64: one rocPRIM look-back scan over n + 1 items
 // (the last reads as 0, so out[n] = total) ----
 struct TailZero {
@@ -376,44 +363,51 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
                                                   uint64_t hwords, KeySrc ks, uint64_t n,
                                                   int32_t* __restrict__ which,
                                                   uint64_t* __restrict__ vsrc,
-                                                  uint64_t* __restrict__ dlen) {
+                                                  uint64_t* __restrict__ dlen,
+                                                  uint64_t* __restrict__ tsum) {
   const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
-  if (k >= n) return;
-  const Query q = make_query<KEYK>(ks, k);
-  int32_t w = -1;
-  uint64_t src = 0, d = 0;
-  // Tables in groups of 64, newest first (tables.iter().rev()). Each lane
-  // first collects its candidate tables of the group as a bit mask (one
-  // broadcast load per table: a wave's 64 keys share a hit word), then every
-  // lane searches its OWN next candidate in the same iteration, so lanes
-  // whose keys live in different tables search concurrently instead of the
-  // wave stepping through the tables one by one.
-  for (uint32_t t0 = 0; t0 < nt && w < 0; t0 += 64) {
-    const uint32_t gn = nt - t0 < 64 ? nt - t0 : 64;
-    uint64_t cand = gn == 64 ? ~0ull : ((1ull << gn) - 1);
-    if (hits) {
-      cand = 0;
-      for (uint32_t i = 0; i < gn; ++i) {
-        const uint64_t row = rows ? rows[t0 + i] : t0 + i;
-        cand |= ((hits[row * hwords + (k >> 6)] >> (k & 63)) & 1) << i;  // the gate
+  uint64_t d = 0;
+  if (k < n) {
+    const Query q = make_query<KEYK>(ks, k);
+    int32_t w = -1;
+    uint64_t src = 0;
+    // Tables in groups of 64, newest first (tables.iter().rev()). Each lane
+    // first collects its candidate tables of the group as a bit mask (one
+    // broadcast load per table: a wave's 64 keys share a hit word), then every
+    // lane searches its OWN next candidate in the same iteration, so lanes
+    // whose keys live in different tables search concurrently instead of the
+    // wave stepping through the tables one by one.
+    for (uint32_t t0 = 0; t0 < nt && w < 0; t0 += 64) {
+      const uint32_t gn = nt - t0 < 64 ? nt - t0 : 64;
+      uint64_t cand = gn == 64 ? ~0ull : ((1ull << gn) - 1);
+      if (hits) {
+        cand = 0;
+        for (uint32_t i = 0; i < gn; ++i) {
+          const uint64_t row = rows ? rows[t0 + i] : t0 + i;
+          cand |= ((hits[row * hwords + (k >> 6)] >> (k & 63)) & 1) << i;  // the gate
+        }
+      }
+      while (cand) {
+        const uint32_t t = t0 + (uint32_t)__builtin_ctzll(cand);
+        cand &= cand - 1;
+        const TableView v = tv[t];
+        LineRec r;
+        if (search(v, q, r) < 0) continue;  // Ok(None)
+        if (r.vdl == kBadValue) continue;   // Err(..) is skipped by `if let Ok(Some(v))`
+        w = (int32_t)t;
+        src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
+        d = r.vdl;
+        break;
       }
     }
-    while (cand) {
-      const uint32_t t = t0 + (uint32_t)__builtin_ctzll(cand);
-      cand &= cand - 1;
-      const TableView v = tv[t];
-      LineRec r;
-      if (search(v, q, r) < 0) continue;  // Ok(None)
-      if (r.vdl == kBadValue) continue;   // Err(..) is skipped by `if let Ok(Some(v))`
-      w = (int32_t)t;
-      src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
-      d = r.vdl;
-      break;
-    }
+    which[k] = w;
+    vsrc[k] = src;
+    dlen[k] = d;
   }
-  which[k] = w;
-  vsrc[k] = src;
-  dlen[k] = d;
+  // this block's value bytes, for k_b64_decode's offsets
+  uint64_t total;
+  (void)block_scan<kNT>(d, &total);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = total;
 }
 
 // ---- base64 decode of the found values ----
@@ -447,23 +441,28 @@ __device__ __forceinline__ void b64_decode_into(const uint8_t* src, uint64_t dl,
 
 constexpr uint32_t kDecodeLds = 16384;  // staged output bytes per block
 
-// The block's values are one contiguous output range [voff[b0], voff[b0+256]).
-// When it fits in LDS, lanes decode into LDS and the block writes the range
-// with aligned dword stores; otherwise lanes write their bytes directly.
+// Value offsets: the block's base is the scanned value-byte tile sum (tsum:
+// k_get_many, then k_tile_scan, which also wrote voff[n] = the total), plus
+// the scan of its own lengths; voff[k] is written here. out ==
+// nullptr, or a total above cap: offsets only. Otherwise the block's values
+// are one contiguous output range; when it fits in LDS, lanes decode into LDS
+// and the block writes the range with aligned dword stores, else lanes write
+// their bytes directly.
 __global__ __launch_bounds__(kNT) void k_b64_decode(const uint64_t* __restrict__ vsrc,
-                                                    const uint64_t* __restrict__ voff, uint64_t n,
+                                                    const uint64_t* __restrict__ dlen,
+                                                    const uint64_t* __restrict__ tsum, uint64_t n,
+                                                    uint64_t* __restrict__ voff,
                                                     uint8_t* __restrict__ out, uint64_t cap) {
   __shared__ uint8_t stage[kDecodeLds];
-  if (voff[n] > cap) return;  // uniform: the output does not fit
   const uint64_t b0 = (uint64_t)blockIdx.x * kNT;
   const uint64_t k = b0 + threadIdx.x;
-  const uint64_t bend = b0 + kNT < n ? b0 + kNT : n;
-  const uint64_t base = voff[b0], total = voff[bend] - base;
-  uint64_t o = 0, dl = 0;
-  if (k < n) {
-    o = voff[k];
-    dl = voff[k + 1] - o;
-  }
+  const uint64_t dl = k < n ? dlen[k] : 0;
+  uint64_t total;
+  const uint64_t pre = block_scan<kNT>(dl, &total);
+  const uint64_t base = tsum[blockIdx.x];  // k_tile_scan: the tiles before
+  const uint64_t o = base + pre;
+  if (k < n) voff[k] = o;
+  if (!out || voff[n] > cap) return;  // uniform (voff[n]: k_tile_scan's total)
   const uint8_t* src = (const uint8_t*)(uintptr_t)(k < n ? vsrc[k] : 0);
   if (total > kDecodeLds) {  // uniform: large values, direct byte stores
     if (dl) b64_decode_into(src, dl, [&](uint64_t j, uint8_t v) { out[o + j] = v; });
@@ -564,33 +563,41 @@ hipError_t launch_table_search(int keyk, const TableView& t, const KeySrc& ks, u
 
 hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uint64_t* hits,
                            const uint32_t* rows, uint64_t hwords, const KeySrc& ks, uint64_t n,
-                           int32_t* which, uint64_t* vsrc, uint64_t* dlen, hipStream_t s) {
+                           int32_t* which, uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum,
+                           hipStream_t s) {
   if (!n) return hipSuccess;
   ProfScope ps("k_get_many", s);
   const dim3 g(blocks_for(n, kNT));
   switch (keyk) {
     case KEY_FIXED16:
       hipLaunchKernelGGL(k_get_many<KEY_FIXED16>, g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks,
-                         n, which, vsrc, dlen);
+                         n, which, vsrc, dlen, tsum);
       break;
     case KEY_FIXED:
       hipLaunchKernelGGL(k_get_many<KEY_FIXED>, g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n,
-                         which, vsrc, dlen);
+                         which, vsrc, dlen, tsum);
       break;
     case KEY_VAR:
       hipLaunchKernelGGL(k_get_many<KEY_VAR>, g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n,
-                         which, vsrc, dlen);
+                         which, vsrc, dlen, tsum);
       break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-hipError_t launch_b64_decode(const uint64_t* vsrc, const uint64_t* voff, uint64_t n, uint8_t* out,
-                             uint64_t cap, hipStream_t s) {
+hipError_t launch_tile_scan(uint64_t* tsum, uint64_t nt, uint64_t* total_out, hipStream_t s) {
+  ProfScope ps("k_tile_scan", s);
+  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, tsum, nt, total_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_b64_decode(const uint64_t* vsrc, const uint64_t* dlen, const uint64_t* tsum,
+                             uint64_t n, uint64_t* voff, uint8_t* out, uint64_t cap, hipStream_t s) {
   if (!n) return hipSuccess;
   ProfScope ps("k_b64_decode", s);
-  hipLaunchKernelGGL(k_b64_decode, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, vsrc, voff, n, out, cap);
+  hipLaunchKernelGGL(k_b64_decode, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, vsrc, dlen, tsum, n, voff,
+                     out, cap);
   return hipGetLastError();
 }
 

@@ -80,13 +80,22 @@ hipError_t launch_table_search(int keyk, const TableView& t, const KeySrc& ks, u
 // where hits (nullable, [rows][hwords]) has bit k of row rows[t] (rows
 // nullable = identity). which[k] = first t whose line decodes as base64,
 // else -1; vsrc[k] the device address of that value's base64 bytes; dlen[k]
-// the decoded length (0 if none).
+// the decoded length (0 if none); tsum[b] = the sum of dlen over key tile b
+// (kDecodeTile keys, get_tiles(n) entries).
+constexpr uint32_t kDecodeTile = 256;
+inline uint64_t get_tiles(uint64_t n) { return (n + kDecodeTile - 1) / kDecodeTile; }
 hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uint64_t* hits,
                            const uint32_t* rows, uint64_t hwords, const KeySrc& ks, uint64_t n,
-                           int32_t* which, uint64_t* vsrc, uint64_t* dlen, hipStream_t s);
-// Decoded values (voff = exclusive scan of dlen) into out + voff[k]; nothing
-// is written when voff[n] > cap (the caller's buffer is too small).
-hipError_t launch_b64_decode(const uint64_t* vsrc, const uint64_t* voff, uint64_t n, uint8_t* out,
-                             uint64_t cap, hipStream_t s);
+                           int32_t* which, uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum,
+                           hipStream_t s);
+// Tile sums -> their exclusive scan in place; *total_out = the sum (one
+// single-block kernel; producers leave one sum per tile, consumers read their
+// block's base in one load, so no full-length scan pass).
+hipError_t launch_tile_scan(uint64_t* tsum, uint64_t nt, uint64_t* total_out, hipStream_t s);
+// voff[0..n) = exclusive scan of dlen from the scanned tsum (voff[n] is the
+// total launch_tile_scan wrote), and the decoded values into out + voff[k];
+// values are written only when out != nullptr and the total fits in cap.
+hipError_t launch_b64_decode(const uint64_t* vsrc, const uint64_t* dlen, const uint64_t* tsum,
+                             uint64_t n, uint64_t* voff, uint8_t* out, uint64_t cap, hipStream_t s);
 
 }  // namespace cb
