@@ -210,6 +210,63 @@ __device__ __forceinline__ void format_line(uint64_t kl, KB kbyte, uint64_t vl, 
   put(o, '\n');
 }
 
+// Byte t (static) of 16 bytes held in memory order as two little-endian words.
+__device__ __forceinline__ uint32_t mem_byte(uint64_t b0, uint64_t b1, uint32_t t) {
+  return t < 8 ? (uint32_t)(b0 >> (8 * t)) & 0xFF : t < 16 ? (uint32_t)(b1 >> (8 * (t - 8))) & 0xFF : 0u;
+}
+
+// dst[j] = bytes [4j, 4j+4) of src shifted up by s (0..3) bytes: src's byte i
+// lands at byte i + s. N output dwords from N-1 input dwords (+ the top one).
+template <int N>
+__device__ __forceinline__ void shift_bytes(const uint32_t* src, uint32_t s, uint32_t* dst) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const uint64_t hi = j < N - 1 ? src[j] : 0u, lo = j ? src[j - 1] : 0u;
+    dst[j] = (uint32_t)(((hi << 32) | lo) >> (32 - 8 * s));
+  }
+}
+
+// A line whose key and value are both <= 16 bytes (words w0/w1: the key as
+// big-endian words; v0/v1: the value's) built in registers: L[0..12) holds
+// its bytes in memory order, zero past the end. Static byte positions only,
+// so nothing spills: the key's 4 dwords, then '\t' + base64 + '\n' built at
+// fixed positions and shifted into place by kl bytes. Returns the length.
+__device__ __forceinline__ uint32_t line16(uint64_t w0, uint64_t w1, uint32_t kl, uint64_t v0, uint64_t v1,
+                                           uint32_t vl, uint32_t L[12]) {
+  const uint64_t k0 = __builtin_bswap64(w0), k1 = __builtin_bswap64(w1);  // memory order
+  const uint32_t K[4] = {(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
+  const uint64_t b0 = __builtin_bswap64(v0), b1 = __builtin_bswap64(v1);
+  const uint32_t g = (vl + 2) / 3;  // base64 quads
+  uint32_t V[8] = {'\t', 0, 0, 0, 0, 0, 0, 0};  // '\t' at 0, quad i at 1+4i, '\n' at 1+4g
+#pragma unroll
+  for (uint32_t i = 0; i < 6; ++i) {
+    if (i < g) {
+      const uint32_t t = 3 * i, r = vl - t;
+      const uint32_t w = mem_byte(b0, b1, t) << 16 | (r > 1 ? mem_byte(b0, b1, t + 1) << 8 : 0u) |
+                         (r > 2 ? mem_byte(b0, b1, t + 2) : 0u);
+      const uint32_t c0 = b64c(w >> 18), c1 = b64c((w >> 12) & 63);
+      const uint32_t c2 = r > 1 ? b64c((w >> 6) & 63) : '=', c3 = r > 2 ? b64c(w & 63) : '=';
+      V[i] |= c0 << 8 | c1 << 16 | c2 << 24;
+      V[i + 1] |= c3;
+    }
+    if (i == g) V[i] |= (uint32_t)'\n' << 8;
+  }
+  if (g == 6) V[6] |= (uint32_t)'\n' << 8;
+  // the key's kl bytes, then V: V shifted up by kl = 4 * (kl >> 2) + (kl & 3)
+  uint32_t S[9];
+  shift_bytes<9>(V, kl & 3, S);
+  const uint32_t ds = kl >> 2;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int d = 0; d <= 4; ++d)
+      if (j - d >= 0 && j - d < 9 && ds == (uint32_t)d) x = S[j - d];
+    L[j] = (j < 4 ? K[j] : 0u) | x;
+  }
+  return kl + 2 + 4 * g;
+}
+
 constexpr uint32_t kFormatLds = 32768;  // staged output bytes per block
 
 // SsTable::create's file and everything derived from it, one lane per entry p
@@ -291,7 +348,7 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   uint64_t v0 = 0, v1 = 0;
   const bool words = kl <= 16 && vl <= 16;
   if (live && words) load16(v, vl, v0, v1);
-  auto emit = [&](auto put) {
+  auto emit = [&](auto put) {  // byte at a time (long lines)
     if (!live) return;
     if (words)
       format_line(kl, [&](uint64_t j) { return be_byte(w0, w1, j); }, vl,
@@ -305,7 +362,27 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
     emit([&](uint64_t j, uint8_t c) { out[o + j] = c; });
     return;
   }
-  emit([&](uint64_t j, uint8_t c) { stage[o - base + sh0 + j] = c; });
+  // Stage the block's range in LDS, ORed into zeroed dwords: the lines of
+  // neighbouring lanes share edge dwords, and ds_or keeps both.
+  const uint32_t nd = (uint32_t)((sh0 + total + 3) / 4);
+  for (uint32_t j = threadIdx.x; j < nd; j += kNT) stage32[j] = 0;
+  __syncthreads();
+  const uint64_t off = o - base + sh0;  // the line's first byte in the stage
+  if (live && words) {
+    uint32_t L[12], M[13];
+    const uint32_t len = line16(w0, w1, (uint32_t)kl, v0, v1, (uint32_t)vl, L);
+    shift_bytes<13>(L, (uint32_t)(off & 3), M);
+    const uint32_t nw = (uint32_t)((off & 3) + len + 3) / 4;
+    uint32_t* dst = stage32 + off / 4;
+#pragma unroll
+    for (uint32_t j = 0; j < 13; ++j)
+      if (j < nw) atomicOr(dst + j, M[j]);
+  } else if (live) {
+    emit([&](uint64_t j, uint8_t c) {
+      const uint64_t b = off + j;
+      atomicOr(stage32 + b / 4, (uint32_t)c << (8 * (b & 3)));
+    });
+  }
   __syncthreads();
   // out[base .. base+total): bytes up to the first 4-aligned address, then
   // aligned dwords (LDS dword-aligned too), then the tail
