@@ -1737,7 +1737,8 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   }
   t->pfx = (uint64_t*)(t->rec + n);
   t->fence = t->pfx + n;
-  HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, tsum, n, t->data, t->rec, t->pfx, t->fence, dr, s));
+  HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, tsum, n, t->data, t->rec, t->pfx, t->fence, dr,
+                            cap_bytes, s));
   // Round trip 2: flags, file length, zone bounds
   HIP_TRY(hipMemcpyAsync(hr, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));

@@ -267,7 +267,10 @@ __device__ __forceinline__ uint32_t line16(uint64_t w0, uint64_t w1, uint32_t kl
   return kl + 2 + 4 * g;
 }
 
-constexpr uint32_t kFormatLds = 32768;  // staged output bytes per block
+// Staged output bytes per block: 16 KiB (more resident blocks) when the
+// average line is short, else 32 KiB; a block whose lines exceed the stage
+// writes its bytes directly.
+constexpr uint32_t kFormatLdsSmall = 16384, kFormatLdsLarge = 32768;
 
 // SsTable::create's file and everything derived from it, one lane per entry p
 // (= line p; entries in key order):
@@ -284,6 +287,7 @@ constexpr uint32_t kFormatLds = 32768;  // staged output bytes per block
 //   a key holds '\n' or '\t' (the caller then re-indexes the file the way
 //   SsTable::get splits it); flags[2] &= keys strictly increasing.
 // - r: the ZoneMap bounds (first / last key); k_tile_scan wrote r->len.
+template <uint32_t LDSB>
 __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ order,
                                                 const uint8_t* __restrict__ kb,
                                                 const uint64_t* __restrict__ ko,
@@ -293,7 +297,7 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
                                                 uint8_t* __restrict__ out, LineRec* __restrict__ rec,
                                                 uint64_t* __restrict__ pfx, uint64_t* __restrict__ fence,
                                                 CreateResult* r) {
-  __shared__ uint32_t stage32[kFormatLds / 4];
+  __shared__ uint32_t stage32[LDSB / 4];
   uint8_t* stage = reinterpret_cast<uint8_t*>(stage32);
   const uint64_t p0 = (uint64_t)blockIdx.x * kNT;
   const uint64_t p = p0 + threadIdx.x;
@@ -358,7 +362,7 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
                   [&](uint64_t j) { return (uint32_t)v[j]; }, put);
   };
   const uint64_t sh0 = base & 3;
-  if (total + sh0 > kFormatLds) {  // uniform: long lines, direct byte stores
+  if (total + sh0 > LDSB) {  // uniform: long lines, direct byte stores
     emit([&](uint64_t j, uint8_t c) { out[o + j] = c; });
     return;
   }
@@ -436,11 +440,16 @@ hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* 
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
-                         hipStream_t s) {
+                         uint64_t bytes_bound, hipStream_t s) {
   if (!n) return hipSuccess;
   ProfScope ps("k_format", s);
-  hipLaunchKernelGGL(k_format, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum,
-                     n, out, rec, pfx, fence, r);
+  const dim3 g(blocks_for(n, kNT));
+  if (bytes_bound / n * kNT * 5 / 4 <= kFormatLdsSmall)
+    hipLaunchKernelGGL(k_format<kFormatLdsSmall>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
+                       rec, pfx, fence, r);
+  else
+    hipLaunchKernelGGL(k_format<kFormatLdsLarge>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
+                       rec, pfx, fence, r);
   return hipGetLastError();
 }
 

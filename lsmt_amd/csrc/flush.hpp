@@ -50,13 +50,13 @@ hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* 
 // zero bytes of slack), its
 // line index without re-reading it (sstable.hpp layout: entry p is line p),
 // and r's flags[1] / flags[2], len and zone bounds, in one pass (n >= 1 for
-// r). The index is valid only when no key holds '\n' or '\t' (a key byte the
+// r). bytes_bound (>= the file's length) picks the LDS stage size. The index is valid only when no key holds '\n' or '\t' (a key byte the
 // reference's line split or TAB search would see): flags[1] |= 1 otherwise,
 // and the caller re-indexes the file. flags[2] &= (keys strictly increasing:
 // the well-formed check).
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
-                         hipStream_t s);
+                         uint64_t bytes_bound, hipStream_t s);
 
 }  // namespace cb
