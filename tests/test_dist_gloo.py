@@ -115,7 +115,8 @@ def _worker(rank, world, port, n_filters, result_q, mode="dense"):
 
 @pytest.mark.parametrize("world,n_filters,mode", [(2, 6, "dense"), (2, 5, "dense"), (3, 7, "dense"),
                                                   (2, 6, "sparse"), (3, 7, "sparse"), (3, 7, "overflow"),
-                                                  (3, 7, "async"), (2, 5, "async_overflow")])
+                                                  (3, 7, "async"), (2, 5, "async_overflow"), (8, 19, "sparse"),
+                                                  (8, 19, "dense")])
 def test_sharded_probe_allgather_gloo(world, n_filters, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
