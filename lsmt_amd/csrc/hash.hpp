@@ -145,11 +145,31 @@ __device__ __forceinline__ void key_positions(const KeySrc& ks, uint64_t k, cons
     a = h1 & mask;
     b = h2 & mask;
   } else if constexpr (MODE == MOD_POW2_32) {
-    H32 h;
-    hash_key<KEYK>(ks, k, h);
+    // ragged or unaligned batches: a key that happens to be 16 bytes on a
+    // 4-byte boundary still takes the dot4 fold (same hash, fewer ops)
+    const uint8_t* p;
+    uint64_t len;
+    if constexpr (KEYK == KEY_FIXED) {
+      p = ks.bytes + k * ks.key_len;
+      len = ks.key_len;
+    } else {
+      const uint64_t o0 = ks.offsets[k];
+      p = ks.bytes + o0;
+      len = ks.offsets[k + 1] - o0;
+    }
+    uint32_t h1, h2;
+    if (len == 16 && !(reinterpret_cast<uintptr_t>(p) & 3u)) {
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+      hash16_u32(make_uint4(w[0], w[1], w[2], w[3]), h1, h2);
+    } else {
+      H32 h;
+      hash_range(p, len, h);
+      h1 = h.h1;
+      h2 = h.h2;
+    }
     const uint32_t mask = static_cast<uint32_t>(mp.mask);
-    a = h.h1 & mask;
-    b = h.h2 & mask;
+    a = h1 & mask;
+    b = h2 & mask;
   } else {
     H64 h;
     hash_key<KEYK>(ks, k, h);
