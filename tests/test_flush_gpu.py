@@ -164,3 +164,17 @@ def test_create_zone_keys_long_and_device(gpu, on_device):
     for k in keys:
         o.insert(k)
     assert np.array_equal(bloom.bools(), o.bools())
+
+
+def test_table_zone_only_for_created_tables(gpu):
+    # cb_table_zone answers for tables SsTable::create made with entries; a
+    # table indexed from an existing file, or an empty one, has no bounds
+    from lsmt_amd._lib import CassBloomError
+    t, _, zone = gpu.sstable_create([(b"b", b"1"), (b"a", b"2")])
+    assert (t._zone(0), t._zone(1)) == (b"a", b"b") == (zone.min, zone.max)
+    with pytest.raises(CassBloomError):
+        gpu.Table(t.data())._zone(0)
+    e, _, ez = gpu.sstable_create([])
+    assert ez.min is None and ez.max is None
+    with pytest.raises(CassBloomError):
+        e._zone(1)
