@@ -112,17 +112,26 @@ __global__ __launch_bounds__(kCT) void k_hits_emit(const uint64_t* __restrict__ 
   }
 }
 
-// First index in p[0..n) with p[i] >= x (p ascending).
-__device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t* p, uint64_t n, uint64_t x) {
-  uint64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if ((uint64_t)p[mid] < x)
-      lo = mid + 1;
-    else
-      hi = mid;
+// First index in p[0..n) with p[i] >= x (p ascending), by one whole wave:
+// each round the 64 lanes probe 64 evenly spaced entries and the ballot of
+// "< x" (a prefix of the lanes) narrows the range 64-fold, so a 70K-entry
+// pack takes 3 rounds of one parallel load instead of 17 dependent ones.
+__device__ __forceinline__ uint64_t wave_lower_bound(const uint32_t* p, uint64_t n, uint64_t x) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t lo = 0, hi = n;  // the answer is in [lo, hi]
+  while (hi - lo > 64) {
+    const uint64_t step = (hi - lo + 63) / 64;
+    const uint64_t i = lo + lane * step;
+    const bool below = i < hi && (uint64_t)p[i] < x;
+    const uint32_t c = (uint32_t)__popcll(__ballot(below));
+    const uint64_t nlo = c ? lo + (uint64_t)(c - 1) * step + 1 : lo;
+    const uint64_t nhi = lo + (uint64_t)c * step < hi ? lo + (uint64_t)c * step : hi;
+    lo = nlo;
+    hi = nhi;
   }
-  return lo;
+  const uint64_t i = lo + lane;
+  const bool below = i < hi && (uint64_t)p[i] < x;
+  return lo + (uint64_t)__popcll(__ballot(below));
 }
 
 __global__ __launch_bounds__(kXT) void k_hits_expand(const uint32_t* __restrict__ packs,
@@ -132,6 +141,7 @@ __global__ __launch_bounds__(kXT) void k_hits_expand(const uint32_t* __restrict_
                                                      uint32_t* __restrict__ ok) {
   __shared__ uint64_t chunk[kChunkWords];
   __shared__ uint64_t seg[kMaxRanks][3];  // per overlapped rank: first entry, end entry, base word
+  __shared__ uint64_t job[kMaxRanks][3];  // per overlapped rank: pack offset, count, first local word
   __shared__ uint32_t nseg;
   const uint32_t tid = threadIdx.x;
   const uint64_t w0 = (uint64_t)blockIdx.x * kChunkWords;
@@ -150,12 +160,22 @@ __global__ __launch_bounds__(kXT) void k_hits_expand(const uint32_t* __restrict_
         continue;
       }
       const uint64_t lw0 = (w0 > rb ? w0 : rb) - rb, lw1 = (w1 < re ? w1 : re) - rb;
-      seg[ns][0] = (uint64_t)r * (2 + cap) + 2 + lower_bound_u32(pk + 2, count, lw0 * 64);
-      seg[ns][1] = (uint64_t)r * (2 + cap) + 2 + lower_bound_u32(pk + 2, count, lw1 * 64);
+      job[ns][0] = (uint64_t)r * (2 + cap) + 2;
+      job[ns][1] = count;
+      job[ns][2] = lw0 | (lw1 << 32);  // local words < 2^32 (positions are u32)
       seg[ns][2] = rb;
       ++ns;
     }
     nseg = ns;
+  }
+  __syncthreads();
+  // the chunk's entry range in each overlapped pack: two wave-wide searches
+  // per rank, one per wave
+  for (uint32_t j = tid >> 6; j < 2 * nseg; j += kXT / 64) {
+    const uint32_t s = j >> 1;
+    const uint64_t lw = (j & 1) ? job[s][2] >> 32 : job[s][2] & 0xFFFFFFFFull;
+    const uint64_t e = wave_lower_bound(packs + job[s][0], job[s][1], lw * 64);
+    if ((tid & 63) == 0) seg[s][j & 1] = job[s][0] + e;
   }
   __syncthreads();
   for (uint32_t s = 0; s < nseg; ++s) {
