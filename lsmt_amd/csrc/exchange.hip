@@ -12,7 +12,7 @@
 //       first cap positions are stored).
 //   k_hits_expand — after the all-gather of packs: each workgroup owns a
 //       32 KiB chunk of the global [total_rows][words] map, finds the
-//       positions that fall in it by binary search in the (sorted) packs of
+//       positions that fall in it by wave-wide 64-ary searches in the (sorted) packs of
 //       the ranks it overlaps, ORs them into the chunk in LDS and writes the
 //       chunk once: the map is written exactly once, with no memset and no
 //       global atomics. A rank whose count exceeds cap contributes nothing and
