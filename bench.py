@@ -256,15 +256,21 @@ def main():
                 out[nm] = {"avg_us": tot.value * 1e3 / cnt.value, "launches": int(cnt.value)}
         return out
 
-    def cold_run(names, fn, reps=8):
+    def cold_run(names, fn, reps=8, clean=False):
         """SURVEY.md §8d timing protocol, cold leg: before every rep a 1 GiB
         streaming device write evicts the L2s and the 256 MiB Infinity Cache,
         then ONE step runs; medians over reps of the step (HIP events on the
-        kernels' stream) and of each kernel (cb_profile events)."""
+        kernels' stream) and of each kernel (cb_profile events). clean: a
+        512 MiB read follows the write, so the caches hold clean unrelated
+        lines and the step does not also pay the write-back of the flush's
+        dirty ones."""
         flush = torch.empty(1 << 28, dtype=torch.int32, device=dev)
+        rd = torch.ones(1 << 27, dtype=torch.int32, device=dev) if clean else None
         step_ms, kus = [], {nm: [] for nm in names}
         for r in range(2 * reps):
             flush.fill_(r)
+            if clean:
+                rd.sum()
             torch.cuda.synchronize(dev)
             if use_dist:
                 dist.barrier()
@@ -278,7 +284,7 @@ def main():
             else:
                 for nm, v in kernel_ms(names, fn, 1).items():
                     kus[nm].append(v["avg_us"])
-        del flush
+        del flush, rd
         torch.cuda.synchronize(dev)
         return (float(np.median(step_ms)),
                 {nm: round(float(np.median(v)), 2) for nm, v in kus.items() if v})
@@ -291,6 +297,10 @@ def main():
         cold_ms, cold_k = cold_run(probe_kernels, step)
         cold = {"value": round(probes_per_step / (cold_ms * 1e-3), 1), "ms_per_step": round(cold_ms, 4),
                 "kernels_us": cold_k, "protocol": "1 GiB device write before each of 8 reps, median"}
+        clean_ms, clean_k = cold_run(probe_kernels, step, clean=True)
+        cold["clean_caches"] = {"value": round(probes_per_step / (clean_ms * 1e-3), 1),
+                                "ms_per_step": round(clean_ms, 4), "kernels_us": clean_k,
+                                "protocol": "the same write, then a 512 MiB read, before each rep"}
 
     # rotating batches: 4 different lookup batches over the same filters, one
     # per step in turn, so a step cannot find the set lines of its own
@@ -523,6 +533,9 @@ def main():
         bcold_ms, bcold_k = cold_run(["k_build_part", "k_build_tile", "k_insert_direct"], build_step)
         bcold = {"value": round(args.build_keys * world / (bcold_ms * 1e-3), 1),
                  "ms_per_step": round(bcold_ms, 4), "kernels_us": bcold_k}
+        bclean_ms, bclean_k = cold_run(["k_build_part", "k_build_tile", "k_insert_direct"], build_step, clean=True)
+        bcold["clean_caches"] = {"value": round(args.build_keys * world / (bclean_ms * 1e-3), 1),
+                                 "ms_per_step": round(bclean_ms, 4), "kernels_us": bclean_k}
     b_alg = 16 * args.build_keys + args.build_m_bits / 8
     build = {"metric": "build keys/s (C2: 1M 16-B keys -> one 16 MiB filter, m=2^27)",
              "value": round(args.build_keys * world / (bel / args.steps), 1), "unit": "keys/s",
