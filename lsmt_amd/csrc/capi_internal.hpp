@@ -1,0 +1,187 @@
+// capi_internal.hpp — what the C ABI's translation units share (capi.cpp:
+// filters, probes, sets, codec, exchange; capi_sstable.cpp: SSTable files,
+// the read path and SsTable::create): the handle structs, error reporting,
+// device buffers, the block pool, per-stream workspaces and key staging.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstddef>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "cassbloom.h"
+#include "exchange.hpp"
+#include "filterset.hpp"
+#include "flush.hpp"
+#include "kernels.hpp"
+#include "sstable.hpp"
+#include "zone.hpp"
+
+struct cb_filter {
+  uint64_t m = 0;
+  int device = 0;
+  uint32_t* words = nullptr;  // device, nwords_alloc words
+  uint64_t nwords_alloc = 0;
+  size_t words_cap = 0;  // pool block size
+  bool known_zero = true;  // logically all-zero (lets the tiled build skip the read)
+  // cb_filter_clear is lazy: the memset is issued by the next operation that
+  // needs the words, and skipped by a fresh tiled build (which writes every
+  // tile). Exchanged atomically so concurrent readers issue it once.
+  std::atomic<bool> needs_zero{false};
+  // Pool blocks are reused, so the padding words past ceil(m/32) are cleared
+  // once (lazily, on the caller's stream) by paths that skip the full fill.
+  std::atomic<bool> needs_pad_zero{false};
+  int mode = 0;
+  cb::ModP mp{};
+};
+
+struct cb_filterset {
+  uint64_t m = 0;
+  int device = 0;
+  uint32_t width = 32;
+  void* words = nullptr;  // device, m (rounded up to 32) words of width bits
+  uint32_t* any = nullptr;  // device, ceil(m/32) words: bit p = (words[p] != 0)
+  uint32_t used = 0;      // 1 + highest assigned slot
+  uint64_t dirty = 0;     // bit s: slot s may hold set bits
+  int mode = 0;
+  cb::ModP mp{};
+  // Per-slot ZoneMap (src/zonemap.rs): host copy, and the device table the
+  // gated probe reads (cb::ZoneView: 64 x 16-B headers, then the bytes).
+  std::vector<std::string> zlo, zhi;
+  std::vector<uint8_t> zhas_lo, zhas_hi;
+  void* zdev = nullptr;
+  size_t zcap = 0;
+  uint64_t zgated = 0;  // slots with both bounds
+};
+
+// An SSTable data file resident in HBM with its line index (sstable.hpp).
+struct cb_table {
+  int device = 0;
+  uint64_t len = 0, nlines = 0;
+  uint8_t* data = nullptr;      // the file + 16 bytes of slack
+  size_t data_cap = 0, rec_cap = 0;  // pool block sizes
+  cb::LineRec* rec = nullptr;   // per-line index record
+  uint64_t* pfx = nullptr;      // per-line 8-byte key prefix
+  uint64_t* fence = nullptr;    // every 64th prefix
+  uint64_t nfence = 0;
+  bool fast = false;  // well-formed: TAB on every line, keys strictly increasing
+  bool has_zone = false;   // made by cb_sstable_create with n >= 1
+  std::string zmin, zmax;  // its ZoneMap bounds (first / last key of the file)
+  cb::TableView view() const {
+    return cb::TableView{data, rec, pfx, fence, nlines, nfence, fast ? 1u : 0u};
+  }
+};
+
+namespace cbx {
+
+using cb::FilterPtrs;
+using cb::KeySrc;
+using cb::ModP;
+using cb::TilePlan;
+
+extern thread_local std::string g_err;  // cb_last_error
+extern thread_local int g_last_path;    // cb_last_path
+
+int fail(int code, const char* what);
+int hip_fail(hipError_t e, const char* where);
+
+#define HIP_TRY(expr)                                       \
+  do {                                                      \
+    hipError_t _e = (expr);                                 \
+    if (_e != hipSuccess) return ::cbx::hip_fail(_e, #expr); \
+  } while (0)
+
+// Device buffer that grows on demand. Growth synchronises the owning stream
+// first, so a buffer still read by queued work is never freed under it.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t bytes, hipStream_t s) {
+    if (bytes <= cap) return hipSuccess;
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+    want = (want + 4095) & ~size_t(4095);
+    e = hipMalloc(&p, want);
+    if (e != hipSuccess) return e;
+    cap = want;
+    return hipSuccess;
+  }
+};
+
+// Device block pool for table and filter storage (capi.cpp). *cap receives
+// the block's size (pass it back to pool_release); release synchronises the
+// device first, as hipFree would.
+hipError_t pool_alloc(int device, size_t bytes, void** p, size_t* cap);
+void pool_release(int device, void* p, size_t cap);
+
+struct Workspace {
+  std::mutex mu;
+  DevBuf keys, offsets, hits, seg, ent, masks, bools, lkey, zone;
+  DevBuf t_views, t_rows, t_which, t_line, t_dlen, t_voff, t_scan, t_vals;
+  DevBuf i_cnt, i_base, i_tmp, i_end, i_err, i_start;                 // line indexing
+  DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_tsum, f_flag;  // SsTable::create
+  DevBuf x_sums;                                                          // cb_hits_compress
+  cb::CreateResult* hres = nullptr;  // pinned host mirror of f_flag (SsTable::create)
+  uint64_t* htot = nullptr;          // pinned: get_many's value byte total
+  hipEvent_t ev = nullptr;           // marks hres's first copy in the stream
+};
+
+Workspace& workspace(int device, hipStream_t s);
+
+// Device-accessible memory (hipMalloc, managed) is used in place; anything
+// else (pageable or pinned host memory) is staged by the library.
+bool is_device_ptr(const void* p);
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+struct StagedKeys {
+  KeySrc ks{};
+  int keyk = cb::KEY_FIXED;
+  bool staged = false;
+};
+
+int stage_fixed(Workspace& ws, const uint8_t* keys, uint32_t key_len, uint64_t n, hipStream_t s,
+                StagedKeys& out);
+int stage_var(Workspace& ws, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+              hipStream_t s, StagedKeys& out);
+// A batched insert with the stream's workspace already locked by the caller.
+int insert_locked(Workspace& ws, cb_filter* f, const uint8_t* keys, const uint64_t* offsets,
+                  uint32_t key_len, uint64_t n, hipStream_t s);
+// Host bytes into an output buffer that may be host or device memory.
+int put_bytes(uint8_t* dst, const void* src, size_t n);
+
+// Device output: used in place when device-resident, else a workspace buffer
+// copied back at the end.
+template <class T>
+int out_buf(DevBuf& b, T* user, size_t count, hipStream_t s, T** dev) {
+  if (is_device_ptr(user)) {
+    *dev = user;
+    return CB_OK;
+  }
+  HIP_TRY(b.reserve(count * sizeof(T) + 8, s));
+  *dev = (T*)b.p;
+  return CB_OK;
+}
+
+}  // namespace cbx

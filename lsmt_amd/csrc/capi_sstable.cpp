@@ -1,0 +1,488 @@
+// capi_sstable.cpp — the C ABI for SSTable data files in HBM (SURVEY.md §8f
+// rows 3 and 4): indexing an existing file (cb_table_create), SsTable::create
+// on the device (cb_sstable_create), the batched binary search and
+// Database::get's newest-first walk (cb_get_many_*).
+//
+// Reference: /root/reference/src/sstable.rs:51-179, src/lib.rs:125-136.
+#include "capi_internal.hpp"
+
+using namespace cbx;
+
+namespace {
+
+bool g_table_exact = false;  // cb_table_force_exact: index files for the exact-trajectory search only
+
+int table_search_impl(const cb_table* t, const uint8_t* keys, const uint64_t* offsets,
+                      uint32_t key_len, uint64_t n, int64_t* line_out, hipStream_t s) {
+  if (!t || !line_out) return fail(CB_EINVAL, "null argument");
+  if (n == 0) return CB_OK;
+  if (offsets == nullptr && keys == nullptr && key_len) return fail(CB_EINVAL, "null keys");
+  DeviceGuard dg(t->device);
+  Workspace& ws = workspace(t->device, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  StagedKeys sk;
+  int rc = offsets ? stage_var(ws, keys, offsets, n, s, sk) : stage_fixed(ws, keys, key_len, n, s, sk);
+  if (rc) return rc;
+  int64_t* dl;
+  if ((rc = out_buf(ws.t_line, line_out, n, s, &dl))) return rc;
+  HIP_TRY(cb::launch_table_search(sk.keyk, t->view(), sk.ks, n, dl, s));
+  if (dl != line_out) {
+    HIP_TRY(hipMemcpyAsync(line_out, dl, n * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  } else if (sk.staged) {
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  return CB_OK;
+}
+
+int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hits,
+                  const uint32_t* hit_rows, const uint8_t* keys, const uint64_t* offsets,
+                  uint32_t key_len, uint64_t n, int32_t* which, uint64_t* val_off, uint8_t* vals,
+                  uint64_t cap, uint64_t* total, hipStream_t s) {
+  if (!which || !val_off || !total || (nt && !tables)) return fail(CB_EINVAL, "null argument");
+  *total = 0;
+  if (n == 0) {
+    const uint64_t z = 0;
+    return put_bytes((uint8_t*)val_off, &z, 8);
+  }
+  if (offsets == nullptr && keys == nullptr && key_len) return fail(CB_EINVAL, "null keys");
+  if (nt == 0) return fail(CB_EINVAL, "no tables");
+  const int dev = tables[0] ? tables[0]->device : 0;
+  std::vector<cb::TableView> views(nt);
+  uint64_t nrows = nt;
+  for (uint32_t i = 0; i < nt; ++i) {
+    if (!tables[i]) return fail(CB_EINVAL, "null table");
+    if (tables[i]->device != dev) return fail(CB_EINVAL, "tables live on different devices");
+    views[i] = tables[i]->view();
+  }
+  std::vector<uint32_t> rows;
+  if (hits && hit_rows) {
+    rows.assign(hit_rows, hit_rows + nt);
+    nrows = 0;
+    for (uint32_t r : rows) nrows = std::max<uint64_t>(nrows, (uint64_t)r + 1);
+  }
+  DeviceGuard dg(dev);
+  Workspace& ws = workspace(dev, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  StagedKeys sk;
+  int rc = offsets ? stage_var(ws, keys, offsets, n, s, sk) : stage_fixed(ws, keys, key_len, n, s, sk);
+  if (rc) return rc;
+  const uint64_t hwords = (n + 63) / 64;
+  const uint64_t* dhits = hits;
+  if (hits && !is_device_ptr(hits)) {
+    HIP_TRY(ws.hits.reserve(nrows * hwords * 8, s));
+    HIP_TRY(hipMemcpyAsync(ws.hits.p, hits, nrows * hwords * 8, hipMemcpyHostToDevice, s));
+    dhits = (const uint64_t*)ws.hits.p;
+  }
+  HIP_TRY(ws.t_views.reserve(nt * sizeof(cb::TableView), s));
+  HIP_TRY(hipMemcpyAsync(ws.t_views.p, views.data(), nt * sizeof(cb::TableView), hipMemcpyHostToDevice, s));
+  const uint32_t* drows = nullptr;
+  if (!rows.empty()) {
+    HIP_TRY(ws.t_rows.reserve(nt * 4, s));
+    HIP_TRY(hipMemcpyAsync(ws.t_rows.p, rows.data(), nt * 4, hipMemcpyHostToDevice, s));
+    drows = (const uint32_t*)ws.t_rows.p;
+  }
+  int32_t* dwhich;
+  uint64_t* dvoff;
+  if ((rc = out_buf(ws.t_which, which, n, s, &dwhich))) return rc;
+  if ((rc = out_buf(ws.t_voff, val_off, n + 1, s, &dvoff))) return rc;
+  HIP_TRY(ws.t_line.reserve(n * 8, s));
+  HIP_TRY(ws.t_dlen.reserve(n * 8, s));
+  HIP_TRY(ws.t_scan.reserve(cb::get_tiles(n) * 8, s));
+  const cb::TableView* dviews = (const cb::TableView*)ws.t_views.p;
+  const uint64_t* vsrc = (const uint64_t*)ws.t_line.p;
+  const uint64_t* dlen = (const uint64_t*)ws.t_dlen.p;
+  uint64_t* tsum = (uint64_t*)ws.t_scan.p;
+  HIP_TRY(cb::launch_get_many(sk.keyk, dviews, nt, dhits, drows, hwords, sk.ks, n, dwhich,
+                              (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, tsum, s));
+  HIP_TRY(cb::launch_tile_scan(tsum, cb::get_tiles(n), dvoff + n, s));
+  if (!ws.htot) HIP_TRY(hipHostMalloc((void**)&ws.htot, 64, hipHostMallocDefault));
+  if (vals && is_device_ptr(vals)) {
+    // device values: offsets and values in one pass (the kernel skips the
+    // value writes when the total exceeds cap): one host round trip
+    HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, vals, cap, s));
+    HIP_TRY(hipMemcpyAsync(ws.htot, dvoff + n, 8, hipMemcpyDeviceToHost, s));
+  } else {
+    HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, nullptr, 0, s));  // offsets only
+    HIP_TRY(hipMemcpyAsync(ws.htot, dvoff + n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint64_t tot = *ws.htot;
+    if (vals && cap >= tot && tot) {
+      uint8_t* dvals;
+      if ((rc = out_buf(ws.t_vals, vals, tot, s, &dvals))) return rc;
+      HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, dvals, tot, s));
+      HIP_TRY(hipMemcpyAsync(vals, dvals, tot, hipMemcpyDeviceToHost, s));
+    }
+  }
+  if (dwhich != which) HIP_TRY(hipMemcpyAsync(which, dwhich, n * 4, hipMemcpyDeviceToHost, s));
+  if (dvoff != val_off) HIP_TRY(hipMemcpyAsync(val_off, dvoff, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  *total = *ws.htot;
+  return CB_OK;
+}
+
+// Line index of t->data[0..t->len) (count -> scan -> emit -> finish -> keys).
+// Temporaries come from the stream's workspace (taken here: callers must not
+// hold its lock); the index itself is one allocation: rec | pfx | fence.
+int index_table(cb_table* t, hipStream_t s) {
+  const uint64_t len = t->len;
+  if (!len) return CB_OK;
+  Workspace& ws = workspace(t->device, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  const uint64_t nb = cb::line_blocks(len);
+  HIP_TRY(ws.i_cnt.reserve(nb * 8, s));
+  HIP_TRY(ws.i_base.reserve((nb + 1) * 8, s));
+  HIP_TRY(ws.i_tmp.reserve(cb::scan_tmp_words(nb) * 8, s));
+  HIP_TRY(ws.i_err.reserve(8, s));
+  uint64_t* cnt = (uint64_t*)ws.i_cnt.p;
+  uint64_t* base = (uint64_t*)ws.i_base.p;
+  uint32_t* err = (uint32_t*)ws.i_err.p;
+  HIP_TRY(cb::launch_line_count(t->data, len, cnt, s));
+  HIP_TRY(cb::launch_scan_u64(cnt, base, nb, (uint64_t*)ws.i_tmp.p, s));
+  HIP_TRY(hipMemcpyAsync(&t->nlines, base + nb, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (!t->nlines) return CB_OK;
+  const uint64_t nl = t->nlines;
+  t->nfence = (nl + cb::kFenceStride - 1) / cb::kFenceStride;
+  const size_t bytes = nl * sizeof(cb::LineRec) + nl * 8 + t->nfence * 8;
+  if (pool_alloc(t->device, bytes, (void**)&t->rec, &t->rec_cap) != hipSuccess) {
+    t->rec = nullptr;
+    return fail(CB_ENOMEM, "device allocation failed for an SSTable index");
+  }
+  t->pfx = (uint64_t*)(t->rec + nl);
+  t->fence = t->pfx + nl;
+  HIP_TRY(ws.i_start.reserve(nl * 8, s));
+  HIP_TRY(ws.i_end.reserve(nl * 8, s));
+  uint64_t* start = (uint64_t*)ws.i_start.p;
+  uint64_t* end = (uint64_t*)ws.i_end.p;
+  HIP_TRY(hipMemsetAsync(end, 0xFF, nl * 8, s));
+  HIP_TRY(hipMemsetAsync(err, 0, 4, s));
+  const uint32_t one = 1;
+  HIP_TRY(hipMemcpyAsync(err + 1, &one, 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(cb::launch_line_emit(t->data, len, base, start, end, s));
+  HIP_TRY(cb::launch_line_finish(t->data, len, nl, start, end, t->rec, err, s));
+  // prefix + fence index, value validity and the well-formed check (sstable.hpp)
+  HIP_TRY(cb::launch_line_keys(t->data, nl, t->rec, t->pfx, t->fence, err + 1, s));
+  uint32_t e[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(e, err, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (e[0]) return fail(CB_EINVAL, "an SSTable line is 4 GiB or longer");
+  t->fast = e[1] != 0 && !g_table_exact;
+  return CB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---- SSTable data files and the batched read path ----
+
+int cb_table_destroy(cb_table* t) {
+  if (!t) return CB_OK;
+  {
+    DeviceGuard dg(t->device);
+    pool_release(t->device, t->data, t->data_cap);
+    pool_release(t->device, t->rec, t->rec_cap);  // rec heads the one index allocation
+  }
+  delete t;
+  return CB_OK;
+}
+
+int cb_table_create(const uint8_t* data, uint64_t len, int device, void* stream, cb_table** out) {
+  if (!out || (!data && len)) return fail(CB_EINVAL, "null argument");
+  *out = nullptr;
+  int rc = cb_init(device);
+  if (rc) return rc;
+  DeviceGuard dg(device);
+  hipStream_t s = (hipStream_t)stream;
+  std::unique_ptr<cb_table, int (*)(cb_table*)> t(new cb_table(), cb_table_destroy);
+  t->device = device;
+  t->len = len;
+  if (pool_alloc(device, len + 16, (void**)&t->data, &t->data_cap) != hipSuccess) {
+    t->data = nullptr;
+    return fail(CB_ENOMEM, "device allocation failed for an SSTable buffer");
+  }
+  HIP_TRY(hipMemsetAsync(t->data + len, 0, 16, s));
+  if (len) HIP_TRY(hipMemcpyAsync(t->data, data, len, hipMemcpyDefault, s));
+  if ((rc = index_table(t.get(), s))) return rc;
+  HIP_TRY(hipStreamSynchronize(s));
+  *out = t.release();
+  return CB_OK;
+}
+
+int cb_table_data(const cb_table* t, const uint8_t** data, uint64_t* len) {
+  if (!t) return fail(CB_EINVAL, "null table");
+  if (data) *data = t->data;
+  if (len) *len = t->len;
+  return CB_OK;
+}
+
+int cb_table_copy(const cb_table* t, uint64_t offset, uint64_t len, uint8_t* out) {
+  if (!t || (!out && len)) return fail(CB_EINVAL, "null argument");
+  if (offset > t->len || len > t->len - offset) return fail(CB_EINVAL, "range outside the file");
+  if (!len) return CB_OK;
+  DeviceGuard dg(t->device);
+  HIP_TRY(hipMemcpy(out, t->data + offset, len, hipMemcpyDefault));
+  return CB_OK;
+}
+
+int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_t* vals,
+                      const uint64_t* val_off, uint64_t n, uint64_t m_bits, int device, void* stream,
+                      cb_table** table_out, cb_filter** bloom_out, uint64_t* zone_min_idx,
+                      uint64_t* zone_max_idx) {
+  if (!table_out || !key_off || !val_off) return fail(CB_EINVAL, "null argument");
+  if (n >= 0xFFFFFFFFull) return fail(CB_EINVAL, "too many entries for one table");
+  *table_out = nullptr;
+  if (bloom_out) *bloom_out = nullptr;
+  if (zone_min_idx) *zone_min_idx = ~0ull;
+  if (zone_max_idx) *zone_max_idx = ~0ull;
+  int rc = cb_init(device);
+  if (rc) return rc;
+  if (bloom_out && n && m_bits == 0)  // BloomFilter::insert's `% 0` (src/bloom.rs:36)
+    return fail(CB_EZEROM, "attempt to calculate the remainder with a divisor of zero");
+  DeviceGuard dg(device);
+  hipStream_t s = (hipStream_t)stream;
+  std::unique_ptr<cb_table, int (*)(cb_table*)> t(new cb_table(), cb_table_destroy);
+  std::unique_ptr<cb_filter, int (*)(cb_filter*)> f(nullptr, cb_filter_destroy);
+  t->device = device;
+  const uint8_t *dk = nullptr, *dv = nullptr;
+  const uint64_t *dko = nullptr, *dvo = nullptr;
+  const cb::SortKey* order = nullptr;
+  uint64_t ktot = 0, vtot = 0;
+  Workspace& ws = workspace(device, s);
+  std::unique_lock<std::mutex> lk(ws.mu);
+  if (!ws.hres) {
+    HIP_TRY(hipHostMalloc((void**)&ws.hres, sizeof(cb::CreateResult), hipHostMallocDefault));
+    HIP_TRY(hipEventCreateWithFlags(&ws.ev, hipEventDisableTiming));
+  }
+  cb::CreateResult* hr = ws.hres;
+  // Offsets: host ones are validated and copied (their totals are known
+  // here); device ones are used in place, their totals read back together
+  // with the sortedness flag in ONE round trip below.
+  auto stage_off = [&](DevBuf& doff, const uint64_t* off, const uint64_t** op, uint64_t* tot,
+                       bool* on_dev) -> int {
+    *on_dev = is_device_ptr(off);
+    if (*on_dev) {
+      *op = off;
+      return CB_OK;
+    }
+    for (uint64_t i = 0; i < n; ++i)
+      if (off[i + 1] < off[i]) return fail(CB_EINVAL, "offsets must be non-decreasing");
+    *tot = off[n];
+    HIP_TRY(doff.reserve((n + 1) * 8, s));
+    HIP_TRY(hipMemcpyAsync(doff.p, off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    *op = (const uint64_t*)doff.p;
+    return CB_OK;
+  };
+  // Bytes: device bytes in place; host bytes copied (device offsets over
+  // host bytes need the total first: one extra round trip, a rare mix).
+  auto stage_bytes = [&](DevBuf& dbytes, const uint8_t* bytes, const uint64_t* off, bool off_dev,
+                         uint64_t* tot, const uint8_t** bp) -> int {
+    if (!bytes || is_device_ptr(bytes)) {
+      *bp = bytes;
+      return CB_OK;
+    }
+    if (off_dev) {
+      HIP_TRY(hipMemcpyAsync(tot, off + n, 8, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+    }
+    if (*tot) {
+      HIP_TRY(dbytes.reserve(*tot, s));
+      HIP_TRY(hipMemcpyAsync(dbytes.p, bytes, *tot, hipMemcpyHostToDevice, s));
+    }
+    *bp = (const uint8_t*)dbytes.p;
+    return CB_OK;
+  };
+  bool kdev = false, vdev = false;
+  if ((rc = stage_off(ws.offsets, key_off, &dko, &ktot, &kdev))) return rc;
+  if ((rc = stage_off(ws.f_vo, val_off, &dvo, &vtot, &vdev))) return rc;
+  if ((rc = stage_bytes(ws.keys, keys, key_off, kdev, &ktot, &dk))) return rc;
+  if ((rc = stage_bytes(ws.f_vb, vals, val_off, vdev, &vtot, &dv))) return rc;
+  if (!keys && n) {  // only a batch of empty keys may come without bytes
+    if (kdev) {
+      HIP_TRY(hipMemcpyAsync(&ktot, dko + n, 8, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+    }
+    if (ktot) return fail(CB_EINVAL, "null bytes");
+  }
+  HIP_TRY(ws.f_flag.reserve(sizeof(cb::CreateResult), s));
+  cb::CreateResult* dr = (cb::CreateResult*)ws.f_flag.p;
+  // Round trip 1: sortedness and the byte totals. Its wait is covered by the
+  // Bloom build, which needs neither (OR is order-free).
+  hr->flags[0] = 1;
+  hr->flags[1] = 0;
+  hr->flags[2] = 1;
+  hr->flags[3] = 0;
+  HIP_TRY(hipMemcpyAsync(dr->flags, hr->flags, 16, hipMemcpyHostToDevice, s));
+  HIP_TRY(ws.f_tsum.reserve(cb::format_tiles(n) * 8, s));
+  uint64_t* tsum = (uint64_t*)ws.f_tsum.p;
+  HIP_TRY(cb::launch_sorted_check(dk, dko, dvo, n, dr, tsum, s));
+  HIP_TRY(hipMemcpyAsync(hr, dr, offsetof(cb::CreateResult, len), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(ws.ev, s));
+  auto build_bloom = [&]() -> int {  // (keys are non-null or all empty here)
+    if (!bloom_out) return CB_OK;
+    cb_filter* fp = nullptr;
+    int r = cb_filter_create(m_bits, device, &fp);
+    if (r) return r;
+    f.reset(fp);
+    return n ? insert_locked(ws, fp, dk, dko, 0, n, s) : CB_OK;
+  };
+  if ((rc = build_bloom())) return rc;
+  HIP_TRY(hipEventSynchronize(ws.ev));
+  if (kdev) ktot = hr->ktot;
+  if (vdev) vtot = hr->vtot;
+  const bool sorted = hr->flags[0] != 0;
+  if ((ktot && !keys) || (vtot && !vals)) return fail(CB_EINVAL, "null bytes");
+  // the file's buffer is sized by the bound sum(k + 2 + 4 ceil(v / 3)) <=
+  // K + 2n + (4V + 8n) / 3, plus slack; its length comes back at the end
+  const uint64_t cap_bytes = ktot + 2 * n + (4 * vtot + 8 * n) / 3 + 1 + 16;
+  if (pool_alloc(device, cap_bytes, (void**)&t->data, &t->data_cap) != hipSuccess) {
+    t->data = nullptr;
+    return fail(CB_ENOMEM, "device allocation failed for an SSTable buffer");
+  }
+  if (!n) {
+    HIP_TRY(hipMemsetAsync(t->data, 0, 16, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (bloom_out) *bloom_out = f.release();
+    *table_out = t.release();
+    return CB_OK;
+  }
+  if (!sorted) {
+    // stable sort by key (memtable flushes arrive sorted and skip this)
+    HIP_TRY(ws.f_sk.reserve(n * sizeof(cb::SortKey), s));
+    HIP_TRY(ws.f_sk2.reserve(n * sizeof(cb::SortKey), s));
+    cb::SortKey* a0 = (cb::SortKey*)ws.f_sk.p;
+    cb::SortKey* a1 = (cb::SortKey*)ws.f_sk2.p;
+    // (rocPRIM's radix sort in three LSD passes over (len, w1, w0) when every
+    // key is <= 16 bytes was measured no faster at 1M entries: 573 vs 577 us)
+    HIP_TRY(cb::launch_sort_keys(dk, dko, n, a0, s));
+    size_t tmp_bytes = 0;
+    HIP_TRY(cb::entry_sort(nullptr, tmp_bytes, a0, a1, n, dk, dko, s));
+    HIP_TRY(ws.f_sort.reserve(tmp_bytes + 16, s));
+    HIP_TRY(cb::entry_sort(ws.f_sort.p, tmp_bytes, a0, a1, n, dk, dko, s));
+    order = a1;
+  }
+  if (order) HIP_TRY(cb::launch_line_sums(order, dko, dvo, n, tsum, s));
+  HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
+  // the line index straight from the entries (entry p is line p), no re-read of the file
+  t->nlines = n;
+  t->nfence = (n + cb::kFenceStride - 1) / cb::kFenceStride;
+  const size_t ibytes = n * sizeof(cb::LineRec) + n * 8 + t->nfence * 8;
+  if (pool_alloc(device, ibytes, (void**)&t->rec, &t->rec_cap) != hipSuccess) {
+    t->rec = nullptr;
+    return fail(CB_ENOMEM, "device allocation failed for an SSTable index");
+  }
+  t->pfx = (uint64_t*)(t->rec + n);
+  t->fence = t->pfx + n;
+  HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, tsum, n, t->data, t->rec, t->pfx, t->fence, dr,
+                            cap_bytes, s));
+  // Round trip 2: flags, file length, zone bounds
+  HIP_TRY(hipMemcpyAsync(hr, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  t->len = hr->len;
+  // zone map: ZoneMap::update over the sorted keys = first / last line
+  if (zone_min_idx) *zone_min_idx = hr->idx_min;
+  if (zone_max_idx) *zone_max_idx = hr->idx_max;
+  for (int w = 0; w < 2; ++w) {
+    const uint64_t kl = hr->zlen[w];
+    std::string& z = w ? t->zmax : t->zmin;
+    z.assign((const char*)hr->zkey[w], (size_t)std::min<uint64_t>(kl, cb::kZoneInline));
+    if (kl > cb::kZoneInline) {  // a long key: the rest in one more copy
+      const uint64_t i = w ? hr->idx_max : hr->idx_min;
+      uint64_t o = 0;
+      HIP_TRY(hipMemcpy(&o, dko + i, 8, hipMemcpyDeviceToHost));
+      z.resize(kl);
+      HIP_TRY(hipMemcpy(&z[cb::kZoneInline], dk + o + cb::kZoneInline, kl - cb::kZoneInline,
+                        hipMemcpyDeviceToHost));
+    }
+  }
+  t->has_zone = true;
+  if (hr->flags[1]) {
+    // a key holds '\n' or '\t': the file's lines are not the entries, so
+    // index it the way SsTable::get splits it (src/sstable.rs:142-146)
+    pool_release(device, t->rec, t->rec_cap);
+    t->rec = nullptr;
+    t->pfx = t->fence = nullptr;
+    t->nlines = t->nfence = 0;
+    lk.unlock();  // index_table takes the workspace itself
+    if ((rc = index_table(t.get(), s))) return rc;
+  } else {
+    t->fast = hr->flags[2] != 0 && !g_table_exact;
+  }
+  if (bloom_out) *bloom_out = f.release();
+  *table_out = t.release();
+  return CB_OK;
+}
+
+int cb_table_zone(const cb_table* t, int which, uint8_t* out, uint64_t cap, uint64_t* len) {
+  if (!t || !len || (which != 0 && which != 1)) return fail(CB_EINVAL, "bad argument");
+  if (!t->has_zone) return fail(CB_EINVAL, "table has no zone bounds (not made by cb_sstable_create, or empty)");
+  const std::string& z = which ? t->zmax : t->zmin;
+  *len = z.size();
+  if (out && cap) std::memcpy(out, z.data(), (size_t)std::min<uint64_t>(cap, z.size()));
+  return CB_OK;
+}
+
+int cb_table_info(const cb_table* t, uint64_t* nlines, uint64_t* bytes) {
+  if (!t) return fail(CB_EINVAL, "null table");
+  if (nlines) *nlines = t->nlines;
+  if (bytes) *bytes = t->len;
+  return CB_OK;
+}
+
+int cb_table_well_formed(const cb_table* t, int* out) {
+  if (!t || !out) return fail(CB_EINVAL, "null argument");
+  *out = t->fast ? 1 : 0;
+  return CB_OK;
+}
+
+int cb_table_force_exact(int on) {
+  g_table_exact = on != 0;
+  return CB_OK;
+}
+
+int cb_table_lines(const cb_table* t, uint64_t* start, uint32_t* key_len, uint32_t* line_len) {
+  if (!t) return fail(CB_EINVAL, "null table");
+  DeviceGuard dg(t->device);
+  if (!t->nlines) return CB_OK;
+  // strided copies out of the 32-byte records
+  const size_t pitch = sizeof(cb::LineRec);
+  const uint8_t* r = (const uint8_t*)t->rec;
+  if (start)
+    HIP_TRY(hipMemcpy2D(start, 8, r + offsetof(cb::LineRec, start), pitch, 8, t->nlines, hipMemcpyDefault));
+  if (key_len)
+    HIP_TRY(hipMemcpy2D(key_len, 4, r + offsetof(cb::LineRec, klen), pitch, 4, t->nlines, hipMemcpyDefault));
+  if (line_len)
+    HIP_TRY(hipMemcpy2D(line_len, 4, r + offsetof(cb::LineRec, llen), pitch, 4, t->nlines, hipMemcpyDefault));
+  return CB_OK;
+}
+
+int cb_table_search_fixed(const cb_table* t, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                          int64_t* line_out, void* stream) {
+  return table_search_impl(t, keys, nullptr, key_len, n, line_out, (hipStream_t)stream);
+}
+
+int cb_table_search_var(const cb_table* t, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                        int64_t* line_out, void* stream) {
+  if (!offsets) return fail(CB_EINVAL, "null offsets");
+  return table_search_impl(t, bytes, offsets, 0, n, line_out, (hipStream_t)stream);
+}
+
+int cb_get_many_fixed(const cb_table* const* tables, uint32_t nt, const uint64_t* hits,
+                      const uint32_t* hit_rows, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                      int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap,
+                      uint64_t* total, void* stream) {
+  return get_many_impl(tables, nt, hits, hit_rows, keys, nullptr, key_len, n, which, val_off, vals,
+                       cap, total, (hipStream_t)stream);
+}
+
+int cb_get_many_var(const cb_table* const* tables, uint32_t nt, const uint64_t* hits,
+                    const uint32_t* hit_rows, const uint8_t* bytes, const uint64_t* offsets,
+                    uint64_t n, int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap,
+                    uint64_t* total, void* stream) {
+  if (!offsets) return fail(CB_EINVAL, "null offsets");
+  return get_many_impl(tables, nt, hits, hit_rows, bytes, offsets, 0, n, which, val_off, vals, cap,
+                       total, (hipStream_t)stream);
+}
+
+}  // extern "C"
