@@ -286,8 +286,11 @@ __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp,
   }
   __syncthreads();
   CB_STAMP(4);
-  uint32_t* out = ent + (size_t)blockIdx.x * (2 * C);
-  for (uint32_t i = tid; i < total; i += NT) out[i] = stage[i];
+  uint32_t* out = ent + (size_t)blockIdx.x * (2 * C);  // 16-B aligned, as is stage
+  const uint32_t n4 = total / 4;
+  for (uint32_t i = tid; i < n4; i += NT)
+    reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(stage)[i];
+  for (uint32_t i = 4 * n4 + tid; i < total; i += NT) out[i] = stage[i];
   CB_STAMP(5);
 }
 
