@@ -366,21 +366,36 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
                                                   uint64_t* __restrict__ dlen,
                                                   uint64_t* __restrict__ tsum) {
   const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  // The gate for the first 64 tables, with every lane of the wave active: a
+  // wave's 64 keys share one hit word per table row, so lane i loads row i's
+  // word (one load instruction for the wave, not one per table) and every
+  // lane takes its bit of each row from lane i by a uniform shuffle.
+  const uint32_t gn0 = nt < 64 ? nt : 64;
+  uint64_t cand0 = gn0 == 64 ? ~0ull : ((1ull << gn0) - 1);
+  if (hits) {
+    const uint64_t wi = ((uint64_t)blockIdx.x * kNT + (threadIdx.x & ~63u)) >> 6;
+    uint64_t hw = 0;
+    if (lane < gn0 && wi < hwords) hw = hits[(uint64_t)(rows ? rows[lane] : lane) * hwords + wi];
+    cand0 = 0;
+    for (uint32_t i = 0; i < gn0; ++i) cand0 |= ((__shfl(hw, (int)i, 64) >> lane) & 1ull) << i;
+  }
   uint64_t d = 0;
   if (k < n) {
     const Query q = make_query<KEYK>(ks, k);
     int32_t w = -1;
     uint64_t src = 0;
     // Tables in groups of 64, newest first (tables.iter().rev()). Each lane
-    // first collects its candidate tables of the group as a bit mask (one
-    // broadcast load per table: a wave's 64 keys share a hit word), then every
-    // lane searches its OWN next candidate in the same iteration, so lanes
-    // whose keys live in different tables search concurrently instead of the
-    // wave stepping through the tables one by one.
+    // holds its candidate tables of the group as a bit mask, then every lane
+    // searches its OWN next candidate in the same iteration, so lanes whose
+    // keys live in different tables search concurrently instead of the wave
+    // stepping through the tables one by one.
     for (uint32_t t0 = 0; t0 < nt && w < 0; t0 += 64) {
       const uint32_t gn = nt - t0 < 64 ? nt - t0 : 64;
       uint64_t cand = gn == 64 ? ~0ull : ((1ull << gn) - 1);
-      if (hits) {
+      if (t0 == 0) {
+        cand = cand0;
+      } else if (hits) {  // tables past the first 64: one broadcast load per table
         cand = 0;
         for (uint32_t i = 0; i < gn; ++i) {
           const uint64_t row = rows ? rows[t0 + i] : t0 + i;
