@@ -217,3 +217,25 @@ def test_get_many_device_out_cap(gpu):
     assert (w[:-2] == 0).all() and (w[-2:] == -1).all()
     vo = voff.cpu().numpy()
     assert vo[-1] == total and vo[-2] == vo[-3] == total
+
+
+def test_get_many_value_lengths(gpu):
+    """Decoded values of every length 0..40 bytes at every alignment (the
+    one-wait path for <= 18-byte values and the 8-char loop above it), against
+    Python's base64 on the same lines (src/sstable.rs:147-153)."""
+    import base64
+
+    rng = np.random.default_rng(11)
+    n = 4000
+    keys = sorted({bytes(rng.integers(97, 123, rng.integers(1, 24), dtype=np.uint8)) for _ in range(n)})
+    vals = [bytes(rng.integers(0, 256, i % 41, dtype=np.uint8)) for i in range(len(keys))]
+    data = b"".join(k + b"\t" + base64.b64encode(v) + b"\n" for k, v in zip(keys, vals))
+    t = gpu.Table(data)
+    look = list(keys) + [b"zzzz-absent", b""]
+    d, o = var(look)
+    which, voff, got = gpu.get_many([t], gpu.KeyBatch(n=len(look), data=d, offsets=o))
+    for i, k in enumerate(look):
+        if i < len(keys):
+            assert which[i] == 0 and got[voff[i]:voff[i + 1]] == vals[i], k
+        else:
+            assert which[i] < 0 and voff[i] == voff[i + 1]
