@@ -160,12 +160,12 @@ def main():
     # before the results are reported
     x_ok = torch.ones(1, dtype=torch.int32, device=dev) if use_sparse else None
 
-    def gather(buf):
+    def gather(buf, s_h=sh):
         if use_sparse:
             gather_hits_sparse(hits_bufs[buf], nf_total, cap,
-                               lambda h, p: lsmt_amd.hits_compress(h, p, stream=sh),
+                               lambda h, p: lsmt_amd.hits_compress(h, p, stream=s_h),
                                lambda pk, w, ro, full, ok: lsmt_amd.hits_expand(pk, w, ro, full, ok=ok,
-                                                                                stream=sh),
+                                                                                stream=s_h),
                                out=hits_all_bufs[buf], ok=x_ok)
             xstats["sparse_steps"] += 1
         else:
@@ -179,14 +179,14 @@ def main():
         reused only after its gather has finished (gather_done)."""
         if not use_dist:
             return
-        if not args.overlap or use_sparse:
+        if not args.overlap:
             gather(buf)
             return
         ev = torch.cuda.Event()
         ev.record(stream)
         with torch.cuda.stream(comm):
             comm.wait_event(ev)
-            gather_hits(hits_bufs[buf], nf_total, out=hits_all_bufs[buf])
+            gather(buf, comm.cuda_stream)  # sparse: compress, all-gather, expand all on comm
             done = torch.cuda.Event()
             done.record(comm)
         gather_done[buf] = done

@@ -373,6 +373,8 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
   // lane takes its bit of each row from lane i by a uniform shuffle.
   const uint32_t gn0 = nt < 64 ? nt : 64;
   uint64_t cand0 = gn0 == 64 ? ~0ull : ((1ull << gn0) - 1);
+  // the key's loads go out with the gate's (independent of it)
+  const Query q = make_query<KEYK>(ks, k < n ? k : 0);
   if (hits) {
     const uint64_t wi = ((uint64_t)blockIdx.x * kNT + (threadIdx.x & ~63u)) >> 6;
     uint64_t hw = 0;
@@ -382,7 +384,6 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
   }
   uint64_t d = 0;
   if (k < n) {
-    const Query q = make_query<KEYK>(ks, k);
     int32_t w = -1;
     uint64_t src = 0;
     // Tables in groups of 64, newest first (tables.iter().rev()). Each lane
@@ -454,6 +455,40 @@ __device__ __forceinline__ void b64_decode_into(const uint8_t* src, uint64_t dl,
   }
 }
 
+// Values of up to 18 bytes (24 chars): the dwords their chars span, loaded
+// unconditionally (indices clamped to the last one, so every load stays inside
+// the span) so the caller can issue them before other work.
+struct SmallB64 {
+  uint32_t x[7];
+  uint32_t sh;
+};
+constexpr uint64_t kSmallB64Bytes = 18;
+
+__device__ __forceinline__ void b64_small_load(const uint8_t* src, uint64_t dl, SmallB64& v) {
+  const uint64_t len = (dl + 2) / 3 * 4;
+  const uintptr_t a = (uintptr_t)src;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  v.sh = (uint32_t)(a & 3);
+  const uint32_t last = (v.sh + (uint32_t)len + 3) / 4 - 1;
+#pragma unroll
+  for (uint32_t i = 0; i < 7; ++i) v.x[i] = w[i < last ? i : last];
+}
+
+// dl <= 18 bytes decoded from the loaded dwords (realigned: y = one quad).
+template <class Put>
+__device__ __forceinline__ void b64_small_decode(const SmallB64& v, uint64_t dl, Put put) {
+  uint64_t j = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 6; ++i) {
+    const uint32_t y = __builtin_amdgcn_alignbyte(v.x[i + 1], v.x[i], v.sh);
+    const uint8_t c[4] = {(uint8_t)y, (uint8_t)(y >> 8), (uint8_t)(y >> 16), (uint8_t)(y >> 24)};
+    const uint32_t q = b64_quad(c);
+    if (j < dl) put(j++, (uint8_t)(q >> 16));
+    if (j < dl) put(j++, (uint8_t)(q >> 8));
+    if (j < dl) put(j++, (uint8_t)q);
+  }
+}
+
 constexpr uint32_t kDecodeLds = 16384;  // staged output bytes per block
 
 // Value offsets: the block's base is the scanned value-byte tile sum (tsum:
@@ -468,22 +503,32 @@ __global__ __launch_bounds__(kNT) void k_b64_decode(const uint64_t* __restrict__
                                                     const uint64_t* __restrict__ tsum, uint64_t n,
                                                     uint64_t* __restrict__ voff,
                                                     uint8_t* __restrict__ out, uint64_t cap) {
-  __shared__ uint8_t stage[kDecodeLds];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kDecodeLds + 4];  // +4: the last dword pair
   const uint64_t b0 = (uint64_t)blockIdx.x * kNT;
   const uint64_t k = b0 + threadIdx.x;
+  // Every independent load first (lengths, sources, the block's base, the
+  // total), then small values' chars, so one memory wait covers each round
+  // and the block scan runs while the chars arrive.
   const uint64_t dl = k < n ? dlen[k] : 0;
+  const uint8_t* src = (const uint8_t*)(uintptr_t)(k < n ? vsrc[k] : 0);
+  const uint64_t base = tsum[blockIdx.x];  // k_tile_scan: the tiles before
+  const uint64_t vn = voff[n];             // k_tile_scan's total
+  const bool write = out && vn <= cap;     // uniform
+  SmallB64 sv;
+  const bool small = dl && dl <= kSmallB64Bytes;
+  if (write && small) b64_small_load(src, dl, sv);
   uint64_t total;
   const uint64_t pre = block_scan<kNT>(dl, &total);
-  const uint64_t base = tsum[blockIdx.x];  // k_tile_scan: the tiles before
   const uint64_t o = base + pre;
   if (k < n) voff[k] = o;
-  if (!out || voff[n] > cap) return;  // uniform (voff[n]: k_tile_scan's total)
-  const uint8_t* src = (const uint8_t*)(uintptr_t)(k < n ? vsrc[k] : 0);
+  if (!write) return;
   if (total > kDecodeLds) {  // uniform: large values, direct byte stores
-    if (dl) b64_decode_into(src, dl, [&](uint64_t j, uint8_t v) { out[o + j] = v; });
+    if (small) b64_small_decode(sv, dl, [&](uint64_t j, uint8_t v) { out[o + j] = v; });
+    else if (dl) b64_decode_into(src, dl, [&](uint64_t j, uint8_t v) { out[o + j] = v; });
     return;
   }
-  if (dl) b64_decode_into(src, dl, [&](uint64_t j, uint8_t v) { stage[o - base + j] = v; });
+  if (small) b64_small_decode(sv, dl, [&](uint64_t j, uint8_t v) { stage[o - base + j] = v; });
+  else if (dl) b64_decode_into(src, dl, [&](uint64_t j, uint8_t v) { stage[o - base + j] = v; });
   __syncthreads();
   // out[base .. base+total): bytes before the first 4-aligned address, then
   // aligned dwords, then the tail
@@ -494,9 +539,9 @@ __global__ __launch_bounds__(kNT) void k_b64_decode(const uint64_t* __restrict__
   const uint64_t body = (total - head) / 4;
   uint32_t* gw = reinterpret_cast<uint32_t*>(g + head);
   for (uint64_t i = threadIdx.x; i < body; i += kNT) {
-    const uint64_t p = head + 4 * i;
-    gw[i] = (uint32_t)stage[p] | (uint32_t)stage[p + 1] << 8 | (uint32_t)stage[p + 2] << 16 |
-            (uint32_t)stage[p + 3] << 24;
+    const uint32_t p = (uint32_t)(head + 4 * i);  // two aligned LDS dwords, realigned
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(stage) + (p >> 2);
+    gw[i] = __builtin_amdgcn_alignbyte(sw[1], sw[0], p & 3);
   }
   const uint64_t tail0 = head + 4 * body;
   if (tail0 + threadIdx.x < total) g[tail0 + threadIdx.x] = stage[tail0 + threadIdx.x];
