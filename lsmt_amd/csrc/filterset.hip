@@ -191,7 +191,16 @@ __global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __re
   typedef typename std::conditional<W == 32, uint32_t, uint64_t>::type word_t;
   typedef const __attribute__((address_space(1))) word_t* gptr;
   __shared__ uint64_t hb[64][kSetWords];
+  __shared__ BoundPrefix zp[2 * W];  // gated 16-byte keys: the bounds' prefixes, staged
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  if constexpr (KEYK == KEY_FIXED16) {
+    if (zv.gated) {  // uniform; issued alongside the key loads below
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(zv.pre);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(zp);
+      for (uint32_t i = threadIdx.x; i < 2 * W * sizeof(BoundPrefix) / 4; i += kSetProbeThreads)
+        dst[i] = src[i];
+    }
+  }
   const uint64_t wbase = (uint64_t)blockIdx.x * kSetWords;
   const gptr sp = (gptr)set;
   const uint64_t k = (wbase + wave) * 64 + lane;
@@ -223,17 +232,18 @@ __global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __re
     vb = va ? sp[pb] : (word_t)0;
   word_t mask = va & vb;
   if (zv.gated) {  // uniform: only gated launches pay for the zone check
+    if constexpr (KEYK == KEY_FIXED16) __syncthreads();  // zp staged
     word_t c = mask & (word_t)zv.gated;
     if constexpr (KEYK == KEY_FIXED16) {
       // 16-byte keys: the key (still in registers from the hash) compared as
-      // 4 big-endian words against the bounds' host-computed prefixes (two
-      // 32-B loads per bound from a 4-KB L2-resident table).
+      // 4 big-endian words against the bounds' host-computed prefixes,
+      // staged in LDS at block start (2 KB for 32 slots).
       if (c) {
         const uint32_t kw[4] = {be32(kv.x), be32(kv.y), be32(kv.z), be32(kv.w)};
         while (c) {
           const uint32_t s = (uint32_t)__builtin_ctzll((uint64_t)c);
           c &= c - 1;
-          if (cmp16(kw, zv.pre[2 * s]) < 0 || cmp16(kw, zv.pre[2 * s + 1]) > 0)
+          if (cmp16(kw, zp[2 * s]) < 0 || cmp16(kw, zp[2 * s + 1]) > 0)
             mask &= ~((word_t)1 << s);
         }
       }

@@ -91,7 +91,7 @@ __device__ __forceinline__ uint32_t be32(uint32_t x) { return __builtin_bswap32(
 
 // Rust str order of a 16-byte key (big-endian words kw) against a bound.
 __device__ __forceinline__ int cmp16(const uint32_t kw[4], const BoundPrefix& b) {
-  // b is read field by field from global memory (L1/L2-resident table)
+  // b is read field by field (LDS-staged in the gated set probe)
   const uint32_t n = b.len < 16 ? b.len : 16;
 #pragma unroll
   for (uint32_t i = 0; i < 4; ++i) {
