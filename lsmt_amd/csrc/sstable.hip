@@ -382,6 +382,17 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
     cand0 = 0;
     for (uint32_t i = 0; i < gn0; ++i) cand0 |= ((__shfl(hw, (int)i, 64) >> lane) & 1ull) << i;
   }
+  // the first 64 tables' views, staged once per block: each lane's search
+  // reads its table's view from LDS instead of a divergent global gather
+  __shared__ TableView stv[64];
+  {
+    static_assert(sizeof(TableView) % 4 == 0, "dword copy");
+    const uint32_t nst = nt < 64 ? nt : 64;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(tv);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(stv);
+    for (uint32_t i = threadIdx.x; i < nst * (uint32_t)(sizeof(TableView) / 4); i += kNT) dst[i] = src[i];
+  }
+  __syncthreads();
   uint64_t d = 0;
   if (k < n) {
     int32_t w = -1;
@@ -406,7 +417,7 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
       while (cand) {
         const uint32_t t = t0 + (uint32_t)__builtin_ctzll(cand);
         cand &= cand - 1;
-        const TableView v = tv[t];
+        const TableView v = t < 64 ? stv[t] : tv[t];
         LineRec r;
         if (search(v, q, r) < 0) continue;  // Ok(None)
         if (r.vdl == kBadValue) continue;   // Err(..) is skipped by `if let Ok(Some(v))`
