@@ -234,13 +234,25 @@ __global__ __launch_bounds__(kNT) void k_line_keys(const uint8_t* __restrict__ d
 // then reads its block's base in one load; see launch_tile_scan.
 __global__ __launch_bounds__(1024) void k_tile_scan(uint64_t* __restrict__ tsum, uint64_t nt,
                                                     uint64_t* __restrict__ total_out) {
+  // 4 consecutive values per thread: 4096 tiles (1M keys at 256 per tile) in
+  // one round of loads, one block scan and one round of stores
+  constexpr uint64_t kPer = 4, kChunk = 1024 * kPer;
   uint64_t carry = 0;
-  for (uint64_t c0 = 0; c0 < nt; c0 += 1024) {
-    const uint64_t i = c0 + threadIdx.x;
-    const uint64_t v = i < nt ? tsum[i] : 0;
+  for (uint64_t c0 = 0; c0 < nt; c0 += kChunk) {
+    const uint64_t i0 = c0 + threadIdx.x * kPer;
+    uint64_t v[kPer], sum = 0;
+#pragma unroll
+    for (uint64_t j = 0; j < kPer; ++j) {
+      v[j] = i0 + j < nt ? tsum[i0 + j] : 0;
+      sum += v[j];
+    }
     uint64_t total;
-    const uint64_t p = block_scan<1024>(v, &total);
-    if (i < nt) tsum[i] = carry + p;
+    uint64_t p = carry + block_scan<1024>(sum, &total);
+#pragma unroll
+    for (uint64_t j = 0; j < kPer; ++j) {
+      if (i0 + j < nt) tsum[i0 + j] = p;
+      p += v[j];
+    }
     carry += total;
   }
   if (threadIdx.x == 0) *total_out = carry;
