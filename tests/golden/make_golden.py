@@ -292,6 +292,10 @@ def main() -> None:
     # 10. SsTable::create's data file (src/sstable.rs:56-72)
     g["create"] = create_fixtures()
 
+    # 11-12. C4 (64 concurrent builds) and C5 (10M keys x 256 filters, per-rank slices)
+    g["c4"] = c4_fixture()
+    g["c5"] = c5_fixture()
+
     with open(os.path.join(HERE, "golden.json"), "w") as fh:
         json.dump(g, fh, indent=1, sort_keys=True)
     print("wrote", os.path.join(HERE, "golden.json"))
@@ -634,5 +638,60 @@ def _varint(v: int) -> bytes:
     return bytes(out)
 
 
+# ---- C4 / C5 (BASELINE configs 4 and 5) --------------------------
+
+def c4_fixture() -> dict:
+    """C4: 64 filters of m = 2^25, filter f built from key(200 + f, i < 2^18):
+    the SHA-256 and popcount of each byte-per-bit array."""
+    nf, m, kpf = 64, 1 << 25, 1 << 18
+    out = {"nf": nf, "m": m, "keys_per_filter": kpf, "seed_base": 200, "bools_sha256": [], "packed_sha256": [],
+           "popcount": []}
+    for f in range(nf):
+        bits = np_build(np_keys(200 + f, np.arange(kpf, dtype=np.uint64)), m)
+        out["bools_sha256"].append(sha(bits))
+        out["packed_sha256"].append(sha(np.packbits(bits, bitorder="little")))
+        out["popcount"].append(int(bits.sum()))
+    return out
+
+
+def c5_fixture() -> dict:
+    """C5: 256 filters of m = 2^26 ("L0-L4"), filter f from key(1000 + f, i < 2^19);
+    10M lookups (even i: key(1000 + j mod 256, (j div 256) mod 2^19), j = i/2;
+    odd i: key(9999, i)). The hit map [256][156250] is recorded per 32-filter
+    rank slice (rank r of 8 holds filters [32r, 32r+32)), as SHA-256 of the
+    little-endian uint64 rows, plus per-filter hit counts."""
+    nf, m, kpf, nl, per = 256, 1 << 26, 1 << 19, 10_000_000, 32
+    lk = lookups(nl, nf, kpf, 1000, 9999)
+    h1, h2 = np_raw_hashes(lk)
+    a = (h1 % np.uint64(m)).astype(np.int64)
+    b = (h2 % np.uint64(m)).astype(np.int64)
+    del h1, h2
+    slices, counts = [], []
+    rows = []
+    for f in range(nf):
+        bits = np_build(np_keys(1000 + f, np.arange(kpf, dtype=np.uint64)), m)
+        hit = (bits[a] & bits[b]).astype(bool)
+        counts.append(int(hit.sum()))
+        rows.append(_pack64(hit).astype("<u8"))
+        if len(rows) == per:
+            slices.append(sha(np.stack(rows)))
+            rows = []
+    return {"nf": nf, "m": m, "keys_per_filter": kpf, "n_lookups": nl, "seed_base": 1000, "absent_seed": 9999,
+            "lookups_sha256": sha(lk), "filters_per_rank": per, "rank_slice_hits_sha256": slices,
+            "hits_per_filter": counts, "hits_popcount": int(sum(counts))}
+
+
 if __name__ == "__main__":
-    main()
+    import sys
+    if len(sys.argv) > 1 and sys.argv[1] == "--only":
+        # regenerate only the named large-config sections into the existing file
+        path = os.path.join(HERE, "golden.json")
+        with open(path) as fh:
+            g = json.load(fh)
+        for name in sys.argv[2:]:
+            g[name] = {"c4": c4_fixture, "c5": c5_fixture}[name]()
+            print("regenerated", name)
+        with open(path, "w") as fh:
+            json.dump(g, fh, indent=1, sort_keys=True)
+    else:
+        main()
