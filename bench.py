@@ -97,7 +97,7 @@ def main():
 
     import lsmt_amd
     from lsmt_amd import _lib, workload
-    from lsmt_amd.shard import gather_hits, gather_hits_sparse, shard_range, sparse_cap
+    from lsmt_amd.shard import Comm, shard_range, sparse_cap
 
     L = _lib.load()
     lsmt_amd.set_path(args.path)
@@ -147,29 +147,37 @@ def main():
     torch.cuda.synchronize(dev)
     set_build_ms = (time.perf_counter() - t0) * 1e3
 
-    # Sparse exchange (shard.gather_hits_sparse): ship set-bit positions
-    # instead of dense rows. Default from 4 ranks up, where the dense gather's
-    # (N-1) x 4 MiB per rank outweighs compress + expand (~28 us measured on
-    # one GPU, tools/xchg_parts.py); CB_SPARSE_EXCHANGE=1/0 forces it on/off.
+    # Sparse exchange (cb_hits_allgather, CB_XCHG_SPARSE): ship set-bit
+    # positions instead of dense rows. Default whenever a pack is under half
+    # the dense rows (every N >= 2 at C3: 1.5 MB vs 4 MiB per rank at N = 2,
+    # 0.5 MB vs 4 MiB at N = 8), since xGMI is point-to-point and the bytes a
+    # rank receives bound the all-gather, while compress + expand cost ~12 us
+    # on the device (profiles/xchg_*_r02); CB_SPARSE_EXCHANGE=1/0 forces it.
+    from lsmt_amd.shard import pack_words
     sparse_env = os.environ.get("CB_SPARSE_EXCHANGE")
-    use_sparse = use_dist and (sparse_env == "1" or (sparse_env != "0" and world >= 4))
     cap = sparse_cap(n, nf_total, world)
+    pack_bytes = 4 * pack_words(F * words, cap)
+    use_sparse = use_dist and (sparse_env == "1" or (sparse_env != "0" and world >= 2 and
+                                                     2 * pack_bytes < 8 * F * words))
     xstats = {"sparse_steps": 0}
     # asynchronous overflow report (no host round trip per step): cleared by
     # k_hits_expand if any rank's set bits ever exceed cap; checked below
     # before the results are reported
     x_ok = torch.ones(1, dtype=torch.int32, device=dev) if use_sparse else None
 
+    # The exchange runs through the C ABI (cb_hits_allgather over the
+    # library's own RCCL communicator, lsmt_amd/csrc/comm.cpp): the same call
+    # a Rust Database::get would make. torch.distributed only hands out the
+    # communicator id and times the run.
+    xcomm = Comm.from_process_group(local) if use_dist else None
+
     def gather(buf, s_h=sh):
         if use_sparse:
-            gather_hits_sparse(hits_bufs[buf], nf_total, cap,
-                               lambda h, p: lsmt_amd.hits_compress(h, p, stream=s_h),
-                               lambda pk, w, ro, full, ok: lsmt_amd.hits_expand(pk, w, ro, full, ok=ok,
-                                                                                stream=s_h),
-                               out=hits_all_bufs[buf], ok=x_ok)
+            xcomm.allgather(hits_bufs[buf], nf_total, hits_all_bufs[buf], sparse=True, cap=cap, ok=x_ok,
+                            stream=s_h)
             xstats["sparse_steps"] += 1
         else:
-            gather_hits(hits_bufs[buf], nf_total, out=hits_all_bufs[buf])
+            xcomm.allgather(hits_bufs[buf], nf_total, hits_all_bufs[buf], stream=s_h)
 
     def exchange(buf):
         """The real exchange step: all-gather this step's hit rows from every
@@ -208,17 +216,23 @@ def main():
         fset.probe(keys_batch, out=hits_bufs[buf], stream=sh)
         exchange(buf)
 
+    region = {}  # HIP events on the kernels' stream around the last timed region
+
     def timed(fn, k):
         if use_dist:
             dist.barrier()
         torch.cuda.synchronize(dev)  # all streams: every exchange of the K steps is inside
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        e0.record(stream)
         for _ in range(k):
             fn()
+        e1.record(stream)
         torch.cuda.synchronize(dev)
         if use_dist:
             dist.barrier()
         el = time.perf_counter() - t0
+        region["ms"], region["k"] = e0.elapsed_time(e1), k
         if use_dist:
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -232,7 +246,8 @@ def main():
             fn()
         el_leg = timed(fn, args.steps)
         legs[name] = {"el": el_leg, "value": probes_per_step / (el_leg / args.steps),
-                      "ms_per_step": el_leg / args.steps * 1e3, "fn": fn}
+                      "ms_per_step": el_leg / args.steps * 1e3, "fn": fn,
+                      "region_us_per_step": region["ms"] * 1e3 / region["k"]}
     best = max(legs, key=lambda k: legs[k]["value"])
     el = legs[best]["el"]
     step = legs[best]["fn"]
@@ -347,13 +362,24 @@ def main():
         alg_def = f"64 B x {sectors} distinct sectors + 16n + F*n/8 (SURVEY.md §8d alternative layout)"
     roof = None
     if dominant:
-        dur_s = kprof[dominant]["avg_us"] * 1e-6
+        # Kernel duration for the roofline: HIP events recorded on the kernels'
+        # stream around the K timed steps, divided by K. Without an exchange
+        # the FilterSet step is exactly one k_set_probe launch, so this is the
+        # kernel's back-to-back average and can never exceed the step time
+        # (per-launch cb_profile events add their own gaps; kept as kernels_us).
+        one_kernel = best == "filterset" and not use_dist
+        kus = legs[best]["region_us_per_step"] if one_kernel else \
+            min(kprof[dominant]["avg_us"], legs[best]["ms_per_step"] * 1e3)
+        kus_src = ("HIP events on the probe stream around the timed region / K (one launch per step)"
+                   if one_kernel else "cb_profile per-launch HIP events, capped at the step time")
+        dur_s = kus * 1e-6
         ach = alg_bytes / dur_s / 1e9
         # PMC bytes are recorded for the default C3 shape only (profiles/pmc_*.json)
         c3_default = (args.workload == "c3" and n == 1 << 20 and F == 32 and m == 1 << 26 and kpf == 1 << 19)
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(dominant) if c3_default else None,
-                "kernel": dominant, "kernel_avg_us": round(kprof[dominant]["avg_us"], 2),
+                "kernel": dominant, "kernel_avg_us": round(kus, 2), "kernel_avg_source": kus_src,
+                "kernel_avg_us_per_launch_events": round(kprof[dominant]["avg_us"], 2),
                 "algorithmic_bytes": int(alg_bytes), "algorithmic_def": alg_def,
                 "step_effective_GBps": round(alg_bytes / (el / args.steps) / 1e9, 1)}
         if best == "filterset":
@@ -590,22 +616,39 @@ def main():
                "alt_per_filter_tiled": {"probes_per_s": round(n * F / t_tiled, 1),
                                         "ms_per_step": round(t_tiled * 1e3, 3)}}
 
-    if args.check and rank == 0:
+    if args.check:
+        # Every rank checks its own rows and, in the exchanged map, the rows
+        # of the next rank, so each rank's slice is verified as received by
+        # another rank; the verdicts are combined over all ranks.
         from oracle import oracle
-        refs = []
-        for f in range(f_lo, f_lo + F):
-            o = oracle.OracleFilter(m)
-            o.insert_fixed(workload.key_range(seed_base + f, kpf))
-            refs.append(o)
-        expect = oracle.probe_fixed(refs, look_np, threads=8)
+
+        def oracle_rows(lo, hi):
+            refs = []
+            for f in range(lo, hi):
+                o = oracle.OracleFilter(m)
+                o.insert_fixed(workload.key_range(seed_base + f, kpf))
+                refs.append(o)
+            return oracle.probe_fixed(refs, look_np, threads=8)
+
         step()  # the headline leg again (the zone leg ran after it)
         torch.cuda.synchronize(dev)
+        expect = oracle_rows(f_lo, f_lo + F)
         got = hits_bufs[(step_no[0] - 1) % 2].cpu().numpy().view(np.uint64)
-        assert np.array_equal(got, expect), "bench hits differ from the oracle"
-        if use_dist:  # the exchanged map: this rank's rows inside the global one
+        good = bool(np.array_equal(got, expect))
+        if use_dist:
             full = hits_all_bufs[(step_no[0] - 1) % 2].cpu().numpy().view(np.uint64)
-            assert np.array_equal(full[f_lo:f_lo + F], expect), "exchanged hits differ from the oracle"
-        log("[check] hits bit-exact vs oracle" + (" (local rows and the exchanged map)" if use_dist else ""))
+            good &= bool(np.array_equal(full[f_lo:f_lo + F], expect))
+            if world > 1:
+                nlo, nhi = shard_range(nf_total, world, (rank + 1) % world)
+                good &= bool(np.array_equal(full[nlo:nhi], oracle_rows(nlo, nhi)))
+            flag = torch.tensor([1 if good else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            good = bool(flag.item())
+        assert good, "bench hits differ from the oracle"
+        if rank == 0:
+            log("[check] hits bit-exact vs oracle" +
+                (" (local rows on every rank, and every rank's rows in another rank's exchanged map)"
+                 if use_dist else ""))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.workload == "c3":
@@ -616,15 +659,21 @@ def main():
     if use_sparse:  # every step's packs held all set bits: every exchanged map was complete
         x_fit = bool(int(x_ok.item()))
         if not x_fit:
-            log(f"[rank {rank}] WARNING: a sparse exchange overflowed cap={cap}; its map was incomplete")
+            log(f"[rank {rank}] ERROR: a sparse exchange overflowed cap={cap}; its map was incomplete, "
+                "so the timed steps did not all exchange the full map: the line is marked invalid")
 
+    # the BASELINE config name only when the shape is exactly that config's
+    c3_shape = (n == 1 << 20 and F == 32 and m == 1 << 26 and kpf == 1 << 19)
+    c5_shape = (n == 10_000_000 and F == 32 and m == 1 << 26 and kpf == 1 << 19 and seed_base == 1000)
+    wl_label = ("C3" if args.workload == "c3" and c3_shape else
+                "C5 rank-slice" if args.workload == "c5" and c5_shape else "custom")
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "probes/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 hex keys, SURVEY.md §8d)",
-            "config": {"workload": f"{args.workload.upper()} probe: {n} 16-B keys x {F} filters/GPU x {m // 8 // 2**20} MiB "
+            "config": {"workload": f"{wl_label} probe: {n} 16-B keys x {F} filters/GPU x {m // 8 // 2**20} MiB "
                                    f"(m=2^{m.bit_length() - 1}), filters built from {kpf} keys each",
                        "n_keys": n, "filters_per_gpu": F, "filters_total": nf_total, "m_bits": m,
                        "keys_per_filter": kpf,
@@ -644,10 +693,15 @@ def main():
                           "bytes": m * (4 if F <= 32 else 8)},
             "cold": cold, "rotating_batches": rot, "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e, "zone_gate": zone, "read_path": read, "flush": flush,
         }
+        if x_fit is False:
+            line["valid"] = False
         print(json.dumps(line), file=result, flush=True)
     if use_dist:
         dist.barrier()
+        xcomm.close()
         dist.destroy_process_group()
+    if x_fit is False:
+        sys.exit(3)
 
 
 def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result):
@@ -790,14 +844,16 @@ def c4_cpu_baseline(nf, kpf, m):
     for k in keys:
         build(k)
     t1 = time.perf_counter() - t0
-    threads = min(16, os.cpu_count() or 1)
+    cpus = host_cpus()
+    threads = cpus["usable"]
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
         list(ex.map(build, keys))
     tn = time.perf_counter() - t0
     return {"value": round(nf * kpf / t1, 1), "unit": "keys/s", "cores": 1, "kind": "port",
             "sample": f"all {nf} C4 builds ({kpf} keys -> m=2^{m.bit_length() - 1} bytes each) on 1 thread, {t1:.2f}s",
-            "all_cores": {"value": round(nf * kpf / tn, 1), "threads": threads, "seconds": round(tn, 3)}}
+            "all_cores": {"value": round(nf * kpf / tn, 1), "threads": threads, "seconds": round(tn, 3),
+                          "note": cpus["note"]}}
 
 
 def cpu_baseline(look_np, F, m, kpf, build_keys, build_m):
@@ -817,19 +873,24 @@ def cpu_baseline(look_np, F, m, kpf, build_keys, build_m):
     for _ in range(reps):
         oracle.probe_fixed(refs, look_np, threads=1)
     t1 = (time.perf_counter() - t0) / reps
-    cores = min(16, os.cpu_count() or 1)
+    cpus = host_cpus()
+    cores = cpus["usable"]
     t0 = time.perf_counter()
     oracle.probe_fixed(refs, look_np, threads=cores)
     tn = time.perf_counter() - t0
     del refs
+    # C2 build on one thread: repeated until at least 1 s of build time
+    # (one rep is ~25 ms), each rep into a fresh zeroed filter
     bk = workload.c2_build_keys(build_keys)
-    tb = 0.0
-    for _ in range(reps):
+    tb_sum, breps = 0.0, 0
+    while tb_sum < 1.0 or breps < 3:
         o = oracle.OracleFilter(build_m)
         t0 = time.perf_counter()
         o.insert_fixed(bk)
-        tb += (time.perf_counter() - t0) / reps
+        tb_sum += time.perf_counter() - t0
+        breps += 1
         del o
+    tb = tb_sum / breps
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as fh:
@@ -842,11 +903,53 @@ def cpu_baseline(look_np, F, m, kpf, build_keys, build_m):
     return {"value": round(n * F / t1, 1), "unit": "probes/s", "cores": 1, "kind": "port",
             "sample": f"full C3 probe: {n} keys x {F} filters (m=2^{m.bit_length() - 1}, byte-per-bit) on 1 thread, "
                       f"{reps} reps of {t1:.2f}s",
-            "all_cores": {"value": round(n * F / tn, 1), "threads": cores, "seconds": round(tn, 3)},
+            "all_cores": {"value": round(n * F / tn, 1), "threads": cores, "seconds": round(tn, 3),
+                          "note": cpus["note"]},
             "build": {"value": round(build_keys / tb, 1), "unit": "keys/s", "cores": 1,
                       "sample": f"C2 build {build_keys} keys into m=2^{build_m.bit_length() - 1} bytes, "
-                                f"{reps} reps of {tb:.3f}s"},
-            "cpu_model": cpu_model, "nproc": os.cpu_count()}
+                                f"{breps} reps of {tb:.3f}s ({tb_sum:.2f}s in all)"},
+            "cpu_model": cpu_model, "nproc": os.cpu_count(), "cpus": cpus}
+
+
+def host_cpus():
+    """CPUs this process can actually run on: os.cpu_count() (the machine),
+    the affinity mask, and the cgroup CPU quota (cpu.max). The all-cores
+    baseline uses min(affinity, quota) threads: on a shared GPU box nproc
+    counts the whole host while the job is limited to its share."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as fh:
+                q, p = fh.read().split()[:2]
+                if q != "max":
+                    quota = max(1, int(int(q) / int(p)))
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+                q = int(fh.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+                p = int(fh.read())
+            if q > 0:
+                quota = max(1, q // p)
+        except (OSError, ValueError):
+            pass
+    usable = min(aff, quota) if quota else aff
+    # the GPU box declares the job's CPU share in OMP_NUM_THREADS (16 per GPU)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    share = int(omp) if omp.isdigit() and int(omp) > 0 else None
+    if share:
+        usable = min(usable, share)
+    note = (f"threads = CPUs this job may use: nproc {nproc} (whole host), affinity {aff}, cgroup quota "
+            f"{quota if quota else 'none'}, OMP_NUM_THREADS {share if share else 'unset'}")
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "omp_share": share, "usable": usable,
+            "note": note}
 
 
 if __name__ == "__main__":

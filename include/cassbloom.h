@@ -297,23 +297,67 @@ int cb_get_many_var(const cb_table* const* tables, uint32_t nt, const uint64_t* 
  * ranks all-gather them so every rank has the [total_rows][words] map that
  * Database::get's fan-out reads (src/lib.rs:129-134). At BASELINE densities
  * the rows are sparse, so a rank can ship the positions of its set bits:
- *   cb_hits_compress: pack = uint32[2 + cap] = {count, 0, positions...};
- *     position = row * words * 64 + bit, ascending; count may exceed cap (then
- *     only the first cap positions are stored: all ranks must fall back to the
- *     dense exchange).
- *     Requires rows * words * 64 <= 2^32. Device pointers, async on stream.
+ *   cb_hits_pack_words: size in uint32 of a pack for rows x words of hits and
+ *     cap positions: 2 + cap + 2 * ceil(rows * words / 2048). Packs that are
+ *     all-gathered must all have the size of the LARGEST shard's pack.
+ *   cb_hits_compress: pack := {count, 0, positions[cap], directory}; position
+ *     = row * words * 64 + bit; the rows are cut into blocks of 2048 words and
+ *     directory entry b = {first slot, number} of block b's positions
+ *     (ascending inside the block). One launch. count may exceed cap: the
+ *     pack is then incomplete (which positions were kept is unspecified) and
+ *     all ranks must fall back to the dense exchange.
+ *     Requires rows * words * 64 < 2^32. Device pointers, async on stream.
  *   cb_hits_expand: full := the dense map holding the positions of packs[r]
- *     (nranks packs of 2 + cap words from cb_hits_compress, as all-gathered)
- *     at global row row_off[r] (host array, ascending, nranks <= 64); every
- *     word of full is written once. Bit-identical to the dense all-gather when no
- *     rank's count exceeds cap. A rank whose count exceeds cap is skipped and
- *     clears *ok (a device uint32, may be NULL): the overflow report is
- *     asynchronous, so the caller checks ok before using full and redoes that
- *     batch's exchange densely when it is 0. */
+ *     (nranks packs, all-gathered with the stride cb_hits_pack_words gives for
+ *     the largest shard) at global row row_off[r] (host array, row_off[0] = 0,
+ *     non-decreasing, nranks <= 64; rank r has rows up to row_off[r+1], the
+ *     last up to total_rows); every word of full is written once. Bit-identical
+ *     to the dense all-gather when no rank's count exceeds cap. A rank whose
+ *     count exceeds cap contributes zeros and clears *ok (a device uint32, may
+ *     be NULL): the overflow report is asynchronous, so the caller checks ok
+ *     before using full and redoes that batch's exchange densely when it is 0. */
+int cb_hits_pack_words(uint64_t rows, uint64_t words, uint64_t cap, uint64_t* out);
 int cb_hits_compress(const uint64_t* hits, uint64_t rows, uint64_t words, uint32_t* pack,
                      uint64_t cap, void* stream);
 int cb_hits_expand(const uint32_t* packs, uint32_t nranks, uint64_t cap, const uint64_t* row_off,
                    uint64_t words, uint64_t total_rows, uint64_t* full, uint32_t* ok, void* stream);
+
+/* The whole exchange behind one call, over RCCL (one process per GPU, xGMI
+ * between the GPUs of a node). Replaces the per-table loop of Database::get
+ * (src/lib.rs:129-134) when the tables' filters are sharded over GPUs: the
+ * table subset of rank r is rows [first_row, first_row + rows) of the global
+ * map, as cb_comm_shard splits total_rows (contiguous, sizes differ by <= 1,
+ * larger shards first).
+ *   cb_comm_unique_id: rank 0 makes the 128-byte id and hands it to every
+ *     rank by any channel (the Rust store: its own RPC; Python: the process
+ *     group's broadcast).
+ *   cb_comm_init: collective over the `world` ranks; binds to `device`. The
+ *     calling thread's current device is left unchanged.
+ *   cb_hits_allgather: collective. local = this rank's [rows][words] uint64
+ *     hits (rows = its shard of total_rows), full = the [total_rows][words]
+ *     map, both device memory on the communicator's device; async on stream.
+ *     mode CB_XCHG_DENSE: one all-gather of the rows. CB_XCHG_SPARSE: compress
+ *     -> all-gather of (2 + cap)-word packs -> expand (cap > 0, the same on
+ *     every rank). With ok == NULL the gathered counts are read back (the
+ *     stream is synchronised) and, if any rank's set bits exceed cap, every
+ *     rank redoes the batch densely: full is always complete. With ok != NULL
+ *     (a device uint32 holding 1) nothing is read back: ok is cleared when a
+ *     rank overflowed, and the caller redoes that batch with CB_XCHG_DENSE.
+ *     *sparse_used (nullable) = 1 when the map came from the packs.
+ *   One exchange at a time per communicator; exchanges on one communicator
+ *   must be issued in the same order on every rank. */
+#define CB_COMM_ID_BYTES 128
+#define CB_XCHG_DENSE 0
+#define CB_XCHG_SPARSE 1
+typedef struct cb_comm cb_comm;
+int cb_comm_unique_id(uint8_t* id /* CB_COMM_ID_BYTES */);
+int cb_comm_init(int rank, int world, const uint8_t* id, int device, cb_comm** out);
+int cb_comm_destroy(cb_comm* c);
+int cb_comm_info(const cb_comm* c, int* rank, int* world, int* device);
+int cb_comm_shard(uint64_t total_rows, int world, int rank, uint64_t* first_row, uint64_t* rows);
+int cb_hits_allgather(cb_comm* c, const uint64_t* local, uint64_t rows, uint64_t words,
+                      uint64_t total_rows, uint64_t* full, int mode, uint64_t cap, uint32_t* ok,
+                      int* sparse_used, void* stream);
 
 /* ---- tuning / introspection (bench + tests) ---- */
 /* Path selection: 0 = auto, 1 = force direct (per-key atomics / gathers),

@@ -24,6 +24,8 @@ CB_EDECODE = -5
 CB_ENODEV = -6
 
 PATH_AUTO, PATH_DIRECT, PATH_TILED = 0, 1, 2
+XCHG_DENSE, XCHG_SPARSE = 0, 1
+COMM_ID_BYTES = 128
 
 _lib = None
 
@@ -80,6 +82,13 @@ def load():
         "cb_host_free": ([P], i32),
         "cb_hits_compress": ([P, u64, u64, P, u64, P], i32),
         "cb_hits_expand": ([P, u32, u64, pu64, u64, u64, P, P, P], i32),
+        "cb_hits_pack_words": ([u64, u64, u64, pu64], i32),
+        "cb_comm_unique_id": ([P], i32),
+        "cb_comm_init": ([i32, i32, P, i32, pp], i32),
+        "cb_comm_destroy": ([P], i32),
+        "cb_comm_info": ([P, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
+        "cb_comm_shard": ([u64, i32, i32, pu64, pu64], i32),
+        "cb_hits_allgather": ([P, P, u64, u64, u64, P, i32, u64, P, ctypes.POINTER(i32), P], i32),
         "cb_filter_create": ([u64, i32, pp], i32),
         "cb_filter_destroy": ([P], i32),
         "cb_filter_bits": ([P, pu64], i32),

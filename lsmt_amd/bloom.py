@@ -266,6 +266,9 @@ class BloomFilter:
         m = ctypes.c_uint64()
         check(_L().cb_filter_bits(self._h, ctypes.byref(m)))
         self._m = int(m.value)
+        d = ctypes.c_int()
+        check(_L().cb_filter_device(self._h, ctypes.byref(d)))
+        self._device = int(d.value)
         self._pending: list[bytes] = []
 
     # src/bloom.rs:17-21
@@ -287,6 +290,10 @@ class BloomFilter:
     @property
     def m(self) -> int:
         return self._m
+
+    @property
+    def device(self) -> int:
+        return self._device
 
     @property
     def handle(self) -> ctypes.c_void_p:
@@ -465,7 +472,7 @@ class FilterSet:
         if not filters:
             raise ValueError("need at least one filter")
         width = width or (32 if len(filters) <= 32 else 64)
-        s = cls(filters[0].m, width)
+        s = cls(filters[0].m, width, device=filters[0].device)
         s.assign_all(filters, stream=stream)
         return s
 
@@ -774,24 +781,37 @@ def unpack_hits(hits: np.ndarray, n: int) -> np.ndarray:
 
 # ---- multi-GPU exchange (lsmt_amd/shard.py) ---------------------
 
-def hits_compress(hits, pack, stream=None) -> None:
-    """pack (int32 device tensor of 2 + cap) := {count, 0, set-bit positions}
-    of hits ([rows][words] int64 device tensor): cb_hits_compress."""
+def _pack_blocks(nw: int) -> int:
+    from .shard import PACK_BLOCK_WORDS
+    return -(-int(nw) // PACK_BLOCK_WORDS)
+
+
+def hits_compress(hits, pack, cap=None, stream=None) -> None:
+    """pack (int32 device tensor) := {count, 0, set-bit positions[cap],
+    directory} of hits ([rows][words] int64 device tensor): cb_hits_compress.
+    cap defaults to what the pack holds after its directory."""
     rows, words = hits.shape
-    cap = int(pack.numel()) - 2
+    if cap is None:
+        cap = int(pack.numel()) - 2 - 2 * _pack_blocks(rows * words)
+    if cap < 0 or int(pack.numel()) < 2 + cap + 2 * _pack_blocks(rows * words):
+        raise ValueError("pack too small for cap positions and the directory")
     hp, k1 = _ptr_of(hits)
     pp, k2 = _ptr_of(pack)
     _raise(_L().cb_hits_compress(hp, rows, words, pp, cap, _stream(stream)))
 
 
-def hits_expand(packs, world: int, row_off, full, ok=None, stream=None) -> None:
+def hits_expand(packs, world: int, row_off, full, ok=None, stream=None, cap=None) -> None:
     """full ([total_rows][words] int64 device tensor) := the OR of every
-    rank's positions (packs: the all-gathered int32 [world * (2 + cap)]).
-    ok: optional int32 device tensor, cleared to 0 when some rank's count
-    exceeds cap (that rank is then missing from full)."""
-    cap = int(packs.numel()) // world - 2
+    rank's positions (packs: the all-gathered int32 [world * stride], stride
+    = cb_hits_pack_words of the largest shard). ok: optional int32 device
+    tensor, cleared to 0 when some rank's count exceeds cap (that rank's rows
+    are then zeros in full)."""
     total_rows, words = full.shape
-    off = (ctypes.c_uint64 * world)(*[int(x) for x in row_off])
+    bounds = [int(x) for x in row_off] + [int(total_rows)]
+    max_rows = max(bounds[r + 1] - bounds[r] for r in range(world))
+    if cap is None:
+        cap = int(packs.numel()) // world - 2 - 2 * _pack_blocks(max_rows * words)
+    off = (ctypes.c_uint64 * world)(*bounds[:world])
     pp, k1 = _ptr_of(packs)
     fp, k2 = _ptr_of(full)
     op, k3 = _ptr_of(ok)

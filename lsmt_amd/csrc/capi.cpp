@@ -98,6 +98,17 @@ Workspace& workspace(int device, hipStream_t s) {
   return *slot;
 }
 
+int compress_state(Workspace& ws, hipStream_t s, cb::CompressState** out) {
+  if (!ws.x_ctl.p) {
+    HIP_TRY(ws.x_ctl.reserve(4 * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(ws.x_ctl.p, 0, 4 * sizeof(uint32_t), s));
+    ws.xst = cb::CompressState{};
+    ws.xst.ctl = (uint32_t*)ws.x_ctl.p;
+  }
+  *out = &ws.xst;
+  return CB_OK;
+}
+
 bool is_device_ptr(const void* p) {
   if (!p) return false;
   hipPointerAttribute_t attr;
@@ -510,8 +521,11 @@ int upload_zones(cb_filterset* set, hipStream_t s) {
   memcpy(tab.data() + cb_zone_hdr_bytes, pre, cb_zone_pre_bytes);
   if (!blob.empty()) memcpy(tab.data() + cb_zone_blob_off, blob.data(), blob.size());
   if (!set->zgated) return CB_OK;
+  // A gated probe queued on ANY stream may still read the old table: wait for
+  // the whole device before freeing or overwriting it (zone updates happen
+  // once per table flush, so a device-wide sync is cheap here).
+  HIP_TRY(hipDeviceSynchronize());
   if (tab.size() > set->zcap) {
-    HIP_TRY(hipStreamSynchronize(s));
     if (set->zdev) (void)hipFree(set->zdev);
     set->zdev = nullptr;
     set->zcap = 0;
@@ -821,7 +835,9 @@ int cb_init(int device) {
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     return fail(CB_ENODEV, "device is not gfx950 (MI355X); this library carries gfx950 code only");
-  HIP_TRY(hipSetDevice(device));
+  // No hipSetDevice here: the calling thread's current device is left as it
+  // was (entry points that work on `device` switch under a DeviceGuard, which
+  // restores the caller's device on return).
   return CB_OK;
 }
 
@@ -833,14 +849,17 @@ int cb_stream_synchronize(void* stream) {
 int cb_hits_compress(const uint64_t* hits, uint64_t rows, uint64_t words, uint32_t* pack,
                      uint64_t cap, void* stream) {
   if (!pack || (rows * words && !hits)) return fail(CB_EINVAL, "null argument");
-  if (rows && words && rows * words > (1ull << 26)) return fail(CB_EINVAL, "rows * words * 64 exceeds 2^32");
+  if (rows && words && (words > cb::kMaxCompressWords || rows * words > cb::kMaxCompressWords))
+    return fail(CB_EINVAL, "rows * words * 64 must be below 2^32");
   hipStream_t s = (hipStream_t)stream;
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   Workspace& ws = workspace(dev, s);
   std::lock_guard<std::mutex> lk(ws.mu);
-  HIP_TRY(ws.x_sums.reserve(cb::kMaxCompressBlocks * 4, s));
-  HIP_TRY(cb::launch_hits_compress(hits, rows, words, pack, cap, (uint32_t*)ws.x_sums.p, s));
+  cb::CompressState* st = nullptr;
+  int rc = compress_state(ws, s, &st);
+  if (rc) return rc;
+  HIP_TRY(cb::launch_hits_compress(hits, rows, words, pack, cap, *st, s));
   return CB_OK;
 }
 
@@ -849,8 +868,21 @@ int cb_hits_expand(const uint32_t* packs, uint32_t nranks, uint64_t cap, const u
   if (!full || (nranks && (!packs || !row_off))) return fail(CB_EINVAL, "null argument");
   if (nranks > cb::kMaxRanks) return fail(CB_EINVAL, "more than 64 ranks");
   cb::RankRows rr{};
-  for (uint32_t r = 0; r < nranks; ++r) rr.row_off[r] = row_off[r];
+  for (uint32_t r = 0; r < nranks; ++r) {
+    rr.row_off[r] = row_off[r];
+    const uint64_t end = r + 1 < nranks ? row_off[r + 1] : total_rows;
+    if ((r == 0 && row_off[0] != 0) || end < row_off[r] || end > total_rows)
+      return fail(CB_EINVAL, "row_off must start at 0 and be non-decreasing up to total_rows");
+    if ((end - row_off[r]) * words > cb::kMaxCompressWords)
+      return fail(CB_EINVAL, "a rank's rows * words * 64 must be below 2^32");
+  }
   HIP_TRY(cb::launch_hits_expand(packs, nranks, cap, rr, words, total_rows, full, ok, (hipStream_t)stream));
+  return CB_OK;
+}
+
+int cb_hits_pack_words(uint64_t rows, uint64_t words, uint64_t cap, uint64_t* out) {
+  if (!out) return fail(CB_EINVAL, "null out");
+  *out = cb::pack_words(rows * words, cap);
   return CB_OK;
 }
 

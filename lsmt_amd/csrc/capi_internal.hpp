@@ -131,13 +131,18 @@ struct Workspace {
   DevBuf t_views, t_rows, t_which, t_line, t_dlen, t_voff, t_scan, t_vals;
   DevBuf i_cnt, i_base, i_tmp, i_end, i_err, i_start;                 // line indexing
   DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_tsum, f_flag;  // SsTable::create
-  DevBuf x_sums;                                                          // cb_hits_compress
+  DevBuf x_ctl;                   // cb_hits_compress: slot / finish counters (zeroed once)
+  cb::CompressState xst;
   cb::CreateResult* hres = nullptr;  // pinned host mirror of f_flag (SsTable::create)
   uint64_t* htot = nullptr;          // pinned: get_many's value byte total
   hipEvent_t ev = nullptr;           // marks hres's first copy in the stream
 };
 
 Workspace& workspace(int device, hipStream_t s);
+
+// The stream's compress state, its counters allocated and zeroed on first
+// use (ws.mu held by the caller).
+int compress_state(Workspace& ws, hipStream_t s, cb::CompressState** out);
 
 // Device-accessible memory (hipMalloc, managed) is used in place; anything
 // else (pageable or pinned host memory) is staged by the library.

@@ -4,18 +4,22 @@
 // lib.rs:129-134) needs every table's answer per key, so the rows are
 // all-gathered. At BASELINE densities the rows are sparse (a present key hits
 // one table, false positives ~(1.55 %)^2 per (key, table)), so a rank ships
-// the POSITIONS of its set bits instead of its dense rows:
-//   k_hits_count / k_hits_emit — pack = {count, 0, positions...} with the
-//       positions (row*words*64 + bit, u32) in ascending order: per-block
-//       popcounts, then each block's base from the blocks before it and an
-//       in-order block scan per pass. count may exceed cap (then only the
-//       first cap positions are stored).
-//   k_hits_expand — after the all-gather of packs: each workgroup owns a
-//       32 KiB chunk of the global [total_rows][words] map, finds the
-//       positions that fall in it by wave-wide 64-ary searches in the (sorted) packs of
-//       the ranks it overlaps, ORs them into the chunk in LDS and writes the
-//       chunk once: the map is written exactly once, with no memset and no
-//       global atomics. A rank whose count exceeds cap contributes nothing and
+// the POSITIONS of its set bits instead of its dense rows.
+//
+// Pack layout (uint32; exchange.hpp): {count, 0, positions[cap], dir[2*D]}.
+// The rank's words are cut into D = ceil(rows*words / 2048) blocks; block b's
+// positions (row*words*64 + bit, ascending inside the block) sit at
+// positions[dir[2b] .. dir[2b] + dir[2b+1]). Blocks claim their slots with
+// one atomic add each, so no block ever waits for another:
+//   k_hits_compress — one block per 2048 words: count, claim, write the
+//       block's positions in order and its directory entry; the last block
+//       to finish writes count. count may exceed cap (the pack is then
+//       unusable: every rank must fall back to the dense exchange).
+//   k_hits_expand — after the all-gather of packs: one block per (rank,
+//       compress block), i.e. per 2048 words of the global map: ORs that
+//       block's positions into the chunk in LDS and writes the chunk once.
+//       The map is written exactly once, with no memset, no search and no
+//       global atomics. A rank whose count exceeds cap writes zeros and
 //       clears *ok (asynchronous overflow report: the caller checks ok before
 //       using the map and redoes that exchange densely).
 // The expanded map is bit-identical to the dense all-gather's.
@@ -27,10 +31,9 @@
 namespace cb {
 namespace {
 
-constexpr uint32_t kCT = 1024, kCW = 4;      // compress: threads per block, words per thread per pass
-constexpr uint64_t kPass = (uint64_t)kCT * kCW;
-constexpr uint32_t kXT = 512;                // expand: threads per block
-constexpr uint32_t kChunkWords = 4096;       // expand: map words per block (32 KiB of LDS)
+constexpr uint32_t kCT = 256, kCW = 8;  // compress: threads per block, words per thread
+static_assert((uint64_t)kCT * kCW == kCompressWords, "one block = kCompressWords words");
+constexpr uint32_t kXT = 256;           // expand: threads per block (one chunk of kCompressWords)
 
 // Inclusive block scan of one uint32 per thread; *total = block sum.
 // wsum: NT/64 words of LDS. Barriers inside: call uniformly.
@@ -57,160 +60,119 @@ __device__ __forceinline__ uint32_t block_incl_scan(uint32_t c, uint32_t* wsum, 
   return before + x;
 }
 
-// sums[b] = set bits in block b's word range [b*per, min((b+1)*per, nw)).
-__global__ __launch_bounds__(kCT) void k_hits_count(const uint64_t* __restrict__ hits, uint64_t nw,
-                                                    uint64_t per, uint32_t* __restrict__ sums) {
+// ctl: two uint64 claim words, one per launch parity: a block adds
+// (1 << 32) | its set bits, so the low half hands out slots and the high half
+// counts finished claims (the block that draws gridDim.x - 1 is the last and
+// knows the total). One relaxed atomic per block, no fence: the only value
+// read across blocks is the atomic word itself. A launch uses word `par` and
+// clears the other for the next launch on the stream.
+__global__ __launch_bounds__(kCT) void k_hits_compress(const uint64_t* __restrict__ hits, uint64_t nw,
+                                                       uint32_t* __restrict__ pack, uint64_t cap,
+                                                       unsigned long long* __restrict__ ctl, uint32_t par) {
   __shared__ uint32_t wsum[kCT / 64];
-  const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < nw ? b0 + per : nw;
+  __shared__ uint32_t s_base;
+  const uint32_t tid = threadIdx.x, b = blockIdx.x;
+  const uint64_t i0 = (uint64_t)b * kCompressWords + (uint64_t)tid * kCW;
+  uint64_t w[kCW];
+  if (i0 + kCW <= nw && !((uintptr_t)hits & 15)) {
+    const ulonglong2* v = reinterpret_cast<const ulonglong2*>(hits + i0);
+#pragma unroll
+    for (uint32_t j = 0; j < kCW / 2; ++j) {
+      const ulonglong2 a = v[j];
+      w[2 * j] = a.x;
+      w[2 * j + 1] = a.y;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < kCW; ++j) w[j] = i0 + j < nw ? hits[i0 + j] : 0ull;
+  }
   uint32_t c = 0;
-  for (uint64_t i = b0 + threadIdx.x; i < b1; i += kCT) c += (uint32_t)__popcll(hits[i]);
+#pragma unroll
+  for (uint32_t j = 0; j < kCW; ++j) c += (uint32_t)__popcll(w[j]);
   uint32_t total;
-  block_incl_scan<kCT>(c, wsum, &total);
-  if (threadIdx.x == 0) sums[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(kCT) void k_hits_emit(const uint64_t* __restrict__ hits, uint64_t nw,
-                                                   uint64_t per, const uint32_t* __restrict__ sums,
-                                                   uint32_t* __restrict__ pack, uint64_t cap) {
-  __shared__ uint32_t wsum[kCT / 64];
-  const uint32_t tid = threadIdx.x;
-  // base = set bits of all earlier blocks; the last block also publishes the count
-  uint32_t mine = 0;
-  for (uint32_t j = tid; j < blockIdx.x; j += kCT) mine += sums[j];
-  uint32_t base;
-  block_incl_scan<kCT>(mine, wsum, &base);
-  if (blockIdx.x == gridDim.x - 1 && tid == 0) {
-    pack[0] = base + sums[blockIdx.x];
-    pack[1] = 0;
-  }
-  const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < nw ? b0 + per : nw;
-  uint64_t run = base;
-  for (uint64_t p0 = b0; p0 < b1; p0 += kPass) {
-    uint64_t w[kCW];
-    uint32_t c = 0;
-#pragma unroll
-    for (int j = 0; j < (int)kCW; ++j) {
-      const uint64_t i = p0 + (uint64_t)tid * kCW + j;
-      w[j] = i < b1 ? hits[i] : 0ull;
-      c += (uint32_t)__popcll(w[j]);
-    }
-    uint32_t total;
-    const uint32_t incl = block_incl_scan<kCT>(c, wsum, &total);
-    uint64_t slot = run + incl - c;
-#pragma unroll
-    for (int j = 0; j < (int)kCW; ++j) {
-      uint64_t v = w[j];
-      const uint64_t pos0 = (p0 + (uint64_t)tid * kCW + j) * 64;  // row * words * 64 + col * 64
-      while (v) {
-        const uint32_t b = (uint32_t)__builtin_ctzll(v);
-        v &= v - 1;
-        if (slot < cap) pack[2 + slot] = (uint32_t)(pos0 + b);
-        ++slot;
-      }
-    }
-    run += total;
-  }
-}
-
-// First index in p[0..n) with p[i] >= x (p ascending), by one whole wave:
-// each round the 64 lanes probe 64 evenly spaced entries and the ballot of
-// "< x" (a prefix of the lanes) narrows the range 64-fold, so a 70K-entry
-// pack takes 3 rounds of one parallel load instead of 17 dependent ones.
-__device__ __forceinline__ uint64_t wave_lower_bound(const uint32_t* p, uint64_t n, uint64_t x) {
-  const uint32_t lane = threadIdx.x & 63u;
-  uint64_t lo = 0, hi = n;  // the answer is in [lo, hi]
-  while (hi - lo > 64) {
-    const uint64_t step = (hi - lo + 63) / 64;
-    const uint64_t i = lo + lane * step;
-    const bool below = i < hi && (uint64_t)p[i] < x;
-    const uint32_t c = (uint32_t)__popcll(__ballot(below));
-    const uint64_t nlo = c ? lo + (uint64_t)(c - 1) * step + 1 : lo;
-    const uint64_t nhi = lo + (uint64_t)c * step < hi ? lo + (uint64_t)c * step : hi;
-    lo = nlo;
-    hi = nhi;
-  }
-  const uint64_t i = lo + lane;
-  const bool below = i < hi && (uint64_t)p[i] < x;
-  return lo + (uint64_t)__popcll(__ballot(below));
-}
-
-__global__ __launch_bounds__(kXT) void k_hits_expand(const uint32_t* __restrict__ packs,
-                                                     uint32_t nranks, uint64_t cap, RankRows rr,
-                                                     uint64_t words, uint64_t total_words,
-                                                     uint64_t* __restrict__ full,
-                                                     uint32_t* __restrict__ ok) {
-  __shared__ uint64_t chunk[kChunkWords];
-  __shared__ uint64_t seg[kMaxRanks][3];  // per overlapped rank: first entry, end entry, base word
-  __shared__ uint64_t job[kMaxRanks][3];  // per overlapped rank: pack offset, count, first local word
-  __shared__ uint32_t nseg;
-  const uint32_t tid = threadIdx.x;
-  const uint64_t w0 = (uint64_t)blockIdx.x * kChunkWords;
-  const uint64_t w1 = w0 + kChunkWords < total_words ? w0 + kChunkWords : total_words;
-  for (uint32_t i = tid; i < kChunkWords; i += kXT) chunk[i] = 0;
+  const uint32_t incl = block_incl_scan<kCT>(c, wsum, &total);
   if (tid == 0) {
-    uint32_t ns = 0;
-    for (uint32_t r = 0; r < nranks; ++r) {
-      const uint64_t rb = rr.row_off[r] * words;
-      const uint64_t re = (r + 1 < nranks ? rr.row_off[r + 1] : total_words / words) * words;
-      if (re <= w0 || rb >= w1) continue;
-      const uint32_t* pk = packs + (size_t)r * (2 + cap);
-      const uint64_t count = pk[0];
-      if (count > cap) {  // this rank's positions do not all fit: the map is incomplete
-        if (ok) atomicAnd(ok, 0u);
-        continue;
-      }
-      const uint64_t lw0 = (w0 > rb ? w0 : rb) - rb, lw1 = (w1 < re ? w1 : re) - rb;
-      job[ns][0] = (uint64_t)r * (2 + cap) + 2;
-      job[ns][1] = count;
-      job[ns][2] = lw0 | (lw1 << 32);  // local words < 2^32 (positions are u32)
-      seg[ns][2] = rb;
-      ++ns;
+    const unsigned long long old = atomicAdd(ctl + par, (1ull << 32) | total);
+    s_base = (uint32_t)old;
+    if ((uint32_t)(old >> 32) == gridDim.x - 1) {  // the last claim: every block's bits are counted
+      pack[0] = (uint32_t)old + total;
+      pack[1] = 0;
     }
-    nseg = ns;
+    if (b == 0) __hip_atomic_store(ctl + (par ^ 1u), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  // the chunk's entry range in each overlapped pack: two wave-wide searches
-  // per rank, one per wave
-  for (uint32_t j = tid >> 6; j < 2 * nseg; j += kXT / 64) {
-    const uint32_t s = j >> 1;
-    const uint64_t lw = (j & 1) ? job[s][2] >> 32 : job[s][2] & 0xFFFFFFFFull;
-    const uint64_t e = wave_lower_bound(packs + job[s][0], job[s][1], lw * 64);
-    if ((tid & 63) == 0) seg[s][j & 1] = job[s][0] + e;
+  const uint64_t base = s_base;
+  uint32_t* dir = pack + 2 + cap;
+  if (tid == 0) {
+    dir[2 * (uint64_t)b] = (uint32_t)base;
+    dir[2 * (uint64_t)b + 1] = total;
   }
-  __syncthreads();
-  for (uint32_t s = 0; s < nseg; ++s) {
-    const uint64_t e0 = seg[s][0], e1 = seg[s][1], rb = seg[s][2];
-    for (uint64_t e = e0 + tid; e < e1; e += kXT) {
-      const uint64_t p = packs[e];
-      atomicOr(reinterpret_cast<unsigned long long*>(&chunk[rb + (p >> 6) - w0]), 1ull << (p & 63));
+  uint64_t slot = base + incl - c;
+#pragma unroll
+  for (uint32_t j = 0; j < kCW; ++j) {
+    uint64_t v = w[j];
+    const uint64_t pos0 = (i0 + j) * 64;  // row * words * 64 + col * 64
+    while (v) {
+      const uint32_t bit = (uint32_t)__builtin_ctzll(v);
+      v &= v - 1;
+      if (slot < cap) pack[2 + slot] = (uint32_t)(pos0 + bit);
+      ++slot;
     }
   }
-  __syncthreads();
-  for (uint64_t i = w0 + tid; i < w1; i += kXT) full[i] = chunk[i - w0];
 }
 
-inline uint64_t compress_plan(uint64_t nw, uint32_t* grid) {
-  uint64_t g = (nw + kPass - 1) / kPass;
-  if (g > kMaxCompressBlocks) g = kMaxCompressBlocks;
-  if (g < 1) g = 1;
-  const uint64_t per = ((nw + g - 1) / g + kPass - 1) / kPass * kPass;
-  *grid = (uint32_t)((nw + per - 1) / per);
-  if (*grid < 1) *grid = 1;
-  return per;
+__global__ __launch_bounds__(kXT) void k_hits_expand(const uint32_t* __restrict__ packs, uint32_t nranks,
+                                                     uint64_t cap, uint64_t stride, ExpandPlan plan,
+                                                     uint64_t words, uint64_t* __restrict__ full,
+                                                     uint32_t* __restrict__ ok) {
+  __shared__ uint64_t chunk[kCompressWords];
+  const uint32_t tid = threadIdx.x;
+  // this block's rank: the last r with blk_off[r] <= blockIdx.x (ranks with
+  // no rows have no blocks and are skipped by the ballot)
+  uint32_t r = 0;
+  for (uint32_t r0 = 0; r0 < nranks; r0 += 64) {
+    const uint32_t rr = r0 + (tid & 63u);
+    const uint64_t m = __ballot(rr < nranks && plan.blk_off[rr] <= blockIdx.x);
+    if (m) r = r0 + 63u - (uint32_t)__builtin_clzll(m);
+  }
+  const uint64_t b = blockIdx.x - plan.blk_off[r];
+  const uint64_t rows_r = plan.row_off[r + 1] - plan.row_off[r];
+  const uint64_t lw0 = b * kCompressWords;
+  const uint64_t lw1 = lw0 + kCompressWords < rows_r * words ? lw0 + kCompressWords : rows_r * words;
+  const uint32_t* pk = packs + (uint64_t)r * stride;
+  const uint64_t count = pk[0];
+  for (uint32_t i = tid; i < kCompressWords; i += kXT) chunk[i] = 0;
+  __syncthreads();
+  if (count > cap) {  // this rank's positions do not all fit: the map is incomplete
+    if (ok && tid == 0 && b == 0) atomicAnd(ok, 0u);
+  } else {
+    const uint32_t* dir = pk + 2 + cap;
+    const uint64_t e0 = dir[2 * b], ne = dir[2 * b + 1];
+    for (uint64_t e = tid; e < ne; e += kXT) {
+      const uint64_t p = pk[2 + e0 + e];
+      atomicOr(reinterpret_cast<unsigned long long*>(&chunk[(p >> 6) - lw0]), 1ull << (p & 63));
+    }
+  }
+  __syncthreads();
+  uint64_t* out = full + plan.row_off[r] * words + lw0;
+  const uint64_t n = lw1 - lw0;
+  for (uint64_t i = tid; i < n; i += kXT) out[i] = chunk[i];
 }
 
 }  // namespace
 
 hipError_t launch_hits_compress(const uint64_t* hits, uint64_t rows, uint64_t words,
-                                uint32_t* pack, uint64_t cap, uint32_t* sums, hipStream_t s) {
+                                uint32_t* pack, uint64_t cap, CompressState& st, hipStream_t s) {
   const uint64_t nw = rows * words;
   if (!nw) return hipMemsetAsync(pack, 0, 8, s);
-  uint32_t grid = 1;
-  const uint64_t per = compress_plan(nw, &grid);
+  if (nw > kMaxCompressWords) return hipErrorInvalidValue;
+  const uint32_t g = (uint32_t)pack_blocks(nw);
   ProfScope ps("k_hits_compress", s);
-  hipLaunchKernelGGL(k_hits_count, dim3(grid), dim3(kCT), 0, s, hits, nw, per, sums);
-  hipLaunchKernelGGL(k_hits_emit, dim3(grid), dim3(kCT), 0, s, hits, nw, per, sums, pack, cap);
-  return hipGetLastError();
+  hipLaunchKernelGGL(k_hits_compress, dim3(g), dim3(kCT), 0, s, hits, nw, pack, cap,
+                     reinterpret_cast<unsigned long long*>(st.ctl), st.parity);
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) st.parity ^= 1u;  // the launch cleared the other pair for the next one
+  return e;
 }
 
 hipError_t launch_hits_expand(const uint32_t* packs, uint32_t nranks, uint64_t cap,
@@ -219,10 +181,23 @@ hipError_t launch_hits_expand(const uint32_t* packs, uint32_t nranks, uint64_t c
   const uint64_t tw = total_rows * words;
   if (!tw) return hipSuccess;
   if (!nranks) return hipMemsetAsync(full, 0, tw * 8, s);
-  const uint64_t g = (tw + kChunkWords - 1) / kChunkWords;
+  ExpandPlan plan{};
+  uint64_t max_rows = 0, nblk = 0;
+  for (uint32_t r = 0; r < nranks; ++r) {
+    const uint64_t end = r + 1 < nranks ? rr.row_off[r + 1] : total_rows;
+    if (end < rr.row_off[r] || end > total_rows) return hipErrorInvalidValue;
+    plan.row_off[r] = rr.row_off[r];
+    plan.blk_off[r] = nblk;
+    nblk += pack_blocks((end - rr.row_off[r]) * words);
+    max_rows = end - rr.row_off[r] > max_rows ? end - rr.row_off[r] : max_rows;
+  }
+  if (rr.row_off[0] != 0) return hipErrorInvalidValue;
+  plan.row_off[nranks] = total_rows;
+  for (uint32_t r = nranks; r < kMaxRanks; ++r) plan.blk_off[r] = ~0ull;
+  if (!nblk) return hipSuccess;
   ProfScope ps("k_hits_expand", s);
-  hipLaunchKernelGGL(k_hits_expand, dim3((uint32_t)g), dim3(kXT), 0, s, packs, nranks, cap, rr, words,
-                     tw, full, ok);
+  hipLaunchKernelGGL(k_hits_expand, dim3((uint32_t)nblk), dim3(kXT), 0, s, packs, nranks, cap,
+                     pack_words(max_rows * words, cap), plan, words, full, ok);
   return hipGetLastError();
 }
 

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from lsmt_amd.shard import shard_range, sparse_cap
+from lsmt_amd.shard import PACK_BLOCK_WORDS, shard_range, sparse_cap
 
 
 def test_shard_range_covers_exactly():
@@ -30,34 +30,44 @@ def _free_port():
     return p
 
 
-def np_compress(h, pack):
+def np_compress(h, pack, cap):
     """CPU stand-in for lsmt_amd.hits_compress (the kernel is covered on the
-    GPU by tests/test_gpu_parity.py::test_hits_compress_expand)."""
+    GPU by tests/test_exchange_gpu.py): {count, 0, positions[cap], directory
+    of {first slot, number} per PACK_BLOCK_WORDS words}, positions grouped by block."""
     a = np.ascontiguousarray(h.numpy()).view(np.uint64).reshape(-1)
     pos = np.flatnonzero(np.unpackbits(a.view(np.uint8), bitorder="little")).astype(np.uint32)
-    cap = pack.numel() - 2
     pk = pack.numpy().view(np.uint32)
     pk[:] = 0
     pk[0] = len(pos)
     k = min(len(pos), cap)
     pk[2:2 + k] = pos[:k]
+    nblk = -(-a.size // PACK_BLOCK_WORDS)
+    blk = (pos >> 6) // PACK_BLOCK_WORDS
+    first = np.searchsorted(blk, np.arange(nblk))
+    cnt = np.bincount(blk, minlength=nblk)[:nblk]
+    pk[2 + cap:2 + cap + 2 * nblk:2] = first
+    pk[3 + cap:3 + cap + 2 * nblk:2] = cnt
 
 
-def np_expand(packs, world, row_off, full, ok=None):
+def np_expand(packs, world, row_off, full, ok, cap):
+    """CPU stand-in for lsmt_amd.hits_expand, reading through the directory."""
     words = full.shape[1]
     fw = full.numpy().view(np.uint64).reshape(-1)
     fw[:] = 0
     pk = packs.numpy().view(np.uint32).reshape(world, -1)
-    cap = pk.shape[1] - 2
+    bounds = list(row_off) + [full.shape[0]]
     for r in range(world):
-        if int(pk[r, 0]) > cap:  # as k_hits_expand: skip the rank, report
+        if int(pk[r, 0]) > cap:  # as k_hits_expand: the rank contributes zeros, ok cleared
             if ok is not None:
                 ok[0] = 0
             continue
-        cnt = int(pk[r, 0])
-        pos = pk[r, 2:2 + cnt].astype(np.uint64)
-        np.bitwise_or.at(fw, row_off[r] * words + (pos >> np.uint64(6)),
-                         np.left_shift(np.uint64(1), pos & np.uint64(63)))
+        nblk = -(-(bounds[r + 1] - bounds[r]) * words // PACK_BLOCK_WORDS)
+        for b in range(nblk):
+            e0, ne = int(pk[r, 2 + cap + 2 * b]), int(pk[r, 3 + cap + 2 * b])
+            pos = pk[r, 2 + e0:2 + e0 + ne].astype(np.uint64)
+            assert ((pos >> np.uint64(6)) // np.uint64(PACK_BLOCK_WORDS) == b).all()
+            np.bitwise_or.at(fw, bounds[r] * words + (pos >> np.uint64(6)),
+                             np.left_shift(np.uint64(1), pos & np.uint64(63)))
 
 
 def _worker(rank, world, port, n_filters, result_q, mode="dense"):
@@ -70,7 +80,7 @@ def _worker(rank, world, port, n_filters, result_q, mode="dense"):
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        m, kpf, n = 1 << 16, 800, 5000
+        m, kpf, n = 1 << 16, 800, 70_000  # 1094 hit words per row: several 2048-word pack blocks per shard
         lo, hi = shard_range(n_filters, world, rank)
         local = []
         for f in range(lo, hi):
@@ -143,3 +153,24 @@ def test_sparse_cap_covers_every_shard(n_keys, f_total):
             j = np.arange(n_keys // 2)
             present = int(((j % f_total >= lo) & (j % f_total < hi)).sum())
             assert cap >= present + 4 * 2.4e-4 * n_keys * (hi - lo), (world, r)
+
+
+def test_comm_shard_matches_shard_range():
+    # the C ABI's split (cb_comm_shard, lsmt_amd/csrc/comm.cpp) is the one the
+    # orchestration above uses; host-only, no GPU call
+    from lsmt_amd.shard import comm_shard
+    for n in (0, 1, 7, 32, 33, 256, 257):
+        for world in (1, 2, 3, 8, 64):
+            for r in range(world):
+                assert comm_shard(n, world, r) == shard_range(n, world, r), (n, world, r)
+
+
+def test_pack_words_matches_c_abi():
+    import ctypes
+
+    from lsmt_amd import _lib
+    from lsmt_amd.shard import pack_words
+    out = ctypes.c_uint64()
+    for rows, words, cap in ((0, 5, 7), (1, 1, 0), (32, 16384, 119570), (3, 1025, 10), (32, 156250, 10 ** 6)):
+        _lib.check(_lib.load().cb_hits_pack_words(rows, words, cap, ctypes.byref(out)))
+        assert out.value == pack_words(rows * words, cap)

@@ -452,58 +452,3 @@ def test_insert_many_matches_oracle(gpu, path, m):
         assert np.array_equal(f.bools(), o.bools()), i
 
 
-def test_hits_compress_expand(gpu):
-    # the sparse multi-GPU exchange kernels (lsmt_amd/shard.py gather_hits_sparse):
-    # compress -> (all-gathered) packs -> expand rebuilds the dense map bit for bit
-    import torch
-    rng = np.random.default_rng(5)
-    shards = []
-    for rows, words in ((3, 1000), (2, 1000), (2, 1000)):
-        h = (rng.random((rows, words * 64)) < 0.02).astype(np.uint8)
-        h[0, :64] = 1  # an all-ones word
-        if rows > 1:
-            h[1] = 0   # an empty row
-        shards.append(np.packbits(h, axis=1, bitorder="little").view(np.uint64))
-    cap = max(int(np.unpackbits(s.view(np.uint8)).sum()) for s in shards) + 10
-    packs = []
-    for s in shards:
-        t = torch.from_numpy(s.view(np.int64).copy()).cuda()
-        pack = torch.full((2 + cap,), -1, dtype=torch.int32, device="cuda")
-        gpu.hits_compress(t, pack)
-        pk = pack.cpu().numpy().view(np.uint32)
-        want = np.flatnonzero(np.unpackbits(s.reshape(-1).view(np.uint8), bitorder="little"))
-        assert pk[0] == len(want) and pk[1] == 0
-        assert np.array_equal(pk[2:2 + len(want)], want)  # ascending, as expand requires
-        packs.append(pack)
-    dense = np.concatenate(shards, 0)
-    full = torch.full(dense.shape, -1, dtype=torch.int64, device="cuda")
-    row_off = [0, 3, 5]
-    ok = torch.ones(1, dtype=torch.int32, device="cuda")
-    gpu.hits_expand(torch.cat(packs), 3, row_off, full, ok=ok)
-    assert np.array_equal(full.cpu().numpy().view(np.uint64), dense) and int(ok.item()) == 1
-    # a pack too small reports the true count, keeps the first cap positions,
-    # and expanding it clears ok
-    t = torch.from_numpy(shards[0].view(np.int64).copy()).cuda()
-    small = torch.zeros(2 + 5, dtype=torch.int32, device="cuda")
-    gpu.hits_compress(t, small)
-    pk = small.cpu().numpy().view(np.uint32)
-    want0 = np.flatnonzero(np.unpackbits(shards[0].reshape(-1).view(np.uint8), bitorder="little"))
-    assert pk[0] == len(want0) and np.array_equal(pk[2:], want0[:5])
-    bad = torch.cat([small] + [torch.zeros(2 + 5, dtype=torch.int32, device="cuda")] * 2)
-    gpu.hits_expand(bad, 3, row_off, full, ok=ok)
-    assert int(ok.item()) == 0
-    # many small rank slices inside one expand chunk (uneven shards, 1-2 rows of 100 words)
-    rng2 = np.random.default_rng(6)
-    sizes = [1, 2, 1, 1, 2, 2, 1, 1, 2, 1]
-    parts = [np.packbits((rng2.random((r, 6400)) < 0.05).astype(np.uint8), axis=1, bitorder="little").view(np.uint64)
-             for r in sizes]
-    cap2 = 1000
-    pks = []
-    for part in parts:
-        pck = torch.empty(2 + cap2, dtype=torch.int32, device="cuda")
-        gpu.hits_compress(torch.from_numpy(part.view(np.int64).copy()).cuda(), pck)
-        pks.append(pck)
-    dense2 = np.concatenate(parts, 0)
-    full2 = torch.full(dense2.shape, -1, dtype=torch.int64, device="cuda")
-    gpu.hits_expand(torch.cat(pks), len(sizes), list(np.cumsum([0] + sizes[:-1])), full2)
-    assert np.array_equal(full2.cpu().numpy().view(np.uint64), dense2)

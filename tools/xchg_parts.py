@@ -2,7 +2,8 @@
 gather_hits_sparse) on one GPU at the per-rank shape of C3 on 8 GPUs: a
 [32][16384] rank slice holding ~66K set bits, 8 packs of that size to expand
 into the [256][16384] global map. Prints one JSON line of microseconds per
-piece (HIP events, median of 50). Diagnostic only."""
+piece (HIP events, median of 50), and the whole C-ABI exchange
+(cb_hits_allgather) at world size 1. Diagnostic only."""
 import json
 import os
 import sys
@@ -56,6 +57,17 @@ def main():
     out["allgather_pack_world1_us"] = timed(lambda: dist.all_gather_into_tensor(one, pack))
     dense = torch.empty((rows, words), dtype=torch.int64, device=dev)
     out["allgather_dense_world1_us"] = timed(lambda: dist.all_gather_into_tensor(dense, h))
+    # the whole exchange through the C ABI (cb_hits_allgather on the library's
+    # own RCCL communicator), world size 1, on torch's current stream
+    from lsmt_amd.shard import Comm
+    c = Comm(0, 1, 0, Comm.unique_id())
+    s = torch.cuda.current_stream(dev).cuda_stream
+    full1 = torch.empty((rows, words), dtype=torch.int64, device=dev)
+    ok = torch.ones(1, dtype=torch.int32, device=dev)
+    out["capi_dense_world1_us"] = timed(lambda: c.allgather(h, rows, full1, stream=s))
+    out["capi_sparse_world1_us"] = timed(lambda: c.allgather(h, rows, full1, sparse=True, cap=cap, ok=ok, stream=s))
+    assert int(ok.item()) == 1 and torch.equal(full1, h)
+    c.close()
     print(json.dumps(out))
     dist.destroy_process_group()
 
