@@ -60,10 +60,9 @@ def parse():
                    help="skip the cold-cache legs (profiles: keeps every k_set_probe launch warm, so "
                         "rocprofv3's average matches the bench line's warm kernel time)")
     p.add_argument("--flush-entries", type=int, default=1 << 20)
-    p.add_argument("--overlap", action="store_true",
-                   help="N>1: run each step's all-gather on a side stream, overlapped with the next "
-                        "step's probe (measured slower on one GPU: the streams share one hardware "
-                        "queue and each cross-stream event adds 10-15 us; profiles/ r01 notes)")
+    p.add_argument("--probe-streams", type=int, default=2, choices=[1, 2, 3],
+                   help="pipeline lanes: consecutive steps alternate over this many streams (each with "
+                        "its own hit buffers and, for N > 1, its own RCCL communicator)")
     p.add_argument("--force-dist", action="store_true",
                    help="initialise the process group and run the exchange path even at N=1")
     return p.parse_args()
@@ -125,14 +124,10 @@ def main():
     look_np = workload.probe_lookups(n, nf_total, kpf, seed_base=seed_base, absent_seed=absent_seed)
     look = torch.from_numpy(look_np).to(dev)
     words = (n + 63) // 64
-    # Two hit buffers: with the exchange overlapped, step i's all-gather reads
-    # hits[i % 2] on the comm stream while step i+1 probes into the other one.
-    hits_bufs = [torch.zeros((F, words), dtype=torch.int64, device=dev) for _ in range(2)]
-    hits = hits_bufs[0]
-    hits_all_bufs = [torch.zeros((nf_total, words), dtype=torch.int64, device=dev) for _ in range(2)] \
-        if use_dist else hits_bufs
-    comm = torch.cuda.Stream(device=dev) if use_dist else None
-    gather_done = [None, None]
+    # one hit buffer (and one gathered map) per pipeline lane (below)
+    hits_bufs = [torch.zeros((F, words), dtype=torch.int64, device=dev) for _ in range(args.probe_streams)]
+    hits_all_bufs = [torch.zeros((nf_total, words), dtype=torch.int64, device=dev)
+                     for _ in range(args.probe_streams)] if use_dist else hits_bufs
     step_no = [0]
     torch.cuda.synchronize(dev)
     log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: {F} filters m={m} built, {n} lookups in HBM")
@@ -165,55 +160,47 @@ def main():
     # before the results are reported
     x_ok = torch.ones(1, dtype=torch.int32, device=dev) if use_sparse else None
 
+    # Pipelined batches: consecutive steps go round-robin to P "lanes", each
+    # with its own HIP stream, hit buffers and (N > 1) RCCL communicator, so
+    # one batch's launch ramp, drain and exchange overlap the next batch's
+    # probe. A step is still one full probe (+ exchange) of one batch; lanes
+    # never share a buffer, so no cross-stream event is needed per step.
+    P = args.probe_streams
+    lane_streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(P - 1)]
+    lane_sh = [st.cuda_stream for st in lane_streams]
     # The exchange runs through the C ABI (cb_hits_allgather over the
-    # library's own RCCL communicator, lsmt_amd/csrc/comm.cpp): the same call
-    # a Rust Database::get would make. torch.distributed only hands out the
-    # communicator id and times the run.
-    xcomm = Comm.from_process_group(local) if use_dist else None
-
-    def gather(buf, s_h=sh):
-        if use_sparse:
-            xcomm.allgather(hits_bufs[buf], nf_total, hits_all_bufs[buf], sparse=True, cap=cap, ok=x_ok,
-                            stream=s_h)
-            xstats["sparse_steps"] += 1
-        else:
-            xcomm.allgather(hits_bufs[buf], nf_total, hits_all_bufs[buf], stream=s_h)
+    # library's own RCCL communicators, lsmt_amd/csrc/comm.cpp): the same
+    # call a Rust Database::get would make. torch.distributed only hands out
+    # the communicator ids and times the run. Every rank issues the lanes'
+    # collectives in the same order, one communicator per lane.
+    xcomms = [Comm.from_process_group(local) for _ in range(P)] if use_dist else []
 
     def exchange(buf):
-        """The real exchange step: all-gather this step's hit rows from every
-        rank (filter-major -> plain concatenation) over RCCL/xGMI, right after
-        the probe. With --overlap it runs on the comm stream after the probe's
-        event while the next step probes into the other buffer; a buffer is
-        reused only after its gather has finished (gather_done)."""
+        """All-gather this step's hit rows from every rank (filter-major ->
+        plain concatenation) over RCCL/xGMI, on the step's lane right after
+        its probe."""
         if not use_dist:
             return
-        if not args.overlap:
-            gather(buf)
-            return
-        ev = torch.cuda.Event()
-        ev.record(stream)
-        with torch.cuda.stream(comm):
-            comm.wait_event(ev)
-            gather(buf, comm.cuda_stream)  # sparse: compress, all-gather, expand all on comm
-            done = torch.cuda.Event()
-            done.record(comm)
-        gather_done[buf] = done
+        if use_sparse:
+            xcomms[buf].allgather(hits_bufs[buf], nf_total, hits_all_bufs[buf], sparse=True, cap=cap,
+                                  ok=x_ok, stream=lane_sh[buf])
+            xstats["sparse_steps"] += 1
+        else:
+            xcomms[buf].allgather(hits_bufs[buf], nf_total, hits_all_bufs[buf], stream=lane_sh[buf])
 
     def claim():
-        buf = step_no[0] % 2
+        buf = step_no[0] % P
         step_no[0] += 1
-        if gather_done[buf] is not None:
-            stream.wait_event(gather_done[buf])
         return buf
 
     def step_tiled():
         buf = claim()
-        lsmt_amd.probe(filters, keys_batch, out=hits_bufs[buf], stream=sh)
+        lsmt_amd.probe(filters, keys_batch, out=hits_bufs[buf], stream=lane_sh[buf])
         exchange(buf)
 
     def step_set():
         buf = claim()
-        fset.probe(keys_batch, out=hits_bufs[buf], stream=sh)
+        fset.probe(keys_batch, out=hits_bufs[buf], stream=lane_sh[buf])
         exchange(buf)
 
     region = {}  # HIP events on the kernels' stream around the last timed region
@@ -225,8 +212,12 @@ def main():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         e0.record(stream)
+        for st in lane_streams[1:]:
+            st.wait_stream(stream)  # the other lanes start after e0
         for _ in range(k):
             fn()
+        for st in lane_streams[1:]:
+            stream.wait_stream(st)  # e1 after every lane's last step
         e1.record(stream)
         torch.cuda.synchronize(dev)
         if use_dist:
@@ -289,6 +280,7 @@ def main():
             torch.cuda.synchronize(dev)
             if use_dist:
                 dist.barrier()
+            step_no[0] = 0  # the rep's step runs on lane 0 (= `stream`, where the events are)
             if r < reps:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
@@ -332,7 +324,7 @@ def main():
 
         def step_rot():
             buf = claim()
-            fset.probe(rot_keys[rot_i[0] % nrot], out=hits_bufs[buf], stream=sh)
+            fset.probe(rot_keys[rot_i[0] % nrot], out=hits_bufs[buf], stream=lane_sh[buf])
             rot_i[0] += 1
             exchange(buf)
 
@@ -370,8 +362,10 @@ def main():
         one_kernel = best == "filterset" and not use_dist
         kus = legs[best]["region_us_per_step"] if one_kernel else \
             min(kprof[dominant]["avg_us"], legs[best]["ms_per_step"] * 1e3)
-        kus_src = ("HIP events on the probe stream around the timed region / K (one launch per step)"
-                   if one_kernel else "cb_profile per-launch HIP events, capped at the step time")
+        kus_src = (("HIP events around the timed region / K (one launch per step; " +
+                    (f"launches overlap {P} deep on {P} lanes, so this is each launch's share of the chip "
+                     f"and kernel_avg_us_per_launch_events is one launch's own duration)" if P > 1 else
+                     "one lane)")) if one_kernel else "cb_profile per-launch HIP events, capped at the step time")
         dur_s = kus * 1e-6
         ach = alg_bytes / dur_s / 1e9
         # PMC bytes are recorded for the default C3 shape only (profiles/pmc_*.json)
@@ -417,14 +411,14 @@ def main():
 
         def step_gated():
             buf = claim()
-            fset.probe(keys_batch, out=hits_bufs[buf], stream=sh, gated=True)
+            fset.probe(keys_batch, out=hits_bufs[buf], stream=lane_sh[buf], gated=True)
             exchange(buf)
 
         for _ in range(args.warmup):
             step_gated()
         gel = timed(step_gated, args.steps)
         gprof = kernel_ms(["k_set_probe_gated"], step_gated, args.steps)
-        gated_hits = int(np.unpackbits(hits_bufs[(step_no[0] - 1) % 2].cpu().numpy().view(np.uint8)).sum())
+        gated_hits = int(np.unpackbits(hits_bufs[(step_no[0] - 1) % P].cpu().numpy().view(np.uint8)).sum())
         zone = {"value": round(probes_per_step / (gel / args.steps), 1), "unit": "gated probes/s",
                 "ms_per_step": round(gel / args.steps * 1e3, 4),
                 "kernels_us": {k: round(v["avg_us"], 2) for k, v in gprof.items()},
@@ -633,10 +627,10 @@ def main():
         step()  # the headline leg again (the zone leg ran after it)
         torch.cuda.synchronize(dev)
         expect = oracle_rows(f_lo, f_lo + F)
-        got = hits_bufs[(step_no[0] - 1) % 2].cpu().numpy().view(np.uint64)
+        got = hits_bufs[(step_no[0] - 1) % P].cpu().numpy().view(np.uint64)
         good = bool(np.array_equal(got, expect))
         if use_dist:
-            full = hits_all_bufs[(step_no[0] - 1) % 2].cpu().numpy().view(np.uint64)
+            full = hits_all_bufs[(step_no[0] - 1) % P].cpu().numpy().view(np.uint64)
             good &= bool(np.array_equal(full[f_lo:f_lo + F], expect))
             if world > 1:
                 nlo, nhi = shard_range(nf_total, world, (rank + 1) % world)
@@ -678,10 +672,11 @@ def main():
                        "n_keys": n, "filters_per_gpu": F, "filters_total": nf_total, "m_bits": m,
                        "keys_per_filter": kpf,
                        "parallelism": "filter-sharded" + (
-                           ", RCCL all-gather of hit bitmaps" + (
+                           (", RCCL all-gather of hit bitmaps" + (
                                " as set-bit positions (sparse packs)" if use_sparse else
-                               (" overlapped with the next step's probe" if args.overlap else " after each probe"))
-                           if use_dist else "")},
+                               " after each probe"))
+                           if use_dist else ""),
+                       "pipeline_lanes": P},
             "exchange": (dict(xstats, mode="sparse", cap=cap, all_fit=x_fit) if use_sparse else
                          {"mode": "dense"} if use_dist else None),
             "path": best,
@@ -698,7 +693,8 @@ def main():
         print(json.dumps(line), file=result, flush=True)
     if use_dist:
         dist.barrier()
-        xcomm.close()
+        for c in xcomms:
+            c.close()
         dist.destroy_process_group()
     if x_fit is False:
         sys.exit(3)

@@ -57,6 +57,7 @@ extern "C" {
 #define CB_EHIP (-4)    /* HIP runtime error */
 #define CB_EDECODE (-5) /* malformed BloomProto bytes */
 #define CB_ENODEV (-6)  /* no usable gfx950 device */
+#define CB_EUTF8 (-7)   /* a data-file key is not UTF-8: SsTable::load returns Err */
 
 typedef struct cb_filter cb_filter;
 typedef struct cb_filterset cb_filterset; /* bit-sliced filter sets, see below */
@@ -258,6 +259,16 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
  * CB_EINVAL for other tables. */
 int cb_table_zone(const cb_table* t, int which, uint8_t* out, uint64_t cap, uint64_t* len);
 int cb_table_info(const cb_table* t, uint64_t* nlines, uint64_t* bytes);
+/* SsTable::load's rebuild when the `.meta` file is missing or undecodable
+ * (src/sstable.rs:109-120), on the device from the table's line index: a new
+ * filter of m_bits (BloomFilter::new(1024) in the reference) holding the key
+ * of every line that has a TAB (bytes before the first TAB; lines without one
+ * are skipped), and the zone map over the same keys, returned as the line
+ * indices of a smallest and a largest key (UINT64_MAX when no line has a
+ * TAB; cb_table_lines + cb_table_copy give the bytes). CB_EUTF8 when a key is
+ * not UTF-8 (the reference's load returns Err; nothing is returned then). */
+int cb_table_rebuild(const cb_table* t, uint64_t m_bits, void* stream, cb_filter** bloom_out,
+                     uint64_t* zone_min_line, uint64_t* zone_max_line);
 /* *out = 1 when the file is well-formed (a TAB on every line, keys strictly
  * increasing — what SsTable::create writes): then any correct search gives
  * the reference's answer and the prefix/fence index is used; otherwise the

@@ -22,6 +22,7 @@ CB_ENOMEM = -3
 CB_EHIP = -4
 CB_EDECODE = -5
 CB_ENODEV = -6
+CB_EUTF8 = -7
 
 PATH_AUTO, PATH_DIRECT, PATH_TILED = 0, 1, 2
 XCHG_DENSE, XCHG_SPARSE = 0, 1
@@ -135,6 +136,7 @@ def load():
         "cb_table_copy": ([P, u64, u64, u8p], i32),
         "cb_sstable_create": ([u8p, P, u8p, P, u64, u64, i32, P, pp, pp, pu64, pu64], i32),
         "cb_table_zone": ([P, i32, u8p, u64, pu64], i32),
+        "cb_table_rebuild": ([P, u64, P, pp, pu64, pu64], i32),
         "cb_table_well_formed": ([P, ctypes.POINTER(i32)], i32),
         "cb_table_force_exact": ([i32], i32),
         "cb_table_search_fixed": ([P, u8p, u32, u64, P, P], i32),

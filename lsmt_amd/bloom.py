@@ -640,6 +640,27 @@ class Table:
         check(_L().cb_table_zone(self._h, int(which), buf, n.value, ctypes.byref(n)))
         return buf.raw[:n.value]
 
+    def rebuild(self, m: int = 1024, stream=None) -> "tuple[BloomFilter, ZoneMap]":
+        """SsTable::load's rebuild from the data file when `.meta` is missing or
+        undecodable (src/sstable.rs:109-120), on the device: (bloom, zone_map)
+        over the keys of the lines that have a TAB. A key that is not UTF-8
+        raises UnicodeDecodeError, as the reference's load returns Err."""
+        h = ctypes.c_void_p()
+        lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = _L().cb_table_rebuild(self._h, int(m), _stream(stream), ctypes.byref(h), ctypes.byref(lo),
+                                   ctypes.byref(hi))
+        if rc == _lib.CB_EUTF8:
+            msg = _L().cb_last_error().decode()
+            raise UnicodeDecodeError("utf-8", b"", 0, 1, msg)
+        _raise(rc)
+        z = ZoneMap()
+        if lo.value != 0xFFFFFFFFFFFFFFFF:
+            st, kl, _ = self.lines()
+            raw = self.data()
+            for li in (lo.value, hi.value):
+                z.update(raw[int(st[li]):int(st[li]) + int(kl[li])])
+        return BloomFilter(0, _handle=h.value), z
+
     @property
     def well_formed(self) -> bool:
         """A TAB on every line and strictly increasing keys (what SsTable::create

@@ -75,7 +75,8 @@ struct cb_table {
   bool has_zone = false;   // made by cb_sstable_create with n >= 1
   std::string zmin, zmax;  // its ZoneMap bounds (first / last key of the file)
   cb::TableView view() const {
-    return cb::TableView{data, rec, pfx, fence, nlines, nfence, fast ? 1u : 0u};
+    return cb::TableView{data, rec, pfx, fence, fence ? fence + nfence : nullptr, nlines, nfence,
+                         cb::fence2_count(nlines), fast ? 1u : 0u};
   }
 };
 

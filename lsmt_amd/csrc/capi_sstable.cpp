@@ -143,8 +143,8 @@ int index_table(cb_table* t, hipStream_t s) {
   HIP_TRY(hipStreamSynchronize(s));
   if (!t->nlines) return CB_OK;
   const uint64_t nl = t->nlines;
-  t->nfence = (nl + cb::kFenceStride - 1) / cb::kFenceStride;
-  const size_t bytes = nl * sizeof(cb::LineRec) + nl * 8 + t->nfence * 8;
+  t->nfence = cb::fence_count(nl);
+  const size_t bytes = nl * sizeof(cb::LineRec) + nl * 8 + cb::fence_words(nl) * 8;
   if (pool_alloc(t->device, bytes, (void**)&t->rec, &t->rec_cap) != hipSuccess) {
     t->rec = nullptr;
     return fail(CB_ENOMEM, "device allocation failed for an SSTable index");
@@ -366,8 +366,8 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
   // the line index straight from the entries (entry p is line p), no re-read of the file
   t->nlines = n;
-  t->nfence = (n + cb::kFenceStride - 1) / cb::kFenceStride;
-  const size_t ibytes = n * sizeof(cb::LineRec) + n * 8 + t->nfence * 8;
+  t->nfence = cb::fence_count(n);
+  const size_t ibytes = n * sizeof(cb::LineRec) + n * 8 + cb::fence_words(n) * 8;
   if (pool_alloc(device, ibytes, (void**)&t->rec, &t->rec_cap) != hipSuccess) {
     t->rec = nullptr;
     return fail(CB_ENOMEM, "device allocation failed for an SSTable index");
@@ -411,6 +411,78 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   }
   if (bloom_out) *bloom_out = f.release();
   *table_out = t.release();
+  return CB_OK;
+}
+
+int cb_table_rebuild(const cb_table* t, uint64_t m_bits, void* stream, cb_filter** bloom_out,
+                     uint64_t* zone_min_line, uint64_t* zone_max_line) {
+  if (!t || !bloom_out) return fail(CB_EINVAL, "null argument");
+  *bloom_out = nullptr;
+  if (zone_min_line) *zone_min_line = ~0ull;
+  if (zone_max_line) *zone_max_line = ~0ull;
+  hipStream_t s = (hipStream_t)stream;
+  cb_filter* fp = nullptr;
+  int rc = cb_filter_create(m_bits, t->device, &fp);  // BloomFilter::new(1024) (src/sstable.rs:111)
+  if (rc) return rc;
+  std::unique_ptr<cb_filter, int (*)(cb_filter*)> f(fp, cb_filter_destroy);
+  const uint64_t nl = t->nlines;
+  if (nl) {
+    DeviceGuard dg(t->device);
+    Workspace& ws = workspace(t->device, s);
+    std::lock_guard<std::mutex> lk(ws.mu);
+    HIP_TRY(ws.i_cnt.reserve((nl + 1) * 8, s));
+    HIP_TRY(ws.i_base.reserve((nl + 1) * 8, s));
+    HIP_TRY(ws.i_start.reserve((nl + 1) * 8, s));
+    HIP_TRY(ws.i_end.reserve((nl + 1) * 8, s));
+    HIP_TRY(ws.i_tmp.reserve(cb::scan_tmp_words(nl) * 8, s));
+    HIP_TRY(ws.i_err.reserve(8, s));
+    uint64_t* has = (uint64_t*)ws.i_cnt.p;
+    uint64_t* has_scan = (uint64_t*)ws.i_base.p;
+    uint64_t* klen = (uint64_t*)ws.i_start.p;
+    uint64_t* len_scan = (uint64_t*)ws.i_end.p;
+    uint64_t* bad = (uint64_t*)ws.i_err.p;
+    HIP_TRY(hipMemsetAsync(bad, 0xFF, 8, s));
+    HIP_TRY(cb::launch_rebuild_mark(t->data, t->rec, nl, has, klen, bad, s));
+    HIP_TRY(cb::launch_scan_u64(has, has_scan, nl, (uint64_t*)ws.i_tmp.p, s));
+    HIP_TRY(cb::launch_scan_u64(klen, len_scan, nl, (uint64_t*)ws.i_tmp.p, s));
+    uint64_t h[3];
+    HIP_TRY(hipMemcpyAsync(&h[0], bad, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&h[1], has_scan + nl, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&h[2], len_scan + nl, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (h[0] != ~0ull) {  // std::str::from_utf8(..).map_err(..)? (src/sstable.rs:115-116)
+      char msg[96];
+      std::snprintf(msg, sizeof msg, "SsTable::load: the key on line %llu is not UTF-8",
+                    (unsigned long long)h[0]);
+      return fail(CB_EUTF8, msg);
+    }
+    const uint64_t nk = h[1], kbytes = h[2];
+    if (nk) {
+      HIP_TRY(ws.lkey.reserve(kbytes + 16, s));
+      HIP_TRY(ws.t_line.reserve((nk + 1) * 8, s));
+      HIP_TRY(ws.t_which.reserve(nk * 8, s));
+      uint8_t* kb = (uint8_t*)ws.lkey.p;
+      uint64_t* ko = (uint64_t*)ws.t_line.p;
+      uint64_t* lmap = (uint64_t*)ws.t_which.p;
+      HIP_TRY(cb::launch_rebuild_gather(t->data, t->rec, nl, has_scan, len_scan, kb, ko, lmap, s));
+      // bloom.insert(key) for every TAB line (src/sstable.rs:117)
+      if ((rc = insert_locked(ws, f.get(), kb, ko, 0, nk, s))) return rc;
+      // zone_map.update(key) for every TAB line (src/sstable.rs:118)
+      HIP_TRY(ws.zone.reserve((2 * 1024 + 2) * 8, s));
+      uint64_t* dtmp = (uint64_t*)ws.zone.p;
+      uint64_t* didx = dtmp + 2 * 1024;
+      HIP_TRY(cb::launch_zone_bounds(cb::KEY_VAR, cb::KeySrc{kb, ko, 0}, nk, dtmp, didx, s));
+      uint64_t idx[2], line[2];
+      HIP_TRY(hipMemcpyAsync(idx, didx, 16, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      HIP_TRY(hipMemcpyAsync(&line[0], lmap + idx[0], 8, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(&line[1], lmap + idx[1], 8, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      if (zone_min_line) *zone_min_line = line[0];
+      if (zone_max_line) *zone_max_line = line[1];
+    }
+  }
+  *bloom_out = f.release();
   return CB_OK;
 }
 

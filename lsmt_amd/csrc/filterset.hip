@@ -166,47 +166,30 @@ __global__ __launch_bounds__(256) void k_set_put_slot(const uint32_t* __restrict
 
 constexpr uint32_t kSetWords = 16;  // hit words (x64 keys) per block: 1024 keys
 constexpr uint32_t kSetProbeThreads = 64 * kSetWords;
+constexpr uint32_t kFlowThreads = 256;  // k_set_probe_flow: 4 waves per block
+constexpr uint32_t kFlowWaves = kFlowThreads / 64;
 
-// One key per lane, one 64-key hit word per wave. SC = the reference's `&&`
-// short-circuit (src/bloom.rs:50): set[b] is read only when set[a] != 0
-// (fewer bytes, but b waits for a). Ballots turn each 64-key word into one
-// hit word per slot, staged in LDS so every slot row leaves as a contiguous
-// 128-byte segment. (Two or four keys per lane, to keep more independent
-// reads in flight, measured no faster: the wave count already saturates the
-// memory pipeline. Non-temporal key loads and hit stores, to keep the
-// streamed bytes out of the set's cache lines, measured no different: 40.4 us.
-// 512-thread blocks (8 hit words) measured 40.9-41.1 us.)
+// One key's answer for every slot: bit s of the result = slot s's
+// may_contain (and, for gated slots, its ZoneMap::contains). SC = the
+// reference's `&&` short-circuit (src/bloom.rs:50): set[b] is read only when
+// set[a] != 0 (fewer bytes, but b waits for a).
 //
 // Zone gate (SsTable::get, src/sstable.rs:138): when zv.gated != 0 each
 // surviving candidate slot s of a gated slot is re-checked with
 // ZoneMap::contains and dropped if the key is outside [min, max]. The
 // reference tests the zone first; the conjunction is the same either way and
 // testing it only for Bloom candidates costs ~0.5 compare pairs per key
-// instead of one per (key, table).
-template <int KEYK, int MODE, int W, bool SC>
-__global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __restrict__ set,
-                                                                const uint32_t* __restrict__ any,
-                                                                uint32_t used, KeySrc ks,
-                                                                uint64_t n, ModP mp, ZoneView zv,
-                                                                uint64_t* __restrict__ hits,
-                                                                uint64_t hwords) {
+// instead of one per (key, table). zp: the bounds' 16-byte prefixes staged in
+// LDS (16-byte keys only).
+// ZP_SYNC: the block barrier that publishes zp is taken here, after the
+// key's loads have issued (callers where every thread calls this exactly once).
+template <int KEYK, int MODE, int W, bool SC, bool ZP_SYNC>
+__device__ __forceinline__ typename std::conditional<W == 32, uint32_t, uint64_t>::type set_key_mask(
+    const void* __restrict__ set, const uint32_t* __restrict__ any, const KeySrc& ks, uint64_t k,
+    bool ok, const ModP& mp, const ZoneView& zv, const BoundPrefix* zp) {
   typedef typename std::conditional<W == 32, uint32_t, uint64_t>::type word_t;
   typedef const __attribute__((address_space(1))) word_t* gptr;
-  __shared__ uint64_t hb[64][kSetWords];
-  __shared__ BoundPrefix zp[2 * W];  // gated 16-byte keys: the bounds' prefixes, staged
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  if constexpr (KEYK == KEY_FIXED16) {
-    if (zv.gated) {  // uniform; issued alongside the key loads below
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(zv.pre);
-      uint32_t* dst = reinterpret_cast<uint32_t*>(zp);
-      for (uint32_t i = threadIdx.x; i < 2 * W * sizeof(BoundPrefix) / 4; i += kSetProbeThreads)
-        dst[i] = src[i];
-    }
-  }
-  const uint64_t wbase = (uint64_t)blockIdx.x * kSetWords;
   const gptr sp = (gptr)set;
-  const uint64_t k = (wbase + wave) * 64 + lane;
-  bool ok = k < n;
   uint64_t pa = 0, pb = 0;
   uint4 kv = make_uint4(0, 0, 0, 0);  // KEY_FIXED16: the key, kept for the zone gate
   if (ok) {
@@ -234,12 +217,11 @@ __global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __re
     vb = va ? sp[pb] : (word_t)0;
   word_t mask = va & vb;
   if (zv.gated) {  // uniform: only gated launches pay for the zone check
-    if constexpr (KEYK == KEY_FIXED16) __syncthreads();  // zp staged
+    if constexpr (ZP_SYNC && KEYK == KEY_FIXED16) __syncthreads();  // zp staged
     word_t c = mask & (word_t)zv.gated;
     if constexpr (KEYK == KEY_FIXED16) {
       // 16-byte keys: the key (still in registers from the hash) compared as
-      // 4 big-endian words against the bounds' host-computed prefixes,
-      // staged in LDS at block start (2 KB for 32 slots).
+      // 4 big-endian words against the bounds' host-computed prefixes.
       if (c) {
         const uint32_t kw[4] = {be32(kv.x), be32(kv.y), be32(kv.z), be32(kv.w)};
         while (c) {
@@ -260,6 +242,41 @@ __global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __re
       }
     }
   }
+  return mask;
+}
+
+// set_key_mask for a 16-byte key already in registers (no union pre-test).
+template <int MODE, int W, bool SC>
+__device__ __forceinline__ typename std::conditional<W == 32, uint32_t, uint64_t>::type set_key_mask_u4(
+    const void* __restrict__ set, const uint4& kv, bool ok, const ModP& mp, const ZoneView& zv,
+    const BoundPrefix* zp) {
+  typedef typename std::conditional<W == 32, uint32_t, uint64_t>::type word_t;
+  typedef const __attribute__((address_space(1))) word_t* gptr;
+  const gptr sp = (gptr)set;
+  uint64_t pa = 0, pb = 0;
+  if (ok) key_positions_u4<MODE>(kv, mp, pa, pb);
+  const word_t va = ok ? sp[pa] : (word_t)0;
+  word_t vb;
+  if constexpr (!SC)
+    vb = ok ? sp[pb] : (word_t)0;
+  else
+    vb = va ? sp[pb] : (word_t)0;
+  word_t mask = va & vb;
+  word_t c = zv.gated ? mask & (word_t)zv.gated : (word_t)0;
+  if (c) {
+    const uint32_t kw[4] = {be32(kv.x), be32(kv.y), be32(kv.z), be32(kv.w)};
+    while (c) {
+      const uint32_t s = (uint32_t)__builtin_ctzll((uint64_t)c);
+      c &= c - 1;
+      if (cmp16(kw, zp[2 * s]) < 0 || cmp16(kw, zp[2 * s + 1]) > 0) mask &= ~((word_t)1 << s);
+    }
+  }
+  return mask;
+}
+
+// The wave's 64 keys' masks -> lane f holds slot f's 64-key hit word.
+template <int W, class word_t>
+__device__ __forceinline__ uint64_t slot_words(word_t mask, uint32_t used, uint32_t lane) {
   uint64_t mine = 0;
 #pragma unroll
   for (uint32_t f = 0; f < (uint32_t)W; ++f) {
@@ -268,12 +285,95 @@ __global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __re
       mine = (lane == f) ? bal : mine;
     }
   }
+  return mine;
+}
+
+template <int KEYK, int W>
+__device__ __forceinline__ void stage_zone_prefixes(const ZoneView& zv, BoundPrefix* zp, uint32_t nthreads) {
+  if constexpr (KEYK == KEY_FIXED16) {
+    if (zv.gated) {  // uniform
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(zv.pre);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(zp);
+      for (uint32_t i = threadIdx.x; i < 2 * W * sizeof(BoundPrefix) / 4; i += nthreads) dst[i] = src[i];
+    }
+  }
+}
+
+// One key per lane, one 64-key hit word per wave, 16 waves per block. Ballots
+// turn each 64-key word into one hit word per slot, staged in LDS so every
+// slot row leaves as a contiguous 128-byte segment. (Two or four keys per
+// lane, to keep more independent reads in flight, measured no faster: the
+// wave count already saturates the memory pipeline. Non-temporal key loads
+// and hit stores, to keep the streamed bytes out of the set's cache lines,
+// measured no different: 40.4 us. 512-thread blocks (8 hit words) measured
+// 40.9-41.1 us.)
+template <int KEYK, int MODE, int W, bool SC>
+__global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __restrict__ set,
+                                                                const uint32_t* __restrict__ any,
+                                                                uint32_t used, KeySrc ks,
+                                                                uint64_t n, ModP mp, ZoneView zv,
+                                                                uint64_t* __restrict__ hits,
+                                                                uint64_t hwords) {
+  __shared__ uint64_t hb[64][kSetWords];
+  __shared__ BoundPrefix zp[2 * W];  // gated 16-byte keys: the bounds' prefixes, staged
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  stage_zone_prefixes<KEYK, W>(zv, zp, kSetProbeThreads);  // issued alongside the key loads
+  const uint64_t wbase = (uint64_t)blockIdx.x * kSetWords;
+  const uint64_t k = (wbase + wave) * 64 + lane;
+  const auto mask = set_key_mask<KEYK, MODE, W, SC, true>(set, any, ks, k, k < n, mp, zv, zp);
+  const uint64_t mine = slot_words<W>(mask, used, lane);
   if (lane < used) hb[lane][wave] = mine;
   __syncthreads();
   const uint64_t nw = (n + 63) / 64;
   for (uint32_t i = threadIdx.x; i < used * kSetWords; i += kSetProbeThreads) {
     const uint32_t f = i / kSetWords, w = i % kSetWords;
     if (wbase + w < nw) hits[(uint64_t)f * hwords + wbase + w] = hb[f][w];
+  }
+}
+
+// Persistent form: a grid sized to the chip (blocks per CU x CUs), each wave
+// striding over 64-key hit words on its own, with no block barrier after the
+// start: a wave whose random reads came back early starts its next word at
+// once instead of waiting for the block's slowest wave, so the launch has no
+// block-round tail. Lane f stores slot f's word directly (one store
+// instruction per wave and word; the 8-byte pieces of a row's 128-byte
+// segment meet in L2).
+template <int KEYK, int MODE, int W, bool SC>
+__global__ __launch_bounds__(kFlowThreads) void k_set_probe_flow(const void* __restrict__ set,
+                                                                 const uint32_t* __restrict__ any,
+                                                                 uint32_t used, KeySrc ks,
+                                                                 uint64_t n, ModP mp, ZoneView zv,
+                                                                 uint64_t* __restrict__ hits,
+                                                                 uint64_t hwords) {
+  __shared__ BoundPrefix zp[2 * W];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  stage_zone_prefixes<KEYK, W>(zv, zp, kFlowThreads);
+  if (KEYK == KEY_FIXED16 && zv.gated) __syncthreads();
+  const uint64_t nw = (n + 63) / 64;
+  const uint64_t stride = (uint64_t)gridDim.x * kFlowWaves;
+  uint64_t w = (uint64_t)blockIdx.x * kFlowWaves + wave;
+  if constexpr (KEYK == KEY_FIXED16) {
+    // software-pipelined: the next word's key load is in flight while this
+    // word's random set reads are outstanding
+    const uint4* kp = reinterpret_cast<const uint4*>(ks.bytes);
+    uint4 next = make_uint4(0, 0, 0, 0);
+    if (w < nw && w * 64 + lane < n) next = kp[w * 64 + lane];
+    for (; w < nw; w += stride) {
+      const uint64_t k = w * 64 + lane;
+      const uint4 kv = next;
+      const uint64_t kn = (w + stride) * 64 + lane;
+      if (w + stride < nw && kn < n) next = kp[kn];
+      const auto mask = set_key_mask_u4<MODE, W, SC>(set, kv, k < n, mp, zv, zp);
+      const uint64_t mine = slot_words<W>(mask, used, lane);
+      if (lane < used) hits[(uint64_t)lane * hwords + w] = mine;
+    }
+  } else {
+    for (; w < nw; w += stride) {
+      const uint64_t k = w * 64 + lane;
+      const auto mask = set_key_mask<KEYK, MODE, W, SC, false>(set, any, ks, k, k < n, mp, zv, zp);
+      const uint64_t mine = slot_words<W>(mask, used, lane);
+      if (lane < used) hits[(uint64_t)lane * hwords + w] = mine;
+    }
   }
 }
 
@@ -351,15 +451,37 @@ hipError_t launch_set_put_slot(const uint32_t* words, uint64_t m, uint32_t slot,
 }
 
 template <int KK, int MM, int WW>
-static void set_probe(bool sc, const void* set, const uint32_t* any, uint32_t used,
+static void set_probe(bool sc, bool flow, const void* set, const uint32_t* any, uint32_t used,
                       const KeySrc& ks, uint64_t n, const ModP& mp, const ZoneView& zv,
                       uint64_t* hits, uint64_t hwords, uint32_t grid, hipStream_t s) {
+  if (flow) {
+    if (sc)
+      hipLaunchKernelGGL((k_set_probe_flow<KK, MM, WW, true>), dim3(grid), dim3(kFlowThreads), 0, s,
+                         set, any, used, ks, n, mp, zv, hits, hwords);
+    else
+      hipLaunchKernelGGL((k_set_probe_flow<KK, MM, WW, false>), dim3(grid), dim3(kFlowThreads), 0, s,
+                         set, any, used, ks, n, mp, zv, hits, hwords);
+    return;
+  }
   if (sc)
     hipLaunchKernelGGL((k_set_probe<KK, MM, WW, true>), dim3(grid), dim3(kSetProbeThreads), 0, s,
                        set, any, used, ks, n, mp, zv, hits, hwords);
   else
     hipLaunchKernelGGL((k_set_probe<KK, MM, WW, false>), dim3(grid), dim3(kSetProbeThreads), 0, s,
                        set, any, used, ks, n, mp, zv, hits, hwords);
+}
+
+// Compute units of the current device (cached per device).
+static uint32_t device_cus() {
+  static uint32_t cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cus[dev] = (uint32_t)v;
+  }
+  return cus[dev];
 }
 
 hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
@@ -384,10 +506,23 @@ hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
   }();
   const ZoneView zv = zones ? *zones : ZoneView{nullptr, nullptr, nullptr, 0};
   const uint64_t nw = (n + 63) / 64;
-  const uint32_t grid = (uint32_t)((nw + kSetWords - 1) / kSetWords);
+  // CB_SET_FLOW=1: the persistent k_set_probe_flow; CB_SET_FLOW_BPC: its
+  // blocks per CU (default 8: 32 waves per CU). Read per launch (tuning).
+  const char* fv = getenv("CB_SET_FLOW");
+  const bool flow = fv && fv[0] == '1' && !use_any;  // the flow form has no union pre-test
+  uint32_t grid;
+  if (flow) {
+    const char* bv = getenv("CB_SET_FLOW_BPC");
+    const uint32_t bpc = bv ? (uint32_t)atoi(bv) : 8u;
+    const uint64_t want = (nw + kFlowWaves - 1) / kFlowWaves;
+    const uint64_t cap = (uint64_t)device_cus() * (bpc ? bpc : 8u);
+    grid = (uint32_t)(want < cap ? want : cap);
+  } else {
+    grid = (uint32_t)((nw + kSetWords - 1) / kSetWords);
+  }
   ProfScope ps(zv.gated ? "k_set_probe_gated" : "k_set_probe", s);
   CB_SET_DISPATCH(keyk, mode, width,
-                  (set_probe<KK, MM, WW>(sc, set, use_any ? any : nullptr, used, ks, n, mp, zv,
+                  (set_probe<KK, MM, WW>(sc, flow, set, use_any ? any : nullptr, used, ks, n, mp, zv,
                                          hits, hwords, grid, s)));
   return hipGetLastError();
 }

@@ -217,6 +217,7 @@ __global__ __launch_bounds__(kNT) void k_line_keys(const uint8_t* __restrict__ d
   if (live) {
     pfx[l] = v;
     if (l % kFenceStride == 0) fence[l / kFenceStride] = v;
+    if (l % kFence2Stride == 0) fence[fence_count(nlines) + l / kFence2Stride] = v;
     if (good && l > 0) {
       const LineRec q = rec[l - 1];  // start/klen only: written by k_line_finish
       good = q.klen != kNoSep && bytes_cmp(data + q.start, q.klen, p, r.klen) < 0;
@@ -256,6 +257,72 @@ __global__ __launch_bounds__(1024) void k_tile_scan(uint64_t* __restrict__ tsum,
     carry += total;
   }
   if (threadIdx.x == 0) *total_out = carry;
+}
+
+// ---- SsTable::load's rebuild from the data file (src/sstable.rs:109-120) ----
+
+// Rust's str::from_utf8 acceptance (Unicode well-formed sequences: no
+// overlongs, no surrogates, nothing above U+10FFFF).
+__device__ __forceinline__ bool utf8_valid(const uint8_t* p, uint64_t n) {
+  uint64_t i = 0;
+  while (i < n) {
+    const uint32_t c = p[i];
+    if (c < 0x80) {
+      ++i;
+      continue;
+    }
+    uint32_t len, lo = 0x80, hi = 0xBF;
+    if (c >= 0xC2 && c <= 0xDF) len = 2;
+    else if (c == 0xE0) { len = 3; lo = 0xA0; }
+    else if ((c >= 0xE1 && c <= 0xEC) || c == 0xEE || c == 0xEF) len = 3;
+    else if (c == 0xED) { len = 3; hi = 0x9F; }
+    else if (c == 0xF0) { len = 4; lo = 0x90; }
+    else if (c >= 0xF1 && c <= 0xF3) len = 4;
+    else if (c == 0xF4) { len = 4; hi = 0x8F; }
+    else return false;
+    if (n - i < len) return false;
+    if (p[i + 1] < lo || p[i + 1] > hi) return false;
+    for (uint32_t k = 2; k < len; ++k)
+      if (p[i + k] < 0x80 || p[i + k] > 0xBF) return false;
+    i += len;
+  }
+  return true;
+}
+
+// Per line: has[l] = 1 when the line has a TAB (its key is inserted), klen[l]
+// = the key's bytes (0 otherwise); *bad = the first line whose key is not
+// UTF-8 (the reference's load returns Err there).
+__global__ __launch_bounds__(kNT) void k_rebuild_mark(const uint8_t* __restrict__ data,
+                                                      const LineRec* __restrict__ rec, uint64_t nlines,
+                                                      uint64_t* __restrict__ has, uint64_t* __restrict__ klen,
+                                                      unsigned long long* __restrict__ bad) {
+  const uint64_t l = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  if (l >= nlines) return;
+  const LineRec r = rec[l];
+  const bool tab = r.klen != kNoSep;
+  has[l] = tab ? 1 : 0;
+  klen[l] = tab ? r.klen : 0;
+  if (tab && !utf8_valid(data + r.start, r.klen)) atomicMin(bad, (unsigned long long)l);
+}
+
+// The TAB lines' keys packed into one ragged batch in file order: key i =
+// out[off[i] .. off[i+1]) is the key of line lmap[i].
+__global__ __launch_bounds__(kNT) void k_rebuild_gather(const uint8_t* __restrict__ data,
+                                                        const LineRec* __restrict__ rec, uint64_t nlines,
+                                                        const uint64_t* __restrict__ has_scan,
+                                                        const uint64_t* __restrict__ len_scan,
+                                                        uint8_t* __restrict__ out, uint64_t* __restrict__ off,
+                                                        uint64_t* __restrict__ lmap) {
+  const uint64_t l = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  if (l >= nlines) return;
+  if (l == nlines - 1) off[has_scan[nlines]] = len_scan[nlines];
+  const LineRec r = rec[l];
+  if (r.klen == kNoSep) return;
+  const uint64_t i = has_scan[l], o = len_scan[l];
+  off[i] = o;
+  lmap[i] = l;
+  const uint8_t* src = data + r.start;
+  for (uint32_t j = 0; j < r.klen; ++j) out[o + j] = src[j];
 }
 
 // ---- exclusive scan of uint64: one rocPRIM look-back scan over n + 1 items
@@ -320,36 +387,78 @@ __device__ __forceinline__ int64_t search_exact(const TableView& t, const Query&
   return -1;
 }
 
-// Well-formed files: lower bound of the key's prefix through the fences (an
-// L2-resident array), then inside one 64-line block of pfx, then record
-// compares only across lines that share the 8-byte prefix.
-__device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& q, LineRec& hit) {
-  uint64_t lo = 0, hi = t.nfence;
+// First index in [lo, hi) with a[i] >= x, or hi (a non-decreasing).
+__device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t* a, uint64_t lo, uint64_t hi, uint64_t x) {
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
-    if (t.fence[mid] < q.w0)
+    if (a[mid] < x)
       lo = mid + 1;
     else
       hi = mid;
   }
-  // fence[lo-1] < w0 <= fence[lo]: the lower bound is in ((lo-1)*64, lo*64]
-  uint64_t b = lo ? (lo - 1) * kFenceStride + 1 : 0;
-  uint64_t e = lo * kFenceStride < t.nlines ? lo * kFenceStride : t.nlines;
-  while (b < e) {
-    const uint64_t mid = (b + e) >> 1;
-    if (t.pfx[mid] < q.w0)
-      b = mid + 1;
-    else
-      e = mid;
+  return lo;
+}
+
+// Line l's key against the query, in a well-formed file: prefix first, then
+// the record (r receives it when the prefixes are equal).
+__device__ __forceinline__ int line_vs_query(const TableView& t, uint64_t l, const Query& q, LineRec& r) {
+  const uint64_t p = t.pfx[l];
+  if (p != q.w0) return p < q.w0 ? -1 : 1;
+  r = t.rec[l];
+  return rec_cmp(t, r, q);
+}
+
+// Well-formed files (keys strictly increasing, so any correct search returns
+// the reference's line): the lower bound of the key's 8-byte prefix through
+// fence2 (every 256th prefix, L2-resident), one 16-entry run of fence and one
+// 16-entry run of pfx (one 128-B line each), then the lines sharing that
+// prefix by a galloping search with record compares: O(log run) for keys that
+// share long prefixes ('user0000...'), one record compare when the prefix is
+// unique.
+__device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& q, LineRec& hit) {
+  // fence2[i2-1] < w0 <= fence2[i2]: the lower bound is in ((i2-1)*256, i2*256]
+  const uint64_t i2 = lower_bound_u64(t.fence2, 0, t.nfence2, q.w0);
+  const uint64_t jlo = i2 ? (i2 - 1) * (kFence2Stride / kFenceStride) + 1 : 0;
+  const uint64_t jhi = i2 * (kFence2Stride / kFenceStride) < t.nfence ? i2 * (kFence2Stride / kFenceStride) : t.nfence;
+  const uint64_t j1 = lower_bound_u64(t.fence, jlo, jhi, q.w0);
+  const uint64_t blo = j1 ? (j1 - 1) * kFenceStride + 1 : 0;
+  const uint64_t bhi = j1 * kFenceStride < t.nlines ? j1 * kFenceStride : t.nlines;
+  const uint64_t b = lower_bound_u64(t.pfx, blo, bhi, q.w0);
+  if (b >= t.nlines) return -1;
+  LineRec r;
+  int c = line_vs_query(t, b, q, r);
+  if (c == 0) {
+    hit = r;
+    return (int64_t)b;
   }
-  for (uint64_t l = b; l < t.nlines && t.pfx[l] == q.w0; ++l) {
-    const LineRec r = t.rec[l];
-    const int c = rec_cmp(t, r, q);
+  if (c > 0) return -1;
+  // every line before lo is below the query; gallop to a line above it
+  uint64_t lo = b + 1, hi = t.nlines, step = 1;
+  while (lo < t.nlines) {
+    const uint64_t p = lo + step - 1 < t.nlines ? lo + step - 1 : t.nlines - 1;
+    c = line_vs_query(t, p, q, r);
     if (c == 0) {
       hit = r;
-      return (int64_t)l;
+      return (int64_t)p;
     }
-    if (c > 0) break;
+    if (c > 0) {
+      hi = p;
+      break;
+    }
+    lo = p + 1;
+    step <<= 1;
+  }
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    c = line_vs_query(t, mid, q, r);
+    if (c == 0) {
+      hit = r;
+      return (int64_t)mid;
+    }
+    if (c < 0)
+      lo = mid + 1;
+    else
+      hi = mid;
   }
   return -1;
 }
@@ -607,6 +716,25 @@ hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, LineRec* rec, 
   ProfScope ps("k_line_keys", s);
   hipLaunchKernelGGL(k_line_keys, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, data, nlines,
                      rec, pfx, fence, ok);
+  return hipGetLastError();
+}
+
+hipError_t launch_rebuild_mark(const uint8_t* data, const LineRec* rec, uint64_t nlines, uint64_t* has,
+                               uint64_t* klen, uint64_t* bad, hipStream_t s) {
+  if (!nlines) return hipSuccess;
+  ProfScope ps("k_rebuild_mark", s);
+  hipLaunchKernelGGL(k_rebuild_mark, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, data, rec, nlines, has,
+                     klen, reinterpret_cast<unsigned long long*>(bad));
+  return hipGetLastError();
+}
+
+hipError_t launch_rebuild_gather(const uint8_t* data, const LineRec* rec, uint64_t nlines,
+                                 const uint64_t* has_scan, const uint64_t* len_scan, uint8_t* out,
+                                 uint64_t* off, uint64_t* lmap, hipStream_t s) {
+  if (!nlines) return hipSuccess;
+  ProfScope ps("k_rebuild_gather", s);
+  hipLaunchKernelGGL(k_rebuild_gather, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, data, rec, nlines,
+                     has_scan, len_scan, out, off, lmap);
   return hipGetLastError();
 }
 

@@ -17,7 +17,13 @@ namespace cb {
 
 constexpr uint32_t kNoSep = 0xFFFFFFFFu;  // line without a TAB: ends a search
 
-constexpr uint32_t kFenceStride = 64;  // lines per fence entry
+constexpr uint32_t kFenceStride = 16;    // lines per fence entry (16 x 8 B = one 128-B line)
+constexpr uint32_t kFence2Stride = 256;  // lines per level-2 fence entry
+// The fence array holds fence_count(nl) entries (pfx[16 j]) and then
+// fence2_count(nl) entries (pfx[256 i]): one allocation, two levels.
+__host__ __device__ inline uint64_t fence_count(uint64_t nl) { return (nl + kFenceStride - 1) / kFenceStride; }
+__host__ __device__ inline uint64_t fence2_count(uint64_t nl) { return (nl + kFence2Stride - 1) / kFence2Stride; }
+__host__ __device__ inline uint64_t fence_words(uint64_t nl) { return fence_count(nl) + fence2_count(nl); }
 constexpr uint32_t kBadValue = 0xFFFFFFFFu;  // value that STANDARD.decode rejects
 
 // Per-line index record (32 B, one load). vdl is computed once at index
@@ -38,14 +44,17 @@ struct alignas(16) LineRec {
 // line has a TAB and the keys are strictly increasing, as SsTable::create
 // writes it — any correct search returns what the reference's binary search
 // returns, so `fast` files are searched through pfx (each key's first 8
-// bytes, big-endian, zero-padded: monotone in the key order) and fence (every
-// 64th pfx, L2-resident). Other files replay the exact (lo+hi)/2 trajectory.
+// bytes, big-endian, zero-padded: monotone in the key order) and two fence
+// levels (every 16th pfx, and every 256th: L2-resident), so a lookup reads
+// one 128-B line of fence, one of pfx, then the record. Other files replay
+// the exact (lo+hi)/2 trajectory.
 struct TableView {
-  const uint8_t* data;   // the file, with 16 bytes of readable slack
-  const LineRec* rec;    // nlines
-  const uint64_t* pfx;   // nlines
-  const uint64_t* fence; // nfence = ceil(nlines / 64)
-  uint64_t nlines, nfence;
+  const uint8_t* data;    // the file, with 16 bytes of readable slack
+  const LineRec* rec;     // nlines
+  const uint64_t* pfx;    // nlines
+  const uint64_t* fence;  // nfence = fence_count(nlines): pfx[16 j]
+  const uint64_t* fence2; // nfence2 = fence2_count(nlines): pfx[256 i]
+  uint64_t nlines, nfence, nfence2;
   uint32_t fast;
 };
 
@@ -71,6 +80,18 @@ hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, LineRec* rec, 
 uint64_t scan_tmp_words(uint64_t n);
 hipError_t launch_scan_u64(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tmp,
                            hipStream_t s);
+
+// ---- SsTable::load's rebuild (src/sstable.rs:109-120) ----
+// has[l] = line l has a TAB, klen[l] = its key length (0 without a TAB);
+// *bad = min(*bad, first line whose key is not UTF-8).
+hipError_t launch_rebuild_mark(const uint8_t* data, const LineRec* rec, uint64_t nlines, uint64_t* has,
+                               uint64_t* klen, uint64_t* bad, hipStream_t s);
+// From the exclusive scans of has / klen (n + 1 entries each): the TAB lines'
+// keys as a ragged batch out/off (has_scan[n] keys, off has_scan[n] + 1
+// entries) and lmap[i] = the line of key i.
+hipError_t launch_rebuild_gather(const uint8_t* data, const LineRec* rec, uint64_t nlines,
+                                 const uint64_t* has_scan, const uint64_t* len_scan, uint8_t* out,
+                                 uint64_t* off, uint64_t* lmap, hipStream_t s);
 
 // ---- resolution ----
 // line[k] = SsTable::binary_search(key k) over one table, or -1.

@@ -750,3 +750,25 @@ void ob_gen_keys(uint64_t seed, uint64_t first, uint64_t n, uint8_t* out) {
     for (int d = 0; d < 16; ++d) o[d] = (uint8_t)hex[(v >> (60 - 4 * d)) & 15];
   }
 }
+
+int ob_table_rebuild(const ob_table* t, uint64_t m, ob_filter* bloom, ob_zone* zone, uint64_t* bad_line) {
+  /* src/sstable.rs:110-120 */
+  int rc = ob_new(bloom, m); /* BloomFilter::new(1024) in the reference; m here */
+  if (rc) return rc;
+  ob_zone_init(zone);
+  if (bad_line) *bad_line = UINT64_MAX;
+  for (uint64_t l = 0; l < t->nlines; ++l) {
+    const uint8_t* line = t->data + t->start[l];
+    const uint64_t n = t->end[l] - t->start[l];
+    const uint8_t* tab = memchr(line, '\t', n);
+    if (!tab) continue; /* `if let Some(pos)`: lines without SEP are skipped */
+    const uint64_t kl = (uint64_t)(tab - line);
+    if (!ob_utf8_valid(line, kl)) { /* from_utf8(..).map_err(..)? */
+      if (bad_line) *bad_line = l;
+      return OB_EUTF8;
+    }
+    if ((rc = ob_insert(bloom, line, kl))) return rc;
+    if ((rc = ob_zone_update(zone, line, kl))) return rc;
+  }
+  return OB_OK;
+}

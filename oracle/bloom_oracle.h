@@ -35,6 +35,7 @@ extern "C" {
 #define OB_EZEROM (-2)   /* reference panics: `h % 0` at src/bloom.rs:36 */
 #define OB_ENOMEM (-3)
 #define OB_EDECODE (-5)  /* reference panics: `decode(..).unwrap()` at src/bloom.rs:75 */
+#define OB_EUTF8 (-7)    /* SsTable::load returns Err: a data-file key is not UTF-8 */
 
 typedef struct ob_filter {
   uint8_t* bits; /* m bytes, each 0 or 1 — the Vec<bool> layout */
@@ -138,6 +139,14 @@ void ob_table_free(ob_table* t);
  * which ends the search). *val / *val_len: the bytes after the TAB. */
 int64_t ob_table_search(const ob_table* t, const uint8_t* key, uint64_t klen, uint64_t* val,
                         uint64_t* val_len);
+/* SsTable::load's rebuild when the `.meta` file is missing or undecodable
+ * (src/sstable.rs:109-120): a fresh BloomFilter of m bits and ZoneMap; for
+ * every non-empty line in file order that has a TAB, key = the bytes before
+ * the first TAB; a key that is not UTF-8 ends the load with an error
+ * (OB_EUTF8, *bad_line = that line); otherwise bloom.insert(key) and
+ * zone_map.update(key). Lines without a TAB are skipped. bloom and zone are
+ * initialised here; free them with ob_free / ob_zone_free. */
+int ob_table_rebuild(const ob_table* t, uint64_t m, ob_filter* bloom, ob_zone* zone, uint64_t* bad_line);
 /* base64 0.21.7 STANDARD engine (the reference's `STANDARD.decode`,
  * src/sstable.rs:148): alphabet A-Z a-z 0-9 + /, canonical '=' padding
  * required (length % 4 == 0), non-zero trailing bits rejected. Returns the

@@ -99,6 +99,7 @@ def lib():
         L.ob_b64_encode.argtypes = [P, u64, P]
         L.ob_b64_encode.restype = u64
         L.ob_get_many.argtypes = [P, u32, P, P, P, u64, P, P, P, u64, ctypes.POINTER(u64)]
+        L.ob_table_rebuild.argtypes = [TP, u64, FP, ZP, ctypes.POINTER(u64)]
         L.ob_sstable_create.argtypes = [P, P, P, P, u64, P, u64]
         L.ob_sstable_create.restype = u64
         L.ob_gen_keys.argtypes = [u64, u64, u64, P]
@@ -333,6 +334,23 @@ class OracleTable:
     @property
     def nlines(self) -> int:
         return int(self._t.nlines)
+
+    def rebuild(self, m: int = 1024):
+        """SsTable::load's rebuild (src/sstable.rs:109-120): (OracleFilter,
+        OracleZone) from the lines' keys, or raises UnicodeDecodeError-like
+        ValueError(bad line) when a key is not UTF-8."""
+        raw = _Filter()
+        z = OracleZone()
+        lib().ob_zone_free(ctypes.byref(z._z))
+        bad = ctypes.c_uint64()
+        rc = lib().ob_table_rebuild(ctypes.byref(self._t), m, ctypes.byref(raw), ctypes.byref(z._z),
+                                    ctypes.byref(bad))
+        f = OracleFilter(m, _raw=raw)
+        if rc == -7:
+            raise ValueError(f"key on line {bad.value} is not UTF-8")
+        if rc:
+            raise RuntimeError(rc)
+        return f, z
 
     def search(self, key: bytes):
         """SsTable::binary_search: (line index, encoded value bytes) or (-1, None)."""

@@ -239,3 +239,81 @@ def test_get_many_value_lengths(gpu):
             assert which[i] == 0 and got[voff[i]:voff[i + 1]] == vals[i], k
         else:
             assert which[i] < 0 and voff[i] == voff[i + 1]
+
+
+def test_search_shared_prefixes(gpu):
+    """Keys that share their first 8+ bytes ('user0000...'): the fast search
+    resolves them through the records (galloping over the equal-prefix run,
+    src/sstable.rs:161-179's answer either way), for runs of 1 to 200k lines,
+    keys of 8 to 40 bytes, and probes between, before, after and equal to a
+    prefix of the lines' keys."""
+    rng = np.random.default_rng(11)
+    keys = set()
+    keys.update(b"user0000" + b"%09d" % i for i in range(0, 400_000, 2))       # a 200k-line run, 17-B keys
+    keys.update(b"acct%04d" % g + b"%06x" % j for g in range(40) for j in range(g * g + 1))  # runs of 1..1522
+    keys.update(b"k" * 8 + bytes(rng.integers(97, 123, rng.integers(0, 33), dtype=np.uint8)) for _ in range(3000))
+    keys.update(b"zz%06d" % i for i in range(5000))                             # exactly 8 bytes
+    keys = sorted(keys)
+    data = oracle.sstable_create([(k, b"v%d" % i) for i, k in enumerate(keys)])
+    t = gpu.Table(data)
+    assert t.well_formed
+    ot = oracle.OracleTable(data)
+    present = [keys[i] for i in rng.integers(0, len(keys), 6000)]
+    absent = ([b"user0000" + b"%09d" % i for i in range(1, 40_000, 37)] +          # odd: between lines
+              [b"user0000", b"user000", b"user00000", b"acct0003", b"a", b"", b"zz", b"zzz", b"\xff" * 20] +
+              [k + b"\x00" for k in present[:500]] + [k[:-1] for k in present[:500] if len(k) > 8])
+    look = present + absent
+    d, o = var(look)
+    got = t.search(gpu.KeyBatch(n=len(look), data=d, offsets=o))
+    exp = [ot.search(k)[0] for k in look]
+    assert list(got) == exp
+    assert (np.array(exp[:len(present)]) >= 0).all()
+    # and through get_many (values decode from the found lines)
+    which, voff, vals = gpu.get_many([t], gpu.KeyBatch(n=len(look), data=d, offsets=o))
+    ow, ovoff, ovals = oracle.get_many([ot], None, d, o)
+    assert np.array_equal(which, ow) and vals == ovals
+
+
+def _check_rebuild(gpu, data: bytes, m: int):
+    t = gpu.Table(data)
+    ot = oracle.OracleTable(data)
+    try:
+        of, oz = ot.rebuild(m)
+    except ValueError:
+        with pytest.raises(UnicodeDecodeError):
+            t.rebuild(m)
+        return None
+    f, z = t.rebuild(m)
+    assert f.m == m
+    assert np.array_equal(f.bools(), of.bools())
+    assert (z.min, z.max) == oz.bounds
+    return f, z
+
+
+@pytest.mark.parametrize("m", [1024, 100003, 1 << 22])
+def test_table_rebuild_vs_oracle(gpu, m):
+    """SsTable::load without a usable .meta (src/sstable.rs:109-120): the
+    filter and zone map rebuilt on the device from the data file equal the
+    oracle's restatement: well-formed files, files with TAB-less and empty
+    lines, unsorted files, empty keys, multi-byte UTF-8 keys, and files whose
+    keys are not UTF-8 (the load fails)."""
+    rng = np.random.default_rng(m % 97)
+    keys = workload.key_range(3100, 50_000)
+    _check_rebuild(gpu, workload.sstable_bytes(keys, workload.table_value(keys, 1)).tobytes(), m)
+    # unsorted, TAB-less and empty lines, empty keys, tabs inside values
+    lines = [b"%s\tQQ==" % bytes(k) for k in keys[:3000]][::-1]
+    lines += [b"no separator here", b"", b"\tempty-key", b"k\twith\ttabs", b"\t", b"zz\t"]
+    rng.shuffle(lines)
+    _check_rebuild(gpu, b"\n".join(lines) + b"\n", m)
+    # multi-byte UTF-8 keys (2-, 3- and 4-byte sequences) and a file with no final newline
+    uk = ["é", "日本", "𝄞x", "a߿", "퟿", "\U0010ffff"]
+    _check_rebuild(gpu, b"\n".join(k.encode() + b"\tQQ==" for k in uk), m)
+    # no TAB anywhere, and an empty file: an empty filter, no zone bounds
+    r = _check_rebuild(gpu, b"just\nlines\n", m)
+    assert r[1].min is None and not r[0].bools().any()
+    # keys that are not UTF-8: overlong, surrogate, > U+10FFFF, truncated, bare continuation
+    for bad in (b"\xc0\xaf", b"\xed\xa0\x80", b"\xf4\x90\x80\x80", b"\xe6\x97", b"\x80", b"ok\xff"):
+        data = b"a\tQQ==\n" + bad + b"\tQQ==\nno-tab-\xff-line\n"
+        assert _check_rebuild(gpu, data, m) is None, bad
+    # invalid bytes on a TAB-less line or after the TAB do not matter
+    assert _check_rebuild(gpu, b"\xff\xfe\nk\t\xff\n", m) is not None
