@@ -514,7 +514,7 @@ def main():
                 step_flush()
             k_fl = max(3, args.steps // 4)
             fel = timed(step_flush, k_fl)
-            fprof = kernel_ms(["k_sorted_check", "k_sort_keys", "rocprim_merge_sort", "k_line_sums", "k_tile_scan",
+            fprof = kernel_ms(["k_sorted_check", "k_sort_keys", "k_entry_sort", "rocprim_merge_sort", "k_line_sums", "k_tile_scan",
                                "k_format", "k_line_count", "k_line_emit", "k_line_finish", "k_line_keys",
                                "k_build_part", "k_build_tile", "k_insert_direct"], step_flush, k_fl)
             out_bytes = made[-1][0].nbytes

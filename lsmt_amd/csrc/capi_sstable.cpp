@@ -4,6 +4,8 @@
 // Database::get's newest-first walk (cb_get_many_*).
 //
 // Reference: /root/reference/src/sstable.rs:51-179, src/lib.rs:125-136.
+#include <cstdlib>
+
 #include "capi_internal.hpp"
 
 using namespace cbx;
@@ -353,13 +355,20 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
     HIP_TRY(ws.f_sk2.reserve(n * sizeof(cb::SortKey), s));
     cb::SortKey* a0 = (cb::SortKey*)ws.f_sk.p;
     cb::SortKey* a1 = (cb::SortKey*)ws.f_sk2.p;
-    // (rocPRIM's radix sort in three LSD passes over (len, w1, w0) when every
-    // key is <= 16 bytes was measured no faster at 1M entries: 573 vs 577 us)
     HIP_TRY(cb::launch_sort_keys(dk, dko, n, a0, s));
-    size_t tmp_bytes = 0;
-    HIP_TRY(cb::entry_sort(nullptr, tmp_bytes, a0, a1, n, dk, dko, s));
-    HIP_TRY(ws.f_sort.reserve(tmp_bytes + 16, s));
-    HIP_TRY(cb::entry_sort(ws.f_sort.p, tmp_bytes, a0, a1, n, dk, dko, s));
+    static const bool use_rocprim = [] {
+      const char* v = getenv("CB_SORT");
+      return v && std::strcmp(v, "rocprim") == 0;
+    }();
+    if (use_rocprim) {  // rocPRIM's merge sort, for comparison (same order)
+      size_t tmp_bytes = 0;
+      HIP_TRY(cb::entry_sort(nullptr, tmp_bytes, a0, a1, n, dk, dko, s));
+      HIP_TRY(ws.f_sort.reserve(tmp_bytes + 16, s));
+      HIP_TRY(cb::entry_sort(ws.f_sort.p, tmp_bytes, a0, a1, n, dk, dko, s));
+    } else {
+      HIP_TRY(ws.f_sort.reserve(cb::entry_sort_tmp_bytes(n), s));
+      HIP_TRY(cb::launch_entry_sort(a0, a1, (cb::SortKey*)ws.f_sort.p, n, dk, dko, s));
+    }
     order = a1;
   }
   if (order) HIP_TRY(cb::launch_line_sums(order, dko, dvo, n, tsum, s));

@@ -42,8 +42,14 @@ hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, const uint
 // tsum = the line tiles in the order of the sort records.
 hipError_t launch_line_sums(const SortKey* order, const uint64_t* ko, const uint64_t* vo, uint64_t n,
                             uint64_t* tsum, hipStream_t s);
-// Stable sort of the records by key (rocPRIM merge sort). tmp == nullptr:
-// only writes the scratch size to tmp_bytes.
+// Stable sort of the records by key, hand-written (sort.hip): LDS block
+// sorts of 2048 records, then merge-path rounds. tmp: entry_sort_tmp_bytes(n)
+// of scratch; in must not alias out or tmp.
+uint64_t entry_sort_tmp_bytes(uint64_t n);
+hipError_t launch_entry_sort(const SortKey* in, SortKey* out, SortKey* tmp, uint64_t n, const uint8_t* kb,
+                             const uint64_t* ko, hipStream_t s);
+// The same order through rocPRIM's merge sort (kept for comparison,
+// CB_SORT=rocprim). tmp == nullptr: only writes the scratch size to tmp_bytes.
 hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* out, uint64_t n,
                       const uint8_t* kb, const uint64_t* ko, hipStream_t s);
 // The file (lines at the offsets tsum and the line lengths give, then 16

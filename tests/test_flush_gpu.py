@@ -178,3 +178,32 @@ def test_table_zone_only_for_created_tables(gpu):
     assert ez.min is None and ez.max is None
     with pytest.raises(CassBloomError):
         e._zone(1)
+
+
+@pytest.mark.parametrize("n,shape", [(2, "random"), (2047, "random"), (2048, "descending"), (2049, "random"),
+                                     (6145, "equal"), (70_001, "long"), (300_001, "random"),
+                                     (1 << 20, "descending")])
+def test_create_sort_sizes(gpu, n, shape):
+    """The hand-written stable sort of unsorted flush batches (sort.hip: LDS
+    block sorts of 2048 records, then merge-path rounds) across tile and
+    round boundaries: random keys, reversed keys, all-equal keys (pure
+    stability) and long keys sharing 16-byte prefixes; the file must equal
+    the oracle's stable sort + format (src/sstable.rs:57-72)."""
+    rng = np.random.default_rng(n)
+    if shape == "equal":
+        keys = [b"same-key"] * n
+    elif shape == "long":
+        pre = [bytes(rng.integers(97, 100, 16, dtype=np.uint8)) for _ in range(7)]
+        keys = [pre[i % 7] + bytes(rng.integers(97, 99, rng.integers(0, 12), dtype=np.uint8)) for i in range(n)]
+    else:
+        k = workload.key_range(5000 + n, n)
+        if shape == "descending":
+            k = workload.sort_keys16(k)[::-1]
+        keys = [bytes(r) for r in k]
+        if shape == "random":  # some duplicates and short keys mixed in
+            for i in rng.integers(0, n, n // 10):
+                keys[i] = keys[rng.integers(0, n)][: rng.integers(0, 17)]
+    vals = [(i % 65536).to_bytes(2, "little") for i in range(n)]
+    t, _, zone = gpu.sstable_create(list(zip(keys, vals)))
+    assert t.data() == oracle.sstable_create(list(zip(keys, vals)))
+    assert (zone.min, zone.max) == (min(keys), max(keys))
