@@ -41,8 +41,8 @@ def parse():
                    help="c3: 1M keys x 32 filters/GPU probe (default, the BASELINE metric); "
                         "c5: 10M keys x 32 filters/GPU probe; c4: 64 concurrent builds of 256K keys "
                         "(m=2^25) split over the GPUs")
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--n-keys", type=int, default=1 << 20)
     p.add_argument("--filters", type=int, default=32, help="filters per GPU")
     p.add_argument("--m-bits", type=int, default=1 << 26)
@@ -427,6 +427,14 @@ def main():
                 "note": "C3 tables hold random keys, so every zone spans ~the whole key space: "
                         "this measures the gate's cost; tests/test_zone_gpu.py covers rejection"}
 
+    # ---- the zone gate where it rejects: range-partitioned tables (an L1-L4
+    # style level, each table holding a contiguous key range), so exactly one
+    # zone contains any key and the gate clears every Bloom false positive
+    # of the other tables (src/sstable.rs:138, src/zonemap.rs:37-42)
+    if not args.no_zone and rank == 0 and world == 1:
+        zone["partitioned"] = zone_partitioned_leg(args, torch, dev, local, sh, F, m, kpf, n, timed, kernel_ms,
+                                                   probes_per_step, lsmt_amd, workload)
+
     # ---- read path: the C3 tables as real SSTable data
     # files in HBM; one step = gated probe + Database::get's newest-first walk
     # (binary search of the candidates, base64 decode of the found values)
@@ -758,6 +766,71 @@ def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result):
     if use_dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def zone_partitioned_leg(args, torch, dev, local, sh, F, m, kpf, n, timed, kernel_ms, probes_per_step,
+                         lsmt_amd, workload):
+    """Gated FilterSet probe over F range-partitioned tables: the F * kpf
+    keys of seed 4000 sorted and cut into F contiguous ranges (table f = the
+    f-th range, its ZoneMap = [first, last key]); lookups: half present keys
+    (key j of table j mod F), half absent keys. Reports gated probes/s, the
+    fraction of Bloom-passing (key, table) pairs the zones reject, and a
+    check of the first 64K lookups' gated hits against the oracle's
+    zone.contains && may_contain (ob_probe_gated_var)."""
+    allk = workload.sort_keys16(workload.key_range(4000, F * kpf))
+    parts = [allk[f * kpf:(f + 1) * kpf] for f in range(F)]
+    filters = []
+    for p in parts:
+        b = lsmt_amd.BloomFilter(m, device=local)
+        b.insert_batch(lsmt_amd.DeviceKeys(torch.from_numpy(p).to(dev)), stream=sh)
+        filters.append(b)
+    fset = lsmt_amd.FilterSet(m, width=32 if F <= 32 else 64, device=local)
+    fset.assign_all(filters, stream=sh)
+    for f, p in enumerate(parts):
+        fset.zone_from_keys(f, lsmt_amd.DeviceKeys(torch.from_numpy(p).to(dev)), stream=sh)
+    j = np.arange(n // 2 + n % 2)
+    look_np = np.empty((n, 16), np.uint8)
+    look_np[0::2] = allk[(j % F) * kpf + (j // F) % kpf]
+    look_np[1::2] = workload.key_range(4999, n // 2)
+    keys = lsmt_amd.DeviceKeys(torch.from_numpy(look_np).to(dev))
+    words = (n + 63) // 64
+    gated = torch.zeros((F, words), dtype=torch.int64, device=dev)
+    plain = torch.zeros((F, words), dtype=torch.int64, device=dev)
+    fset.probe(keys, out=plain, stream=sh)
+
+    def step():
+        fset.probe(keys, out=gated, stream=sh, gated=True)
+
+    for _ in range(args.warmup):
+        step()
+    el = timed(step, args.steps)
+    prof = kernel_ms(["k_set_probe_gated"], step, args.steps)
+    torch.cuda.synchronize(dev)
+    g = gated.cpu().numpy().view(np.uint64)
+    pl = plain.cpu().numpy().view(np.uint64)
+    bits = lambda a: int(np.unpackbits(a.view(np.uint8)).sum())
+    bloom_pass, gate_pass = bits(pl), bits(g)
+    out = {"value": round(probes_per_step / (el / args.steps), 1), "unit": "gated probes/s",
+           "ms_per_step": round(el / args.steps * 1e3, 4),
+           "kernels_us": {k: round(v["avg_us"], 2) for k, v in prof.items()},
+           "bloom_pass_pairs": bloom_pass, "gate_pass_pairs": gate_pass,
+           "zone_rejected_fraction_of_bloom_pass": round(1 - gate_pass / max(bloom_pass, 1), 4),
+           "tables": f"{F} range-partitioned tables of {kpf} keys (sorted key(4000, i) cut in {F})"}
+    if not args.no_cpu:  # oracle check on a sample (CPU restatement as the checker only)
+        from oracle import oracle
+        sample = 1 << 16
+        refs = []
+        for p in parts:
+            o = oracle.OracleFilter(m)
+            o.insert_fixed(p)
+            refs.append(o)
+        zones = [oracle.OracleZone(bytes(p[0]), bytes(p[-1])) for p in parts]
+        d = np.ascontiguousarray(look_np[:sample].reshape(-1))
+        offs = np.arange(0, 16 * (sample + 1), 16, dtype=np.uint64)
+        exp = oracle.probe_gated(refs, zones, d, offs)
+        out["oracle_sample_bit_exact"] = bool(np.array_equal(g[:, :sample // 64], exp))
+        del refs
+    return out
 
 
 def _set_sectors(filters, look_np, m, F):
