@@ -425,7 +425,7 @@ def main():
                 "zone_build_keys_per_s": round(F * kpf / zone_build_s, 1),
                 "gated_hits_last_step": gated_hits,
                 "note": "C3 tables hold random keys, so every zone spans ~the whole key space: "
-                        "this measures the gate's cost; tests/test_zone_gpu.py covers rejection"}
+                        "this measures the gate's cost; 'partitioned' measures it where it rejects"}
 
     # ---- the zone gate where it rejects: range-partitioned tables (an L1-L4
     # style level, each table holding a contiguous key range), so exactly one

@@ -28,6 +28,28 @@ def main():
     if stats:
         for r in csv.DictReader(open(stats[0])):
             dur[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3}
+    # busy time per launch: the union of each kernel's [start, end) intervals
+    # over its dispatches, / dispatches (= the average duration when launches
+    # do not overlap; the per-step share when pipeline lanes overlap them)
+    busy = {}
+    traces = glob.glob(os.path.join(root, "kt", "*kernel_trace.csv"))
+    if traces:
+        iv = collections.defaultdict(list)
+        for r in csv.DictReader(open(traces[0])):
+            iv[short(r["Kernel_Name"])].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+        for k, lst in iv.items():
+            lst.sort()
+            tot, cur_s, cur_e = 0, None, None
+            for s0, e0 in lst:
+                if cur_e is None or s0 > cur_e:
+                    if cur_e is not None:
+                        tot += cur_e - cur_s
+                    cur_s, cur_e = s0, e0
+                else:
+                    cur_e = max(cur_e, e0)
+            if cur_e is not None:
+                tot += cur_e - cur_s
+            busy[k] = tot / len(lst) / 1e3
     ctr = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(root, "pmc*", "*counter_collection.csv")):
         per = collections.defaultdict(float)
@@ -39,6 +61,8 @@ def main():
     for k in sorted(set(dur) | set(ctr)):
         c = {n: sum(v) / len(v) for n, v in ctr[k].items()}
         e = {"avg_us": round(dur.get(k, {}).get("avg_us", 0.0), 3), "calls": dur.get(k, {}).get("calls", 0)}
+        if k in busy:
+            e["busy_us_per_launch"] = round(busy[k], 3)
         e.update({n: round(v, 1) for n, v in c.items()})
         if all(n in c for n in ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")):
             rd = 32 * c["TCC_EA0_RDREQ_32B_sum"] + 64 * c["TCC_EA0_RDREQ_64B_sum"] + 128 * c["TCC_EA0_RDREQ_128B_sum"]
@@ -47,8 +71,9 @@ def main():
             e["write_bytes"] = int(c["WRITE_SIZE"] * 1024)
         if "read_bytes" in e and "write_bytes" in e:
             e["hbm_bytes_per_launch"] = e["read_bytes"] + e["write_bytes"]
-            if e["avg_us"]:
-                e["hbm_GBps"] = round(e["hbm_bytes_per_launch"] / (e["avg_us"] * 1e3), 1)
+            t = e.get("busy_us_per_launch") or e["avg_us"]
+            if t:
+                e["hbm_GBps"] = round(e["hbm_bytes_per_launch"] / (t * 1e3), 1)
         res[k] = e
     for k, e in res.items():
         print(k, json.dumps(e))

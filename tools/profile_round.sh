@@ -7,8 +7,13 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-BENCH="python bench.py --no-cpu --no-e2e --no-cold --steps 10 --warmup 2 $*"
+# the trace pass runs the bench as configured (two pipeline lanes: launches
+# overlap, so per-dispatch durations are ~2x the per-step share; pmc_summary
+# reports the union of each kernel's busy intervals per launch beside them);
+# the PMC passes run one lane so every dispatch's counters are its own
+BENCH="python bench.py --no-cpu --no-e2e --no-cold --steps 50 --warmup 5 $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $BENCH > $OUT/kt_bench.json 2> $OUT/kt.err || exit 1
+BENCH="$BENCH --probe-streams 1"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum" "TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_DRAM_sum"; do
   i=$((i+1))
