@@ -544,13 +544,16 @@ def main():
                                      "sample": f"oracle sstable_create on {sample} unsorted entries (file only)"}
 
     # ---- C2 build: 1M keys -> one fresh 16 MiB filter (zero-fill + batched insert)
+    # (a step builds one fresh filter; consecutive steps go to the pipeline
+    # lanes, each lane with its own filter, stream and workspace)
     bk = torch.from_numpy(workload.c2_build_keys(args.build_keys)).to(dev)
-    bf = lsmt_amd.BloomFilter(args.build_m_bits, device=local)
+    bfs = [lsmt_amd.BloomFilter(args.build_m_bits, device=local) for _ in range(P)]
     bkb = lsmt_amd.DeviceKeys(bk)
 
     def build_step():
-        bf.clear(stream=sh)
-        bf.insert_batch(bkb, stream=sh)
+        i = claim()
+        bfs[i].clear(stream=lane_sh[i])
+        bfs[i].insert_batch(bkb, stream=lane_sh[i])
 
     for _ in range(args.warmup):
         build_step()
@@ -564,6 +567,12 @@ def main():
         bclean_ms, bclean_k = cold_run(["k_build_part", "k_build_tile", "k_insert_direct"], build_step, clean=True)
         bcold["clean_caches"] = {"value": round(args.build_keys * world / (bclean_ms * 1e-3), 1),
                                  "ms_per_step": round(bclean_ms, 4), "kernels_us": bclean_k}
+    if args.check:  # every lane's filter holds the C2 bits
+        from oracle import oracle
+        o = oracle.OracleFilter(args.build_m_bits)
+        o.insert_fixed(workload.c2_build_keys(args.build_keys))
+        assert all(np.array_equal(f.bools(), o.bools()) for f in bfs), "C2 build differs from the oracle"
+        del o
     b_alg = 16 * args.build_keys + args.build_m_bits / 8
     build = {"metric": "build keys/s (C2: 1M 16-B keys -> one 16 MiB filter, m=2^27)",
              "value": round(args.build_keys * world / (bel / args.steps), 1), "unit": "keys/s",
@@ -571,7 +580,7 @@ def main():
              "kernels": {k: round(v["avg_us"], 2) for k, v in bprof.items()},
              "algorithmic_bytes": int(b_alg),
              "step_effective_GBps": round(b_alg / (bel / args.steps) / 1e9, 1),
-             "cold": bcold}
+             "pipeline_lanes": P, "cold": bcold}
 
     # ---- PCIe-inclusive end-to-end probe (pinned host keys -> host hits)
     e2e = None
@@ -717,15 +726,22 @@ def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result):
     from lsmt_amd.shard import shard_range
     nf_total, kpf, m = 64, 1 << 18, 1 << 25
     lo, hi = shard_range(nf_total, world, rank)
-    sh = torch.cuda.current_stream(dev).cuda_stream
+    # pipeline lanes as in the probe: consecutive steps alternate between P
+    # sets of this GPU's filters, each set on its own stream
+    P = args.probe_streams
+    lanes = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(P - 1)]
     keys = [torch.from_numpy(workload.c4_filter_keys(f, kpf)).to(dev) for f in range(lo, hi)]
-    fs = [lsmt_amd.BloomFilter(m, device=local) for _ in range(lo, hi)]
+    fsets = [[lsmt_amd.BloomFilter(m, device=local) for _ in range(lo, hi)] for _ in range(P)]
     batches = [lsmt_amd.DeviceKeys(k) for k in keys]
+    nstep = [0]
 
     def step():
-        for f in fs:
+        i = nstep[0] % P
+        nstep[0] += 1
+        sh = lanes[i].cuda_stream
+        for f in fsets[i]:
             f.clear(stream=sh)
-        lsmt_amd.insert_many(fs, batches, stream=sh)
+        lsmt_amd.insert_many(fsets[i], batches, stream=sh)
 
     for _ in range(args.warmup):
         step()
@@ -735,7 +751,7 @@ def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(dev)
+    torch.cuda.synchronize(dev)  # every lane
     if use_dist:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -745,10 +761,10 @@ def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result):
         el = float(t.item())
     if args.check and rank == 0:
         from oracle import oracle
-        for i, f in enumerate(fs[:4]):
+        for i in range(min(4, hi - lo)):
             o = oracle.OracleFilter(m)
             o.insert_fixed(workload.c4_filter_keys(lo + i, kpf))
-            assert np.array_equal(f.bools(), o.bools()), "C4 build differs from the oracle"
+            assert all(np.array_equal(fl[i].bools(), o.bools()) for fl in fsets), "C4 build differs from the oracle"
         log("[check] C4 filters bit-exact vs oracle")
     if rank == 0:
         alg = nf_total * (16 * kpf + m / 8)
@@ -758,7 +774,7 @@ def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result):
                 "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
                 "data": "synthetic (splitmix64 hex keys, SURVEY.md §8d)",
                 "config": {"workload": "C4: 64 filters x 2^18 keys -> m=2^25 each, one subset per GPU",
-                           "parallelism": "filter-sharded, no collective"},
+                           "parallelism": "filter-sharded, no collective", "pipeline_lanes": P},
                 "algorithmic_bytes_total": int(alg),
                 "step_effective_GBps_all_gpus": round(alg / (el / args.steps) / 1e9, 1),
                 "cpu_baseline": c4_cpu_baseline(nf_total, kpf, m) if world == 1 and not args.no_cpu else None}
