@@ -376,6 +376,12 @@ def main():
                 "kernel_avg_us_per_launch_events": round(kprof[dominant]["avg_us"], 2),
                 "algorithmic_bytes": int(alg_bytes), "algorithmic_def": alg_def,
                 "step_effective_GBps": round(alg_bytes / (el / args.steps) / 1e9, 1)}
+        if roof["traffic"]:  # the memory-side bytes the kernel moves (PMC), at the same time per launch
+            roof["traffic_GBps"] = round(roof["traffic"] / dur_s / 1e9, 1)
+            roof["traffic_frac"] = round(roof["traffic"] / dur_s / 1e9 / HBM_PEAK_GBS, 4)
+            roof["traffic_note"] = ("every random 4-B set read fills a whole 128-B L2 line (PMC: TCC_EA0_RDREQ_128B), "
+                                    "so the fabric moves ~2.2x the algorithmic bytes; hipDeviceMallocUncached "
+                                    "memory and non-temporal loads fetch the same (profiles/ubench_random_r01.json)")
         if best == "filterset":
             rr = _random_read_roofline()
             if rr:

@@ -69,14 +69,12 @@ struct cb_table {
   size_t data_cap = 0, rec_cap = 0;  // pool block sizes
   cb::LineRec* rec = nullptr;   // per-line index record
   uint64_t* pfx = nullptr;      // per-line 8-byte key prefix
-  uint64_t* fence = nullptr;    // every 64th prefix
-  uint64_t nfence = 0;
+  uint64_t* fence = nullptr;    // the fence levels above pfx (sstable.hpp)
   bool fast = false;  // well-formed: TAB on every line, keys strictly increasing
   bool has_zone = false;   // made by cb_sstable_create with n >= 1
   std::string zmin, zmax;  // its ZoneMap bounds (first / last key of the file)
   cb::TableView view() const {
-    return cb::TableView{data, rec, pfx, fence, fence ? fence + nfence : nullptr, nlines, nfence,
-                         cb::fence2_count(nlines), fast ? 1u : 0u};
+    return cb::TableView{data, rec, pfx, fence, nlines, cb::fence_levels(nlines), fast ? 1u : 0u};
   }
 };
 

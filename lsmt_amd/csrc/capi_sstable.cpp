@@ -145,7 +145,6 @@ int index_table(cb_table* t, hipStream_t s) {
   HIP_TRY(hipStreamSynchronize(s));
   if (!t->nlines) return CB_OK;
   const uint64_t nl = t->nlines;
-  t->nfence = cb::fence_count(nl);
   const size_t bytes = nl * sizeof(cb::LineRec) + nl * 8 + cb::fence_words(nl) * 8;
   if (pool_alloc(t->device, bytes, (void**)&t->rec, &t->rec_cap) != hipSuccess) {
     t->rec = nullptr;
@@ -375,7 +374,6 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
   // the line index straight from the entries (entry p is line p), no re-read of the file
   t->nlines = n;
-  t->nfence = cb::fence_count(n);
   const size_t ibytes = n * sizeof(cb::LineRec) + n * 8 + cb::fence_words(n) * 8;
   if (pool_alloc(device, ibytes, (void**)&t->rec, &t->rec_cap) != hipSuccess) {
     t->rec = nullptr;
@@ -412,7 +410,7 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
     pool_release(device, t->rec, t->rec_cap);
     t->rec = nullptr;
     t->pfx = t->fence = nullptr;
-    t->nlines = t->nfence = 0;
+    t->nlines = 0;
     lk.unlock();  // index_table takes the workspace itself
     if ((rc = index_table(t.get(), s))) return rc;
   } else {

@@ -336,8 +336,7 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
     lr.pad = 0;
     rec[p] = lr;
     pfx[p] = w0;
-    if (p % kFenceStride == 0) fence[p / kFenceStride] = w0;
-    if (p % kFence2Stride == 0) fence[fence_count(n) + p / kFence2Stride] = w0;
+    fence_put(fence, n, p, w0);
     if (p > 0) not_inc = key_cmp(kb, ko, pi, pkl, pw0, pw1, i, kl, w0, w1) >= 0;
   }
   if (__syncthreads_or(special) && threadIdx.x == 0) atomicOr(&r->flags[1], 1u);

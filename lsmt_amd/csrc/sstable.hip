@@ -12,6 +12,8 @@
 // gathers its candidate tables first and then searches its own next
 // candidate, so a wave's lanes search different tables concurrently.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
@@ -216,8 +218,7 @@ __global__ __launch_bounds__(kNT) void k_line_keys(const uint8_t* __restrict__ d
   }
   if (live) {
     pfx[l] = v;
-    if (l % kFenceStride == 0) fence[l / kFenceStride] = v;
-    if (l % kFence2Stride == 0) fence[fence_count(nlines) + l / kFence2Stride] = v;
+    fence_put(fence, nlines, l, v);
     if (good && l > 0) {
       const LineRec q = rec[l - 1];  // start/klen only: written by k_line_finish
       good = q.klen != kNoSep && bytes_cmp(data + q.start, q.klen, p, r.klen) < 0;
@@ -408,23 +409,9 @@ __device__ __forceinline__ int line_vs_query(const TableView& t, uint64_t l, con
   return rec_cmp(t, r, q);
 }
 
-// Well-formed files (keys strictly increasing, so any correct search returns
-// the reference's line): the lower bound of the key's 8-byte prefix through
-// fence2 (every 256th prefix, L2-resident), one 16-entry run of fence and one
-// 16-entry run of pfx (one 128-B line each), then the lines sharing that
-// prefix by a galloping search with record compares: O(log run) for keys that
-// share long prefixes ('user0000...'), one record compare when the prefix is
-// unique.
-__device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& q, LineRec& hit) {
-  // fence2[i2-1] < w0 <= fence2[i2]: the lower bound is in ((i2-1)*256, i2*256]
-  const uint64_t i2 = lower_bound_u64(t.fence2, 0, t.nfence2, q.w0);
-  const uint64_t jlo = i2 ? (i2 - 1) * (kFence2Stride / kFenceStride) + 1 : 0;
-  const uint64_t jhi = i2 * (kFence2Stride / kFenceStride) < t.nfence ? i2 * (kFence2Stride / kFenceStride) : t.nfence;
-  const uint64_t j1 = lower_bound_u64(t.fence, jlo, jhi, q.w0);
-  const uint64_t blo = j1 ? (j1 - 1) * kFenceStride + 1 : 0;
-  const uint64_t bhi = j1 * kFenceStride < t.nlines ? j1 * kFenceStride : t.nlines;
-  const uint64_t b = lower_bound_u64(t.pfx, blo, bhi, q.w0);
-  if (b >= t.nlines) return -1;
+// The lines from b on that share the query's prefix, by a galloping search
+// with record compares (b: the prefix's lower bound, < nlines).
+__device__ __forceinline__ int64_t resolve_from(const TableView& t, const Query& q, uint64_t b, LineRec& hit) {
   LineRec r;
   int c = line_vs_query(t, b, q, r);
   if (c == 0) {
@@ -461,6 +448,37 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
       hi = mid;
   }
   return -1;
+}
+
+// Level j's array (0: pfx).
+__device__ __forceinline__ const uint64_t* level_array(const TableView& t, uint32_t j) {
+  return j ? t.fence + level_offset(t.nlines, j) : t.pfx;
+}
+
+// The range of level j-1 that holds the lower bound, from level j's answer i
+// (E_j[i-1] < x <= E_j[i], E_j[i] = E_{j-1}[16 i]): at most 16 entries.
+__device__ __forceinline__ void level_down(const TableView& t, uint32_t j, uint64_t i, uint64_t& lo, uint64_t& hi) {
+  const uint64_t cnt = level_count(t.nlines, j - 1);
+  lo = i ? ((i - 1) << kFanBits) + 1 : 0;
+  hi = (i << kFanBits) < cnt ? (i << kFanBits) : cnt;
+}
+
+// Well-formed files (keys strictly increasing, so any correct search returns
+// the reference's line): the lower bound of the key's 8-byte prefix down the
+// fence levels (one run of at most 16 entries, one 128-B line, per level),
+// then the lines sharing that prefix by a galloping search with record
+// compares: O(log run) for keys that share long prefixes ('user0000...'), one
+// record compare when the prefix is unique.
+__device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& q, LineRec& hit) {
+  uint64_t lo = 0, hi = level_count(t.nlines, t.nlev);
+  for (uint32_t j = t.nlev;; --j) {
+    const uint64_t i = lower_bound_u64(level_array(t, j), lo, hi, q.w0);
+    if (!j) {
+      if (i >= t.nlines) return -1;
+      return resolve_from(t, q, i, hit);
+    }
+    level_down(t, j, i, lo, hi);
+  }
 }
 
 __device__ __forceinline__ int64_t search(const TableView& t, const Query& q, LineRec& hit) {

@@ -17,13 +17,40 @@ namespace cb {
 
 constexpr uint32_t kNoSep = 0xFFFFFFFFu;  // line without a TAB: ends a search
 
-constexpr uint32_t kFenceStride = 16;    // lines per fence entry (16 x 8 B = one 128-B line)
-constexpr uint32_t kFence2Stride = 256;  // lines per level-2 fence entry
-// The fence array holds fence_count(nl) entries (pfx[16 j]) and then
-// fence2_count(nl) entries (pfx[256 i]): one allocation, two levels.
-__host__ __device__ inline uint64_t fence_count(uint64_t nl) { return (nl + kFenceStride - 1) / kFenceStride; }
-__host__ __device__ inline uint64_t fence2_count(uint64_t nl) { return (nl + kFence2Stride - 1) / kFence2Stride; }
-__host__ __device__ inline uint64_t fence_words(uint64_t nl) { return fence_count(nl) + fence2_count(nl); }
+// The prefix index of a well-formed table is a fan-out-16 tree kept as
+// levels of sampled prefixes: level 0 is pfx itself, level j >= 1 holds
+// pfx[l] for every l that is a multiple of 16^j, up to the first level of at
+// most 16 entries. A lookup reads one run of at most 16 consecutive entries
+// (one 128-B line) per level. Levels 1..L are stored one after another in
+// the fence array.
+constexpr uint32_t kFanBits = 4;
+constexpr uint32_t kFanout = 1u << kFanBits;
+__host__ __device__ inline uint64_t level_count(uint64_t nl, uint32_t j) {
+  return (nl + (1ull << (kFanBits * j)) - 1) >> (kFanBits * j);
+}
+// L: the top level (0 when the table has at most 16 lines)
+__host__ __device__ inline uint32_t fence_levels(uint64_t nl) {
+  uint32_t L = 0;
+  while (level_count(nl, L) > kFanout) ++L;
+  return L;
+}
+// offset of level j >= 1 in the fence array
+__host__ __device__ inline uint64_t level_offset(uint64_t nl, uint32_t j) {
+  uint64_t o = 0;
+  for (uint32_t i = 1; i < j; ++i) o += level_count(nl, i);
+  return o;
+}
+__host__ __device__ inline uint64_t fence_words(uint64_t nl) { return level_offset(nl, fence_levels(nl) + 1); }
+// level j >= 1 entry of line l (a multiple of 16^j): fence[level_offset(nl, j) + (l >> 4j)]
+__device__ __forceinline__ void fence_put(uint64_t* fence, uint64_t nl, uint64_t l, uint64_t v) {
+  const uint32_t L = fence_levels(nl);
+  uint64_t off = 0;
+  for (uint32_t j = 1; j <= L; ++j) {
+    if (l & ((1ull << (kFanBits * j)) - 1)) break;
+    fence[off + (l >> (kFanBits * j))] = v;
+    off += level_count(nl, j);
+  }
+}
 constexpr uint32_t kBadValue = 0xFFFFFFFFu;  // value that STANDARD.decode rejects
 
 // Per-line index record (32 B, one load). vdl is computed once at index
@@ -44,17 +71,17 @@ struct alignas(16) LineRec {
 // line has a TAB and the keys are strictly increasing, as SsTable::create
 // writes it — any correct search returns what the reference's binary search
 // returns, so `fast` files are searched through pfx (each key's first 8
-// bytes, big-endian, zero-padded: monotone in the key order) and two fence
-// levels (every 16th pfx, and every 256th: L2-resident), so a lookup reads
-// one 128-B line of fence, one of pfx, then the record. Other files replay
-// the exact (lo+hi)/2 trajectory.
+// bytes, big-endian, zero-padded: monotone in the key order) and the fence
+// levels above it (fence_levels), so a lookup reads one run of at most 16
+// entries per level, then the record. Other files replay the exact
+// (lo+hi)/2 trajectory.
 struct TableView {
   const uint8_t* data;    // the file, with 16 bytes of readable slack
   const LineRec* rec;     // nlines
   const uint64_t* pfx;    // nlines
-  const uint64_t* fence;  // nfence = fence_count(nlines): pfx[16 j]
-  const uint64_t* fence2; // nfence2 = fence2_count(nlines): pfx[256 i]
-  uint64_t nlines, nfence, nfence2;
+  const uint64_t* fence;  // fence_words(nlines): levels 1..nlev
+  uint64_t nlines;
+  uint32_t nlev;          // fence_levels(nlines)
   uint32_t fast;
 };
 

@@ -85,7 +85,7 @@ def test_index_random_bytes(gpu, seed):
 
 def test_search_random_files_vs_oracle(gpu):
     rng = np.random.default_rng(5)
-    for n in (1, 2, 3, 1000, 70_001):
+    for n in (1, 2, 3, 16, 17, 256, 257, 1000, 4097, 70_001):  # fence levels L = 0..4
         keys = workload.key_range(900 + n, n)
         data = workload.sstable_bytes(keys, workload.table_value(keys, 3)).tobytes()
         t = gpu.Table(data)
