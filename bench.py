@@ -198,10 +198,19 @@ def main():
         lsmt_amd.probe(filters, keys_batch, out=hits_bufs[buf], stream=lane_sh[buf])
         exchange(buf)
 
+    def set_step(buf, gated=False):
+        """One FilterSet step. N > 1: the probe and the exchange are one C call
+        (cb_set_probe_allgather_fixed): in sparse mode the probe kernel writes
+        the pack itself, so no separate compress pass reads the rows again."""
+        if use_dist:
+            xcomms[buf].probe_allgather(fset, look, nf_total, hits_bufs[buf], hits_all_bufs[buf], sparse=use_sparse,
+                                        cap=cap, ok=x_ok, gated=gated, stream=lane_sh[buf])
+            xstats["sparse_steps"] += int(use_sparse)
+        else:
+            fset.probe(keys_batch, out=hits_bufs[buf], stream=lane_sh[buf], gated=gated)
+
     def step_set():
-        buf = claim()
-        fset.probe(keys_batch, out=hits_bufs[buf], stream=lane_sh[buf])
-        exchange(buf)
+        set_step(claim())
 
     region = {}  # HIP events on the kernels' stream around the last timed region
 
@@ -416,9 +425,7 @@ def main():
         del zkeys
 
         def step_gated():
-            buf = claim()
-            fset.probe(keys_batch, out=hits_bufs[buf], stream=lane_sh[buf], gated=True)
-            exchange(buf)
+            set_step(claim(), gated=True)
 
         for _ in range(args.warmup):
             step_gated()

@@ -370,6 +370,31 @@ int cb_hits_allgather(cb_comm* c, const uint64_t* local, uint64_t rows, uint64_t
                       uint64_t total_rows, uint64_t* full, int mode, uint64_t cap, uint32_t* ok,
                       int* sparse_used, void* stream);
 
+/* The probe and the exchange in one call: this rank's FilterSet probe (its
+ * `used` slots must equal its shard of total_rows) of a device-resident batch
+ * of fixed-length keys, writing local_hits ([used][ceil(n/64)], device), then
+ * the all-gather into full. In sparse mode the probe kernel itself writes the
+ * pack (no separate compress pass): positions as cb_hits_compress's, with
+ * one directory entry per probe block of 16 hit words of every slot
+ * (cb_set_pack_words). ok / sparse_used / overflow as cb_hits_allgather.
+ * gated != 0 applies the zone gate (cb_set_probe_gated_fixed). */
+int cb_set_probe_allgather_fixed(cb_comm* c, const cb_filterset* set, const uint8_t* keys, uint32_t key_len,
+                                 uint64_t n, int gated, uint64_t* local_hits, uint64_t total_rows,
+                                 uint64_t* full, int mode, uint64_t cap, uint32_t* ok, int* sparse_used,
+                                 void* stream);
+/* Its pieces, for callers that move the packs themselves: the pack size for
+ * a batch of n keys and cap positions (2 + cap + 2 * ceil(ceil(n/64)/16)
+ * uint32); the probe writing hits and pack (device buffers, async); and the
+ * expand of nranks such packs (all-gathered, each of cb_set_pack_words) into
+ * the [total_rows][ceil(n/64)] map, rank r's rows starting at row_off[r]
+ * (<= 64 rows per rank). A rank whose count exceeds cap clears *ok and
+ * leaves its rows zero. */
+int cb_set_pack_words(uint64_t n, uint64_t cap, uint64_t* out);
+int cb_set_probe_pack_fixed(const cb_filterset* set, const uint8_t* keys, uint32_t key_len, uint64_t n, int gated,
+                            uint64_t* hits, uint32_t* pack, uint64_t cap, void* stream);
+int cb_hits_expand_set(const uint32_t* packs, uint32_t nranks, uint64_t cap, const uint64_t* row_off, uint64_t n,
+                       uint64_t total_rows, uint64_t* full, uint32_t* ok, void* stream);
+
 /* ---- tuning / introspection (bench + tests) ---- */
 /* Path selection: 0 = auto, 1 = force direct (per-key atomics / gathers),
  * 2 = force tiled (LDS-staged filter tiles). Process-wide. */

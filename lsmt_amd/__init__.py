@@ -28,9 +28,10 @@ from .bloom import (  # noqa: E402
     ZoneMap,
     hits_compress,
     hits_expand,
+    hits_expand_set,
 )
 
 __all__ = ["BloomFilter", "BloomProto", "DeviceKeys", "FilterSet", "insert_many", "KeyBatch", "device_count", "last_path",
            "probe", "set_path", "unpack_hits", "zone_bounds", "ZoneMap", "TableMeta", "Table", "get_many", "sstable_create",
-           "hits_compress", "hits_expand"]
+           "hits_compress", "hits_expand", "hits_expand_set"]
 __version__ = "0.1.0"

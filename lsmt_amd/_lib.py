@@ -90,6 +90,11 @@ def load():
         "cb_comm_info": ([P, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
         "cb_comm_shard": ([u64, i32, i32, pu64, pu64], i32),
         "cb_hits_allgather": ([P, P, u64, u64, u64, P, i32, u64, P, ctypes.POINTER(i32), P], i32),
+        "cb_set_probe_allgather_fixed": ([P, P, u8p, u32, u64, i32, P, u64, P, i32, u64, P, ctypes.POINTER(i32), P],
+                                         i32),
+        "cb_set_pack_words": ([u64, u64, pu64], i32),
+        "cb_set_probe_pack_fixed": ([P, u8p, u32, u64, i32, P, P, u64, P], i32),
+        "cb_hits_expand_set": ([P, u32, u64, pu64, u64, u64, P, P, P], i32),
         "cb_filter_create": ([u64, i32, pp], i32),
         "cb_filter_destroy": ([P], i32),
         "cb_filter_bits": ([P, pu64], i32),

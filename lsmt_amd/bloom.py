@@ -549,6 +549,23 @@ class FilterSet:
             kp, k1 = _ptr_of(b.keys)
             _raise(_L().cb_set_zone_from_keys_fixed(self._h, int(slot), kp, b.key_len, b.n, s))
 
+    def probe_pack(self, keys, hits, pack, cap: int, gated: bool = False, stream=None) -> None:
+        """The probe writing the exchange pack too (cb_set_probe_pack_fixed):
+        keys uint8[n, key_len], hits int64[used][ceil(n/64)] and pack int32
+        [pack_words(n, cap)], all device tensors."""
+        n = int(keys.shape[0])
+        kp, k1 = _ptr_of(keys)
+        hp, k2 = _ptr_of(hits)
+        pp, k3 = _ptr_of(pack)
+        _raise(_L().cb_set_probe_pack_fixed(self._h, kp, int(keys.shape[1]), n, int(bool(gated)), hp, pp, int(cap),
+                                            _stream(stream)))
+
+    @staticmethod
+    def pack_words(n: int, cap: int) -> int:
+        out = ctypes.c_uint64()
+        check(_L().cb_set_pack_words(int(n), int(cap), ctypes.byref(out)))
+        return int(out.value)
+
     def probe(self, keys, out=None, stream=None, gated: bool = False) -> np.ndarray:
         """uint64[used, ceil(n/64)]: row s = slot s's may_contain bits; with
         gated=True, SsTable::get's full gate zone.contains && may_contain
@@ -837,3 +854,15 @@ def hits_expand(packs, world: int, row_off, full, ok=None, stream=None, cap=None
     fp, k2 = _ptr_of(full)
     op, k3 = _ptr_of(ok)
     _raise(_L().cb_hits_expand(pp, world, cap, off, words, total_rows, fp, op, _stream(stream)))
+
+
+def hits_expand_set(packs, world: int, row_off, n: int, full, cap: int, ok=None, stream=None) -> None:
+    """full ([total_rows][ceil(n/64)] int64 device tensor) := every rank's
+    rows from packs written by FilterSet.probe_pack (all-gathered int32,
+    world x FilterSet.pack_words(n, cap)): cb_hits_expand_set."""
+    total_rows = int(full.shape[0])
+    off = (ctypes.c_uint64 * world)(*[int(x) for x in row_off])
+    pp, k1 = _ptr_of(packs)
+    fp, k2 = _ptr_of(full)
+    op, k3 = _ptr_of(ok)
+    _raise(_L().cb_hits_expand_set(pp, world, int(cap), off, int(n), total_rows, fp, op, _stream(stream)))

@@ -485,6 +485,53 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
   return CB_OK;
 }
 
+}  // namespace
+
+namespace cbx {
+
+int set_probe_device(const cb_filterset* set, const uint8_t* keys, uint32_t key_len, uint64_t n, bool gated,
+                     uint64_t* hits, uint32_t* sink_pack, uint64_t cap, hipStream_t s) {
+  if (!set) return fail(CB_EINVAL, "null set");
+  if (!n || !set->used) {
+    if (sink_pack) {  // no rows or no keys: an empty pack (count 0, every directory entry empty)
+      DeviceGuard dg(set->device);
+      HIP_TRY(hipMemsetAsync(sink_pack, 0, 8, s));
+      if (n) HIP_TRY(hipMemsetAsync(sink_pack + 2 + cap, 0, 8 * cb::set_probe_blocks(n), s));
+    }
+    return CB_OK;
+  }
+  if (!hits || (!keys && key_len)) return fail(CB_EINVAL, "null argument");
+  if (!is_device_ptr(hits) || (key_len && !is_device_ptr(keys)) || (sink_pack && !is_device_ptr(sink_pack)))
+    return fail(CB_EINVAL, "keys, hits and pack must be device memory");
+  const uint64_t hwords = (n + 63) / 64;
+  if (sink_pack && (uint64_t)set->used * hwords * 64 > (1ull << 32))
+    return fail(CB_EINVAL, "used * ceil(n/64) * 64 must not exceed 2^32 (u32 positions)");
+  DeviceGuard dg(set->device);
+  Workspace& ws = workspace(set->device, s);
+  std::lock_guard<std::mutex> lk(ws.mu);
+  const cb::ZoneView zv{(const uint32_t*)set->zdev,
+                       (const cb::BoundPrefix*)((const uint8_t*)set->zdev + cb_zone_hdr_bytes),
+                       (const uint8_t*)set->zdev + cb_zone_blob_off, set->zgated};
+  const int keyk = (key_len == 16 && !((uintptr_t)keys & 15)) ? cb::KEY_FIXED16 : cb::KEY_FIXED;
+  const cb::KeySrc ks{keys, nullptr, key_len};
+  cb::PackSink sink{};
+  cb::CompressState* st = nullptr;
+  if (sink_pack) {
+    int rc = compress_state(ws, s, &st);
+    if (rc) return rc;
+    sink = cb::PackSink{sink_pack, cap, reinterpret_cast<unsigned long long*>(st->ctl), st->parity};
+  }
+  HIP_TRY(cb::launch_set_probe(keyk, set->mode, set->width, set->words, set->any, set->used, ks, n, set->mp,
+                               (gated && set->zgated) ? &zv : nullptr, hits, hwords, s, sink_pack ? &sink : nullptr));
+  if (st) st->parity ^= 1u;  // the launch cleared the other claim word for the next one
+  g_last_path = 3;
+  return CB_OK;
+}
+
+}  // namespace cbx
+
+namespace {
+
 // Rebuild and upload the set's zone table (cb::ZoneView layout). Called on
 // zone updates, which happen once per table flush: the upload is ordered on
 // stream s and waited for, so the host staging vector can be reused.
@@ -883,6 +930,34 @@ int cb_hits_expand(const uint32_t* packs, uint32_t nranks, uint64_t cap, const u
 int cb_hits_pack_words(uint64_t rows, uint64_t words, uint64_t cap, uint64_t* out) {
   if (!out) return fail(CB_EINVAL, "null out");
   *out = cb::pack_words(rows * words, cap);
+  return CB_OK;
+}
+
+int cb_set_pack_words(uint64_t n, uint64_t cap, uint64_t* out) {
+  if (!out) return fail(CB_EINVAL, "null out");
+  *out = 2 + cap + 2 * cb::set_probe_blocks(n);
+  return CB_OK;
+}
+
+int cb_set_probe_pack_fixed(const cb_filterset* set, const uint8_t* keys, uint32_t key_len, uint64_t n, int gated,
+                            uint64_t* hits, uint32_t* pack, uint64_t cap, void* stream) {
+  if (!pack) return fail(CB_EINVAL, "null pack");
+  return set_probe_device(set, keys, key_len, n, gated != 0, hits, pack, cap, (hipStream_t)stream);
+}
+
+int cb_hits_expand_set(const uint32_t* packs, uint32_t nranks, uint64_t cap, const uint64_t* row_off, uint64_t n,
+                       uint64_t total_rows, uint64_t* full, uint32_t* ok, void* stream) {
+  if (!full || (nranks && (!packs || !row_off))) return fail(CB_EINVAL, "null argument");
+  if (!nranks || nranks > cb::kMaxRanks) return fail(CB_EINVAL, "need 1..64 ranks");
+  cb::RankRows rr{};
+  for (uint32_t r = 0; r < nranks; ++r) rr.row_off[r] = row_off[r];
+  const uint64_t nblk = cb::set_probe_blocks(n);
+  const uint64_t stride = 2 + cap + 2 * nblk;
+  hipError_t e = cb::launch_hits_expand_blocks(packs, nranks, cap, stride, rr, (n + 63) / 64, total_rows,
+                                               (uint32_t)nblk, cb::kSetWords, full, ok, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue)
+    return fail(CB_EINVAL, "row_off must start at 0 and grow to total_rows with at most 64 rows per rank");
+  HIP_TRY(e);
   return CB_OK;
 }
 

@@ -143,6 +143,13 @@ Workspace& workspace(int device, hipStream_t s);
 // use (ws.mu held by the caller).
 int compress_state(Workspace& ws, hipStream_t s, cb::CompressState** out);
 
+// The FilterSet probe of a device-resident fixed-length key batch into
+// device hits, optionally (sink_pack != nullptr) also writing the exchange
+// pack (filterset.hpp PackSink; the stream's compress state supplies the
+// claim words). Used by cb_set_probe_pack_fixed and the comm layer.
+int set_probe_device(const cb_filterset* set, const uint8_t* keys, uint32_t key_len, uint64_t n, bool gated,
+                     uint64_t* hits, uint32_t* sink_pack, uint64_t cap, hipStream_t s);
+
 // Device-accessible memory (hipMalloc, managed) is used in place; anything
 // else (pageable or pinned host memory) is staged by the library.
 bool is_device_ptr(const void* p);

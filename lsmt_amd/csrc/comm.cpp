@@ -192,4 +192,58 @@ int cb_hits_allgather(cb_comm* c, const uint64_t* local, uint64_t rows, uint64_t
   return CB_OK;
 }
 
+int cb_set_probe_allgather_fixed(cb_comm* c, const cb_filterset* set, const uint8_t* keys, uint32_t key_len,
+                                 uint64_t n, int gated, uint64_t* local_hits, uint64_t total_rows, uint64_t* full,
+                                 int mode, uint64_t cap, uint32_t* ok, int* sparse_used, void* stream) {
+  if (!c || !set) return fail(CB_EINVAL, "null comm or set");
+  if (sparse_used) *sparse_used = 0;
+  if (mode != CB_XCHG_DENSE && mode != CB_XCHG_SPARSE) return fail(CB_EINVAL, "mode must be dense or sparse");
+  if (set->device != c->device) return fail(CB_EINVAL, "the set and the communicator live on different devices");
+  uint64_t lo, rows;
+  shard_rows(total_rows, c->world, c->rank, &lo, &rows);
+  if (rows != set->used) return fail(CB_EINVAL, "the set's used slots differ from this rank's shard of total_rows");
+  if (!n || !total_rows) return CB_OK;
+  if (!local_hits || !full) return fail(CB_EINVAL, "null hits");
+  const uint64_t hwords = (n + 63) / 64;
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == CB_XCHG_DENSE) {
+    int rc = set_probe_device(set, keys, key_len, n, gated != 0, local_hits, nullptr, 0, s);
+    if (rc) return rc;
+    return cb_hits_allgather(c, local_hits, rows, hwords, total_rows, full, CB_XCHG_DENSE, 0, nullptr, nullptr,
+                             stream);
+  }
+  if (!cap) return fail(CB_EINVAL, "sparse exchange needs cap > 0");
+  const uint64_t max_rows = (total_rows + (uint64_t)c->world - 1) / (uint64_t)c->world;
+  if (max_rows > 64) return fail(CB_EINVAL, "more than 64 rows per rank");
+  const uint64_t nblk = cb::set_probe_blocks(n);
+  const size_t pack_words = 2 + cap + 2 * nblk;  // equal on every rank
+  DeviceGuard dg(c->device);
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c->pack.reserve(pack_words * 4, s));
+  HIP_TRY(c->packs.reserve(pack_words * 4 * (size_t)c->world, s));
+  uint32_t* pack = (uint32_t*)c->pack.p;
+  uint32_t* packs = (uint32_t*)c->packs.p;
+  // the probe writes this rank's rows and its pack in one launch
+  int rc = set_probe_device(set, keys, key_len, n, gated != 0, local_hits, pack, cap, s);
+  if (rc) return rc;
+  NCCL_TRY(ncclAllGather(pack, packs, pack_words, ncclUint32, c->comm, s));
+  if (!ok) {  // synchronous overflow check (as cb_hits_allgather): dense redo on every rank
+    c->counts.assign((size_t)c->world, 0);
+    HIP_TRY(hipMemcpy2DAsync(c->counts.data(), 4, packs, pack_words * 4, 4, (size_t)c->world,
+                             hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (uint32_t v : c->counts)
+      if (v > cap) return allgather_dense(c, local_hits, rows, hwords, total_rows, full, s);
+  }
+  cb::RankRows rr{};
+  for (int r = 0; r < c->world; ++r) {
+    uint64_t cnt;
+    shard_rows(total_rows, c->world, r, &rr.row_off[r], &cnt);
+  }
+  HIP_TRY(cb::launch_hits_expand_blocks(packs, (uint32_t)c->world, cap, pack_words, rr, hwords, total_rows,
+                                        (uint32_t)nblk, cb::kSetWords, full, ok, s));
+  if (sparse_used) *sparse_used = 1;
+  return CB_OK;
+}
+
 }  // extern "C"

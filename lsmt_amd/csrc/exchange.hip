@@ -159,6 +159,40 @@ __global__ __launch_bounds__(kXT) void k_hits_expand(const uint32_t* __restrict_
   for (uint64_t i = tid; i < n; i += kXT) out[i] = chunk[i];
 }
 
+constexpr uint32_t kBlkRows = 64, kBlkWordsMax = 16;
+
+__global__ __launch_bounds__(kXT) void k_hits_expand_blocks(const uint32_t* __restrict__ packs, uint64_t cap,
+                                                            uint64_t stride, ExpandPlan plan, uint64_t hwords,
+                                                            uint32_t nblk, uint32_t bw,
+                                                            uint64_t* __restrict__ full,
+                                                            uint32_t* __restrict__ ok) {
+  __shared__ uint64_t chunk[kBlkRows * kBlkWordsMax];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t r = blockIdx.x / nblk, b = blockIdx.x % nblk;
+  const uint32_t rows = (uint32_t)(plan.row_off[r + 1] - plan.row_off[r]);
+  const uint64_t w0 = (uint64_t)b * bw;
+  for (uint32_t i = tid; i < rows * bw; i += kXT) chunk[i] = 0;
+  __syncthreads();
+  const uint32_t* pk = packs + (uint64_t)r * stride;
+  if (pk[0] > cap) {  // this rank's positions do not all fit: its rows stay zero
+    if (ok && tid == 0 && b == 0) atomicAnd(ok, 0u);
+  } else {
+    const uint32_t* dir = pk + 2 + cap;
+    const uint64_t e0 = dir[2 * (uint64_t)b], ne = dir[2 * (uint64_t)b + 1];
+    for (uint64_t e = tid; e < ne; e += kXT) {
+      const uint32_t p = pk[2 + e0 + e];
+      const uint32_t wl = p >> 6;  // row * hwords + word (< 2^26)
+      const uint32_t row = (uint32_t)(wl / (uint32_t)hwords), word = wl - row * (uint32_t)hwords;
+      atomicOr(reinterpret_cast<unsigned long long*>(&chunk[row * bw + (word - (uint32_t)w0)]), 1ull << (p & 63));
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < rows * bw; i += kXT) {
+    const uint32_t f = i / bw, w = i % bw;
+    if (w0 + w < hwords) full[(plan.row_off[r] + f) * hwords + w0 + w] = chunk[i];
+  }
+}
+
 }  // namespace
 
 hipError_t launch_hits_compress(const uint64_t* hits, uint64_t rows, uint64_t words,
@@ -198,6 +232,30 @@ hipError_t launch_hits_expand(const uint32_t* packs, uint32_t nranks, uint64_t c
   ProfScope ps("k_hits_expand", s);
   hipLaunchKernelGGL(k_hits_expand, dim3((uint32_t)nblk), dim3(kXT), 0, s, packs, nranks, cap,
                      pack_words(max_rows * words, cap), plan, words, full, ok);
+  return hipGetLastError();
+}
+
+}  // namespace cb
+
+namespace cb {
+
+hipError_t launch_hits_expand_blocks(const uint32_t* packs, uint32_t nranks, uint64_t cap, uint64_t stride,
+                                     const RankRows& rr, uint64_t hwords, uint64_t total_rows, uint32_t nblk,
+                                     uint32_t block_words, uint64_t* full, uint32_t* ok, hipStream_t s) {
+  if (!total_rows || !hwords || !nranks || !nblk) return hipSuccess;
+  if (block_words > kBlkWordsMax || rr.row_off[0] != 0) return hipErrorInvalidValue;
+  ExpandPlan plan{};
+  for (uint32_t r = 0; r < nranks; ++r) {
+    const uint64_t end = r + 1 < nranks ? rr.row_off[r + 1] : total_rows;
+    // a rank's rows fit one workgroup's chunk, and its positions fit 32 bits
+    if (end < rr.row_off[r] || end - rr.row_off[r] > kBlkRows || (end - rr.row_off[r]) * hwords * 64 > (1ull << 32))
+      return hipErrorInvalidValue;
+    plan.row_off[r] = rr.row_off[r];
+  }
+  plan.row_off[nranks] = total_rows;
+  ProfScope ps("k_hits_expand_blocks", s);
+  hipLaunchKernelGGL(k_hits_expand_blocks, dim3(nranks * nblk), dim3(kXT), 0, s, packs, cap, stride, plan, hwords,
+                     nblk, block_words, full, ok);
   return hipGetLastError();
 }
 

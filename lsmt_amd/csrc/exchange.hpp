@@ -48,4 +48,13 @@ hipError_t launch_hits_expand(const uint32_t* packs, uint32_t nranks, uint64_t c
                               const RankRows& rr, uint64_t words, uint64_t total_rows,
                               uint64_t* full, uint32_t* ok, hipStream_t s);
 
+// The expand for packs written by the set probe itself (filterset.hpp
+// PackSink: one directory entry per probe block of kBlockWords words of
+// every row): one workgroup per (rank, probe block) rebuilds that block's
+// rows x kBlockWords words in LDS and writes each row's segment once.
+// nblk = probe blocks per rank (the same on every rank); rows of a rank <= 64.
+hipError_t launch_hits_expand_blocks(const uint32_t* packs, uint32_t nranks, uint64_t cap, uint64_t stride,
+                                     const RankRows& rr, uint64_t hwords, uint64_t total_rows, uint32_t nblk,
+                                     uint32_t block_words, uint64_t* full, uint32_t* ok, hipStream_t s);
+
 }  // namespace cb

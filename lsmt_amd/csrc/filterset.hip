@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "blockscan.hpp"
 #include "filterset.hpp"
 #include "profile.hpp"
 #include "zone.hpp"
@@ -164,8 +165,7 @@ __global__ __launch_bounds__(256) void k_set_put_slot(const uint32_t* __restrict
   }
 }
 
-constexpr uint32_t kSetWords = 16;  // hit words (x64 keys) per block: 1024 keys
-constexpr uint32_t kSetProbeThreads = 64 * kSetWords;
+constexpr uint32_t kSetProbeThreads = 64 * kSetWords;  // one 64-key hit word per wave
 constexpr uint32_t kFlowThreads = 256;  // k_set_probe_flow: 4 waves per block
 constexpr uint32_t kFlowWaves = kFlowThreads / 64;
 
@@ -299,6 +299,43 @@ __device__ __forceinline__ void stage_zone_prefixes(const ZoneView& zv, BoundPre
   }
 }
 
+// The block's hit positions into the exchange pack (PackSink): the block's
+// set bits are counted (one entry per thread: thread i = slot i / 16, word
+// i % 16), one relaxed atomic add claims their slots (low half: slots, high
+// half: finished blocks, so the last block writes the total), and each
+// thread writes its word's positions in order. Words past the batch are zero
+// (their keys were never probed), so they add nothing.
+__device__ __forceinline__ void emit_positions(const PackSink& sink, const uint64_t (&hb)[64][kSetWords],
+                                               uint32_t used, uint64_t wbase, uint64_t hwords) {
+  __shared__ uint32_t s_base;
+  const uint32_t i = threadIdx.x;
+  const uint64_t v = i < used * kSetWords ? hb[i / kSetWords][i % kSetWords] : 0ull;
+  uint64_t total;
+  const uint64_t excl = block_scan<kSetProbeThreads>((uint64_t)__popcll(v), &total);
+  uint32_t* dir = sink.pack + 2 + sink.cap;
+  if (i == 0) {
+    const unsigned long long old = atomicAdd(sink.ctl + sink.par, (1ull << 32) | total);
+    s_base = (uint32_t)old;
+    if ((uint32_t)(old >> 32) == gridDim.x - 1) {  // the last claim: every block is counted
+      sink.pack[0] = (uint32_t)old + (uint32_t)total;
+      sink.pack[1] = 0;
+    }
+    if (blockIdx.x == 0)
+      __hip_atomic_store(sink.ctl + (sink.par ^ 1u), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    dir[2 * (uint64_t)blockIdx.x] = (uint32_t)old;
+    dir[2 * (uint64_t)blockIdx.x + 1] = (uint32_t)total;
+  }
+  __syncthreads();
+  uint64_t slot = (uint64_t)s_base + excl, bits = v;
+  const uint64_t pos0 = ((uint64_t)(i / kSetWords) * hwords + wbase + i % kSetWords) * 64;
+  while (bits) {
+    const uint32_t b = (uint32_t)__builtin_ctzll(bits);
+    bits &= bits - 1;
+    if (slot < sink.cap) sink.pack[2 + slot] = (uint32_t)(pos0 + b);
+    ++slot;
+  }
+}
+
 // One key per lane, one 64-key hit word per wave, 16 waves per block. Ballots
 // turn each 64-key word into one hit word per slot, staged in LDS so every
 // slot row leaves as a contiguous 128-byte segment. (Two or four keys per
@@ -313,7 +350,7 @@ __global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __re
                                                                 uint32_t used, KeySrc ks,
                                                                 uint64_t n, ModP mp, ZoneView zv,
                                                                 uint64_t* __restrict__ hits,
-                                                                uint64_t hwords) {
+                                                                uint64_t hwords, PackSink sink) {
   __shared__ uint64_t hb[64][kSetWords];
   __shared__ BoundPrefix zp[2 * W];  // gated 16-byte keys: the bounds' prefixes, staged
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -329,6 +366,7 @@ __global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __re
     const uint32_t f = i / kSetWords, w = i % kSetWords;
     if (wbase + w < nw) hits[(uint64_t)f * hwords + wbase + w] = hb[f][w];
   }
+  if (sink.pack) emit_positions(sink, hb, used, wbase, hwords);
 }
 
 // Persistent form: a grid sized to the chip (blocks per CU x CUs), each wave
@@ -453,7 +491,7 @@ hipError_t launch_set_put_slot(const uint32_t* words, uint64_t m, uint32_t slot,
 template <int KK, int MM, int WW>
 static void set_probe(bool sc, bool flow, const void* set, const uint32_t* any, uint32_t used,
                       const KeySrc& ks, uint64_t n, const ModP& mp, const ZoneView& zv,
-                      uint64_t* hits, uint64_t hwords, uint32_t grid, hipStream_t s) {
+                      uint64_t* hits, uint64_t hwords, uint32_t grid, hipStream_t s, const PackSink& sink) {
   if (flow) {
     if (sc)
       hipLaunchKernelGGL((k_set_probe_flow<KK, MM, WW, true>), dim3(grid), dim3(kFlowThreads), 0, s,
@@ -465,10 +503,10 @@ static void set_probe(bool sc, bool flow, const void* set, const uint32_t* any, 
   }
   if (sc)
     hipLaunchKernelGGL((k_set_probe<KK, MM, WW, true>), dim3(grid), dim3(kSetProbeThreads), 0, s,
-                       set, any, used, ks, n, mp, zv, hits, hwords);
+                       set, any, used, ks, n, mp, zv, hits, hwords, sink);
   else
     hipLaunchKernelGGL((k_set_probe<KK, MM, WW, false>), dim3(grid), dim3(kSetProbeThreads), 0, s,
-                       set, any, used, ks, n, mp, zv, hits, hwords);
+                       set, any, used, ks, n, mp, zv, hits, hwords, sink);
 }
 
 // Compute units of the current device (cached per device).
@@ -487,8 +525,9 @@ static uint32_t device_cus() {
 hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
                             const uint32_t* any, uint32_t used, const KeySrc& ks, uint64_t n,
                             const ModP& mp, const ZoneView* zones, uint64_t* hits,
-                            uint64_t hwords, hipStream_t s) {
+                            uint64_t hwords, hipStream_t s, const PackSink* sink) {
   if (!n || !used) return hipSuccess;
+  const PackSink nosink{nullptr, 0, nullptr, 0};
   // CB_SET_SC=0 reads set[b] unconditionally (one latency, more bytes);
   // default keeps the reference's short-circuit.
   static const bool sc = [] {
@@ -509,7 +548,7 @@ hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
   // CB_SET_FLOW=1: the persistent k_set_probe_flow; CB_SET_FLOW_BPC: its
   // blocks per CU (default 8: 32 waves per CU). Read per launch (tuning).
   const char* fv = getenv("CB_SET_FLOW");
-  const bool flow = fv && fv[0] == '1' && !use_any;  // the flow form has no union pre-test
+  const bool flow = fv && fv[0] == '1' && !use_any && !sink;  // no union pre-test or pack in the flow form
   uint32_t grid;
   if (flow) {
     const char* bv = getenv("CB_SET_FLOW_BPC");
@@ -523,7 +562,7 @@ hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
   ProfScope ps(zv.gated ? "k_set_probe_gated" : "k_set_probe", s);
   CB_SET_DISPATCH(keyk, mode, width,
                   (set_probe<KK, MM, WW>(sc, flow, set, use_any ? any : nullptr, used, ks, n, mp, zv,
-                                         hits, hwords, grid, s)));
+                                         hits, hwords, grid, s, sink ? *sink : nosink)));
   return hipGetLastError();
 }
 

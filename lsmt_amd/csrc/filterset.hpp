@@ -19,11 +19,29 @@ hipError_t launch_set_or_slot(const uint32_t* words, uint64_t m, uint32_t slot, 
 // slot := packed filter words (words == nullptr clears the slot): full pass.
 hipError_t launch_set_put_slot(const uint32_t* words, uint64_t m, uint32_t slot, uint32_t width,
                                void* set, uint32_t* any, hipStream_t s);
+// The probe block: kSetWords hit words (64 keys each) of every slot.
+constexpr uint32_t kSetWords = 16;
+inline uint64_t set_probe_blocks(uint64_t n) { return ((n + 63) / 64 + kSetWords - 1) / kSetWords; }
+
+// Optional sparse output of the probe for the multi-GPU exchange (the
+// compress step fused into the probe): pack = {count, 0, positions[cap],
+// dir[2 * set_probe_blocks(n)]}, position = slot * hwords * 64 + key, and
+// dir[2b], dir[2b+1] = first slot and number of probe block b's positions
+// (kSetWords words of every slot). ctl: the stream's claim words
+// (CompressState), par: this launch's parity.
+struct PackSink {
+  uint32_t* pack;
+  uint64_t cap;
+  unsigned long long* ctl;
+  uint32_t par;
+};
+
 // hits[slot][ceil(n/64)] for slots 0..used-1. zones (nullable): the
-// SsTable::get zone gate, applied to the slots in zones->gated.
+// SsTable::get zone gate, applied to the slots in zones->gated. sink
+// (nullable): also write the hit positions as a pack (the block form only).
 hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
                             const uint32_t* any, uint32_t used, const KeySrc& ks, uint64_t n,
                             const ModP& mp, const ZoneView* zones, uint64_t* hits,
-                            uint64_t hwords, hipStream_t s);
+                            uint64_t hwords, hipStream_t s, const PackSink* sink = nullptr);
 
 }  // namespace cb

@@ -207,3 +207,25 @@ class Comm:
                                              _lib.XCHG_SPARSE if sparse else _lib.XCHG_DENSE, cap, op,
                                              ctypes.byref(used), _stream(stream)))
         return bool(used.value)
+
+    def probe_allgather(self, fset, keys, n_total: int, local_out, out, sparse: bool = False, cap: int = 0,
+                        ok=None, gated: bool = False, stream=None) -> bool:
+        """This rank's FilterSet probe and the exchange in one C call
+        (cb_set_probe_allgather_fixed): keys uint8[n, key_len] on the device;
+        local_out [used][ceil(n/64)] and out [n_total][ceil(n/64)] int64
+        device tensors. In sparse mode the probe kernel writes the pack
+        itself. Returns whether the map came from the packs."""
+        import ctypes
+
+        from . import _lib
+        from .bloom import _ptr_of, _stream
+        n = int(keys.shape[0])
+        kp, k1 = _ptr_of(keys)
+        lp, k2 = _ptr_of(local_out)
+        fp, k3 = _ptr_of(out)
+        op, k4 = _ptr_of(ok)
+        used = ctypes.c_int(0)
+        _lib.check(self._L.cb_set_probe_allgather_fixed(
+            self._h, fset._h, kp, int(keys.shape[1]), n, int(bool(gated)), lp, n_total, fp,
+            _lib.XCHG_SPARSE if sparse else _lib.XCHG_DENSE, cap, op, ctypes.byref(used), _stream(stream)))
+        return bool(used.value)

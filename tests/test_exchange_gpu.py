@@ -180,3 +180,122 @@ def test_comm_checks_shapes(gpu, comm1, probed_rows):
         comm1.allgather(local, nf + 1, full)
     with pytest.raises(Exception):  # sparse needs a capacity
         comm1.allgather(local, nf, full[:nf], sparse=True, cap=0)
+
+
+# ---- the probe writing the pack itself (cb_set_probe_pack_fixed / cb_hits_expand_set) ----
+
+@pytest.fixture(scope="module")
+def rank_sets():
+    """Four 'ranks' on one GPU: FilterSets of 3, 2, 0 and 2 slots over 7
+    filters, the same lookup batch, and the oracle's hit rows."""
+    import torch
+
+    import lsmt_amd
+    from oracle import oracle
+    m, kpf, n = 1 << 18, 3000, 70_001
+    look = workload.probe_lookups(n, 7, kpf, seed_base=100, absent_seed=999)
+    gf, of = [], []
+    for f in range(7):
+        keys = workload.key_range(100 + f, kpf)
+        b = lsmt_amd.BloomFilter(m)
+        b.insert_batch(keys)
+        o = oracle.OracleFilter(m)
+        o.insert_fixed(keys)
+        gf.append(b)
+        of.append(o)
+    sizes = [3, 2, 0, 2]
+    sets, lo = [], 0
+    for sz in sizes:
+        s = lsmt_amd.FilterSet(m, 32)
+        if sz:
+            s.assign_all(gf[lo:lo + sz])
+        sets.append(s)
+        lo += sz
+    expect = oracle.probe_fixed(of, look)
+    return sets, sizes, torch.from_numpy(look).cuda(), expect
+
+
+@pytest.mark.parametrize("overflow_rank", [None, 1])
+def test_probe_pack_expand_ranks(gpu, rank_sets, overflow_rank):
+    import torch
+    sets, sizes, keys, expect = rank_sets
+    n = keys.shape[0]
+    words = (n + 63) // 64
+    nbits = int(np.unpackbits(expect.view(np.uint8)).sum())
+    cap = nbits + 10
+    stride = gpu.FilterSet.pack_words(n, cap)
+    packs = torch.full((len(sizes) * stride,), -1, dtype=torch.int32, device="cuda")
+    for r, (s, sz) in enumerate(zip(sets, sizes)):
+        hits = torch.full((max(sz, 1), words), -1, dtype=torch.int64, device="cuda")
+        s.probe_pack(keys, hits, packs[r * stride:(r + 1) * stride], cap=cap)
+        if sz:
+            lo = sum(sizes[:r])
+            assert np.array_equal(hits.cpu().numpy().view(np.uint64), expect[lo:lo + sz])
+            pk = packs[r * stride:(r + 1) * stride].cpu().numpy().view(np.uint32)
+            assert pk[0] == int(np.unpackbits(expect[lo:lo + sz].view(np.uint8)).sum())
+    if overflow_rank is not None:
+        packs[overflow_rank * stride] = cap + 1
+    full = torch.full((sum(sizes), words), -1, dtype=torch.int64, device="cuda")
+    ok = torch.ones(1, dtype=torch.int32, device="cuda")
+    row_off = list(np.cumsum([0] + sizes[:-1]))
+    gpu.hits_expand_set(packs, len(sizes), row_off, n, full, cap, ok=ok)
+    got = full.cpu().numpy().view(np.uint64)
+    if overflow_rank is None:
+        assert int(ok.item()) == 1 and np.array_equal(got, expect)
+    else:
+        lo = row_off[overflow_rank]
+        hi = lo + sizes[overflow_rank]
+        assert int(ok.item()) == 0 and not got[lo:hi].any()
+        keep = np.r_[0:lo, hi:len(got)]
+        assert np.array_equal(got[keep], expect[keep])
+
+
+@pytest.mark.parametrize("mode", ["dense", "sparse", "sparse_async", "overflow_sync", "overflow_async", "gated"])
+def test_comm_probe_allgather_world1(gpu, comm1, mode):
+    """cb_set_probe_allgather_fixed at world size 1: the probe (writing the
+    pack itself in sparse mode) and the exchange in one call, against the
+    oracle's probe (and, gated, its zone && bloom gate)."""
+    import torch
+
+    import lsmt_amd
+    from oracle import oracle
+    m, kpf, n, nf = 1 << 18, 3000, 40_001, 5
+    look = workload.probe_lookups(n, nf, kpf, seed_base=300, absent_seed=998)
+    gf, of, zones = [], [], []
+    for f in range(nf):
+        keys = workload.key_range(300 + f, kpf)
+        b = lsmt_amd.BloomFilter(m)
+        b.insert_batch(keys)
+        o = oracle.OracleFilter(m)
+        o.insert_fixed(keys)
+        gf.append(b)
+        of.append(o)
+        srt = workload.sort_keys16(keys)
+        zones.append((bytes(srt[kpf // 4]), bytes(srt[3 * kpf // 4])))  # half-width zones: the gate rejects
+    s = lsmt_amd.FilterSet.from_filters(gf)
+    if mode == "gated":
+        for f, (lo, hi) in enumerate(zones):
+            s.set_zone(f, (lo, hi))
+        d = np.ascontiguousarray(look.reshape(-1))
+        offs = np.arange(0, 16 * (n + 1), 16, dtype=np.uint64)
+        expect = oracle.probe_gated(of, [oracle.OracleZone(lo, hi) for lo, hi in zones], d, offs)
+    else:
+        expect = oracle.probe_fixed(of, look)
+    words = (n + 63) // 64
+    keys = torch.from_numpy(look).cuda()
+    local = torch.full((nf, words), -1, dtype=torch.int64, device="cuda")
+    full = torch.full((nf, words), -1, dtype=torch.int64, device="cuda")
+    nbits = int(np.unpackbits(expect.view(np.uint8)).sum())
+    cap = 7 if mode.startswith("overflow") else nbits + 100
+    ok = torch.ones(1, dtype=torch.int32, device="cuda") if mode.endswith("async") else None
+    used = comm1.probe_allgather(s, keys, nf, local, full, sparse=mode != "dense", cap=cap, ok=ok,
+                                 gated=mode == "gated")
+    torch.cuda.synchronize()
+    assert np.array_equal(local.cpu().numpy().view(np.uint64), expect)
+    if mode == "overflow_async":
+        assert int(ok.item()) == 0 and used
+        comm1.allgather(local, nf, full, sparse=False)
+        torch.cuda.synchronize()
+    else:
+        assert used == (mode in ("sparse", "sparse_async", "gated"))
+    assert np.array_equal(full.cpu().numpy().view(np.uint64), expect)

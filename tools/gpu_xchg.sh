@@ -8,8 +8,6 @@ timeout -k 10 300 python -u -m pytest tests/test_exchange_gpu.py -m gpu -x -v --
 tail -1 gpurun_out/pytest_xchg.log
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -1 gpurun_out/pytest_gpu.log
-timeout -k 10 180 python tools/xchg_parts.py > gpurun_out/xchg_parts.json 2> gpurun_out/xchg_parts.err || { tail -20 gpurun_out/xchg_parts.err; exit 1; }
-cat gpurun_out/xchg_parts.json
 for sp in 0 1; do
   CB_SPARSE_EXCHANGE=$sp timeout -k 10 300 python bench.py --no-cpu --no-e2e --no-zone --no-flush --no-cold --force-dist --check > gpurun_out/d_sp$sp.json 2> gpurun_out/d_sp$sp.err || { tail -20 gpurun_out/d_sp$sp.err; exit 1; }
   grep check gpurun_out/d_sp$sp.err
