@@ -103,3 +103,44 @@ def test_c5_rank_slice(gpu, golden, c5_lookups_dev, rank):
     out.zero_()
     gpu.probe(filters, keys, out=out)
     assert sha(out.cpu().numpy().view(np.uint64).astype("<u8")) == g["rank_slice_hits_sha256"][rank]
+
+
+def test_c5_all_ranks_exchanged(gpu, golden, c5_lookups_dev):
+    """C5 end to end on one GPU: eight 'ranks' (FilterSets of 32 filters of
+    m = 2^26, 256 tables in all) each probe the 10M lookups writing their
+    sparse exchange pack (cb_set_probe_pack_fixed, the probe of
+    cb_set_probe_allgather_fixed), the eight packs are expanded into the
+    [256][156250] map the all-gather would leave on every rank
+    (cb_hits_expand_set), and every rank's rows match the golden SHA-256s
+    (src/lib.rs:129-134 over 256 tables)."""
+    import torch
+
+    from lsmt_amd.shard import shard_range, sparse_cap
+    g = golden["c5"]
+    per, m, kpf, n, nf = g["filters_per_rank"], g["m"], g["keys_per_filter"], g["n_lookups"], g["nf"]
+    world = nf // per
+    words = (n + 63) // 64
+    cap = sparse_cap(n, nf, world)
+    stride = gpu.FilterSet.pack_words(n, cap)
+    packs = torch.zeros(world * stride, dtype=torch.int32, device="cuda")
+    hits = torch.empty((per, words), dtype=torch.int64, device="cuda")
+    for r in range(world):
+        lo, hi = shard_range(nf, world, r)
+        s = gpu.FilterSet(m, 32)
+        for slot, f in enumerate(range(lo, hi)):
+            b = gpu.BloomFilter(m)
+            b.insert_batch(gpu.DeviceKeys(torch.from_numpy(workload.c5_filter_keys(f, kpf)).cuda()))
+            s.assign(slot, b)
+            del b
+        s.probe_pack(c5_lookups_dev, hits, packs[r * stride:(r + 1) * stride], cap=cap)
+        assert sha(hits.cpu().numpy().view(np.uint64).astype("<u8")) == g["rank_slice_hits_sha256"][r], r
+        del s
+    counts = packs.view(world, stride)[:, 0].cpu().numpy()
+    assert (counts <= cap).all() and int(counts.sum()) == g["hits_popcount"]
+    full = torch.full((nf, words), -1, dtype=torch.int64, device="cuda")
+    ok = torch.ones(1, dtype=torch.int32, device="cuda")
+    gpu.hits_expand_set(packs, world, [shard_range(nf, world, r)[0] for r in range(world)], n, full, cap, ok=ok)
+    assert int(ok.item()) == 1
+    got = full.cpu().numpy().view(np.uint64)
+    for r in range(world):
+        assert sha(got[r * per:(r + 1) * per].astype("<u8")) == g["rank_slice_hits_sha256"][r], r
