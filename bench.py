@@ -467,28 +467,35 @@ def main():
         del files
         newest_first = tables[::-1]  # Database::get: tables.iter().rev()
         rows = np.arange(F)[::-1].copy()
-        which_d = torch.empty(n, dtype=torch.int32, device=dev)
-        voff_d = torch.empty(n + 1, dtype=torch.int64, device=dev)
-        vals_d = torch.empty(n * 16, dtype=torch.uint8, device=dev)
-        hits_r = torch.empty((F, words), dtype=torch.int64, device=dev)
-        got = [0]
+        # one batch per step, batches alternating over the lanes (as the probe
+        # legs): each lane has its own gate rows and outputs, and get_many
+        # only enqueues (total read from val_off[n] afterwards), so one
+        # batch's search overlaps the next batch's gated probe
+        which_l = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(P)]
+        voff_l = [torch.empty(n + 1, dtype=torch.int64, device=dev) for _ in range(P)]
+        vals_l = [torch.empty(n * 16, dtype=torch.uint8, device=dev) for _ in range(P)]
+        hits_l = [torch.empty((F, words), dtype=torch.int64, device=dev) for _ in range(P)]
 
         def step_read():
-            fset.probe(keys_batch, out=hits_r, stream=sh, gated=True)
-            got[0] = lsmt_amd.get_many(newest_first, keys_batch, hits=hits_r, hit_rows=rows,
-                                       out=(which_d, voff_d, vals_d), stream=sh)[2]
+            b = claim()
+            fset.probe(keys_batch, out=hits_l[b], stream=lane_sh[b], gated=True)
+            lsmt_amd.get_many(newest_first, keys_batch, hits=hits_l[b], hit_rows=rows,
+                              out=(which_l[b], voff_l[b], vals_l[b]), stream=lane_sh[b], wait=False)
 
         for _ in range(args.warmup):
             step_read()
         rel = timed(step_read, args.steps)
         rprof = kernel_ms(["k_set_probe_gated", "k_get_many", "k_tile_scan", "k_b64_decode"], step_read, args.steps)
-        found = int((which_d >= 0).sum().item())
+        torch.cuda.synchronize(dev)
+        found = int((which_l[0] >= 0).sum().item())
+        got = [int(voff_l[0][n].item())]
+        assert all(torch.equal(which_l[0], w) and torch.equal(voff_l[0], v) for w, v in zip(which_l, voff_l))
         read = {"metric": "gets/s: 1M keys through zone+Bloom gate, binary search and base64 decode over "
                           f"{F} SSTable data files ({kpf} lines each) in HBM",
                 "value": round(n / (rel / args.steps), 1), "unit": "keys/s",
                 "ms_per_step": round(rel / args.steps * 1e3, 4),
                 "kernels_us": {k: round(v["avg_us"], 2) for k, v in rprof.items()},
-                "found": found, "value_bytes": got[0],
+                "found": found, "value_bytes": got[0], "pipeline_lanes": P,
                 "files_bytes": file_bytes, "index_build_GBps": round(file_bytes / index_s / 1e9, 2),
                 "file_generation_s": round(gen_s, 2)}
         if rank == 0 and world == 1 and not args.no_cpu:
@@ -496,7 +503,7 @@ def main():
             sample = 1 << 15
             ot = [oracle.OracleTable(workload.sstable_bytes(k, workload.table_value(k, f)))
                   for f, k in ((f, workload.key_range(seed_base + f, kpf)) for f in range(f_lo, f_lo + F))][::-1]
-            hs = hits_r.cpu().numpy().view(np.uint64)[rows]
+            hs = hits_l[0].cpu().numpy().view(np.uint64)[rows]
             hs = np.ascontiguousarray(hs[:, : sample // 64])
             t0 = time.perf_counter()
             oracle.get_many(ot, hs, np.ascontiguousarray(look_np[:sample].reshape(-1)),

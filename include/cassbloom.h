@@ -293,7 +293,12 @@ int cb_table_search_var(const cb_table* t, const uint8_t* bytes, const uint64_t*
  * line found AND value decodes as base64 (base64 0.21.7 STANDARD; an Err
  * falls through to older tables) — or -1. val_off[n+1] = offsets of the
  * decoded values; *total = their byte count; the values are written to vals
- * only if cap >= *total (call with vals = NULL to size). */
+ * only if cap >= *total (call with vals = NULL to size).
+ * total = NULL: the call only enqueues the work on stream and returns without
+ * waiting (keys, hits, which, val_off and vals must then be device memory;
+ * val_off[n] holds the total once the stream has run, and vals is written
+ * only if cap >= that total). Calls that repeat the same tables and hit_rows
+ * upload nothing, so batches on two streams overlap. */
 int cb_get_many_fixed(const cb_table* const* tables, uint32_t nt, const uint64_t* hits,
                       const uint32_t* hit_rows, const uint8_t* keys, uint32_t key_len, uint64_t n,
                       int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap,

@@ -760,7 +760,7 @@ def _to_var(b: KeyBatch) -> KeyBatch:
     return KeyBatch(n=b.n, data=data, offsets=offs)
 
 
-def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=None, out=None):
+def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=None, out=None, wait=True):
     """Database::get's newest-first walk for a key batch (tables[0] newest).
     hits: optional per-table gate bitmaps (e.g. FilterSet.probe(gated=True));
     table t uses row hit_rows[t] (default t). Returns (which int32[n]: table
@@ -768,7 +768,9 @@ def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=Non
 
     out=(which, val_off, vals) with preallocated (e.g. device) buffers runs
     one pass and returns (which, val_off, total); values are written only if
-    vals is large enough for total."""
+    vals is large enough for total. With wait=False (out, keys and hits on the
+    device) the call only enqueues the work on stream and returns total None:
+    val_off[n] holds it once the stream has run."""
     b = as_batch(keys)
     nt = len(tables)
     arr = (ctypes.c_void_p * max(nt, 1))(*[t.handle.value for t in tables])
@@ -778,6 +780,9 @@ def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=Non
         rows = np.ascontiguousarray(hit_rows, dtype=np.uint32)
     rp = rows.ctypes.data if rows is not None else None
     total = ctypes.c_uint64()
+    if not wait and out is None:
+        raise ValueError("wait=False needs out= device buffers")
+    tref = ctypes.byref(total) if wait else None
     s = _stream(stream)
     L = _L()
     if out is not None:
@@ -794,16 +799,16 @@ def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=Non
 
         def call(vp, cap):
             _raise(L.cb_get_many_var(ctypes.cast(arr, ctypes.c_void_p), nt, hp, rp, dp, offp, b.n,
-                                     wp, vo, vp, cap, ctypes.byref(total), s))
+                                     wp, vo, vp, cap, tref, s))
     else:
         kp, k1 = _ptr_of(b.keys)
 
         def call(vp, cap):
             _raise(L.cb_get_many_fixed(ctypes.cast(arr, ctypes.c_void_p), nt, hp, rp, kp, b.key_len, b.n,
-                                       wp, vo, vp, cap, ctypes.byref(total), s))
+                                       wp, vo, vp, cap, tref, s))
     if out is not None:
         call(_ptr_of(vals)[0], cap)
-        return which, voff, int(total.value)
+        return which, voff, (int(total.value) if wait else None)
     call(None, 0)
     vals = np.zeros(max(int(total.value), 1), np.uint8)
     call(vals.ctypes.data, int(total.value))

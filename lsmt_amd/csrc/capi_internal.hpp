@@ -70,11 +70,15 @@ struct cb_table {
   cb::LineRec* rec = nullptr;   // per-line index record
   uint64_t* pfx = nullptr;      // per-line 8-byte key prefix
   uint64_t* fence = nullptr;    // the fence levels above pfx (sstable.hpp)
+  uint32_t* dir = nullptr;      // the radix directory (sstable.hpp; nullptr under 256 lines)
+  uint64_t pfx_first = 0, pfx_last = 0;  // pfx[0], pfx[nlines - 1] (the directory's key)
   bool fast = false;  // well-formed: TAB on every line, keys strictly increasing
   bool has_zone = false;   // made by cb_sstable_create with n >= 1
   std::string zmin, zmax;  // its ZoneMap bounds (first / last key of the file)
   cb::TableView view() const {
-    return cb::TableView{data, rec, pfx, fence, nlines, cb::fence_levels(nlines), fast ? 1u : 0u};
+    return cb::TableView{data, rec, pfx, fence, nlines, cb::fence_levels(nlines), fast ? 1u : 0u,
+                         dir, dir ? cb::dir_bits(nlines) : 0u,
+                         pfx_first == pfx_last ? 64u : (uint32_t)__builtin_clzll(pfx_first ^ pfx_last), pfx_first};
   }
 };
 
@@ -128,6 +132,9 @@ struct Workspace {
   std::mutex mu;
   DevBuf keys, offsets, hits, seg, ent, masks, bools, lkey, zone;
   DevBuf t_views, t_rows, t_which, t_line, t_dlen, t_voff, t_scan, t_vals;
+  // what t_views / t_rows hold (a call with the same tables and rows uploads nothing)
+  std::vector<uint8_t> t_views_host;
+  std::vector<uint32_t> t_rows_host;
   DevBuf i_cnt, i_base, i_tmp, i_end, i_err, i_start;                 // line indexing
   DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_tsum, f_flag;  // SsTable::create
   DevBuf x_ctl;                   // cb_hits_compress: slot / finish counters (zeroed once)

@@ -5,6 +5,7 @@
 //
 // Reference: /root/reference/src/sstable.rs:51-179, src/lib.rs:125-136.
 #include <cstdlib>
+#include <cstring>
 
 #include "capi_internal.hpp"
 
@@ -41,10 +42,20 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
                   const uint32_t* hit_rows, const uint8_t* keys, const uint64_t* offsets,
                   uint32_t key_len, uint64_t n, int32_t* which, uint64_t* val_off, uint8_t* vals,
                   uint64_t cap, uint64_t* total, hipStream_t s) {
-  if (!which || !val_off || !total || (nt && !tables)) return fail(CB_EINVAL, "null argument");
-  *total = 0;
+  if (!which || !val_off || (nt && !tables)) return fail(CB_EINVAL, "null argument");
+  // total == NULL: enqueue only (every buffer on the device; val_off[n] = the total)
+  const bool async = total == nullptr;
+  if (async && (!is_device_ptr(which) || !is_device_ptr(val_off) || (vals && !is_device_ptr(vals)) ||
+                (hits && !is_device_ptr(hits)) || (n && keys && !is_device_ptr(keys)) ||
+                (offsets && !is_device_ptr(offsets))))
+    return fail(CB_EINVAL, "total may be NULL only when keys, hits and outputs are device memory");
+  if (total) *total = 0;
   if (n == 0) {
     const uint64_t z = 0;
+    if (async) {
+      HIP_TRY(hipMemsetAsync(val_off, 0, 8, s));
+      return CB_OK;
+    }
     return put_bytes((uint8_t*)val_off, &z, 8);
   }
   if (offsets == nullptr && keys == nullptr && key_len) return fail(CB_EINVAL, "null keys");
@@ -76,12 +87,24 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
     HIP_TRY(hipMemcpyAsync(ws.hits.p, hits, nrows * hwords * 8, hipMemcpyHostToDevice, s));
     dhits = (const uint64_t*)ws.hits.p;
   }
-  HIP_TRY(ws.t_views.reserve(nt * sizeof(cb::TableView), s));
-  HIP_TRY(hipMemcpyAsync(ws.t_views.p, views.data(), nt * sizeof(cb::TableView), hipMemcpyHostToDevice, s));
+  // views and rows: uploaded only when they differ from what the workspace
+  // holds (stream-ordered, so earlier launches have read the old ones)
+  const size_t vbytes = nt * sizeof(cb::TableView);
+  const uint8_t* vb = (const uint8_t*)views.data();
+  if (ws.t_views_host.size() != vbytes || memcmp(ws.t_views_host.data(), vb, vbytes)) {
+    HIP_TRY(ws.t_views.reserve(vbytes, s));
+    HIP_TRY(hipMemcpyAsync(ws.t_views.p, vb, vbytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));  // the source is pageable
+    ws.t_views_host.assign(vb, vb + vbytes);
+  }
   const uint32_t* drows = nullptr;
   if (!rows.empty()) {
-    HIP_TRY(ws.t_rows.reserve(nt * 4, s));
-    HIP_TRY(hipMemcpyAsync(ws.t_rows.p, rows.data(), nt * 4, hipMemcpyHostToDevice, s));
+    if (ws.t_rows_host != rows) {
+      HIP_TRY(ws.t_rows.reserve(nt * 4, s));
+      HIP_TRY(hipMemcpyAsync(ws.t_rows.p, rows.data(), nt * 4, hipMemcpyHostToDevice, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      ws.t_rows_host = rows;
+    }
     drows = (const uint32_t*)ws.t_rows.p;
   }
   int32_t* dwhich;
@@ -99,6 +122,10 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
                               (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, tsum, s));
   HIP_TRY(cb::launch_tile_scan(tsum, cb::get_tiles(n), dvoff + n, s));
   if (!ws.htot) HIP_TRY(hipHostMalloc((void**)&ws.htot, 64, hipHostMallocDefault));
+  if (async) {
+    HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, vals, vals ? cap : 0, s));
+    return CB_OK;
+  }
   if (vals && is_device_ptr(vals)) {
     // device values: offsets and values in one pass (the kernel skips the
     // value writes when the total exceeds cap): one host round trip
@@ -123,6 +150,17 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
   return CB_OK;
 }
 
+// The index of nl lines is one allocation: rec | pfx | fence | dir.
+size_t index_bytes(uint64_t nl) {
+  return nl * sizeof(cb::LineRec) + nl * 8 + cb::fence_words(nl) * 8 + cb::dir_words(nl) * 4;
+}
+void carve_index(cb_table* t) {
+  const uint64_t nl = t->nlines;
+  t->pfx = (uint64_t*)(t->rec + nl);
+  t->fence = t->pfx + nl;
+  t->dir = cb::dir_words(nl) ? (uint32_t*)(t->fence + cb::fence_words(nl)) : nullptr;
+}
+
 // Line index of t->data[0..t->len) (count -> scan -> emit -> finish -> keys).
 // Temporaries come from the stream's workspace (taken here: callers must not
 // hold its lock); the index itself is one allocation: rec | pfx | fence.
@@ -145,13 +183,12 @@ int index_table(cb_table* t, hipStream_t s) {
   HIP_TRY(hipStreamSynchronize(s));
   if (!t->nlines) return CB_OK;
   const uint64_t nl = t->nlines;
-  const size_t bytes = nl * sizeof(cb::LineRec) + nl * 8 + cb::fence_words(nl) * 8;
+  const size_t bytes = index_bytes(nl);
   if (pool_alloc(t->device, bytes, (void**)&t->rec, &t->rec_cap) != hipSuccess) {
     t->rec = nullptr;
     return fail(CB_ENOMEM, "device allocation failed for an SSTable index");
   }
-  t->pfx = (uint64_t*)(t->rec + nl);
-  t->fence = t->pfx + nl;
+  carve_index(t);
   HIP_TRY(ws.i_start.reserve(nl * 8, s));
   HIP_TRY(ws.i_end.reserve(nl * 8, s));
   uint64_t* start = (uint64_t*)ws.i_start.p;
@@ -164,8 +201,11 @@ int index_table(cb_table* t, hipStream_t s) {
   HIP_TRY(cb::launch_line_finish(t->data, len, nl, start, end, t->rec, err, s));
   // prefix + fence index, value validity and the well-formed check (sstable.hpp)
   HIP_TRY(cb::launch_line_keys(t->data, nl, t->rec, t->pfx, t->fence, err + 1, s));
+  if (t->dir) HIP_TRY(cb::launch_table_dir(t->pfx, nl, t->dir, s));
   uint32_t e[2] = {0, 0};
   HIP_TRY(hipMemcpyAsync(e, err, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&t->pfx_first, t->pfx, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&t->pfx_last, t->pfx + nl - 1, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   if (e[0]) return fail(CB_EINVAL, "an SSTable line is 4 GiB or longer");
   t->fast = e[1] != 0 && !g_table_exact;
@@ -374,15 +414,18 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
   // the line index straight from the entries (entry p is line p), no re-read of the file
   t->nlines = n;
-  const size_t ibytes = n * sizeof(cb::LineRec) + n * 8 + cb::fence_words(n) * 8;
-  if (pool_alloc(device, ibytes, (void**)&t->rec, &t->rec_cap) != hipSuccess) {
+  if (pool_alloc(device, index_bytes(n), (void**)&t->rec, &t->rec_cap) != hipSuccess) {
     t->rec = nullptr;
     return fail(CB_ENOMEM, "device allocation failed for an SSTable index");
   }
-  t->pfx = (uint64_t*)(t->rec + n);
-  t->fence = t->pfx + n;
+  carve_index(t.get());
   HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, tsum, n, t->data, t->rec, t->pfx, t->fence, dr,
                             cap_bytes, s));
+  if (t->dir) {
+    HIP_TRY(cb::launch_table_dir(t->pfx, n, t->dir, s));
+    HIP_TRY(hipMemcpyAsync(&t->pfx_first, t->pfx, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&t->pfx_last, t->pfx + n - 1, 8, hipMemcpyDeviceToHost, s));
+  }
   // Round trip 2: flags, file length, zone bounds
   HIP_TRY(hipMemcpyAsync(hr, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -410,6 +453,7 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
     pool_release(device, t->rec, t->rec_cap);
     t->rec = nullptr;
     t->pfx = t->fence = nullptr;
+    t->dir = nullptr;
     t->nlines = 0;
     lk.unlock();  // index_table takes the workspace itself
     if ((rc = index_table(t.get(), s))) return rc;

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
@@ -412,8 +413,12 @@ __device__ __forceinline__ int line_vs_query(const TableView& t, uint64_t l, con
 // The lines from b on that share the query's prefix, by a galloping search
 // with record compares (b: the prefix's lower bound, < nlines).
 __device__ __forceinline__ int64_t resolve_from(const TableView& t, const Query& q, uint64_t b, LineRec& hit) {
-  LineRec r;
-  int c = line_vs_query(t, b, q, r);
+  // line b's prefix and record in one round trip (the record is needed
+  // whenever the prefix matches, i.e. for every key that is present)
+  const uint64_t p0 = t.pfx[b];
+  LineRec r = t.rec[b];
+  if (p0 != q.w0) return -1;  // p0 > q.w0: b is the prefix's lower bound
+  int c = rec_cmp(t, r, q);
   if (c == 0) {
     hit = r;
     return (int64_t)b;
@@ -463,6 +468,50 @@ __device__ __forceinline__ void level_down(const TableView& t, uint32_t j, uint6
   hi = (i << kFanBits) < cnt ? (i << kFanBits) : cnt;
 }
 
+// Whether table t's directory applies: the shared prefix bits plus the
+// bucket bits fit the 64-bit prefix (dshift and dp0 set by the kernel).
+__device__ __forceinline__ bool dir_usable(const TableView& t) {
+  return t.dbits && t.dshift + t.dbits <= 64;
+}
+
+// Where x's descent starts: level j and the run [lo, hi) of at most 16
+// entries holding its lower bound (returns false), or the lower bound b itself
+// (returns true) when x lies outside the table's shared prefix bits or in an
+// empty bucket. Lines before dir[B] have smaller buckets (so smaller
+// prefixes) and lines from dir[B+1] on larger ones, so on every level the
+// entries sampled from [dir[B], dir[B+1]] bracket x's lower bound.
+__device__ __forceinline__ bool dir_start(const TableView& t, uint64_t x, uint32_t& j, uint64_t& lo, uint64_t& hi,
+                                          uint64_t& b) {
+  j = t.nlev;
+  lo = 0;
+  hi = level_count(t.nlines, j);
+  if (!dir_usable(t)) return false;
+  const uint32_t sh = t.dshift;
+  if (sh && ((x ^ t.dp0) >> (64 - sh))) {
+    b = x < t.dp0 ? 0 : t.nlines;
+    return true;
+  }
+  const uint64_t bk = (x << sh) >> (64 - t.dbits);
+  const uint64_t a = t.dir[bk], e = t.dir[bk + 1];
+  if (a == e) {
+    b = a;
+    return true;
+  }
+  for (uint32_t l = 0; l < t.nlev; ++l) {
+    const uint64_t l0 = a >> (kFanBits * l);
+    const uint64_t c = level_count(t.nlines, l);
+    uint64_t l1 = (e + (1ull << (kFanBits * l)) - 1) >> (kFanBits * l);
+    l1 = l1 < c ? l1 : c;
+    if (l1 - l0 <= kFanout) {
+      j = l;
+      lo = l0;
+      hi = l1;
+      return false;
+    }
+  }
+  return false;  // the top level (at most 16 entries)
+}
+
 // Well-formed files (keys strictly increasing, so any correct search returns
 // the reference's line): the lower bound of the key's 8-byte prefix down the
 // fence levels (one run of at most 16 entries, one 128-B line, per level),
@@ -470,8 +519,10 @@ __device__ __forceinline__ void level_down(const TableView& t, uint32_t j, uint6
 // compares: O(log run) for keys that share long prefixes ('user0000...'), one
 // record compare when the prefix is unique.
 __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& q, LineRec& hit) {
-  uint64_t lo = 0, hi = level_count(t.nlines, t.nlev);
-  for (uint32_t j = t.nlev;; --j) {
+  uint32_t j;
+  uint64_t lo, hi, b;
+  if (dir_start(t, q.w0, j, lo, hi, b)) return b < t.nlines ? resolve_from(t, q, b, hit) : -1;
+  for (;; --j) {
     const uint64_t i = lower_bound_u64(level_array(t, j), lo, hi, q.w0);
     if (!j) {
       if (i >= t.nlines) return -1;
@@ -483,6 +534,59 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
 
 __device__ __forceinline__ int64_t search(const TableView& t, const Query& q, LineRec& hit) {
   return t.fast ? search_fast(t, q, hit) : search_exact(t, q, hit);
+}
+
+// dir[B] for B in [0, 2^dbits]: the lower bound of bucket B's smallest prefix.
+__global__ __launch_bounds__(kNT) void k_table_dir(const uint64_t* __restrict__ pfx, uint64_t nl, uint32_t dbits,
+                                                   uint32_t* __restrict__ dir) {
+  const uint64_t B = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  const uint64_t nb = 1ull << dbits;
+  if (B > nb) return;
+  if (B == nb) {
+    dir[B] = (uint32_t)nl;
+    return;
+  }
+  const uint64_t p0 = pfx[0], p1 = pfx[nl - 1];
+  const uint32_t shared = p0 == p1 ? 64u : (uint32_t)__builtin_clzll(p0 ^ p1);
+  if (shared + dbits > 64) {  // unused (dir_usable is false)
+    dir[B] = 0;
+    return;
+  }
+  const uint64_t hi_bits = shared ? p0 & ~(~0ull >> shared) : 0ull;
+  const uint64_t w = hi_bits | ((B << (64 - dbits)) >> shared);
+  dir[B] = (uint32_t)lower_bound_u64(pfx, 0, nl, w);
+}
+
+// A block's views of the first min(nt, 64) tables into LDS. Barrier inside.
+// The first min(nt, 64) tables' views, staged once per block into LDS: loaded
+// into registers first (issued with the key and gate loads, so their round
+// trip overlaps those), then stored after the gate. Barrier in store_views.
+constexpr uint32_t kViewDw = sizeof(TableView) / 4;
+constexpr uint32_t kViewPer = (64 * kViewDw + kNT - 1) / kNT;
+static_assert(sizeof(TableView) % 4 == 0, "dword copy");
+struct ViewRegs {
+  uint32_t w[kViewPer];
+};
+__device__ __forceinline__ ViewRegs load_views(const TableView* tv, uint32_t nt) {
+  ViewRegs v;
+  const uint32_t nd = (nt < 64 ? nt : 64) * kViewDw;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(tv);
+#pragma unroll
+  for (uint32_t i = 0; i < kViewPer; ++i) {
+    const uint32_t d = threadIdx.x + i * kNT;
+    v.w[i] = d < nd ? src[d] : 0u;
+  }
+  return v;
+}
+__device__ __forceinline__ void store_views(const ViewRegs& v, uint32_t nt, TableView* stv) {
+  const uint32_t nd = (nt < 64 ? nt : 64) * kViewDw;
+  uint32_t* dst = reinterpret_cast<uint32_t*>(stv);
+#pragma unroll
+  for (uint32_t i = 0; i < kViewPer; ++i) {
+    const uint32_t d = threadIdx.x + i * kNT;
+    if (d < nd) dst[d] = v.w[i];
+  }
+  __syncthreads();
 }
 
 template <int KEYK>
@@ -510,6 +614,7 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
   // wave's 64 keys share one hit word per table row, so lane i loads row i's
   // word (one load instruction for the wave, not one per table) and every
   // lane takes its bit of each row from lane i by a uniform shuffle.
+  const ViewRegs vr = load_views(tv, nt);
   const uint32_t gn0 = nt < 64 ? nt : 64;
   uint64_t cand0 = gn0 == 64 ? ~0ull : ((1ull << gn0) - 1);
   // the key's loads go out with the gate's (independent of it)
@@ -524,14 +629,7 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
   // the first 64 tables' views, staged once per block: each lane's search
   // reads its table's view from LDS instead of a divergent global gather
   __shared__ TableView stv[64];
-  {
-    static_assert(sizeof(TableView) % 4 == 0, "dword copy");
-    const uint32_t nst = nt < 64 ? nt : 64;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(tv);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(stv);
-    for (uint32_t i = threadIdx.x; i < nst * (uint32_t)(sizeof(TableView) / 4); i += kNT) dst[i] = src[i];
-  }
-  __syncthreads();
+  store_views(vr, nt, stv);
   uint64_t d = 0;
   if (k < n) {
     int32_t w = -1;
@@ -787,6 +885,14 @@ hipError_t launch_table_search(int keyk, const TableView& t, const KeySrc& ks, u
     case KEY_VAR: hipLaunchKernelGGL(k_table_search<KEY_VAR>, g, dim3(kNT), 0, s, t, ks, n, line); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_table_dir(const uint64_t* pfx, uint64_t nlines, uint32_t* dir, hipStream_t s) {
+  const uint32_t db = dir_bits(nlines);
+  if (!db) return hipSuccess;
+  ProfScope ps("k_table_dir", s);
+  hipLaunchKernelGGL(k_table_dir, dim3(blocks_for((1ull << db) + 1, kNT)), dim3(kNT), 0, s, pfx, nlines, db, dir);
   return hipGetLastError();
 }
 

@@ -51,6 +51,23 @@ __device__ __forceinline__ void fence_put(uint64_t* fence, uint64_t nl, uint64_t
     off += level_count(nl, j);
   }
 }
+// Radix directory of a well-formed table: below the prefix bits every line
+// shares (dshift = clz(pfx[0] ^ pfx[nlines-1])), the next dbits bits of a
+// prefix name its bucket; dir[B] = the first line whose bucket is >= B
+// (dir[2^dbits] = nlines). A lookup reads dir[B], dir[B+1] and starts the
+// fence descent at the lowest level where the bucket spans at most 16
+// entries: ~2^kDirLineBits lines per bucket, so random keys start at level 1
+// instead of the top. Tables of fewer than 256 lines have none.
+constexpr uint32_t kDirLineBits = 3;
+__host__ __device__ inline uint32_t dir_bits(uint64_t nl) {
+  if (nl < (1ull << (kDirLineBits + 2)) || nl >= (1ull << 32)) return 0;
+  const uint32_t b = 63u - (uint32_t)__builtin_clzll(nl) - kDirLineBits;
+  return b > 24 ? 24 : b;
+}
+inline uint64_t dir_words(uint64_t nl) {  // uint32 words
+  const uint32_t b = dir_bits(nl);
+  return b ? (1ull << b) + 1 : 0;
+}
 constexpr uint32_t kBadValue = 0xFFFFFFFFu;  // value that STANDARD.decode rejects
 
 // Per-line index record (32 B, one load). vdl is computed once at index
@@ -83,6 +100,10 @@ struct TableView {
   uint64_t nlines;
   uint32_t nlev;          // fence_levels(nlines)
   uint32_t fast;
+  const uint32_t* dir;    // dir_words(nlines) (nullptr: none)
+  uint32_t dbits;         // dir_bits(nlines)
+  uint32_t dshift;        // prefix bits every line shares (64: directory unused)
+  uint64_t dp0;           // pfx[0]
 };
 
 // ---- line index build: count -> scan -> emit -> finish ----
@@ -102,6 +123,10 @@ hipError_t launch_line_finish(const uint8_t* data, uint64_t len, uint64_t nlines
 // *ok &= (every line has a TAB and key[l-1] < key[l]).
 hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, LineRec* rec, uint64_t* pfx,
                             uint64_t* fence, uint32_t* ok, hipStream_t s);
+
+// dir[0 .. dir_words(nlines)) of a table whose pfx is sorted (built for every
+// table; used only when the table is well-formed).
+hipError_t launch_table_dir(const uint64_t* pfx, uint64_t nlines, uint32_t* dir, hipStream_t s);
 
 // Exclusive scan of n uint64 (out[n] = total). tmp: scan_tmp_words(n) words.
 uint64_t scan_tmp_words(uint64_t n);

@@ -317,3 +317,131 @@ def test_table_rebuild_vs_oracle(gpu, m):
         assert _check_rebuild(gpu, data, m) is None, bad
     # invalid bytes on a TAB-less line or after the TAB do not matter
     assert _check_rebuild(gpu, b"\xff\xfe\nk\t\xff\n", m) is not None
+
+
+def _keys_hi(hi: np.ndarray, seed: int) -> np.ndarray:
+    """16-byte keys whose first 8 bytes are hi (big-endian), the rest random."""
+    lo = np.random.default_rng(seed).integers(0, 1 << 63, len(hi), dtype=np.uint64)
+    k = np.empty((len(hi), 2), dtype=">u8")
+    k[:, 0], k[:, 1] = hi, lo
+    b = k.view(np.uint8).reshape(-1, 16).copy()
+    b[(b == 9) | (b == 10)] = 11  # no TAB / newline inside a key
+    return np.unique(b, axis=0)
+
+
+@pytest.mark.parametrize("shape", ["uniform", "shared20", "shared60", "clustered", "equal"])
+def test_search_directory_vs_oracle(gpu, shape):
+    """The radix directory (sstable.hpp dir_bits / dir_start) under prefix
+    distributions that move its bucket bits: uniform prefixes, 20 and 60
+    shared leading bits (the latter leaves no room: directory unused), a
+    clustered set with long runs of empty buckets, and one equal prefix.
+    Probes: present keys, absent keys, prefixes at bucket edges and prefixes
+    outside the shared bits on both sides. t.search, get_many (the staged
+    kernel, <= 64 tables) and the exact trajectory agree with the oracle."""
+    rng = np.random.default_rng({"uniform": 1, "shared20": 2, "shared60": 3, "clustered": 4, "equal": 5}[shape])
+    for n in (255, 256, 257, 5000, 70_001):
+        if shape == "uniform":
+            hi = rng.integers(0, 1 << 64, n, dtype=np.uint64)
+        elif shape == "shared20":
+            hi = (np.uint64(0xABCDE) << np.uint64(44)) | rng.integers(0, 1 << 44, n, dtype=np.uint64)
+        elif shape == "shared60":
+            hi = (np.uint64(0x123456789ABCDEF) << np.uint64(4)) | rng.integers(0, 16, n, dtype=np.uint64)
+        elif shape == "clustered":
+            a = rng.integers(0, 1 << 40, n // 2, dtype=np.uint64) + np.uint64(1 << 62)
+            b = rng.integers(0, 1 << 64, n - n // 2, dtype=np.uint64)
+            hi = np.concatenate([a, b])
+        else:
+            hi = np.full(n, 0x7573657230303030, dtype=np.uint64)
+        keys = _keys_hi(hi, n)
+        data = workload.sstable_bytes(keys, workload.table_value(keys, 2)).tobytes()
+        t = gpu.Table(data)
+        assert t.well_formed
+        ot = oracle.OracleTable(data)
+        h = keys[:, :8].copy().view(">u8").reshape(-1).astype(np.uint64)
+        edges = []
+        for x in h[rng.integers(0, len(h), 200)]:
+            for bits in (4, 12, 20, 40):  # bucket-edge prefixes around present keys
+                m = np.uint64((1 << bits) - 1)
+                edges += [x & ~m, x | m]
+        edges += [0, (1 << 64) - 1, int(h.min()) - 1 if h.min() else 0, int(h.max()) + 1 if h.max() < (1 << 64) - 1 else 0]
+        eh = np.array(edges, dtype=np.uint64)
+        absent = _keys_hi(np.concatenate([eh, rng.integers(0, 1 << 64, 2000, dtype=np.uint64)]), 7)
+        look = np.concatenate([keys[rng.integers(0, len(keys), 3000)], absent, keys[:1], keys[-1:]])
+        exp = [ot.search(bytes(k))[0] for k in look]
+        assert list(t.search(look)) == exp, n
+        which, voff, vals = gpu.get_many([t], look)
+        d = np.ascontiguousarray(look.reshape(-1))
+        offs = np.arange(0, 16 * (len(look) + 1), 16, dtype=np.uint64)
+        ow, ovoff, ovals = oracle.get_many([ot], None, d, offs)
+        assert np.array_equal(which, ow) and vals == ovals, n
+
+
+def test_get_many_past_64_tables_vs_oracle(gpu):
+    """More than 64 tables: get_many's lane-per-search form (tables past the
+    first 64 read their views from HBM, the first 64 from LDS with their
+    directories), gated and ungated, against the oracle."""
+    rng = np.random.default_rng(21)
+    nt = 70
+    per = [workload.key_range(3000 + t, 300 + 40 * t) for t in range(nt)]
+    files = [workload.sstable_bytes(k, workload.table_value(k, t)) for t, k in enumerate(per)]
+    tables = [gpu.Table(f) for f in files]
+    otables = [oracle.OracleTable(f.tobytes()) for f in files]
+    look = np.concatenate([per[t][rng.integers(0, len(per[t]), 100)] for t in range(nt)] +
+                          [workload.key_range(99, 3000)])
+    look = look[rng.permutation(len(look))]
+    d = np.ascontiguousarray(look.reshape(-1))
+    offs = np.arange(0, 16 * (len(look) + 1), 16, dtype=np.uint64)
+    ow, ovoff, ovals = oracle.get_many(otables, None, d, offs)
+    which, voff, vals = gpu.get_many(tables, look)
+    assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals
+    assert (ow >= 0).sum() == 100 * nt and (ow >= 64).any()
+
+
+def test_get_many_async_and_view_cache(gpu):
+    """get_many(wait=False) (C ABI total = NULL): enqueue only, the total in
+    val_off[n]; consecutive calls on one stream with different table lists and
+    hit rows (the views / rows upload cache must refresh) and the same lists
+    again all give the synchronous answers."""
+    import torch
+    rng = np.random.default_rng(8)
+    per = [workload.key_range(5100 + t, 2000 + 700 * t) for t in range(5)]
+    tables = [gpu.Table(workload.sstable_bytes(k, workload.table_value(k, t))) for t, k in enumerate(per)]
+    look = np.concatenate([per[t][rng.integers(0, len(per[t]), 500)] for t in range(5)] +
+                          [workload.key_range(42, 1000)])
+    look = look[rng.permutation(len(look))]
+    dk = gpu.DeviceKeys(torch.from_numpy(look.copy()).cuda())
+    n = len(look)
+    lists = [tables, tables[::-1], tables[1:4], tables]
+    s = torch.cuda.Stream()
+    outs = []
+    for tl in lists:
+        o = (torch.empty(n, dtype=torch.int32, device="cuda"), torch.empty(n + 1, dtype=torch.int64, device="cuda"),
+             torch.empty(n * 16, dtype=torch.uint8, device="cuda"))
+        assert gpu.get_many(tl, dk, out=o, stream=s, wait=False)[2] is None
+        outs.append(o)
+    s.synchronize()
+    for tl, (w, vo, vals) in zip(lists, outs):
+        ew, evo, evals = gpu.get_many(tl, look)
+        tot = int(vo[n].item())
+        assert np.array_equal(w.cpu().numpy(), ew) and tot == len(evals)
+        assert np.array_equal(vo.cpu().numpy().astype(np.uint64), evo)
+        assert bytes(vals[:tot].cpu().numpy()) == evals
+    # hit rows change between calls on one stream
+    hits = np.zeros((5, (n + 63) // 64), dtype=np.uint64)
+    hits[0::2] = ~np.uint64(0)  # rows 0, 2, 4 admit every key, rows 1, 3 none
+    hd = torch.from_numpy(hits.view(np.int64)).cuda()
+    res = []
+    for rows in (np.array([1, 2, 3, 4, 0]), np.arange(5)):
+        o = (torch.empty(n, dtype=torch.int32, device="cuda"), torch.empty(n + 1, dtype=torch.int64, device="cuda"),
+             torch.empty(n * 16, dtype=torch.uint8, device="cuda"))
+        gpu.get_many(tables, dk, hits=hd, hit_rows=rows, out=o, stream=s, wait=False)
+        res.append(o)
+    s.synchronize()
+    for rows, (w, _, _) in zip((np.array([1, 2, 3, 4, 0]), np.arange(5)), res):
+        ew, _, _ = gpu.get_many(tables, look, hits=hits, hit_rows=rows)
+        assert np.array_equal(w.cpu().numpy(), ew)
+    assert not np.array_equal(res[0][0].cpu().numpy(), res[1][0].cpu().numpy())
+    # host outputs are refused without a total
+    with pytest.raises(Exception):
+        gpu.get_many(tables, look, out=(np.zeros(n, np.int32), np.zeros(n + 1, np.uint64), np.zeros(16, np.uint8)),
+                     wait=False)
