@@ -136,7 +136,7 @@ struct Workspace {
   std::vector<uint8_t> t_views_host;
   std::vector<uint32_t> t_rows_host;
   DevBuf i_cnt, i_base, i_tmp, i_end, i_err, i_start;                 // line indexing
-  DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_tsum, f_flag;  // SsTable::create
+  DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_tsum, f_flag, f_vsp;  // SsTable::create
   DevBuf x_ctl;                   // cb_hits_compress: slot / finish counters (zeroed once)
   cb::CompressState xst;
   cb::CreateResult* hres = nullptr;  // pinned host mirror of f_flag (SsTable::create)

@@ -289,6 +289,7 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   const uint8_t *dk = nullptr, *dv = nullptr;
   const uint64_t *dko = nullptr, *dvo = nullptr;
   const cb::SortKey* order = nullptr;
+  ulonglong2* vsp = nullptr;  // sorted value spans (hand-written sort)
   uint64_t ktot = 0, vtot = 0;
   Workspace& ws = workspace(device, s);
   std::unique_lock<std::mutex> lk(ws.mu);
@@ -394,23 +395,27 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
     HIP_TRY(ws.f_sk2.reserve(n * sizeof(cb::SortKey), s));
     cb::SortKey* a0 = (cb::SortKey*)ws.f_sk.p;
     cb::SortKey* a1 = (cb::SortKey*)ws.f_sk2.p;
-    HIP_TRY(cb::launch_sort_keys(dk, dko, n, a0, s));
     static const bool use_rocprim = [] {
       const char* v = getenv("CB_SORT");
       return v && std::strcmp(v, "rocprim") == 0;
     }();
     if (use_rocprim) {  // rocPRIM's merge sort, for comparison (same order)
+      HIP_TRY(cb::launch_sort_keys(dk, dko, n, a0, s));
       size_t tmp_bytes = 0;
       HIP_TRY(cb::entry_sort(nullptr, tmp_bytes, a0, a1, n, dk, dko, s));
       HIP_TRY(ws.f_sort.reserve(tmp_bytes + 16, s));
       HIP_TRY(cb::entry_sort(ws.f_sort.p, tmp_bytes, a0, a1, n, dk, dko, s));
+      HIP_TRY(cb::launch_line_sums(a1, dko, dvo, n, tsum, s));
     } else {
+      // records built inside the block sort; the last round also leaves the
+      // value spans and the line tiles in sorted order for k_format
       HIP_TRY(ws.f_sort.reserve(cb::entry_sort_tmp_bytes(n), s));
-      HIP_TRY(cb::launch_entry_sort(a0, a1, (cb::SortKey*)ws.f_sort.p, n, dk, dko, s));
+      HIP_TRY(ws.f_vsp.reserve(n * sizeof(ulonglong2), s));
+      vsp = (ulonglong2*)ws.f_vsp.p;
+      HIP_TRY(cb::launch_entry_sort(nullptr, a1, (cb::SortKey*)ws.f_sort.p, n, dk, dko, s, dvo, vsp, tsum));
     }
     order = a1;
   }
-  if (order) HIP_TRY(cb::launch_line_sums(order, dko, dvo, n, tsum, s));
   HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
   // the line index straight from the entries (entry p is line p), no re-read of the file
   t->nlines = n;
@@ -420,7 +425,7 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   }
   carve_index(t.get());
   HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, tsum, n, t->data, t->rec, t->pfx, t->fence, dr,
-                            cap_bytes, s));
+                            cap_bytes, s, vsp));
   if (t->dir) {
     HIP_TRY(cb::launch_table_dir(t->pfx, n, t->dir, s));
     HIP_TRY(hipMemcpyAsync(&t->pfx_first, t->pfx, 8, hipMemcpyDeviceToHost, s));

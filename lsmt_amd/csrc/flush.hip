@@ -26,43 +26,23 @@ constexpr uint32_t kNT = 256;  // = kFormatTile
 inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
 
 
-// The first min(len, 16) bytes at src as zero-padded big-endian words, from
-// the aligned dwords that contain them (a dword never crosses a page edge, so
-// these loads stay inside mapped memory however src is aligned).
-__device__ __forceinline__ void load16(const uint8_t* src, uint64_t len, uint64_t& w0, uint64_t& w1) {
-  const uint64_t m = len < 16 ? len : 16;
-  uint32_t d[5] = {0, 0, 0, 0, 0};
-  const uint64_t a0 = (uint64_t)(uintptr_t)src;
-  const uint32_t* base = reinterpret_cast<const uint32_t*>((uintptr_t)(a0 & ~3ull));
-  const uint32_t sh = (uint32_t)(a0 & 3);
-  const uint32_t nd = m ? (uint32_t)((sh + m + 3) / 4) : 0;  // dwords holding the first m bytes
-#pragma unroll
-  for (uint32_t j = 0; j < 5; ++j)
-    if (j < nd) d[j] = base[j];
-  uint32_t x[4];
-#pragma unroll
-  for (uint32_t j = 0; j < 4; ++j) x[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
-  // little-endian bytes -> big-endian words, bytes past m cleared
-  const uint64_t lo = (uint64_t)x[1] << 32 | x[0], hi = (uint64_t)x[3] << 32 | x[2];
-  const uint64_t b0 = __builtin_bswap64(lo), b1 = __builtin_bswap64(hi);
-  w0 = m >= 8 ? b0 : (m ? b0 & ~(~0ull >> (8 * m)) : 0);
-  w1 = m >= 16 ? b1 : (m > 8 ? b1 & ~(~0ull >> (8 * (m - 8))) : 0);
-}
-
 // The first 16 bytes of key p (output order) as zero-padded big-endian words,
 // and its length. Unsorted input: the sort record already holds them; sorted
 // input: load16 of the key's bytes.
 __device__ __forceinline__ void key_words(const SortKey* order, const uint8_t* kb,
                                           const uint64_t* ko, uint64_t p, uint64_t& i,
                                           uint64_t& kl, uint64_t& w0, uint64_t& w1) {
-  i = order ? order[p].idx : p;
-  const uint64_t o0 = ko[i];
-  kl = ko[i + 1] - o0;
-  if (order) {
-    w0 = order[p].w0;
-    w1 = order[p].w1;
+  if (order) {  // the record holds the words and (unless clamped) the length
+    const SortKey sk = order[p];
+    i = sk.idx;
+    w0 = sk.w0;
+    w1 = sk.w1;
+    kl = sk.len != 0xFFFFFFFFu ? sk.len : ko[i + 1] - ko[i];
     return;
   }
+  i = p;
+  const uint64_t o0 = ko[i];
+  kl = ko[i + 1] - o0;
   load16(kb + o0, kl, w0, w1);
 }
 
@@ -80,14 +60,7 @@ __global__ __launch_bounds__(kNT) void k_sort_keys(const uint8_t* __restrict__ k
                                                    SortKey* __restrict__ out) {
   const uint64_t p = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   if (p >= n) return;
-  uint64_t i, kl, w0, w1;
-  key_words(nullptr, kb, ko, p, i, kl, w0, w1);
-  SortKey s;
-  s.w0 = w0;
-  s.w1 = w1;
-  s.len = kl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)kl;
-  s.idx = (uint32_t)p;
-  out[p] = s;
+  out[p] = sort_record(kb, ko, p);
 }
 
 // Rust str order of keys q and p (q, p index the key batch) given their first
@@ -103,9 +76,6 @@ __device__ __forceinline__ int key_cmp(const uint8_t* kb, const uint64_t* ko, ui
   return bytes_cmp(kb + ko[q], ql, kb + ko[p], pl);
 }
 
-// Line p's byte length: key, TAB, base64 of the value, newline
-// (src/sstable.rs:66-70); 0 past the last line.
-__device__ __forceinline__ uint64_t line_len(uint64_t kl, uint64_t vl) { return kl + 1 + (vl + 2) / 3 * 4 + 1; }
 
 // The sum of each kFormatTile-line tile's lengths (order == nullptr: input
 // order), for k_format's offsets. Call uniformly.
@@ -296,7 +266,7 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
                                                 const uint64_t* __restrict__ tsum, uint64_t n,
                                                 uint8_t* __restrict__ out, LineRec* __restrict__ rec,
                                                 uint64_t* __restrict__ pfx, uint64_t* __restrict__ fence,
-                                                CreateResult* r) {
+                                                CreateResult* r, const ulonglong2* __restrict__ vsp) {
   __shared__ uint32_t stage32[LDSB / 4];
   uint8_t* stage = reinterpret_cast<uint8_t*>(stage32);
   const uint64_t p0 = (uint64_t)blockIdx.x * kNT;
@@ -310,7 +280,15 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   uint64_t pkl = __shfl_up(kl, 1, 64), pw0 = __shfl_up(w0, 1, 64), pw1 = __shfl_up(w1, 1, 64);
   uint64_t pi = __shfl_up(i, 1, 64);
   if (live && lane == 0 && p > 0) key_words(order, kb, ko, p - 1, pi, pkl, pw0, pw1);
-  const uint64_t vo0 = live ? vo[i] : 0, vl = live ? vo[i + 1] - vo0 : 0;
+  uint64_t vo0 = 0, vl = 0;
+  if (live && vsp) {  // sorted by launch_entry_sort: in output order, one coalesced load
+    const ulonglong2 e = vsp[p];
+    vo0 = e.x;
+    vl = e.y;
+  } else if (live) {
+    vo0 = vo[i];
+    vl = vo[i + 1] - vo0;
+  }
   // the line's offset: the tiles before this block, then the scan inside it
   uint64_t total;
   const uint64_t pre = block_scan<kNT>(live ? line_len(kl, vl) : 0, &total);
@@ -347,19 +325,16 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
     // 16 zero bytes after the file: the readable slack of the table's buffer
     if (threadIdx.x < 16) out[base + total + threadIdx.x] = 0;
   }
-  const uint8_t* k = kb + (live ? ko[i] : 0);
+  const uint8_t* k = kb + (live && kl > 16 ? ko[i] : 0);  // key bytes: only past 16 (else the words)
   const uint8_t* v = vb + vo0;
   uint64_t v0 = 0, v1 = 0;
   const bool words = kl <= 16 && vl <= 16;
-  if (live && words) load16(v, vl, v0, v1);
+  if (live && vl <= 16) load16(v, vl, v0, v1);
   auto emit = [&](auto put) {  // byte at a time (long lines)
     if (!live) return;
-    if (words)
-      format_line(kl, [&](uint64_t j) { return be_byte(w0, w1, j); }, vl,
-                  [&](uint64_t j) { return be_byte(v0, v1, j); }, put);
-    else
-      format_line(kl, [&](uint64_t j) { return (uint32_t)k[j]; }, vl,
-                  [&](uint64_t j) { return (uint32_t)v[j]; }, put);
+    auto kbyte = [&](uint64_t j) { return kl <= 16 ? be_byte(w0, w1, j) : (uint32_t)k[j]; };
+    auto vbyte = [&](uint64_t j) { return vl <= 16 ? be_byte(v0, v1, j) : (uint32_t)v[j]; };
+    format_line(kl, kbyte, vl, vbyte, put);
   };
   const uint64_t sh0 = base & 3;
   if (total + sh0 > LDSB) {  // uniform: long lines, direct byte stores
@@ -440,16 +415,16 @@ hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* 
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
-                         uint64_t bytes_bound, hipStream_t s) {
+                         uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp) {
   if (!n) return hipSuccess;
   ProfScope ps("k_format", s);
   const dim3 g(blocks_for(n, kNT));
   if (bytes_bound / n * kNT * 5 / 4 <= kFormatLdsSmall)
     hipLaunchKernelGGL(k_format<kFormatLdsSmall>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
-                       rec, pfx, fence, r);
+                       rec, pfx, fence, r, order ? vsp : nullptr);
   else
     hipLaunchKernelGGL(k_format<kFormatLdsLarge>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
-                       rec, pfx, fence, r);
+                       rec, pfx, fence, r, order ? vsp : nullptr);
   return hipGetLastError();
 }
 

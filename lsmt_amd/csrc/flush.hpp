@@ -15,6 +15,43 @@ struct SortKey {
   uint32_t len, idx;
 };
 
+// The first min(len, 16) bytes at src as zero-padded big-endian words, from
+// the aligned dwords that contain them (a dword never crosses a page edge, so
+// these loads stay inside mapped memory however src is aligned).
+__device__ __forceinline__ void load16(const uint8_t* src, uint64_t len, uint64_t& w0, uint64_t& w1) {
+  const uint64_t m = len < 16 ? len : 16;
+  uint32_t d[5] = {0, 0, 0, 0, 0};
+  const uint64_t a0 = (uint64_t)(uintptr_t)src;
+  const uint32_t* base = reinterpret_cast<const uint32_t*>((uintptr_t)(a0 & ~3ull));
+  const uint32_t sh = (uint32_t)(a0 & 3);
+  const uint32_t nd = m ? (uint32_t)((sh + m + 3) / 4) : 0;  // dwords holding the first m bytes
+#pragma unroll
+  for (uint32_t j = 0; j < 5; ++j)
+    if (j < nd) d[j] = base[j];
+  uint32_t x[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) x[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+  // little-endian bytes -> big-endian words, bytes past m cleared
+  const uint64_t lo = (uint64_t)x[1] << 32 | x[0], hi = (uint64_t)x[3] << 32 | x[2];
+  const uint64_t b0 = __builtin_bswap64(lo), b1 = __builtin_bswap64(hi);
+  w0 = m >= 8 ? b0 : (m ? b0 & ~(~0ull >> (8 * m)) : 0);
+  w1 = m >= 16 ? b1 : (m > 8 ? b1 & ~(~0ull >> (8 * (m - 8))) : 0);
+}
+
+// The sort record of entry p of a key batch (kb, ko).
+__device__ __forceinline__ SortKey sort_record(const uint8_t* kb, const uint64_t* ko, uint64_t p) {
+  const uint64_t o0 = ko[p], kl = ko[p + 1] - o0;
+  SortKey s;
+  load16(kb + o0, kl, s.w0, s.w1);
+  s.len = kl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)kl;
+  s.idx = (uint32_t)p;
+  return s;
+}
+
+// Line p's byte length: key, TAB, base64 of the value, newline
+// (src/sstable.rs:66-70).
+__host__ __device__ inline uint64_t line_len(uint64_t kl, uint64_t vl) { return kl + 1 + (vl + 2) / 3 * 4 + 1; }
+
 // What SsTable::create hands back to the host, assembled on the device so that
 // each of its two host round trips is one copy into pinned memory.
 constexpr uint32_t kZoneInline = 256;  // zone bound key bytes carried inline
@@ -44,10 +81,15 @@ hipError_t launch_line_sums(const SortKey* order, const uint64_t* ko, const uint
                             uint64_t* tsum, hipStream_t s);
 // Stable sort of the records by key, hand-written (sort.hip): LDS block
 // sorts of 2048 records, then merge-path rounds. tmp: entry_sort_tmp_bytes(n)
-// of scratch; in must not alias out or tmp.
+// of scratch; in must not alias out or tmp. in == nullptr: the block sort
+// builds the records from the key batch itself (no launch_sort_keys pass).
+// vo != nullptr: the last launch also writes, for every output p, vsp[p] =
+// {vo[idx], value length} and tsum = the line tiles in sorted order (what
+// launch_line_sums would), from the records it holds in registers.
 uint64_t entry_sort_tmp_bytes(uint64_t n);
 hipError_t launch_entry_sort(const SortKey* in, SortKey* out, SortKey* tmp, uint64_t n, const uint8_t* kb,
-                             const uint64_t* ko, hipStream_t s);
+                             const uint64_t* ko, hipStream_t s, const uint64_t* vo = nullptr,
+                             ulonglong2* vsp = nullptr, uint64_t* tsum = nullptr);
 // The same order through rocPRIM's merge sort (kept for comparison,
 // CB_SORT=rocprim). tmp == nullptr: only writes the scratch size to tmp_bytes.
 hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* out, uint64_t n,
@@ -60,9 +102,11 @@ hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* 
 // reference's line split or TAB search would see): flags[1] |= 1 otherwise,
 // and the caller re-indexes the file. flags[2] &= (keys strictly increasing:
 // the well-formed check).
+// vsp (nullable, with order): entry p's {value offset, value length} in
+// sorted order (launch_entry_sort's), read instead of vo[order[p].idx].
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
-                         uint64_t bytes_bound, hipStream_t s);
+                         uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp = nullptr);
 
 }  // namespace cb
