@@ -140,7 +140,7 @@ struct Workspace {
   DevBuf x_ctl;                   // cb_hits_compress: slot / finish counters (zeroed once)
   cb::CompressState xst;
   cb::CreateResult* hres = nullptr;  // pinned host mirror of f_flag (SsTable::create)
-  uint64_t* htot = nullptr;          // pinned: get_many's value byte total
+  uint64_t* htot = nullptr;          // pinned, 64 B: get_many's value byte total; index_table's read-backs
   hipEvent_t ev = nullptr;           // marks hres's first copy in the stream
 };
 

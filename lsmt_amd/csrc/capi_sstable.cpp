@@ -202,11 +202,17 @@ int index_table(cb_table* t, hipStream_t s) {
   // prefix + fence index, value validity and the well-formed check (sstable.hpp)
   HIP_TRY(cb::launch_line_keys(t->data, nl, t->rec, t->pfx, t->fence, err + 1, s));
   if (t->dir) HIP_TRY(cb::launch_table_dir(t->pfx, nl, t->dir, s));
-  uint32_t e[2] = {0, 0};
-  HIP_TRY(hipMemcpyAsync(e, err, 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(&t->pfx_first, t->pfx, 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(&t->pfx_last, t->pfx + nl - 1, 8, hipMemcpyDeviceToHost, s));
+  // the error words and the directory's key (first / last prefix) in one
+  // pinned copy set, one wait
+  if (!ws.htot) HIP_TRY(hipHostMalloc((void**)&ws.htot, 64, hipHostMallocDefault));
+  HIP_TRY(hipMemcpyAsync(ws.htot, err, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(ws.htot + 1, t->pfx, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(ws.htot + 2, t->pfx + nl - 1, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  uint32_t e[2];
+  memcpy(e, ws.htot, 8);
+  t->pfx_first = ws.htot[1];
+  t->pfx_last = ws.htot[2];
   if (e[0]) return fail(CB_EINVAL, "an SSTable line is 4 GiB or longer");
   t->fast = e[1] != 0 && !g_table_exact;
   return CB_OK;
@@ -425,16 +431,13 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   }
   carve_index(t.get());
   HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, tsum, n, t->data, t->rec, t->pfx, t->fence, dr,
-                            cap_bytes, s, vsp));
-  if (t->dir) {
-    HIP_TRY(cb::launch_table_dir(t->pfx, n, t->dir, s));
-    HIP_TRY(hipMemcpyAsync(&t->pfx_first, t->pfx, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(&t->pfx_last, t->pfx + n - 1, 8, hipMemcpyDeviceToHost, s));
-  }
+                            cap_bytes, s, vsp, t->dir));
   // Round trip 2: flags, file length, zone bounds
   HIP_TRY(hipMemcpyAsync(hr, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   t->len = hr->len;
+  t->pfx_first = hr->pfx_lo;
+  t->pfx_last = hr->pfx_hi;
   // zone map: ZoneMap::update over the sorted keys = first / last line
   if (zone_min_idx) *zone_min_idx = hr->idx_min;
   if (zone_max_idx) *zone_max_idx = hr->idx_max;

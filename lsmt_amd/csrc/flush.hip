@@ -114,6 +114,8 @@ __global__ __launch_bounds__(kNT) void k_sorted_check(const uint8_t* __restrict_
   }
   uint64_t i = 0, kl = 0, w0 = 0, w1 = 0;
   if (p < n) key_words(nullptr, kb, ko, p, i, kl, w0, w1);
+  if (p == 0) r->pfx_lo = w0;  // the file's first and last prefix if the input is in order
+  if (p + 1 == n) r->pfx_hi = w0;
   uint64_t pkl = __shfl_up(kl, 1, 64), pw0 = __shfl_up(w0, 1, 64), pw1 = __shfl_up(w1, 1, 64);
   uint64_t pi = p - 1;
   if (p < n && lane == 0 && p > 0) key_words(nullptr, kb, ko, p - 1, pi, pkl, pw0, pw1);
@@ -237,6 +239,34 @@ __device__ __forceinline__ uint32_t line16(uint64_t w0, uint64_t w1, uint32_t kl
   return kl + 2 + 4 * g;
 }
 
+// Wave-cooperative fill: every lane holds a range dir[s, s + c) to set to v.
+// The wave walks the non-empty ranges one by one, all 64 lanes storing each,
+// so one long range (a wide gap between two lines' buckets: keys whose bytes
+// leave many buckets empty) costs its length / 64 stores per lane instead of
+// one lane's serial loop. Whole wave.
+__device__ __forceinline__ void wave_fill(uint32_t* dir, uint64_t s, uint64_t c, uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t m = __ballot(c != 0);
+  while (m) {
+    const int L = __builtin_ctzll(m);
+    m &= m - 1;
+    const uint64_t ls = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)s, L) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(s >> 32), L) << 32;
+    const uint64_t lc = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)c, L) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(c >> 32), L) << 32;
+    const uint32_t lv = (uint32_t)__builtin_amdgcn_readlane((int)v, L);
+    uint32_t* d = dir + ls;
+    uint64_t j = lane;
+    for (; j + 192 < lc; j += 256) {  // 4 contiguous 256-B stores per round
+      d[j] = lv;
+      d[j + 64] = lv;
+      d[j + 128] = lv;
+      d[j + 192] = lv;
+    }
+    for (; j < lc; j += 64) d[j] = lv;
+  }
+}
+
 // Staged output bytes per block: 16 KiB (more resident blocks) when the
 // average line is short, else 32 KiB; a block whose lines exceed the stage
 // writes its bytes directly.
@@ -266,7 +296,8 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
                                                 const uint64_t* __restrict__ tsum, uint64_t n,
                                                 uint8_t* __restrict__ out, LineRec* __restrict__ rec,
                                                 uint64_t* __restrict__ pfx, uint64_t* __restrict__ fence,
-                                                CreateResult* r, const ulonglong2* __restrict__ vsp) {
+                                                CreateResult* r, const ulonglong2* __restrict__ vsp,
+                                                uint32_t* __restrict__ dir, uint32_t dbits) {
   __shared__ uint32_t stage32[LDSB / 4];
   uint8_t* stage = reinterpret_cast<uint8_t*>(stage32);
   const uint64_t p0 = (uint64_t)blockIdx.x * kNT;
@@ -275,6 +306,13 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   const uint64_t pend = p0 + kNT < n ? p0 + kNT : n;
   const bool live = p < n;
   uint64_t i = 0, kl = 0, w0 = 0, w1 = 0;
+  // the directory's key: the file's first and last prefix (sorted records,
+  // or k_sorted_check's for input already in order), loaded up front
+  uint64_t f0 = 0, f1 = 0;
+  if (dir) {
+    f0 = order ? order[0].w0 : r->pfx_lo;
+    f1 = order ? order[n - 1].w0 : r->pfx_hi;
+  }
   if (live) key_words(order, kb, ko, p, i, kl, w0, w1);
   // the previous entry's key: the neighbour lane's, or loaded by lane 0
   uint64_t pkl = __shfl_up(kl, 1, 64), pw0 = __shfl_up(w0, 1, 64), pw1 = __shfl_up(w1, 1, 64);
@@ -314,11 +352,35 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
     lr.pad = 0;
     rec[p] = lr;
     pfx[p] = w0;
+    if (p == 0) r->pfx_lo = w0;
+    if (p == n - 1) r->pfx_hi = w0;
     fence_put(fence, n, p, w0);
     if (p > 0) not_inc = key_cmp(kb, ko, pi, pkl, pw0, pw1, i, kl, w0, w1) >= 0;
   }
   if (__syncthreads_or(special) && threadIdx.x == 0) atomicOr(&r->flags[1], 1u);
   if (__syncthreads_or(not_inc) && threadIdx.x == 0) atomicAnd(&r->flags[2], 0u);
+  if (dir) {
+    // the radix directory (sstable.hpp dir_bits): dir[B] = p for the
+    // buckets B in (bucket(line p-1), bucket(line p)], and n past the last
+    // line's
+    const uint32_t sh = f0 == f1 ? 64u : (uint32_t)__builtin_clzll(f0 ^ f1);
+    if (sh + dbits <= 64) {
+      const uint64_t nb = 1ull << dbits;
+      auto bucket = [&](uint64_t w) { return (w << sh) >> (64 - dbits); };
+      uint64_t s0 = 0, c0 = 0, s1 = 0, c1 = 0;
+      if (live) {
+        const uint64_t b1 = bucket(w0);
+        s0 = p ? bucket(pw0) + 1 : 0;
+        c0 = b1 + 1 - s0;
+        if (p == n - 1) {
+          s1 = b1 + 1;
+          c1 = nb + 1 - s1;
+        }
+      }
+      wave_fill(dir, s0, c0, (uint32_t)p);
+      wave_fill(dir, s1, c1, (uint32_t)n);
+    }
+  }
   if (blockIdx.x == 0) zone_bound(order, kb, ko, 0, 0, r);
   if (pend == n) {
     zone_bound(order, kb, ko, n - 1, 1, r);
@@ -415,16 +477,16 @@ hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* 
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
-                         uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp) {
+                         uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp, uint32_t* dir) {
   if (!n) return hipSuccess;
   ProfScope ps("k_format", s);
   const dim3 g(blocks_for(n, kNT));
   if (bytes_bound / n * kNT * 5 / 4 <= kFormatLdsSmall)
     hipLaunchKernelGGL(k_format<kFormatLdsSmall>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
-                       rec, pfx, fence, r, order ? vsp : nullptr);
+                       rec, pfx, fence, r, order ? vsp : nullptr, dir, dir ? dir_bits(n) : 0u);
   else
     hipLaunchKernelGGL(k_format<kFormatLdsLarge>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
-                       rec, pfx, fence, r, order ? vsp : nullptr);
+                       rec, pfx, fence, r, order ? vsp : nullptr, dir, dir ? dir_bits(n) : 0u);
   return hipGetLastError();
 }
 

@@ -61,6 +61,7 @@ struct CreateResult {
   uint64_t len;               // the file's length
   uint64_t idx_min, idx_max;  // input indices of the first / last key in file order
   uint32_t zlen[2];           // their full lengths
+  uint64_t pfx_lo, pfx_hi;    // the first and last line's 8-byte prefix (the directory's key)
   uint8_t zkey[2][kZoneInline];
 };
 
@@ -104,9 +105,12 @@ hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* 
 // the well-formed check).
 // vsp (nullable, with order): entry p's {value offset, value length} in
 // sorted order (launch_entry_sort's), read instead of vo[order[p].idx].
+// dir (nullable): the table's radix directory (dir_words(n)), written here
+// from the lines' prefixes (what launch_table_dir would build).
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
-                         uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp = nullptr);
+                         uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp = nullptr,
+                         uint32_t* dir = nullptr);
 
 }  // namespace cb

@@ -74,8 +74,12 @@ __device__ __forceinline__ SortKey sentinel() {
 // and len | idx << 32, the record's third word), so that a thread walking
 // its own 8 consecutive records and its neighbours walking theirs hit
 // different banks (record i sits at word i + i/8 of each array).
-constexpr uint32_t kPadded = kTile + kTile / 8;
-__device__ __forceinline__ uint32_t pad(uint32_t i) { return i + (i >> 3); }
+#ifndef CB_SORT_PADB
+#define CB_SORT_PADB 3
+#endif
+constexpr uint32_t kPadBits = CB_SORT_PADB;
+constexpr uint32_t kPadded = kTile + (kTile >> kPadBits);
+__device__ __forceinline__ uint32_t pad(uint32_t i) { return i + (i >> kPadBits); }
 
 struct LdsTile {
   uint64_t* w;  // 3 * kPadded words

@@ -340,40 +340,53 @@ def test_search_directory_vs_oracle(gpu, shape):
     kernel, <= 64 tables) and the exact trajectory agree with the oracle."""
     rng = np.random.default_rng({"uniform": 1, "shared20": 2, "shared60": 3, "clustered": 4, "equal": 5}[shape])
     for n in (255, 256, 257, 5000, 70_001):
-        if shape == "uniform":
-            hi = rng.integers(0, 1 << 64, n, dtype=np.uint64)
-        elif shape == "shared20":
-            hi = (np.uint64(0xABCDE) << np.uint64(44)) | rng.integers(0, 1 << 44, n, dtype=np.uint64)
-        elif shape == "shared60":
-            hi = (np.uint64(0x123456789ABCDEF) << np.uint64(4)) | rng.integers(0, 16, n, dtype=np.uint64)
-        elif shape == "clustered":
-            a = rng.integers(0, 1 << 40, n // 2, dtype=np.uint64) + np.uint64(1 << 62)
-            b = rng.integers(0, 1 << 64, n - n // 2, dtype=np.uint64)
-            hi = np.concatenate([a, b])
-        else:
-            hi = np.full(n, 0x7573657230303030, dtype=np.uint64)
-        keys = _keys_hi(hi, n)
+        keys = _dir_keys(shape, n, rng)
         data = workload.sstable_bytes(keys, workload.table_value(keys, 2)).tobytes()
-        t = gpu.Table(data)
-        assert t.well_formed
         ot = oracle.OracleTable(data)
-        h = keys[:, :8].copy().view(">u8").reshape(-1).astype(np.uint64)
-        edges = []
-        for x in h[rng.integers(0, len(h), 200)]:
-            for bits in (4, 12, 20, 40):  # bucket-edge prefixes around present keys
-                m = np.uint64((1 << bits) - 1)
-                edges += [x & ~m, x | m]
-        edges += [0, (1 << 64) - 1, int(h.min()) - 1 if h.min() else 0, int(h.max()) + 1 if h.max() < (1 << 64) - 1 else 0]
-        eh = np.array(edges, dtype=np.uint64)
-        absent = _keys_hi(np.concatenate([eh, rng.integers(0, 1 << 64, 2000, dtype=np.uint64)]), 7)
-        look = np.concatenate([keys[rng.integers(0, len(keys), 3000)], absent, keys[:1], keys[-1:]])
-        exp = [ot.search(bytes(k))[0] for k in look]
-        assert list(t.search(look)) == exp, n
-        which, voff, vals = gpu.get_many([t], look)
-        d = np.ascontiguousarray(look.reshape(-1))
-        offs = np.arange(0, 16 * (len(look) + 1), 16, dtype=np.uint64)
-        ow, ovoff, ovals = oracle.get_many([ot], None, d, offs)
-        assert np.array_equal(which, ow) and vals == ovals, n
+        _check_dir_table(gpu, gpu.Table(data), ot, keys, rng, n)
+        # the same file from the device flush (its k_format writes the
+        # directory), from sorted and from shuffled entries
+        ents = [(bytes(k), bytes(v)) for k, v in zip(keys, workload.table_value(keys, 2))]
+        for order in (None, rng.permutation(len(ents))):
+            t2, _, _ = gpu.sstable_create(ents if order is None else [ents[i] for i in order])
+            _check_dir_table(gpu, t2, ot, keys, rng, n)
+
+
+def _dir_keys(shape, n, rng):
+    if shape == "uniform":
+        hi = rng.integers(0, 1 << 64, n, dtype=np.uint64)
+    elif shape == "shared20":
+        hi = (np.uint64(0xABCDE) << np.uint64(44)) | rng.integers(0, 1 << 44, n, dtype=np.uint64)
+    elif shape == "shared60":
+        hi = (np.uint64(0x123456789ABCDEF) << np.uint64(4)) | rng.integers(0, 16, n, dtype=np.uint64)
+    elif shape == "clustered":
+        a = rng.integers(0, 1 << 40, n // 2, dtype=np.uint64) + np.uint64(1 << 62)
+        b = rng.integers(0, 1 << 64, n - n // 2, dtype=np.uint64)
+        hi = np.concatenate([a, b])
+    else:
+        hi = np.full(n, 0x7573657230303030, dtype=np.uint64)
+    return _keys_hi(hi, n)
+
+
+def _check_dir_table(gpu, t, ot, keys, rng, n):
+    assert t.well_formed
+    h = keys[:, :8].copy().view(">u8").reshape(-1).astype(np.uint64)
+    edges = []
+    for x in h[rng.integers(0, len(h), 200)]:
+        for bits in (4, 12, 20, 40):  # bucket-edge prefixes around present keys
+            m = np.uint64((1 << bits) - 1)
+            edges += [x & ~m, x | m]
+    edges += [0, (1 << 64) - 1, int(h.min()) - 1 if h.min() else 0, int(h.max()) + 1 if h.max() < (1 << 64) - 1 else 0]
+    eh = np.array(edges, dtype=np.uint64)
+    absent = _keys_hi(np.concatenate([eh, rng.integers(0, 1 << 64, 2000, dtype=np.uint64)]), 7)
+    look = np.concatenate([keys[rng.integers(0, len(keys), 3000)], absent, keys[:1], keys[-1:]])
+    exp = [ot.search(bytes(k))[0] for k in look]
+    assert list(t.search(look)) == exp, n
+    which, voff, vals = gpu.get_many([t], look)
+    d = np.ascontiguousarray(look.reshape(-1))
+    offs = np.arange(0, 16 * (len(look) + 1), 16, dtype=np.uint64)
+    ow, ovoff, ovals = oracle.get_many([ot], None, d, offs)
+    assert np.array_equal(which, ow) and vals == ovals, n
 
 
 def test_get_many_past_64_tables_vs_oracle(gpu):
