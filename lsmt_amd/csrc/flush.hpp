@@ -81,7 +81,7 @@ hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, const uint
 hipError_t launch_line_sums(const SortKey* order, const uint64_t* ko, const uint64_t* vo, uint64_t n,
                             uint64_t* tsum, hipStream_t s);
 // Stable sort of the records by key, hand-written (sort.hip): LDS block
-// sorts of 2048 records, then merge-path rounds. tmp: entry_sort_tmp_bytes(n)
+// sorts of 4096 records, then merge-path rounds. tmp: entry_sort_tmp_bytes(n)
 // of scratch; in must not alias out or tmp. in == nullptr: the block sort
 // builds the records from the key batch itself (no launch_sort_keys pass).
 // vo != nullptr: the last launch also writes, for every output p, vsp[p] =

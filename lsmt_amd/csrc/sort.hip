@@ -8,14 +8,15 @@
 // idx — a strict total order whose ties on the key are broken by input
 // position, i.e. exactly the stable order.
 //
-//   k_sort_block — one 512-thread block per tile of kTile = 2048 records
+//   k_sort_block — one 1024-thread block per tile of kTile = 4096 records
 //       (built from the key batch itself): each thread sorts its 4 records in
-//       registers, then log2(512) merge passes inside LDS (each thread finds
+//       registers, then log2(1024) merge passes inside LDS (each thread finds
 //       its 4 outputs' merge-path split by binary search and merges them
-//       sequentially). 512 x 4 beat 256 x 8 (184 vs 223 us at 1M entries):
-//       the same LDS per block, twice the waves to hide each pass's latency.
+//       sequentially). At 1M entries 1024 x 4 (8 merge rounds) took 192 us,
+//       512 x 4 (9 rounds) 207 us and 256 x 8 223 us: a round costs one
+//       block's latency chain, so fewer, fatter rounds win.
 //   k_sort_merge — log2(tiles) rounds of pairwise run merges: each block
-//       owns 2048 outputs, finds its two splits with wave-wide 64-ary
+//       owns 4096 outputs, finds its two splits with wave-wide 64-ary
 //       merge-path searches in global memory (3-4 dependent rounds for runs
 //       of up to 2^20 records), stages the two input pieces in LDS and merges
 //       them as in the block sort; loads and stores are coalesced through LDS.
@@ -32,7 +33,7 @@
 namespace cb {
 namespace {
 
-constexpr uint32_t kST = 512;           // threads per block
+constexpr uint32_t kST = 1024;          // threads per block
 constexpr uint32_t kIPT = 4;            // records per thread
 constexpr uint32_t kTile = kST * kIPT;  // records per block
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;
@@ -74,10 +75,7 @@ __device__ __forceinline__ SortKey sentinel() {
 // and len | idx << 32, the record's third word), so that a thread walking
 // its own 8 consecutive records and its neighbours walking theirs hit
 // different banks (record i sits at word i + i/8 of each array).
-#ifndef CB_SORT_PADB
-#define CB_SORT_PADB 3
-#endif
-constexpr uint32_t kPadBits = CB_SORT_PADB;
+constexpr uint32_t kPadBits = 3;
 constexpr uint32_t kPadded = kTile + (kTile >> kPadBits);
 __device__ __forceinline__ uint32_t pad(uint32_t i) { return i + (i >> kPadBits); }
 

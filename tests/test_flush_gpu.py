@@ -181,11 +181,12 @@ def test_table_zone_only_for_created_tables(gpu):
 
 
 @pytest.mark.parametrize("n,shape", [(2, "random"), (2047, "random"), (2048, "descending"), (2049, "random"),
+                                     (4095, "random"), (4096, "descending"), (4097, "equal"), (8193, "random"),
                                      (6145, "equal"), (70_001, "long"), (300_001, "random"),
                                      (1 << 20, "descending")])
 def test_create_sort_sizes(gpu, n, shape):
     """The hand-written stable sort of unsorted flush batches (sort.hip: LDS
-    block sorts of 2048 records, then merge-path rounds) across tile and
+    block sorts of 4096 records, then merge-path rounds) across tile and
     round boundaries: random keys, reversed keys, all-equal keys (pure
     stability) and long keys sharing 16-byte prefixes; the file must equal
     the oracle's stable sort + format (src/sstable.rs:57-72)."""
