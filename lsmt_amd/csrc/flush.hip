@@ -377,8 +377,39 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
           c1 = nb + 1 - s1;
         }
       }
+      // ranges longer than a wave's store go to the block's list, which all
+      // kNT threads fill together (a wide gap in the keys is one line's
+      // range: spread over the block, not one wave)
+      __shared__ uint64_t big_s[2 * kNT], big_c[2 * kNT];
+      __shared__ uint32_t big_v[2 * kNT], nbig;
+      if (threadIdx.x == 0) nbig = 0;
+      __syncthreads();
+      auto defer = [&](uint64_t st, uint64_t& c, uint32_t v) {
+        if (c <= 64) return;
+        const uint32_t k = atomicAdd(&nbig, 1u);
+        big_s[k] = st;
+        big_c[k] = c;
+        big_v[k] = v;
+        c = 0;
+      };
+      defer(s0, c0, (uint32_t)p);
+      defer(s1, c1, (uint32_t)n);
       wave_fill(dir, s0, c0, (uint32_t)p);
       wave_fill(dir, s1, c1, (uint32_t)n);
+      __syncthreads();
+      for (uint32_t k = 0; k < nbig; ++k) {
+        uint32_t* d = dir + big_s[k];
+        const uint64_t c = big_c[k];
+        const uint32_t v = big_v[k];
+        uint64_t j = threadIdx.x;
+        for (; j + 3 * kNT < c; j += 4 * kNT) {
+          d[j] = v;
+          d[j + kNT] = v;
+          d[j + 2 * kNT] = v;
+          d[j + 3 * kNT] = v;
+        }
+        for (; j < c; j += kNT) d[j] = v;
+      }
     }
   }
   if (blockIdx.x == 0) zone_bound(order, kb, ko, 0, 0, r);

@@ -412,12 +412,11 @@ __device__ __forceinline__ int line_vs_query(const TableView& t, uint64_t l, con
 
 // The lines from b on that share the query's prefix, by a galloping search
 // with record compares (b: the prefix's lower bound, < nlines).
-__device__ __forceinline__ int64_t resolve_from(const TableView& t, const Query& q, uint64_t b, LineRec& hit) {
-  // line b's prefix and record in one round trip (the record is needed
-  // whenever the prefix matches, i.e. for every key that is present)
-  const uint64_t p0 = t.pfx[b];
-  LineRec r = t.rec[b];
-  if (p0 != q.w0) return -1;  // p0 > q.w0: b is the prefix's lower bound
+// Line b (the prefix's lower bound, its prefix equal to the query's) with
+// its record r already loaded: the record compare, then the lines after b
+// that share the prefix by a galloping search.
+__device__ __forceinline__ int64_t resolve_rec(const TableView& t, const Query& q, uint64_t b, LineRec r,
+                                               LineRec& hit) {
   int c = rec_cmp(t, r, q);
   if (c == 0) {
     hit = r;
@@ -455,6 +454,15 @@ __device__ __forceinline__ int64_t resolve_from(const TableView& t, const Query&
   return -1;
 }
 
+__device__ __forceinline__ int64_t resolve_from(const TableView& t, const Query& q, uint64_t b, LineRec& hit) {
+  // line b's prefix and record in one round trip (the record is needed
+  // whenever the prefix matches, i.e. for every key that is present)
+  const uint64_t p0 = t.pfx[b];
+  const LineRec r = t.rec[b];
+  if (p0 != q.w0) return -1;  // p0 > q.w0: b is the prefix's lower bound
+  return resolve_rec(t, q, b, r, hit);
+}
+
 // Level j's array (0: pfx).
 __device__ __forceinline__ const uint64_t* level_array(const TableView& t, uint32_t j) {
   return j ? t.fence + level_offset(t.nlines, j) : t.pfx;
@@ -467,6 +475,8 @@ __device__ __forceinline__ void level_down(const TableView& t, uint32_t j, uint6
   lo = i ? ((i - 1) << kFanBits) + 1 : 0;
   hi = (i << kFanBits) < cnt ? (i << kFanBits) : cnt;
 }
+
+constexpr uint32_t kWin = 8;  // buckets of up to this many lines: one round of prefix loads
 
 // Whether table t's directory applies: the shared prefix bits plus the
 // bucket bits fit the 64-bit prefix (dshift and dp0 set by the kernel).
@@ -521,7 +531,27 @@ __device__ __forceinline__ bool dir_start(const TableView& t, uint64_t x, uint32
 __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& q, LineRec& hit) {
   uint32_t j;
   uint64_t lo, hi, b;
-  if (dir_start(t, q.w0, j, lo, hi, b)) return b < t.nlines ? resolve_from(t, q, b, hit) : -1;
+  // outside the lines' shared prefix bits, or an empty bucket: absent
+  if (dir_start(t, q.w0, j, lo, hi, b)) return -1;
+  if (j == 0 && hi - lo <= kWin) {
+    // [lo, hi) is the key's whole bucket (or the whole table): its prefixes
+    // in one round of independent loads, with the record when it is one line
+    uint64_t v[kWin];
+#pragma unroll
+    for (uint32_t k = 0; k < kWin; ++k) v[k] = lo + k < hi ? t.pfx[lo + k] : ~0ull;
+    LineRec r1;
+    if (hi - lo == 1) r1 = t.rec[lo];
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kWin; ++k) c += (lo + k < hi && v[k] < q.w0) ? 1u : 0u;
+    // every line below the key: the next one is in a larger bucket
+    if (lo + c == hi) return -1;
+    uint64_t p0 = v[0];
+#pragma unroll
+    for (uint32_t k = 1; k < kWin; ++k) p0 = k == c ? v[k] : p0;
+    if (p0 != q.w0) return -1;
+    return resolve_rec(t, q, lo + c, hi - lo == 1 ? r1 : t.rec[lo + c], hit);
+  }
   for (;; --j) {
     const uint64_t i = lower_bound_u64(level_array(t, j), lo, hi, q.w0);
     if (!j) {

@@ -54,11 +54,12 @@ __device__ __forceinline__ void fence_put(uint64_t* fence, uint64_t nl, uint64_t
 // Radix directory of a well-formed table: below the prefix bits every line
 // shares (dshift = clz(pfx[0] ^ pfx[nlines-1])), the next dbits bits of a
 // prefix name its bucket; dir[B] = the first line whose bucket is >= B
-// (dir[2^dbits] = nlines). A lookup reads dir[B], dir[B+1] and starts the
-// fence descent at the lowest level where the bucket spans at most 16
-// entries: ~2^kDirLineBits lines per bucket, so random keys start at level 1
-// instead of the top. Tables of fewer than 256 lines have none.
-constexpr uint32_t kDirLineBits = 3;
+// (dir[2^dbits] = nlines). A lookup reads dir[B], dir[B+1]: a bucket of at
+// most 8 lines (~4 on average) is searched with one round of prefix loads
+// (and its record loaded with them when it holds one line); a larger one
+// starts the fence descent at the lowest level where it spans at most 16
+// entries. Tables of fewer than 16 lines have none.
+constexpr uint32_t kDirLineBits = 2;
 __host__ __device__ inline uint32_t dir_bits(uint64_t nl) {
   if (nl < (1ull << (kDirLineBits + 2)) || nl >= (1ull << 32)) return 0;
   const uint32_t b = 63u - (uint32_t)__builtin_clzll(nl) - kDirLineBits;
