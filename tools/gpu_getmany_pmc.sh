@@ -1,20 +1,19 @@
 #!/bin/bash
-# PMC passes on the read leg (one lane), for both get_many forms: where
-# k_get_many's time goes.
+# PMC passes on the read leg (one lane): where k_get_many's time goes.
 set -o pipefail
 mkdir -p gpurun_out/gm
 export TMPDIR=/tmp
 B="python3 bench.py --no-cpu --no-e2e --no-cold --no-flush --probe-streams 1 --steps 20 --warmup 2"
-for form in staged lane; do
+for form in cur; do
 i=0
 for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES" "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum" "TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TOTAL_CACHE_ACCESSES_sum" "SQ_INST_LEVEL_VMEM SQ_INST_CYCLES_VMEM_RD SQ_LEVEL_WAVES SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS"; do
   i=$((i+1))
-  CB_GET=$form timeout -s KILL 120 rocprofv3 --pmc $grp -d gpurun_out/gm/$form$i -o p$i --output-format csv -- $B > /dev/null 2> gpurun_out/gm/$form$i.err || { echo "pass $form $i failed"; tail -3 gpurun_out/gm/$form$i.err; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $grp -d gpurun_out/gm/$form$i -o p$i --output-format csv -- $B > /dev/null 2> gpurun_out/gm/$form$i.err || { echo "pass $form $i failed"; tail -3 gpurun_out/gm/$form$i.err; exit 1; }
 done
 done
 python3 - <<'PY'
 import csv, glob, collections
-for form in ("staged", "lane"):
+for form in ("cur",):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(f"gpurun_out/gm/{form}*/*counter_collection.csv"):
         per = collections.defaultdict(float)
@@ -23,7 +22,7 @@ for form in ("staged", "lane"):
             per[(r["Dispatch_Id"], k, r["Counter_Name"])] += float(r["Counter_Value"])
         for (d, k, c), v in per.items():
             agg[k][c].append(v)
-    for k in ("k_get_many_staged", "k_get_many"):
+    for k in ("k_get_many", "k_b64_decode", "k_set_probe"):
         if agg[k]:
             print(form, k, {c: round(sum(v) / len(v)) for c, v in sorted(agg[k].items())})
 PY
