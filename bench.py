@@ -60,7 +60,7 @@ def parse():
                    help="skip the cold-cache legs (profiles: keeps every k_set_probe launch warm, so "
                         "rocprofv3's average matches the bench line's warm kernel time)")
     p.add_argument("--flush-entries", type=int, default=1 << 20)
-    p.add_argument("--probe-streams", type=int, default=2, choices=[1, 2, 3],
+    p.add_argument("--probe-streams", type=int, default=3, choices=[1, 2, 3, 4],
                    help="pipeline lanes: consecutive steps alternate over this many streams (each with "
                         "its own hit buffers and, for N > 1, its own RCCL communicator)")
     p.add_argument("--force-dist", action="store_true",
