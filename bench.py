@@ -506,11 +506,16 @@ def main():
             hs = hits_l[0].cpu().numpy().view(np.uint64)[rows]
             hs = np.ascontiguousarray(hs[:, : sample // 64])
             t0 = time.perf_counter()
-            oracle.get_many(ot, hs, np.ascontiguousarray(look_np[:sample].reshape(-1)),
-                            np.arange(0, 16 * (sample + 1), 16, dtype=np.uint64))
+            ow, ovoff, ovals = oracle.get_many(ot, hs, np.ascontiguousarray(look_np[:sample].reshape(-1)),
+                                               np.arange(0, 16 * (sample + 1), 16, dtype=np.uint64))
             read["cpu_baseline"] = {"value": round(sample / (time.perf_counter() - t0), 1), "unit": "keys/s",
                                     "cores": 1, "kind": "port",
                                     "sample": f"oracle get_many over the first {sample} keys with the same gate bits"}
+            # the same sample checked: table index, value offsets and value bytes
+            gvo = voff_l[0][: sample + 1].cpu().numpy().astype(np.uint64)
+            read["oracle_sample_bit_exact"] = bool(
+                np.array_equal(which_l[0][:sample].cpu().numpy(), ow) and np.array_equal(gvo, ovoff) and
+                bytes(vals_l[0][: int(gvo[-1])].cpu().numpy()) == ovals)
             del ot
         del tables, dfiles
     if zone is not None:
@@ -546,6 +551,8 @@ def main():
                                "k_format", "k_line_count", "k_line_emit", "k_line_finish", "k_line_keys",
                                "k_build_part", "k_build_tile", "k_insert_direct"], step_flush, k_fl)
             out_bytes = made[-1][0].nbytes
+            if label == "unsorted" and rank == 0 and world == 1 and not args.no_cpu:
+                flush_file = made[-1][0].data()  # checked against the oracle below
             res[label] = {"entries_per_s": round(nf_e / (fel / k_fl), 1), "ms_per_flush": round(fel / k_fl * 1e3, 3),
                           "file_bytes": out_bytes, "file_GBps": round(out_bytes / (fel / k_fl) / 1e9, 2),
                           "kernels_us": {k: round(v["avg_us"], 2) for k, v in fprof.items()}}
@@ -562,6 +569,10 @@ def main():
             flush["cpu_baseline"] = {"value": round(sample / (time.perf_counter() - t0), 1), "unit": "entries/s",
                                      "cores": 1, "kind": "port",
                                      "sample": f"oracle sstable_create on {sample} unsorted entries (file only)"}
+            # the timed unsorted flush's whole file against the oracle's stable sort + format
+            ents = [(bytes(fk[i]), bytes(fv[i])) for i in range(nf_e)]
+            flush["oracle_file_bit_exact"] = bool(oracle.sstable_create(ents) == flush_file)
+            del ents, flush_file
 
     # ---- C2 build: 1M keys -> one fresh 16 MiB filter (zero-fill + batched insert)
     # (a step builds one fresh filter; consecutive steps go to the pipeline
