@@ -7,7 +7,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-# the trace pass runs the bench as configured (two pipeline lanes: launches
+# the trace pass runs the bench as configured (three pipeline lanes: launches
 # overlap, so per-dispatch durations are ~2x the per-step share; pmc_summary
 # reports the union of each kernel's busy intervals per launch beside them);
 # the PMC passes run one lane so every dispatch's counters are its own
