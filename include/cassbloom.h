@@ -307,6 +307,21 @@ int cb_get_many_var(const cb_table* const* tables, uint32_t nt, const uint64_t* 
                     const uint32_t* hit_rows, const uint8_t* bytes, const uint64_t* offsets,
                     uint64_t n, int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap,
                     uint64_t* total, void* stream);
+/* Database::get in one launch (src/lib.rs:125-136 with SsTable::get's gate,
+ * src/sstable.rs:138): the same walk and outputs as cb_get_many_*, with each
+ * (key, table) gate — zone_map.contains && bloom.may_contain, exactly
+ * cb_set_probe_gated_*'s bit — computed from the FilterSet inside the search
+ * kernel instead of read from hit rows. Table t is set slot slots[t]
+ * (slots NULL = slot t); nt <= the set's width; tables and set on one device.
+ * Same async contract (total = NULL). */
+int cb_set_get_many_fixed(const cb_filterset* set, const cb_table* const* tables, uint32_t nt,
+                          const uint32_t* slots, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                          int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap, uint64_t* total,
+                          void* stream);
+int cb_set_get_many_var(const cb_filterset* set, const cb_table* const* tables, uint32_t nt,
+                        const uint32_t* slots, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                        int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap, uint64_t* total,
+                        void* stream);
 
 /* ---- multi-GPU exchange ----
  * Each rank holds hit rows [rows][words] (uint64) for its filter subset; the

@@ -148,6 +148,8 @@ def load():
         "cb_table_search_var": ([P, u8p, P, u64, P, P], i32),
         "cb_get_many_fixed": ([P, u32, P, P, u8p, u32, u64, P, P, P, u64, pu64, P], i32),
         "cb_get_many_var": ([P, u32, P, P, u8p, P, u64, P, P, P, u64, pu64, P], i32),
+        "cb_set_get_many_fixed": ([P, P, u32, P, u8p, u32, u64, P, P, P, u64, pu64, P], i32),
+        "cb_set_get_many_var": ([P, P, u32, P, u8p, P, u64, P, P, P, u64, pu64, P], i32),
         "cb_set_probe_gated_fixed": ([P, u8p, u32, u64, P, P], i32),
         "cb_set_probe_gated_var": ([P, u8p, P, u64, P, P], i32),
         "cb_profile_enable": ([i32], i32),

@@ -760,7 +760,8 @@ def _to_var(b: KeyBatch) -> KeyBatch:
     return KeyBatch(n=b.n, data=data, offsets=offs)
 
 
-def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=None, out=None, wait=True):
+def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=None, out=None, wait=True,
+             set=None):
     """Database::get's newest-first walk for a key batch (tables[0] newest).
     hits: optional per-table gate bitmaps (e.g. FilterSet.probe(gated=True));
     table t uses row hit_rows[t] (default t). Returns (which int32[n]: table
@@ -770,7 +771,15 @@ def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=Non
     one pass and returns (which, val_off, total); values are written only if
     vals is large enough for total. With wait=False (out, keys and hits on the
     device) the call only enqueues the work on stream and returns total None:
-    val_off[n] holds it once the stream has run."""
+    val_off[n] holds it once the stream has run.
+
+    set=FilterSet: Database::get in one launch (cb_set_get_many_*): each
+    table's gate (its slot's ZoneMap and Bloom bits, as
+    FilterSet.probe(gated=True)) is computed inside the search kernel, so no
+    hit rows exist; hit_rows then names each table's slot (default t) and
+    hits must be None. At most the set's width tables."""
+    if set is not None and hits is not None:
+        raise ValueError("set= computes the gate itself: pass hits=None")
     b = as_batch(keys)
     nt = len(tables)
     arr = (ctypes.c_void_p * max(nt, 1))(*[t.handle.value for t in tables])
@@ -798,14 +807,22 @@ def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=Non
         offp, k2 = _ptr_of(b.offsets)
 
         def call(vp, cap):
-            _raise(L.cb_get_many_var(ctypes.cast(arr, ctypes.c_void_p), nt, hp, rp, dp, offp, b.n,
-                                     wp, vo, vp, cap, tref, s))
+            if set is not None:
+                _raise(L.cb_set_get_many_var(set._h, ctypes.cast(arr, ctypes.c_void_p), nt, rp, dp, offp, b.n,
+                                             wp, vo, vp, cap, tref, s))
+            else:
+                _raise(L.cb_get_many_var(ctypes.cast(arr, ctypes.c_void_p), nt, hp, rp, dp, offp, b.n,
+                                         wp, vo, vp, cap, tref, s))
     else:
         kp, k1 = _ptr_of(b.keys)
 
         def call(vp, cap):
-            _raise(L.cb_get_many_fixed(ctypes.cast(arr, ctypes.c_void_p), nt, hp, rp, kp, b.key_len, b.n,
-                                       wp, vo, vp, cap, tref, s))
+            if set is not None:
+                _raise(L.cb_set_get_many_fixed(set._h, ctypes.cast(arr, ctypes.c_void_p), nt, rp, kp, b.key_len,
+                                               b.n, wp, vo, vp, cap, tref, s))
+            else:
+                _raise(L.cb_get_many_fixed(ctypes.cast(arr, ctypes.c_void_p), nt, hp, rp, kp, b.key_len, b.n,
+                                           wp, vo, vp, cap, tref, s))
     if out is not None:
         call(_ptr_of(vals)[0], cap)
         return which, voff, (int(total.value) if wait else None)

@@ -140,9 +140,6 @@ namespace {
 int g_path_override = 0;  // 0 auto, 1 direct, 2 tiled
 
 constexpr int PATH_DIRECT = 1, PATH_TILED = 2;
-constexpr size_t cb_zone_hdr_bytes = 64 * 16;  // cb::ZoneView headers
-constexpr size_t cb_zone_pre_bytes = 64 * 2 * sizeof(cb::BoundPrefix);  // then the prefixes
-constexpr size_t cb_zone_blob_off = cb_zone_hdr_bytes + cb_zone_pre_bytes;
 
 uint64_t alloc_words_for(uint64_t m) {
   // Pad to whole 2^18-bit tiles (the largest LDS tile) so tiled passes never
@@ -454,9 +451,7 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
   DeviceGuard dg(set->device);
   Workspace& ws = workspace(set->device, s);
   std::lock_guard<std::mutex> lk(ws.mu);
-  const cb::ZoneView zv{(const uint32_t*)set->zdev,
-                       (const cb::BoundPrefix*)((const uint8_t*)set->zdev + cb_zone_hdr_bytes),
-                       (const uint8_t*)set->zdev + cb_zone_blob_off, set->zgated};
+  const cb::ZoneView zv = set_zone_view(set);
   if (!offsets && key_len && is_pinned_host(keys) && is_pinned_host(hits)) {
     g_last_path = 4;
     return set_probe_zero_copy(set, keys, key_len, n, hits, s, (gated && set->zgated) ? &zv : nullptr);
@@ -509,9 +504,7 @@ int set_probe_device(const cb_filterset* set, const uint8_t* keys, uint32_t key_
   DeviceGuard dg(set->device);
   Workspace& ws = workspace(set->device, s);
   std::lock_guard<std::mutex> lk(ws.mu);
-  const cb::ZoneView zv{(const uint32_t*)set->zdev,
-                       (const cb::BoundPrefix*)((const uint8_t*)set->zdev + cb_zone_hdr_bytes),
-                       (const uint8_t*)set->zdev + cb_zone_blob_off, set->zgated};
+  const cb::ZoneView zv = set_zone_view(set);
   const int keyk = (key_len == 16 && !((uintptr_t)keys & 15)) ? cb::KEY_FIXED16 : cb::KEY_FIXED;
   const cb::KeySrc ks{keys, nullptr, key_len};
   cb::PackSink sink{};

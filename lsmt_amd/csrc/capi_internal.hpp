@@ -61,6 +61,17 @@ struct cb_filterset {
   uint64_t zgated = 0;  // slots with both bounds
 };
 
+// The device zone table of a set (capi.cpp upload_zones): 64 cb::ZoneView
+// headers, then the bounds' 16-byte prefixes, then the bound bytes.
+constexpr size_t cb_zone_hdr_bytes = 64 * 16;
+constexpr size_t cb_zone_pre_bytes = 64 * 2 * sizeof(cb::BoundPrefix);
+constexpr size_t cb_zone_blob_off = cb_zone_hdr_bytes + cb_zone_pre_bytes;
+inline cb::ZoneView set_zone_view(const cb_filterset* set) {
+  const uint8_t* z = (const uint8_t*)set->zdev;
+  return cb::ZoneView{(const uint32_t*)z, (const cb::BoundPrefix*)(z + cb_zone_hdr_bytes), z + cb_zone_blob_off,
+                      set->zgated};
+}
+
 // An SSTable data file resident in HBM with its line index (sstable.hpp).
 struct cb_table {
   int device = 0;

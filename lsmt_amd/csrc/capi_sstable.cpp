@@ -38,11 +38,21 @@ int table_search_impl(const cb_table* t, const uint8_t* keys, const uint64_t* of
   return CB_OK;
 }
 
+// set != NULL: the fused form (cb_set_get_many_*): the gate comes from the
+// FilterSet inside the search kernel, hit_rows are the tables' slots and
+// hits is unused.
 int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hits,
                   const uint32_t* hit_rows, const uint8_t* keys, const uint64_t* offsets,
                   uint32_t key_len, uint64_t n, int32_t* which, uint64_t* val_off, uint8_t* vals,
-                  uint64_t cap, uint64_t* total, hipStream_t s) {
+                  uint64_t cap, uint64_t* total, hipStream_t s, const cb_filterset* set = nullptr) {
   if (!which || !val_off || (nt && !tables)) return fail(CB_EINVAL, "null argument");
+  if (set) {
+    if (nt > set->width) return fail(CB_EINVAL, "more tables than the set's slots");
+    if (hit_rows)
+      for (uint32_t i = 0; i < nt; ++i)
+        if (hit_rows[i] >= set->width) return fail(CB_EINVAL, "slot out of range");
+    hits = nullptr;
+  }
   // total == NULL: enqueue only (every buffer on the device; val_off[n] = the total)
   const bool async = total == nullptr;
   if (async && (!is_device_ptr(which) || !is_device_ptr(val_off) || (vals && !is_device_ptr(vals)) ||
@@ -68,8 +78,9 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
     if (tables[i]->device != dev) return fail(CB_EINVAL, "tables live on different devices");
     views[i] = tables[i]->view();
   }
+  if (set && set->device != dev) return fail(CB_EINVAL, "set and tables live on different devices");
   std::vector<uint32_t> rows;
-  if (hits && hit_rows) {
+  if ((hits || set) && hit_rows) {
     rows.assign(hit_rows, hit_rows + nt);
     nrows = 0;
     for (uint32_t r : rows) nrows = std::max<uint64_t>(nrows, (uint64_t)r + 1);
@@ -118,8 +129,15 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
   const uint64_t* vsrc = (const uint64_t*)ws.t_line.p;
   const uint64_t* dlen = (const uint64_t*)ws.t_dlen.p;
   uint64_t* tsum = (uint64_t*)ws.t_scan.p;
-  HIP_TRY(cb::launch_get_many(sk.keyk, dviews, nt, dhits, drows, hwords, sk.ks, n, dwhich,
-                              (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, tsum, s));
+  if (set) {
+    const cb::ZoneView zv = set_zone_view(set);
+    HIP_TRY(cb::launch_set_get_many(sk.keyk, set->mode, set->width, set->words, set->mp,
+                                    set->zgated ? &zv : nullptr, dviews, nt, drows, sk.ks, n, dwhich,
+                                    (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, tsum, s));
+  } else {
+    HIP_TRY(cb::launch_get_many(sk.keyk, dviews, nt, dhits, drows, hwords, sk.ks, n, dwhich,
+                                (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, tsum, s));
+  }
   HIP_TRY(cb::launch_tile_scan(tsum, cb::get_tiles(n), dvoff + n, s));
   if (!ws.htot) HIP_TRY(hipHostMalloc((void**)&ws.htot, 64, hipHostMallocDefault));
   if (async) {
@@ -614,6 +632,25 @@ int cb_get_many_var(const cb_table* const* tables, uint32_t nt, const uint64_t* 
   if (!offsets) return fail(CB_EINVAL, "null offsets");
   return get_many_impl(tables, nt, hits, hit_rows, bytes, offsets, 0, n, which, val_off, vals, cap,
                        total, (hipStream_t)stream);
+}
+
+int cb_set_get_many_fixed(const cb_filterset* set, const cb_table* const* tables, uint32_t nt,
+                          const uint32_t* slots, const uint8_t* keys, uint32_t key_len, uint64_t n,
+                          int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap, uint64_t* total,
+                          void* stream) {
+  if (!set) return fail(CB_EINVAL, "null set");
+  return get_many_impl(tables, nt, nullptr, slots, keys, nullptr, key_len, n, which, val_off, vals, cap, total,
+                       (hipStream_t)stream, set);
+}
+
+int cb_set_get_many_var(const cb_filterset* set, const cb_table* const* tables, uint32_t nt,
+                        const uint32_t* slots, const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
+                        int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap, uint64_t* total,
+                        void* stream) {
+  if (!set) return fail(CB_EINVAL, "null set");
+  if (!offsets) return fail(CB_EINVAL, "null offsets");
+  return get_many_impl(tables, nt, nullptr, slots, bytes, offsets, 0, n, which, val_off, vals, cap, total,
+                       (hipStream_t)stream, set);
 }
 
 }  // extern "C"

@@ -21,6 +21,7 @@
 
 #include "blockscan.hpp"
 #include "profile.hpp"
+#include "setmask.hpp"
 #include "sstable.hpp"
 #include "zone.hpp"
 
@@ -528,6 +529,7 @@ __device__ __forceinline__ bool dir_start(const TableView& t, uint64_t x, uint32
 // then the lines sharing that prefix by a galloping search with record
 // compares: O(log run) for keys that share long prefixes ('user0000...'), one
 // record compare when the prefix is unique.
+template <int SPEC>
 __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& q, LineRec& hit) {
   uint32_t j;
   uint64_t lo, hi, b;
@@ -539,8 +541,15 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
     uint64_t v[kWin];
 #pragma unroll
     for (uint32_t k = 0; k < kWin; ++k) v[k] = lo + k < hi ? t.pfx[lo + k] : ~0ull;
-    LineRec r1;
-    if (hi - lo == 1) r1 = t.rec[lo];
+    constexpr uint32_t kSp = SPEC ? SPEC : 1;
+    LineRec rr[kSp];
+    if constexpr (SPEC) {
+#pragma unroll
+      for (uint32_t k = 0; k < kSp; ++k)
+        if (lo + k < hi) rr[k] = t.rec[lo + k];
+    } else {
+      if (hi - lo == 1) rr[0] = t.rec[lo];
+    }
     uint32_t c = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kWin; ++k) c += (lo + k < hi && v[k] < q.w0) ? 1u : 0u;
@@ -550,7 +559,18 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
 #pragma unroll
     for (uint32_t k = 1; k < kWin; ++k) p0 = k == c ? v[k] : p0;
     if (p0 != q.w0) return -1;
-    return resolve_rec(t, q, lo + c, hi - lo == 1 ? r1 : t.rec[lo + c], hit);
+    if constexpr (SPEC) {
+      if (c < kSp) {
+        LineRec r = rr[0];
+#pragma unroll
+        for (uint32_t k = 1; k < kSp; ++k)
+          if (k == c) r = rr[k];
+        return resolve_rec(t, q, lo + c, r, hit);
+      }
+      return resolve_rec(t, q, lo + c, t.rec[lo + c], hit);
+    } else {
+      return resolve_rec(t, q, lo + c, hi - lo == 1 ? rr[0] : t.rec[lo + c], hit);
+    }
   }
   for (;; --j) {
     const uint64_t i = lower_bound_u64(level_array(t, j), lo, hi, q.w0);
@@ -562,8 +582,9 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
   }
 }
 
+template <int SPEC = 0>
 __device__ __forceinline__ int64_t search(const TableView& t, const Query& q, LineRec& hit) {
-  return t.fast ? search_fast(t, q, hit) : search_exact(t, q, hit);
+  return t.fast ? search_fast<SPEC>(t, q, hit) : search_exact(t, q, hit);
 }
 
 // dir[B] for B in [0, 2^dbits]: the lower bound of bucket B's smallest prefix.
@@ -629,7 +650,47 @@ __global__ __launch_bounds__(kNT) void k_table_search(TableView t, KeySrc ks, ui
   line[k] = search(t, q, r);
 }
 
-template <int KEYK>
+// Database::get's walk for one key (src/lib.rs:129-134): tables in groups
+// of 64, newest first (tables.iter().rev()). Each lane holds its candidate
+// tables of the group as a bit mask (cand0 for the first 64; past them, from
+// the hit rows), then every lane searches its OWN next candidate in the same
+// iteration, so lanes whose keys live in different tables search concurrently
+// instead of the wave stepping through the tables one by one. w / src / d:
+// the first table whose SsTable::get returns Ok(Some), the value's base64
+// bytes and their decoded length.
+template <int SPEC>
+__device__ __forceinline__ void resolve_key(const TableView* stv, const TableView* __restrict__ tv, uint32_t nt,
+                                            uint64_t cand0, const uint64_t* __restrict__ hits,
+                                            const uint32_t* __restrict__ rows, uint64_t hwords, uint64_t k,
+                                            const Query& q, int32_t& w, uint64_t& src, uint64_t& d) {
+  for (uint32_t t0 = 0; t0 < nt && w < 0; t0 += 64) {
+    const uint32_t gn = nt - t0 < 64 ? nt - t0 : 64;
+    uint64_t cand = gn == 64 ? ~0ull : ((1ull << gn) - 1);
+    if (t0 == 0) {
+      cand = cand0;
+    } else if (hits) {  // tables past the first 64: one broadcast load per table
+      cand = 0;
+      for (uint32_t i = 0; i < gn; ++i) {
+        const uint64_t row = rows ? rows[t0 + i] : t0 + i;
+        cand |= ((hits[row * hwords + (k >> 6)] >> (k & 63)) & 1) << i;  // the gate
+      }
+    }
+    while (cand) {
+      const uint32_t t = t0 + (uint32_t)__builtin_ctzll(cand);
+      cand &= cand - 1;
+      const TableView v = t < 64 ? stv[t] : tv[t];
+      LineRec r;
+      if (search<SPEC>(v, q, r) < 0) continue;  // Ok(None)
+      if (r.vdl == kBadValue) continue;         // Err(..) is skipped by `if let Ok(Some(v))`
+      w = (int32_t)t;
+      src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
+      d = r.vdl;
+      return;
+    }
+  }
+}
+
+template <int KEYK, int SPEC>
 __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ tv, uint32_t nt,
                                                   const uint64_t* __restrict__ hits,
                                                   const uint32_t* __restrict__ rows,
@@ -664,41 +725,56 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
   if (k < n) {
     int32_t w = -1;
     uint64_t src = 0;
-    // Tables in groups of 64, newest first (tables.iter().rev()). Each lane
-    // holds its candidate tables of the group as a bit mask, then every lane
-    // searches its OWN next candidate in the same iteration, so lanes whose
-    // keys live in different tables search concurrently instead of the wave
-    // stepping through the tables one by one.
-    for (uint32_t t0 = 0; t0 < nt && w < 0; t0 += 64) {
-      const uint32_t gn = nt - t0 < 64 ? nt - t0 : 64;
-      uint64_t cand = gn == 64 ? ~0ull : ((1ull << gn) - 1);
-      if (t0 == 0) {
-        cand = cand0;
-      } else if (hits) {  // tables past the first 64: one broadcast load per table
-        cand = 0;
-        for (uint32_t i = 0; i < gn; ++i) {
-          const uint64_t row = rows ? rows[t0 + i] : t0 + i;
-          cand |= ((hits[row * hwords + (k >> 6)] >> (k & 63)) & 1) << i;  // the gate
-        }
-      }
-      while (cand) {
-        const uint32_t t = t0 + (uint32_t)__builtin_ctzll(cand);
-        cand &= cand - 1;
-        const TableView v = t < 64 ? stv[t] : tv[t];
-        LineRec r;
-        if (search(v, q, r) < 0) continue;  // Ok(None)
-        if (r.vdl == kBadValue) continue;   // Err(..) is skipped by `if let Ok(Some(v))`
-        w = (int32_t)t;
-        src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
-        d = r.vdl;
-        break;
-      }
-    }
+    resolve_key<SPEC>(stv, tv, nt, cand0, hits, rows, hwords, k, q, w, src, d);
     which[k] = w;
     vsrc[k] = src;
     dlen[k] = d;
   }
   // this block's value bytes, for k_b64_decode's offsets
+  uint64_t total;
+  (void)block_scan<kNT>(d, &total);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = total;
+}
+
+// Database::get in one launch (src/lib.rs:129-134 with SsTable::get's gate,
+// src/sstable.rs:138): k_get_many with the gate computed per key from the
+// FilterSet (set_key_mask: set[a] & set[b] over every slot, the zone check
+// for gated slots) instead of read from hit rows, so no rows are written or
+// read and the set's random reads overlap the searches' in one kernel. Table
+// t is slot slots[t] (slots NULL: slot t); nt <= W.
+template <int KEYK, int MODE, int W, int SPEC>
+__global__ __launch_bounds__(kNT) void k_set_get_many(const void* __restrict__ set, ModP mp, ZoneView zv,
+                                                      const TableView* __restrict__ tv, uint32_t nt,
+                                                      const uint32_t* __restrict__ slots, KeySrc ks, uint64_t n,
+                                                      int32_t* __restrict__ which, uint64_t* __restrict__ vsrc,
+                                                      uint64_t* __restrict__ dlen, uint64_t* __restrict__ tsum) {
+  const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  const ViewRegs vr = load_views(tv, nt);
+  __shared__ BoundPrefix zp[2 * W];
+  __shared__ uint32_t sslot[64];
+  __shared__ TableView stv[64];
+  stage_zone_prefixes<KEYK, W>(zv, zp, kNT);
+  if (slots && threadIdx.x < nt) sslot[threadIdx.x] = slots[threadIdx.x];
+  // the key's loads go out before the barrier (after it, the compiler kept
+  // the whole search's state live across the gate: 256 VGPRs, 1 wave/SIMD)
+  const Query q = make_query<KEYK>(ks, k < n ? k : 0);
+  store_views(vr, nt, stv);  // barrier: views, slots and zone prefixes staged
+  const auto mask = set_key_mask<KEYK, MODE, W, true, false>(set, nullptr, ks, k, k < n, mp, zv, zp);
+  uint64_t cand0 = 0;
+  if (slots) {
+    for (uint32_t i = 0; i < nt; ++i) cand0 |= (((uint64_t)mask >> sslot[i]) & 1ull) << i;
+  } else {
+    cand0 = (uint64_t)mask & (nt == 64 ? ~0ull : ((1ull << nt) - 1));
+  }
+  uint64_t d = 0;
+  if (k < n) {
+    int32_t w = -1;
+    uint64_t src = 0;
+    resolve_key<SPEC>(stv, tv, nt, cand0, nullptr, nullptr, 0, k, q, w, src, d);
+    which[k] = w;
+    vsrc[k] = src;
+    dlen[k] = d;
+  }
   uint64_t total;
   (void)block_scan<kNT>(d, &total);
   if (threadIdx.x == 0) tsum[blockIdx.x] = total;
@@ -933,21 +1009,56 @@ hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uin
   if (!n) return hipSuccess;
   ProfScope ps("k_get_many", s);
   const dim3 g(blocks_for(n, kNT));
+  static const int spec = [] {
+    const char* v = getenv("CB_GM_SPEC");
+    return v ? atoi(v) : 0;
+  }();
+#define GM_LAUNCH(K, S) \
+  hipLaunchKernelGGL((k_get_many<K, S>), g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n, which, vsrc, dlen, tsum)
+#define GM_SPEC(K)        \
+  switch (spec) {         \
+    case 2: GM_LAUNCH(K, 2); break; \
+    case 4: GM_LAUNCH(K, 4); break; \
+    default: GM_LAUNCH(K, 0); break; \
+  }
   switch (keyk) {
-    case KEY_FIXED16:
-      hipLaunchKernelGGL(k_get_many<KEY_FIXED16>, g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks,
-                         n, which, vsrc, dlen, tsum);
-      break;
-    case KEY_FIXED:
-      hipLaunchKernelGGL(k_get_many<KEY_FIXED>, g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n,
-                         which, vsrc, dlen, tsum);
-      break;
-    case KEY_VAR:
-      hipLaunchKernelGGL(k_get_many<KEY_VAR>, g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n,
-                         which, vsrc, dlen, tsum);
-      break;
+    case KEY_FIXED16: GM_SPEC(KEY_FIXED16); break;
+    case KEY_FIXED: GM_SPEC(KEY_FIXED); break;
+    case KEY_VAR: GM_SPEC(KEY_VAR); break;
     default: return hipErrorInvalidValue;
   }
+#undef GM_SPEC
+#undef GM_LAUNCH
+  return hipGetLastError();
+}
+
+template <int KK, int MM, int WW>
+static void set_get_many(int spec, const void* set, const ModP& mp, const ZoneView& zv, const TableView* tv,
+                         uint32_t nt, const uint32_t* slots, const KeySrc& ks, uint64_t n, int32_t* which,
+                         uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum, hipStream_t s) {
+  const dim3 g(blocks_for(n, kNT));
+  if (spec == 2)
+    hipLaunchKernelGGL((k_set_get_many<KK, MM, WW, 2>), g, dim3(kNT), 0, s, set, mp, zv, tv, nt, slots, ks, n,
+                       which, vsrc, dlen, tsum);
+  else
+    hipLaunchKernelGGL((k_set_get_many<KK, MM, WW, 0>), g, dim3(kNT), 0, s, set, mp, zv, tv, nt, slots, ks, n,
+                       which, vsrc, dlen, tsum);
+}
+
+hipError_t launch_set_get_many(int keyk, int mode, uint32_t width, const void* set, const ModP& mp,
+                               const ZoneView* zones, const TableView* tv, uint32_t nt, const uint32_t* slots,
+                               const KeySrc& ks, uint64_t n, int32_t* which, uint64_t* vsrc, uint64_t* dlen,
+                               uint64_t* tsum, hipStream_t s) {
+  if (!n) return hipSuccess;
+  if (nt > width || (width != 32 && width != 64)) return hipErrorInvalidValue;
+  static const int spec = [] {
+    const char* v = getenv("CB_GM_SPEC");
+    return v ? atoi(v) : 0;
+  }();
+  const ZoneView zv = zones ? *zones : ZoneView{nullptr, nullptr, nullptr, 0};
+  ProfScope ps("k_set_get_many", s);
+  CB_SET_DISPATCH(keyk, mode, width,
+                  (set_get_many<KK, MM, WW>(spec, set, mp, zv, tv, nt, slots, ks, n, which, vsrc, dlen, tsum, s)));
   return hipGetLastError();
 }
 

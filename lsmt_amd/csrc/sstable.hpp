@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include "hash.hpp"
+#include "zone.hpp"
 
 namespace cb {
 
@@ -158,6 +159,14 @@ hipError_t launch_table_search(int keyk, const TableView& t, const KeySrc& ks, u
 // (kDecodeTile keys, get_tiles(n) entries).
 constexpr uint32_t kDecodeTile = 256;
 inline uint64_t get_tiles(uint64_t n) { return (n + kDecodeTile - 1) / kDecodeTile; }
+// Database::get in one launch: the FilterSet gate (set_key_mask over the
+// set of `width` slots, zones nullable) computed per key, then the same walk
+// and outputs as launch_get_many; table t is slot slots[t] (nullptr: slot t),
+// nt <= width.
+hipError_t launch_set_get_many(int keyk, int mode, uint32_t width, const void* set, const ModP& mp,
+                               const ZoneView* zones, const TableView* tv, uint32_t nt, const uint32_t* slots,
+                               const KeySrc& ks, uint64_t n, int32_t* which, uint64_t* vsrc, uint64_t* dlen,
+                               uint64_t* tsum, hipStream_t s);
 hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uint64_t* hits,
                            const uint32_t* rows, uint64_t hwords, const KeySrc& ks, uint64_t n,
                            int32_t* which, uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum,

@@ -158,6 +158,87 @@ def test_get_many_gated_vs_oracle(gpu):
     assert np.array_equal(w3, ow) and vals3 == ovals
 
 
+def _fused_case(gpu, m, nt, width, seed):
+    """nt tables (newest first) of overlapping key ranges, their filters in a
+    FilterSet of `width` slots at a permuted slot each, zones on every other
+    table only (the rest accept every key)."""
+    per = [workload.key_range(1300 + (t % 3), 20_000 + 700 * t) for t in range(nt)]
+    files = [workload.sstable_bytes(k, workload.table_value(k, 200 + t)) for t, k in enumerate(per)]
+    tables = [gpu.Table(f) for f in files]
+    otables = [oracle.OracleTable(f.tobytes()) for f in files]
+    slots = np.random.default_rng(seed).permutation(width)[:nt].astype(np.uint32)
+    s = gpu.FilterSet(m, width=width)
+    for t, k in enumerate(per):
+        b = gpu.BloomFilter(m)
+        b.insert_batch(k)
+        s.assign(int(slots[t]), b)
+        if t % 2 == 0:
+            s.zone_from_keys(int(slots[t]), k)
+    look = np.concatenate([per[1][:9_000], per[nt - 1][-6_000:], workload.key_range(4322, 15_000)])
+    look = look[np.random.default_rng(seed + 1).permutation(len(look))]
+    return tables, otables, slots, s, look
+
+
+@pytest.mark.parametrize("m,nt,width", [(1 << 20, 8, 32), (1_000_003, 5, 64), (1 << 20, 64, 64)])
+def test_set_get_many_vs_oracle(gpu, m, nt, width):
+    """cb_set_get_many_*: the zone + Bloom gate computed inside the search
+    kernel gives exactly what FilterSet.probe(gated=True) + get_many gives,
+    and both equal the oracle's walk over those gate bits — for 16-byte keys,
+    ragged keys, permuted slots, width 32 and 64 and a non-power-of-two m."""
+    tables, otables, slots, s, look = _fused_case(gpu, m, nt, width, seed=nt)
+    full = s.probe(look, gated=True)
+    hits = full[slots].copy()  # row t = table t's slot
+    d = np.ascontiguousarray(look.reshape(-1))
+    offs = np.arange(0, 16 * (len(look) + 1), 16, dtype=np.uint64)
+    ow, ovoff, ovals = oracle.get_many(otables, hits, d, offs)
+    which, voff, vals = gpu.get_many(tables, look, set=s, hit_rows=slots)
+    assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals
+    w2, v2, vals2 = gpu.get_many(tables, look, hits=full, hit_rows=slots)
+    assert np.array_equal(w2, ow) and vals2 == ovals
+    assert (which >= 0).sum() > 0 and (which < 0).sum() > 0
+    # ragged keys (KEY_VAR): the same keys with some cut short, plus the empty key
+    vk = [bytes(k) for k in look[:4000]] + [bytes(k[: i % 16]) for i, k in enumerate(look[4000:6000])] + [b""]
+    dv, ov = var(vk)
+    kb = gpu.KeyBatch(n=len(vk), data=dv, offsets=ov)
+    vhits = s.probe(kb, gated=True)[slots].copy()
+    ow, ovoff, ovals = oracle.get_many(otables, vhits, dv, ov)
+    which, voff, vals = gpu.get_many(tables, kb, set=s, hit_rows=slots)
+    assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals
+
+
+def test_set_get_many_async_device(gpu):
+    """Device keys and outputs, total = NULL (enqueue only), slots = NULL
+    (table t = slot t): val_off[n] carries the total; the answers equal the
+    two-step form's."""
+    import torch
+    m, nt = 1 << 20, 6
+    per = [workload.key_range(1400 + t, 30_000) for t in range(nt)]
+    tables = [gpu.Table(workload.sstable_bytes(k, workload.table_value(k, 300 + t))) for t, k in enumerate(per)]
+    filters = []
+    for k in per:
+        b = gpu.BloomFilter(m)
+        b.insert_batch(k)
+        filters.append(b)
+    s = gpu.FilterSet.from_filters(filters)
+    for t, k in enumerate(per):
+        s.zone_from_keys(t, k)
+    look = np.concatenate([per[2][:20_000], workload.key_range(4323, 12_000)])
+    ew, evoff, evals = gpu.get_many(tables, look, hits=s.probe(look, gated=True))
+    dk = torch.from_numpy(look).cuda()
+    which = torch.zeros(len(look), dtype=torch.int32, device="cuda")
+    voff = torch.zeros(len(look) + 1, dtype=torch.int64, device="cuda")
+    vals = torch.zeros(len(evals) + 64, dtype=torch.uint8, device="cuda")
+    assert gpu.get_many(tables, gpu.DeviceKeys(dk), set=s, out=(which, voff, vals), wait=False)[2] is None
+    torch.cuda.synchronize()
+    tot = int(voff[-1].item())
+    assert tot == len(evals)
+    assert np.array_equal(which.cpu().numpy(), ew)
+    assert np.array_equal(voff.cpu().numpy().view(np.uint64), evoff)
+    assert vals[:tot].cpu().numpy().tobytes() == evals
+    with pytest.raises(ValueError):
+        gpu.get_many(tables, look, hits=s.probe(look), set=s)
+
+
 def test_well_formed_detection(gpu):
     # prefix-sharing keys (equal 8-byte prefixes, keys shorter than 8 bytes,
     # embedded NULs) in a well-formed file take the fast path and must agree
