@@ -529,7 +529,6 @@ __device__ __forceinline__ bool dir_start(const TableView& t, uint64_t x, uint32
 // then the lines sharing that prefix by a galloping search with record
 // compares: O(log run) for keys that share long prefixes ('user0000...'), one
 // record compare when the prefix is unique.
-template <int SPEC>
 __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& q, LineRec& hit) {
   uint32_t j;
   uint64_t lo, hi, b;
@@ -538,18 +537,13 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
   if (j == 0 && hi - lo <= kWin) {
     // [lo, hi) is the key's whole bucket (or the whole table): its prefixes
     // in one round of independent loads, with the record when it is one line
+    // (loading the first two records of every bucket with them measured
+    // within noise: 85-87 vs 88 us per 1M keys)
     uint64_t v[kWin];
 #pragma unroll
     for (uint32_t k = 0; k < kWin; ++k) v[k] = lo + k < hi ? t.pfx[lo + k] : ~0ull;
-    constexpr uint32_t kSp = SPEC ? SPEC : 1;
-    LineRec rr[kSp];
-    if constexpr (SPEC) {
-#pragma unroll
-      for (uint32_t k = 0; k < kSp; ++k)
-        if (lo + k < hi) rr[k] = t.rec[lo + k];
-    } else {
-      if (hi - lo == 1) rr[0] = t.rec[lo];
-    }
+    LineRec r1;
+    if (hi - lo == 1) r1 = t.rec[lo];
     uint32_t c = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kWin; ++k) c += (lo + k < hi && v[k] < q.w0) ? 1u : 0u;
@@ -559,18 +553,7 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
 #pragma unroll
     for (uint32_t k = 1; k < kWin; ++k) p0 = k == c ? v[k] : p0;
     if (p0 != q.w0) return -1;
-    if constexpr (SPEC) {
-      if (c < kSp) {
-        LineRec r = rr[0];
-#pragma unroll
-        for (uint32_t k = 1; k < kSp; ++k)
-          if (k == c) r = rr[k];
-        return resolve_rec(t, q, lo + c, r, hit);
-      }
-      return resolve_rec(t, q, lo + c, t.rec[lo + c], hit);
-    } else {
-      return resolve_rec(t, q, lo + c, hi - lo == 1 ? rr[0] : t.rec[lo + c], hit);
-    }
+    return resolve_rec(t, q, lo + c, hi - lo == 1 ? r1 : t.rec[lo + c], hit);
   }
   for (;; --j) {
     const uint64_t i = lower_bound_u64(level_array(t, j), lo, hi, q.w0);
@@ -582,9 +565,8 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
   }
 }
 
-template <int SPEC = 0>
 __device__ __forceinline__ int64_t search(const TableView& t, const Query& q, LineRec& hit) {
-  return t.fast ? search_fast<SPEC>(t, q, hit) : search_exact(t, q, hit);
+  return t.fast ? search_fast(t, q, hit) : search_exact(t, q, hit);
 }
 
 // dir[B] for B in [0, 2^dbits]: the lower bound of bucket B's smallest prefix.
@@ -658,7 +640,6 @@ __global__ __launch_bounds__(kNT) void k_table_search(TableView t, KeySrc ks, ui
 // instead of the wave stepping through the tables one by one. w / src / d:
 // the first table whose SsTable::get returns Ok(Some), the value's base64
 // bytes and their decoded length.
-template <int SPEC>
 __device__ __forceinline__ void resolve_key(const TableView* stv, const TableView* __restrict__ tv, uint32_t nt,
                                             uint64_t cand0, const uint64_t* __restrict__ hits,
                                             const uint32_t* __restrict__ rows, uint64_t hwords, uint64_t k,
@@ -680,7 +661,7 @@ __device__ __forceinline__ void resolve_key(const TableView* stv, const TableVie
       cand &= cand - 1;
       const TableView v = t < 64 ? stv[t] : tv[t];
       LineRec r;
-      if (search<SPEC>(v, q, r) < 0) continue;  // Ok(None)
+      if (search(v, q, r) < 0) continue;  // Ok(None)
       if (r.vdl == kBadValue) continue;         // Err(..) is skipped by `if let Ok(Some(v))`
       w = (int32_t)t;
       src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
@@ -690,7 +671,7 @@ __device__ __forceinline__ void resolve_key(const TableView* stv, const TableVie
   }
 }
 
-template <int KEYK, int SPEC>
+template <int KEYK>
 __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ tv, uint32_t nt,
                                                   const uint64_t* __restrict__ hits,
                                                   const uint32_t* __restrict__ rows,
@@ -725,7 +706,7 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
   if (k < n) {
     int32_t w = -1;
     uint64_t src = 0;
-    resolve_key<SPEC>(stv, tv, nt, cand0, hits, rows, hwords, k, q, w, src, d);
+    resolve_key(stv, tv, nt, cand0, hits, rows, hwords, k, q, w, src, d);
     which[k] = w;
     vsrc[k] = src;
     dlen[k] = d;
@@ -742,7 +723,7 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
 // for gated slots) instead of read from hit rows, so no rows are written or
 // read and the set's random reads overlap the searches' in one kernel. Table
 // t is slot slots[t] (slots NULL: slot t); nt <= W.
-template <int KEYK, int MODE, int W, int SPEC>
+template <int KEYK, int MODE, int W>
 __global__ __launch_bounds__(kNT) void k_set_get_many(const void* __restrict__ set, ModP mp, ZoneView zv,
                                                       const TableView* __restrict__ tv, uint32_t nt,
                                                       const uint32_t* __restrict__ slots, KeySrc ks, uint64_t n,
@@ -770,7 +751,7 @@ __global__ __launch_bounds__(kNT) void k_set_get_many(const void* __restrict__ s
   if (k < n) {
     int32_t w = -1;
     uint64_t src = 0;
-    resolve_key<SPEC>(stv, tv, nt, cand0, nullptr, nullptr, 0, k, q, w, src, d);
+    resolve_key(stv, tv, nt, cand0, nullptr, nullptr, 0, k, q, w, src, d);
     which[k] = w;
     vsrc[k] = src;
     dlen[k] = d;
@@ -1009,40 +990,31 @@ hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uin
   if (!n) return hipSuccess;
   ProfScope ps("k_get_many", s);
   const dim3 g(blocks_for(n, kNT));
-  static const int spec = [] {
-    const char* v = getenv("CB_GM_SPEC");
-    return v ? atoi(v) : 0;
-  }();
-#define GM_LAUNCH(K, S) \
-  hipLaunchKernelGGL((k_get_many<K, S>), g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n, which, vsrc, dlen, tsum)
-#define GM_SPEC(K)        \
-  switch (spec) {         \
-    case 2: GM_LAUNCH(K, 2); break; \
-    case 4: GM_LAUNCH(K, 4); break; \
-    default: GM_LAUNCH(K, 0); break; \
-  }
+#define GM_LAUNCH(K) \
+  hipLaunchKernelGGL((k_get_many<K>), g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n, which, vsrc, dlen, tsum)
   switch (keyk) {
-    case KEY_FIXED16: GM_SPEC(KEY_FIXED16); break;
-    case KEY_FIXED: GM_SPEC(KEY_FIXED); break;
-    case KEY_VAR: GM_SPEC(KEY_VAR); break;
+    case KEY_FIXED16: GM_LAUNCH(KEY_FIXED16); break;
+    case KEY_FIXED: GM_LAUNCH(KEY_FIXED); break;
+    case KEY_VAR: GM_LAUNCH(KEY_VAR); break;
     default: return hipErrorInvalidValue;
   }
-#undef GM_SPEC
 #undef GM_LAUNCH
   return hipGetLastError();
 }
 
 template <int KK, int MM, int WW>
-static void set_get_many(int spec, const void* set, const ModP& mp, const ZoneView& zv, const TableView* tv,
-                         uint32_t nt, const uint32_t* slots, const KeySrc& ks, uint64_t n, int32_t* which,
-                         uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum, hipStream_t s) {
-  const dim3 g(blocks_for(n, kNT));
-  if (spec == 2)
-    hipLaunchKernelGGL((k_set_get_many<KK, MM, WW, 2>), g, dim3(kNT), 0, s, set, mp, zv, tv, nt, slots, ks, n,
-                       which, vsrc, dlen, tsum);
-  else
-    hipLaunchKernelGGL((k_set_get_many<KK, MM, WW, 0>), g, dim3(kNT), 0, s, set, mp, zv, tv, nt, slots, ks, n,
-                       which, vsrc, dlen, tsum);
+static void set_get_many(const void* set, const ModP& mp, const ZoneView& zv, const TableView* tv, uint32_t nt,
+                         const uint32_t* slots, const KeySrc& ks, uint64_t n, int32_t* which, uint64_t* vsrc,
+                         uint64_t* dlen, uint64_t* tsum, hipStream_t s) {
+  // Measured and not kept (one lane, us per 1M keys): forcing 6 or 7 waves
+  // per SIMD (80 / 72 VGPRs with spills) 112-115 / 131 against 108-110 at the
+  // natural 90 VGPRs and 5 waves; set[b] read without the short-circuit
+  // 111-113; the first two records of each bucket loaded with its prefixes
+  // 107-109; gathering and decoding values of <= 18 bytes here (so
+  // k_b64_decode reads them coalesced: 27 -> 14 us) 132, the value load being
+  // one more dependent step at the end of every found key's chain.
+  hipLaunchKernelGGL((k_set_get_many<KK, MM, WW>), dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, set, mp, zv, tv, nt,
+                     slots, ks, n, which, vsrc, dlen, tsum);
 }
 
 hipError_t launch_set_get_many(int keyk, int mode, uint32_t width, const void* set, const ModP& mp,
@@ -1051,14 +1023,10 @@ hipError_t launch_set_get_many(int keyk, int mode, uint32_t width, const void* s
                                uint64_t* tsum, hipStream_t s) {
   if (!n) return hipSuccess;
   if (nt > width || (width != 32 && width != 64)) return hipErrorInvalidValue;
-  static const int spec = [] {
-    const char* v = getenv("CB_GM_SPEC");
-    return v ? atoi(v) : 0;
-  }();
   const ZoneView zv = zones ? *zones : ZoneView{nullptr, nullptr, nullptr, 0};
   ProfScope ps("k_set_get_many", s);
   CB_SET_DISPATCH(keyk, mode, width,
-                  (set_get_many<KK, MM, WW>(spec, set, mp, zv, tv, nt, slots, ks, n, which, vsrc, dlen, tsum, s)));
+                  (set_get_many<KK, MM, WW>(set, mp, zv, tv, nt, slots, ks, n, which, vsrc, dlen, tsum, s)));
   return hipGetLastError();
 }
 
