@@ -632,6 +632,26 @@ __global__ __launch_bounds__(kNT) void k_table_search(TableView t, KeySrc ks, ui
   line[k] = search(t, q, r);
 }
 
+// One group of up to 64 tables (t0 .. t0 + 63): every candidate in cand,
+// newest first, until a table answers Ok(Some). Returns whether one did.
+__device__ __forceinline__ bool resolve_group(const TableView* stv, const TableView* __restrict__ tv, uint32_t t0,
+                                              uint64_t cand, const Query& q, int32_t& w, uint64_t& src,
+                                              uint64_t& d) {
+  while (cand) {
+    const uint32_t t = t0 + (uint32_t)__builtin_ctzll(cand);
+    cand &= cand - 1;
+    const TableView v = t < 64 ? stv[t] : tv[t];
+    LineRec r;
+    if (search(v, q, r) < 0) continue;  // Ok(None)
+    if (r.vdl == kBadValue) continue;   // Err(..) is skipped by `if let Ok(Some(v))`
+    w = (int32_t)t;
+    src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
+    d = r.vdl;
+    return true;
+  }
+  return false;
+}
+
 // Database::get's walk for one key (src/lib.rs:129-134): tables in groups
 // of 64, newest first (tables.iter().rev()). Each lane holds its candidate
 // tables of the group as a bit mask (cand0 for the first 64; past them, from
@@ -644,7 +664,7 @@ __device__ __forceinline__ void resolve_key(const TableView* stv, const TableVie
                                             uint64_t cand0, const uint64_t* __restrict__ hits,
                                             const uint32_t* __restrict__ rows, uint64_t hwords, uint64_t k,
                                             const Query& q, int32_t& w, uint64_t& src, uint64_t& d) {
-  for (uint32_t t0 = 0; t0 < nt && w < 0; t0 += 64) {
+  for (uint32_t t0 = 0; t0 < nt; t0 += 64) {
     const uint32_t gn = nt - t0 < 64 ? nt - t0 : 64;
     uint64_t cand = gn == 64 ? ~0ull : ((1ull << gn) - 1);
     if (t0 == 0) {
@@ -656,18 +676,7 @@ __device__ __forceinline__ void resolve_key(const TableView* stv, const TableVie
         cand |= ((hits[row * hwords + (k >> 6)] >> (k & 63)) & 1) << i;  // the gate
       }
     }
-    while (cand) {
-      const uint32_t t = t0 + (uint32_t)__builtin_ctzll(cand);
-      cand &= cand - 1;
-      const TableView v = t < 64 ? stv[t] : tv[t];
-      LineRec r;
-      if (search(v, q, r) < 0) continue;  // Ok(None)
-      if (r.vdl == kBadValue) continue;         // Err(..) is skipped by `if let Ok(Some(v))`
-      w = (int32_t)t;
-      src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
-      d = r.vdl;
-      return;
-    }
+    if (resolve_group(stv, tv, t0, cand, q, w, src, d)) return;
   }
 }
 
@@ -751,7 +760,7 @@ __global__ __launch_bounds__(kNT) void k_set_get_many(const void* __restrict__ s
   if (k < n) {
     int32_t w = -1;
     uint64_t src = 0;
-    resolve_key(stv, tv, nt, cand0, nullptr, nullptr, 0, k, q, w, src, d);
+    (void)resolve_group(stv, tv, 0, cand0, q, w, src, d);  // nt <= 64: one group
     which[k] = w;
     vsrc[k] = src;
     dlen[k] = d;
@@ -1012,7 +1021,10 @@ static void set_get_many(const void* set, const ModP& mp, const ZoneView& zv, co
   // 111-113; the first two records of each bucket loaded with its prefixes
   // 107-109; gathering and decoding values of <= 18 bytes here (so
   // k_b64_decode reads them coalesced: 27 -> 14 us) 132, the value load being
-  // one more dependent step at the end of every found key's chain.
+  // one more dependent step at the end of every found key's chain;
+  // compacting the searches (the gate for 2 or 3 keys per lane, the keys
+  // with a candidate queued in LDS, then one queue entry per lane, so search
+  // waves run full) 243-249: the wave count, not lane occupancy, bounds it.
   hipLaunchKernelGGL((k_set_get_many<KK, MM, WW>), dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, set, mp, zv, tv, nt,
                      slots, ks, n, which, vsrc, dlen, tsum);
 }
