@@ -206,6 +206,30 @@ def test_set_get_many_vs_oracle(gpu, m, nt, width):
     assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals
 
 
+def test_get_many_batches_of_changing_size(gpu):
+    """Consecutive calls on one stream (reused workspaces: tile sums, value
+    offsets) with batch sizes from 1 key to 70K keys, alternating the
+    two-step and the fused form, each equal to the oracle."""
+    per = [workload.key_range(1500 + t, 30_000) for t in range(3)]
+    files = [workload.sstable_bytes(k, workload.table_value(k, 400 + t)) for t, k in enumerate(per)]
+    tables = [gpu.Table(f) for f in files]
+    otables = [oracle.OracleTable(f.tobytes()) for f in files]
+    s = gpu.FilterSet(1 << 20)
+    for t, k in enumerate(per):
+        b = gpu.BloomFilter(1 << 20)
+        b.insert_batch(k)
+        s.assign(t, b)
+    pool = np.concatenate([per[0], per[2], workload.key_range(4324, 30_000)])
+    pool = pool[np.random.default_rng(5).permutation(len(pool))]
+    for i, nk in enumerate([70_000, 300, 40_000, 1, 16_384, 16_385, 20_000]):
+        look = np.ascontiguousarray(pool[:nk])
+        d = np.ascontiguousarray(look.reshape(-1))
+        offs = np.arange(0, 16 * (nk + 1), 16, dtype=np.uint64)
+        ow, ovoff, ovals = oracle.get_many(otables, None, d, offs)
+        which, voff, vals = gpu.get_many(tables, look, set=s) if i % 2 else gpu.get_many(tables, look)
+        assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals, nk
+
+
 def test_set_get_many_async_device(gpu):
     """Device keys and outputs, total = NULL (enqueue only), slots = NULL
     (table t = slot t): val_off[n] carries the total; the answers equal the
