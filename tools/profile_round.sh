@@ -14,6 +14,9 @@ mkdir -p $OUT
 BENCH="python bench.py --no-cpu --no-e2e --no-cold --steps 50 --warmup 5 $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $BENCH > $OUT/kt_bench.json 2> $OUT/kt.err || exit 1
 BENCH="$BENCH --probe-streams 1"
+# the same with one lane: launches do not overlap, so each dispatch's
+# duration is the kernel's own time, comparable with the bench line's
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt1 -o kt1 --output-format csv -- $BENCH > $OUT/kt1_bench.json 2> $OUT/kt1.err || exit 1
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum" "TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_DRAM_sum"; do
   i=$((i+1))
