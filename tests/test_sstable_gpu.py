@@ -230,6 +230,50 @@ def test_get_many_batches_of_changing_size(gpu):
         assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals, nk
 
 
+def test_set_get_many_long_keys_and_exact_tables(gpu):
+    """The fused form over ragged keys of 0..40 bytes (the long-key compares
+    past the 16-byte index words), with one table indexed for the exact
+    reference trajectory and one holding undecodable values (Err falls
+    through to older tables), zones on every slot; equal to the oracle's walk
+    over FilterSet.probe(gated=True)'s bits."""
+    import base64
+    rng = np.random.default_rng(17)
+    alpha = np.frombuffer(b"abcxyz019_:", np.uint8)
+    def rkey():
+        return bytes(alpha[rng.integers(0, len(alpha), rng.integers(0, 41))])
+    nt = 4
+    keysets = [sorted({rkey() for _ in range(6000)}) for _ in range(nt)]
+    keysets[1] = sorted(set(keysets[1]) | set(keysets[0][::3]))  # shared keys: the newer table wins
+    def line(k, t, i):
+        v = bytes([(t * 31 + i + j) % 256 for j in range(i % 23)])
+        enc = base64.b64encode(v) if not (t == 2 and i % 5 == 0) else b"!!!"  # undecodable
+        return k + b"\t" + enc + b"\n"
+    files = [b"".join(line(k, t, i) for i, k in enumerate(ks)) for t, ks in enumerate(keysets)]
+    gpu.Table.force_exact(True)
+    try:
+        t3 = gpu.Table(files[3])
+    finally:
+        gpu.Table.force_exact(False)
+    tables = [gpu.Table(f) for f in files[:3]] + [t3]
+    otables = [oracle.OracleTable(f) for f in files]
+    s = gpu.FilterSet(1 << 18)
+    for t, ks in enumerate(keysets):
+        d, o = var(ks)
+        kb = gpu.KeyBatch(n=len(ks), data=d, offsets=o)
+        b = gpu.BloomFilter(1 << 18)
+        b.insert_batch(kb)
+        s.assign(t, b)
+        s.zone_from_keys(t, kb)
+    look = [k for ks in keysets for k in ks[::7]] + [rkey() for _ in range(3000)]
+    d, o = var(look)
+    kb = gpu.KeyBatch(n=len(look), data=d, offsets=o)
+    hits = s.probe(kb, gated=True)
+    ow, ovoff, ovals = oracle.get_many(otables, hits, d, o)
+    which, voff, vals = gpu.get_many(tables, kb, set=s)
+    assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals
+    assert (which == 3).any() and (which == 0).any() and (which < 0).any()
+
+
 def test_set_get_many_async_device(gpu):
     """Device keys and outputs, total = NULL (enqueue only), slots = NULL
     (table t = slot t): val_off[n] carries the total; the answers equal the
