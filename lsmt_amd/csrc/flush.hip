@@ -380,13 +380,17 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
       // ranges longer than a wave's store go to the block's list, which all
       // kNT threads fill together (a wide gap in the keys is one line's
       // range: spread over the block, not one wave)
-      __shared__ uint64_t big_s[2 * kNT], big_c[2 * kNT];
-      __shared__ uint32_t big_v[2 * kNT], nbig;
+      // (a short list: LDS per block sets how many blocks share a CU; a range
+      // that finds the list full stays with its wave)
+      constexpr uint32_t kBig = 64;
+      __shared__ uint64_t big_s[kBig], big_c[kBig];
+      __shared__ uint32_t big_v[kBig], nbig;
       if (threadIdx.x == 0) nbig = 0;
       __syncthreads();
       auto defer = [&](uint64_t st, uint64_t& c, uint32_t v) {
         if (c <= 64) return;
         const uint32_t k = atomicAdd(&nbig, 1u);
+        if (k >= kBig) return;
         big_s[k] = st;
         big_c[k] = c;
         big_v[k] = v;
@@ -397,7 +401,8 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
       wave_fill(dir, s0, c0, (uint32_t)p);
       wave_fill(dir, s1, c1, (uint32_t)n);
       __syncthreads();
-      for (uint32_t k = 0; k < nbig; ++k) {
+      const uint32_t nb_ = nbig < kBig ? nbig : kBig;
+      for (uint32_t k = 0; k < nb_; ++k) {
         uint32_t* d = dir + big_s[k];
         const uint64_t c = big_c[k];
         const uint32_t v = big_v[k];
