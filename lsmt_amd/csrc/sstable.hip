@@ -634,20 +634,31 @@ __global__ __launch_bounds__(kNT) void k_table_search(TableView t, KeySrc ks, ui
 
 // One group of up to 64 tables (t0 .. t0 + 63): every candidate in cand,
 // newest first, until a table answers Ok(Some). Returns whether one did.
+// LDS_VIEWS (every table among the first 64): the search reads its table's
+// view fields from LDS where it uses them instead of copying the 56-byte view
+// into registers (88 -> 80 VGPRs: 6 waves per SIMD instead of 5).
+template <bool LDS_VIEWS = false>
 __device__ __forceinline__ bool resolve_group(const TableView* stv, const TableView* __restrict__ tv, uint32_t t0,
                                               uint64_t cand, const Query& q, int32_t& w, uint64_t& src,
                                               uint64_t& d) {
   while (cand) {
     const uint32_t t = t0 + (uint32_t)__builtin_ctzll(cand);
     cand &= cand - 1;
-    const TableView v = t < 64 ? stv[t] : tv[t];
-    LineRec r;
-    if (search(v, q, r) < 0) continue;  // Ok(None)
-    if (r.vdl == kBadValue) continue;   // Err(..) is skipped by `if let Ok(Some(v))`
-    w = (int32_t)t;
-    src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
-    d = r.vdl;
-    return true;
+    auto try_table = [&](const TableView& v) {
+      LineRec r;
+      if (search(v, q, r) < 0) return false;  // Ok(None)
+      if (r.vdl == kBadValue) return false;   // Err(..) is skipped by `if let Ok(Some(v))`
+      w = (int32_t)t;
+      src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
+      d = r.vdl;
+      return true;
+    };
+    if constexpr (LDS_VIEWS) {
+      if (try_table(stv[t])) return true;
+    } else {
+      const TableView v = t < 64 ? stv[t] : tv[t];
+      if (try_table(v)) return true;
+    }
   }
   return false;
 }
@@ -760,7 +771,7 @@ __global__ __launch_bounds__(kNT) void k_set_get_many(const void* __restrict__ s
   if (k < n) {
     int32_t w = -1;
     uint64_t src = 0;
-    (void)resolve_group(stv, tv, 0, cand0, q, w, src, d);  // nt <= 64: one group
+    (void)resolve_group<true>(stv, tv, 0, cand0, q, w, src, d);  // nt <= 64: one group
     which[k] = w;
     vsrc[k] = src;
     dlen[k] = d;
