@@ -671,6 +671,7 @@ __device__ __forceinline__ bool resolve_group(const TableView* stv, const TableV
 // instead of the wave stepping through the tables one by one. w / src / d:
 // the first table whose SsTable::get returns Ok(Some), the value's base64
 // bytes and their decoded length.
+template <bool LDS_VIEWS>
 __device__ __forceinline__ void resolve_key(const TableView* stv, const TableView* __restrict__ tv, uint32_t nt,
                                             uint64_t cand0, const uint64_t* __restrict__ hits,
                                             const uint32_t* __restrict__ rows, uint64_t hwords, uint64_t k,
@@ -687,11 +688,12 @@ __device__ __forceinline__ void resolve_key(const TableView* stv, const TableVie
         cand |= ((hits[row * hwords + (k >> 6)] >> (k & 63)) & 1) << i;  // the gate
       }
     }
-    if (resolve_group(stv, tv, t0, cand, q, w, src, d)) return;
+    if (resolve_group<LDS_VIEWS>(stv, tv, t0, cand, q, w, src, d)) return;
   }
 }
 
-template <int KEYK>
+// LDS_VIEWS: nt <= 64 (every view staged in LDS; see resolve_group).
+template <int KEYK, bool LDS_VIEWS>
 __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ tv, uint32_t nt,
                                                   const uint64_t* __restrict__ hits,
                                                   const uint32_t* __restrict__ rows,
@@ -726,7 +728,10 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
   if (k < n) {
     int32_t w = -1;
     uint64_t src = 0;
-    resolve_key(stv, tv, nt, cand0, hits, rows, hwords, k, q, w, src, d);
+    if constexpr (LDS_VIEWS)
+      (void)resolve_group<true>(stv, tv, 0, cand0, q, w, src, d);  // one group
+    else
+      resolve_key<false>(stv, tv, nt, cand0, hits, rows, hwords, k, q, w, src, d);
     which[k] = w;
     vsrc[k] = src;
     dlen[k] = d;
@@ -1010,8 +1015,13 @@ hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uin
   if (!n) return hipSuccess;
   ProfScope ps("k_get_many", s);
   const dim3 g(blocks_for(n, kNT));
-#define GM_LAUNCH(K) \
-  hipLaunchKernelGGL((k_get_many<K>), g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n, which, vsrc, dlen, tsum)
+#define GM_LAUNCH(K)                                                                                              \
+  if (nt <= 64)                                                                                                   \
+    hipLaunchKernelGGL((k_get_many<K, true>), g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n, which, vsrc, \
+                       dlen, tsum);                                                                               \
+  else                                                                                                            \
+    hipLaunchKernelGGL((k_get_many<K, false>), g, dim3(kNT), 0, s, tv, nt, hits, rows, hwords, ks, n, which,      \
+                       vsrc, dlen, tsum)
   switch (keyk) {
     case KEY_FIXED16: GM_LAUNCH(KEY_FIXED16); break;
     case KEY_FIXED: GM_LAUNCH(KEY_FIXED); break;
