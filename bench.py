@@ -487,7 +487,7 @@ def main():
             zone + Bloom gate computed from the FilterSet inside the search
             kernel, so no gate rows are written or read."""
             b = claim()
-            lsmt_amd.get_many(newest_first, keys_batch, set=fset, hit_rows=rows,
+            lsmt_amd.get_many(newest_first, keys_batch, filterset=fset, hit_rows=rows,
                               out=(which_l[b], voff_l[b], vals_l[b]), stream=lane_sh[b], wait=False)
 
         rforms = {}

@@ -761,7 +761,7 @@ def _to_var(b: KeyBatch) -> KeyBatch:
 
 
 def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=None, out=None, wait=True,
-             set=None):
+             filterset=None):
     """Database::get's newest-first walk for a key batch (tables[0] newest).
     hits: optional per-table gate bitmaps (e.g. FilterSet.probe(gated=True));
     table t uses row hit_rows[t] (default t). Returns (which int32[n]: table
@@ -773,13 +773,13 @@ def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=Non
     device) the call only enqueues the work on stream and returns total None:
     val_off[n] holds it once the stream has run.
 
-    set=FilterSet: Database::get in one launch (cb_set_get_many_*): each
+    filterset=FilterSet: Database::get in one launch (cb_set_get_many_*): each
     table's gate (its slot's ZoneMap and Bloom bits, as
     FilterSet.probe(gated=True)) is computed inside the search kernel, so no
     hit rows exist; hit_rows then names each table's slot (default t) and
     hits must be None. At most the set's width tables."""
-    if set is not None and hits is not None:
-        raise ValueError("set= computes the gate itself: pass hits=None")
+    if filterset is not None and hits is not None:
+        raise ValueError("filterset= computes the gate itself: pass hits=None")
     b = as_batch(keys)
     nt = len(tables)
     arr = (ctypes.c_void_p * max(nt, 1))(*[t.handle.value for t in tables])
@@ -807,8 +807,8 @@ def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=Non
         offp, k2 = _ptr_of(b.offsets)
 
         def call(vp, cap):
-            if set is not None:
-                _raise(L.cb_set_get_many_var(set._h, ctypes.cast(arr, ctypes.c_void_p), nt, rp, dp, offp, b.n,
+            if filterset is not None:
+                _raise(L.cb_set_get_many_var(filterset._h, ctypes.cast(arr, ctypes.c_void_p), nt, rp, dp, offp, b.n,
                                              wp, vo, vp, cap, tref, s))
             else:
                 _raise(L.cb_get_many_var(ctypes.cast(arr, ctypes.c_void_p), nt, hp, rp, dp, offp, b.n,
@@ -817,8 +817,8 @@ def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=Non
         kp, k1 = _ptr_of(b.keys)
 
         def call(vp, cap):
-            if set is not None:
-                _raise(L.cb_set_get_many_fixed(set._h, ctypes.cast(arr, ctypes.c_void_p), nt, rp, kp, b.key_len,
+            if filterset is not None:
+                _raise(L.cb_set_get_many_fixed(filterset._h, ctypes.cast(arr, ctypes.c_void_p), nt, rp, kp, b.key_len,
                                                b.n, wp, vo, vp, cap, tref, s))
             else:
                 _raise(L.cb_get_many_fixed(ctypes.cast(arr, ctypes.c_void_p), nt, hp, rp, kp, b.key_len, b.n,

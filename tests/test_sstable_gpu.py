@@ -191,7 +191,7 @@ def test_set_get_many_vs_oracle(gpu, m, nt, width):
     d = np.ascontiguousarray(look.reshape(-1))
     offs = np.arange(0, 16 * (len(look) + 1), 16, dtype=np.uint64)
     ow, ovoff, ovals = oracle.get_many(otables, hits, d, offs)
-    which, voff, vals = gpu.get_many(tables, look, set=s, hit_rows=slots)
+    which, voff, vals = gpu.get_many(tables, look, filterset=s, hit_rows=slots)
     assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals
     w2, v2, vals2 = gpu.get_many(tables, look, hits=full, hit_rows=slots)
     assert np.array_equal(w2, ow) and vals2 == ovals
@@ -202,7 +202,7 @@ def test_set_get_many_vs_oracle(gpu, m, nt, width):
     kb = gpu.KeyBatch(n=len(vk), data=dv, offsets=ov)
     vhits = s.probe(kb, gated=True)[slots].copy()
     ow, ovoff, ovals = oracle.get_many(otables, vhits, dv, ov)
-    which, voff, vals = gpu.get_many(tables, kb, set=s, hit_rows=slots)
+    which, voff, vals = gpu.get_many(tables, kb, filterset=s, hit_rows=slots)
     assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals
 
 
@@ -226,7 +226,7 @@ def test_get_many_batches_of_changing_size(gpu):
         d = np.ascontiguousarray(look.reshape(-1))
         offs = np.arange(0, 16 * (nk + 1), 16, dtype=np.uint64)
         ow, ovoff, ovals = oracle.get_many(otables, None, d, offs)
-        which, voff, vals = gpu.get_many(tables, look, set=s) if i % 2 else gpu.get_many(tables, look)
+        which, voff, vals = gpu.get_many(tables, look, filterset=s) if i % 2 else gpu.get_many(tables, look)
         assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals, nk
 
 
@@ -269,7 +269,7 @@ def test_set_get_many_long_keys_and_exact_tables(gpu):
     kb = gpu.KeyBatch(n=len(look), data=d, offsets=o)
     hits = s.probe(kb, gated=True)
     ow, ovoff, ovals = oracle.get_many(otables, hits, d, o)
-    which, voff, vals = gpu.get_many(tables, kb, set=s)
+    which, voff, vals = gpu.get_many(tables, kb, filterset=s)
     assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals
     assert (which == 3).any() and (which == 0).any() and (which < 0).any()
 
@@ -296,7 +296,7 @@ def test_set_get_many_async_device(gpu):
     which = torch.zeros(len(look), dtype=torch.int32, device="cuda")
     voff = torch.zeros(len(look) + 1, dtype=torch.int64, device="cuda")
     vals = torch.zeros(len(evals) + 64, dtype=torch.uint8, device="cuda")
-    assert gpu.get_many(tables, gpu.DeviceKeys(dk), set=s, out=(which, voff, vals), wait=False)[2] is None
+    assert gpu.get_many(tables, gpu.DeviceKeys(dk), filterset=s, out=(which, voff, vals), wait=False)[2] is None
     torch.cuda.synchronize()
     tot = int(voff[-1].item())
     assert tot == len(evals)
@@ -304,7 +304,7 @@ def test_set_get_many_async_device(gpu):
     assert np.array_equal(voff.cpu().numpy().view(np.uint64), evoff)
     assert vals[:tot].cpu().numpy().tobytes() == evals
     with pytest.raises(ValueError):
-        gpu.get_many(tables, look, hits=s.probe(look), set=s)
+        gpu.get_many(tables, look, hits=s.probe(look), filterset=s)
 
 
 def test_well_formed_detection(gpu):
