@@ -13,6 +13,7 @@
 // candidate, so a wave's lanes search different tables concurrently.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_scan.hpp>
@@ -370,12 +371,37 @@ __device__ __forceinline__ int rec_cmp(const TableView& t, const LineRec& r, con
   return line_cmp(t.data + r.start, r.klen, q.p, q.len);
 }
 
+// Index loads as global (not flat) loads: every index array is device memory,
+// and a flat load also holds the LDS counter, so the LDS-resident views and
+// the search's loads would wait on each other.
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(1))) u64x2* g64x2;
+static_assert(sizeof(LineRec) == 32 && offsetof(LineRec, pfx2) == 8 && offsetof(LineRec, klen) == 16 &&
+                  offsetof(LineRec, llen) == 20 && offsetof(LineRec, vdl) == 24,
+              "grec reads LineRec as two 16-byte words");
+__device__ __forceinline__ LineRec grec(const LineRec* r, uint64_t i) {
+  const g64x2 p = (g64x2)(r + i);
+  const u64x2 lo = p[0], hi = p[1];
+  LineRec o;
+  o.start = lo.x;
+  o.pfx2 = lo.y;
+  o.klen = (uint32_t)hi.x;
+  o.llen = (uint32_t)(hi.x >> 32);
+  o.vdl = (uint32_t)hi.y;
+  o.pad = (uint32_t)(hi.y >> 32);
+  return o;
+}
+__device__ __forceinline__ uint64_t g64(const uint64_t* p, uint64_t i) {
+  return ((const __attribute__((address_space(1))) uint64_t*)p)[i];
+}
+
 // SsTable::binary_search (src/sstable.rs:161-179), same mid sequence.
 __device__ __forceinline__ int64_t search_exact(const TableView& t, const Query& q, LineRec& hit) {
   uint64_t lo = 0, hi = t.nlines;
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
-    const LineRec r = t.rec[mid];
+    const LineRec r = grec(t.rec, mid);
     if (r.klen == kNoSep) break;
     const int c = line_cmp(t.data + r.start, r.klen, q.p, q.len);
     if (c < 0)
@@ -394,7 +420,7 @@ __device__ __forceinline__ int64_t search_exact(const TableView& t, const Query&
 __device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t* a, uint64_t lo, uint64_t hi, uint64_t x) {
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
-    if (a[mid] < x)
+    if (g64(a, mid) < x)
       lo = mid + 1;
     else
       hi = mid;
@@ -405,9 +431,9 @@ __device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t* a, uint64_t 
 // Line l's key against the query, in a well-formed file: prefix first, then
 // the record (r receives it when the prefixes are equal).
 __device__ __forceinline__ int line_vs_query(const TableView& t, uint64_t l, const Query& q, LineRec& r) {
-  const uint64_t p = t.pfx[l];
+  const uint64_t p = g64(t.pfx, l);
   if (p != q.w0) return p < q.w0 ? -1 : 1;
-  r = t.rec[l];
+  r = grec(t.rec, l);
   return rec_cmp(t, r, q);
 }
 
@@ -458,8 +484,8 @@ __device__ __forceinline__ int64_t resolve_rec(const TableView& t, const Query& 
 __device__ __forceinline__ int64_t resolve_from(const TableView& t, const Query& q, uint64_t b, LineRec& hit) {
   // line b's prefix and record in one round trip (the record is needed
   // whenever the prefix matches, i.e. for every key that is present)
-  const uint64_t p0 = t.pfx[b];
-  const LineRec r = t.rec[b];
+  const uint64_t p0 = g64(t.pfx, b);
+  const LineRec r = grec(t.rec, b);
   if (p0 != q.w0) return -1;  // p0 > q.w0: b is the prefix's lower bound
   return resolve_rec(t, q, b, r, hit);
 }
@@ -503,7 +529,10 @@ __device__ __forceinline__ bool dir_start(const TableView& t, uint64_t x, uint32
     return true;
   }
   const uint64_t bk = (x << sh) >> (64 - t.dbits);
-  const uint64_t a = t.dir[bk], e = t.dir[bk + 1];
+  // dir[B] and dir[B + 1] as one 8-byte load (one L2 request, not two: the
+  // search is bound by the requests a CU keeps in flight)
+  const u32x2 ae = *(const __attribute__((address_space(1))) u32x2*)(t.dir + bk);
+  const uint64_t a = ae.x, e = ae.y;
   if (a == e) {
     b = a;
     return true;
@@ -540,10 +569,22 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
     // (loading the first two records of every bucket with them measured
     // within noise: 85-87 vs 88 us per 1M keys)
     uint64_t v[kWin];
+    // in pairs: two neighbouring prefixes as one 16-byte load where both
+    // are in the bucket (one L2 request per pair, not per prefix)
+
 #pragma unroll
-    for (uint32_t k = 0; k < kWin; ++k) v[k] = lo + k < hi ? t.pfx[lo + k] : ~0ull;
+    for (uint32_t k = 0; k < kWin; k += 2) {
+      if (lo + k + 1 < hi) {
+        const u64x2 pr = *(g64x2)(t.pfx + lo + k);
+        v[k] = pr.x;
+        v[k + 1] = pr.y;
+      } else {
+        v[k] = lo + k < hi ? g64(t.pfx, lo + k) : ~0ull;
+        v[k + 1] = ~0ull;
+      }
+    }
     LineRec r1;
-    if (hi - lo == 1) r1 = t.rec[lo];
+    if (hi - lo == 1) r1 = grec(t.rec, lo);
     uint32_t c = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kWin; ++k) c += (lo + k < hi && v[k] < q.w0) ? 1u : 0u;
@@ -553,7 +594,7 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
 #pragma unroll
     for (uint32_t k = 1; k < kWin; ++k) p0 = k == c ? v[k] : p0;
     if (p0 != q.w0) return -1;
-    return resolve_rec(t, q, lo + c, hi - lo == 1 ? r1 : t.rec[lo + c], hit);
+    return resolve_rec(t, q, lo + c, hi - lo == 1 ? r1 : grec(t.rec, lo + c), hit);
   }
   for (;; --j) {
     const uint64_t i = lower_bound_u64(level_array(t, j), lo, hi, q.w0);

@@ -22,7 +22,7 @@ for form in ("cur",):
             per[(r["Dispatch_Id"], k, r["Counter_Name"])] += float(r["Counter_Value"])
         for (d, k, c), v in per.items():
             agg[k][c].append(v)
-    for k in ("k_get_many", "k_b64_decode", "k_set_probe"):
+    for k in ("k_set_get_many", "k_get_many", "k_b64_decode", "k_set_probe"):
         if agg[k]:
             print(form, k, {c: round(sum(v) / len(v)) for c, v in sorted(agg[k].items())})
 PY
