@@ -946,10 +946,10 @@ def _random_read_roofline():
 
 def _pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/pmc_*.json, FETCH_SIZE/WRITE_SIZE with the gfx950 corrections), or
+    (profiles/pmc_rNN.json, FETCH_SIZE/WRITE_SIZE with the gfx950 corrections), or
     None when no PMC run has been recorded for the current kernels."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r[0-9]*.json")))  # the round summaries
     if not files:
         return None
     try:
