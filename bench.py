@@ -12,12 +12,19 @@ baseline (rank 0, N = 1), and the PCIe-inclusive end-to-end probe rate.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+`python bench.py --gpus N` (N > 1, no WORLD_SIZE in the environment) starts
+the N rank processes itself through torch.distributed.run before anything
+touches the GPU, and relays rank 0's JSON line; inside a rank, --gpus must
+equal WORLD_SIZE. --dry-run joins a gloo group and reports every rank's
+RANK / LOCAL_RANK / WORLD_SIZE without any GPU call (the launcher's CPU test).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -62,28 +69,90 @@ def parse():
     p.add_argument("--flush-entries", type=int, default=1 << 20)
     p.add_argument("--probe-streams", type=int, default=3, choices=[1, 2, 3, 4],
                    help="pipeline lanes: consecutive steps alternate over this many streams (each with "
-                        "its own hit buffers and, for N > 1, its own RCCL communicator)")
+                        "its own hit buffers; for N > 1 they share the rank's one RCCL communicator)")
     p.add_argument("--force-dist", action="store_true",
                    help="initialise the process group and run the exchange path even at N=1")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launch / join the ranks over gloo and report them; no GPU work")
     return p.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes
+    (python -m torch.distributed.run, one per GPU, rendezvous on 127.0.0.1)
+    running this same command line, relay rank 0's JSON line to stdout, and
+    return the launcher's exit status (non-zero when any rank failed). The
+    parent never imports torch or touches HIP: each rank initialises its own
+    GPU."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, CB_BENCH_LAUNCHER="bench.py")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL over dmabuf IPC on this host driver
+    log(f"[launcher] {args.gpus} ranks: {' '.join(cmd)}")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    out = []
+    for line in p.stdout:  # the ranks' stderr is inherited (progress stays visible)
+        if line.lstrip().startswith("{"):
+            out.append(line.strip())
+        elif line.strip():
+            log(line.rstrip())
+    rc = p.wait()
+    if rc == 0 and len(out) != 1:
+        log(f"[launcher] error: expected one JSON line from rank 0, got {len(out)}")
+        return 1
+    if rc == 0:
+        print(out[0], flush=True)
+    else:
+        log(f"[launcher] a rank failed (exit status {rc}); no result line")
+    return rc
+
+
+def dry_run(args, world, rank, local, result) -> None:
+    """Join the ranks over gloo and report each one's identity (no GPU)."""
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    me = {"rank": rank, "local_rank": local, "world_size": int(os.environ.get("WORLD_SIZE", "1")),
+          "pid": os.getpid()}
+    every = [None] * world
+    dist.all_gather_object(every, me)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "gpus_arg": args.gpus,
+                          "launcher": os.environ.get("CB_BENCH_LAUNCHER", "external"), "ranks": every}),
+              file=result, flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))  # before anything touches the GPU
     # The contract is ONE JSON line on stdout. Libraries (RCCL's banner, ...)
     # write to fd 1 directly, so fd 1 is pointed at stderr for the whole run
     # and the result line goes to a saved copy of the original stdout.
     out_fd = os.dup(1)
     os.dup2(2, 1)
     result = os.fdopen(out_fd, "w")
-    import torch
-    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world}: run `bench.py --gpus N` alone (it starts the N "
+            "ranks) or under a launcher with --nproc-per-node N")
+        sys.exit(2)
+    if args.dry_run:
+        return dry_run(args, world, rank, local, result)
+    import torch
+    import torch.distributed as dist
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_dist = world > 1 or args.force_dist
@@ -169,11 +238,15 @@ def main():
     lane_streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(P - 1)]
     lane_sh = [st.cuda_stream for st in lane_streams]
     # The exchange runs through the C ABI (cb_hits_allgather over the
-    # library's own RCCL communicators, lsmt_amd/csrc/comm.cpp): the same
-    # call a Rust Database::get would make. torch.distributed only hands out
-    # the communicator ids and times the run. Every rank issues the lanes'
-    # collectives in the same order, one communicator per lane.
-    xcomms = [Comm.from_process_group(local) for _ in range(P)] if use_dist else []
+    # library's own RCCL communicator, lsmt_amd/csrc/comm.cpp): the same call
+    # a Rust Database::get would make. torch.distributed only hands out the
+    # communicator id and times the run. ONE communicator per rank, shared by
+    # the lanes: the library keeps each lane's packs apart and runs the
+    # collectives in issue order (every rank issues them in the same order),
+    # so no two collectives are ever in flight at once.
+    xcomm = Comm.from_process_group(local) if use_dist else None
+    if xcomm is not None and xcomm.world != world:
+        raise RuntimeError(f"RCCL communicator has {xcomm.world} ranks, WORLD_SIZE is {world}")
 
     def exchange(buf):
         """All-gather this step's hit rows from every rank (filter-major ->
@@ -182,11 +255,11 @@ def main():
         if not use_dist:
             return
         if use_sparse:
-            xcomms[buf].allgather(hits_bufs[buf], nf_total, hits_all_bufs[buf], sparse=True, cap=cap,
-                                  ok=x_ok, stream=lane_sh[buf])
+            xcomm.allgather(hits_bufs[buf], nf_total, hits_all_bufs[buf], sparse=True, cap=cap,
+                            ok=x_ok, stream=lane_sh[buf])
             xstats["sparse_steps"] += 1
         else:
-            xcomms[buf].allgather(hits_bufs[buf], nf_total, hits_all_bufs[buf], stream=lane_sh[buf])
+            xcomm.allgather(hits_bufs[buf], nf_total, hits_all_bufs[buf], stream=lane_sh[buf])
 
     def claim():
         buf = step_no[0] % P
@@ -203,8 +276,8 @@ def main():
         (cb_set_probe_allgather_fixed): in sparse mode the probe kernel writes
         the pack itself, so no separate compress pass reads the rows again."""
         if use_dist:
-            xcomms[buf].probe_allgather(fset, look, nf_total, hits_bufs[buf], hits_all_bufs[buf], sparse=use_sparse,
-                                        cap=cap, ok=x_ok, gated=gated, stream=lane_sh[buf])
+            xcomm.probe_allgather(fset, look, nf_total, hits_bufs[buf], hits_all_bufs[buf], sparse=use_sparse,
+                                  cap=cap, ok=x_ok, gated=gated, stream=lane_sh[buf])
             xstats["sparse_steps"] += int(use_sparse)
         else:
             fset.probe(keys_batch, out=hits_bufs[buf], stream=lane_sh[buf], gated=gated)
@@ -567,7 +640,7 @@ def main():
                 step_flush()
             k_fl = max(3, args.steps // 4)
             fel = timed(step_flush, k_fl)
-            fprof = kernel_ms(["k_sorted_check", "k_sort_keys", "k_entry_sort", "rocprim_merge_sort", "k_line_sums", "k_tile_scan",
+            fprof = kernel_ms(["k_sorted_check", "k_entry_sort", "k_tile_scan",
                                "k_format", "k_line_count", "k_line_emit", "k_line_finish", "k_line_keys",
                                "k_build_part", "k_build_tile", "k_insert_direct"], step_flush, k_fl)
             out_bytes = made[-1][0].nbytes
@@ -678,6 +751,13 @@ def main():
                "alt_per_filter_tiled": {"probes_per_s": round(n * F / t_tiled, 1),
                                         "ms_per_step": round(t_tiled * 1e3, 3)}}
 
+    # ---- the per-key drop-in call (SsTable::get's bloom.may_contain(key),
+    # src/sstable.rs:138): one host thread through the C ABI, host mirror vs
+    # one-key GPU probe, at the product's m = 1024 and the C3 filter size
+    may_contain = None
+    if rank == 0 and world == 1:
+        may_contain = may_contain_latency()
+
     if args.check:
         # Every rank checks its own rows and, in the exchanged map, the rows
         # of the next rank, so each rank's slice is verified as received by
@@ -731,7 +811,8 @@ def main():
                 "C5 rank-slice" if args.workload == "c5" and c5_shape else "custom")
     if rank == 0:
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "probes/s", "n_gpus": world,
+            "metric": METRIC, "value": round(value, 1), "unit": "probes/s",
+            "n_gpus": xcomm.world if xcomm is not None else world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (splitmix64 hex keys, SURVEY.md §8d)",
@@ -754,15 +835,15 @@ def main():
             "alt_kernels_us": {k: round(v["avg_us"], 2) for k, v in kprof_alt.items()},
             "filterset": {"build_all_ms": round(set_build_ms, 3), "assign_one_empty_slot_ms": round(set_assign_ms, 3),
                           "bytes": m * (4 if F <= 32 else 8)},
-            "cold": cold, "rotating_batches": rot, "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e, "zone_gate": zone, "read_path": read, "flush": flush,
+            "cold": cold, "rotating_batches": rot, "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e,
+            "zone_gate": zone, "read_path": read, "flush": flush, "may_contain": may_contain,
         }
         if x_fit is False:
             line["valid"] = False
         print(json.dumps(line), file=result, flush=True)
     if use_dist:
         dist.barrier()
-        for c in xcomms:
-            c.close()
+        xcomm.close()
         dist.destroy_process_group()
     if x_fit is False:
         sys.exit(3)
@@ -897,6 +978,26 @@ def zone_partitioned_leg(args, torch, dev, local, sh, F, m, kpf, n, timed, kerne
         exp = oracle.probe_gated(refs, zones, d, offs)
         out["oracle_sample_bit_exact"] = bool(np.array_equal(g[:, :sample // 64], exp))
         del refs
+    return out
+
+
+def may_contain_latency():
+    """tests/cpp/may_contain_latency (plain C over include/cassbloom.h, built
+    by __graft_entry__.build()): per-key cb_may_contain from one host thread,
+    the host mirror (steady state and the first call after the build) against
+    a one-key GPU probe per call; the two agree on every probe key."""
+    exe = os.path.join(ROOT, "build", "tests", "may_contain_latency")
+    if not os.path.exists(exe):
+        return {"error": "build/tests/may_contain_latency not built"}
+    out = {"metric": "single-key may_contain latency, one host thread, C ABI (SsTable::get's per-table "
+                     "bloom.may_contain, src/sstable.rs:138)"}
+    for label, m, nk in (("m1024", 1024, 100), ("m2^26", 1 << 26, 1 << 19)):
+        try:
+            r = subprocess.run([exe, str(m), str(nk), "400000"], capture_output=True, text=True, timeout=120)
+            d = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {"error": r.stderr[-400:]}
+        except Exception as e:  # reported in the line, never fatal to the headline
+            d = {"error": repr(e)}
+        out[label] = d
     return out
 
 

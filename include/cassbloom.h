@@ -111,8 +111,20 @@ int cb_probe_fixed(const cb_filter* const* filters, uint32_t nf, const uint8_t* 
                    uint32_t key_len, uint64_t n, uint64_t* hits, void* stream);
 int cb_probe_var(const cb_filter* const* filters, uint32_t nf, const uint8_t* bytes,
                  const uint64_t* offsets, uint64_t n, uint64_t* hits, void* stream);
-/* Single-key may_contain (host key, synchronous). *out = 0/1. */
+/* Single-key may_contain (host key, synchronous). *out = 0/1. The per-key
+ * call of SsTable::get (src/sstable.rs:138) answers from a host mirror of the
+ * filter's packed words when the mirror is on: the first call after a write
+ * (build, import, clear) waits for that write's stream position and copies
+ * ceil(m/32) words back once; later calls are two host word loads, no GPU
+ * round trip. With the mirror off every call is a one-key GPU probe.
+ * Reentrant: concurrent callers may share a filter (`&self`). */
 int cb_may_contain(const cb_filter* f, const uint8_t* key, uint64_t len, int* out);
+/* Host mirror policy: 1 on, 0 off, -1 auto (the default: on when m <= 2^28,
+ * i.e. up to 32 MiB of host words). */
+int cb_filter_host_mirror(cb_filter* f, int mode);
+/* *on = whether cb_may_contain uses the mirror; *current = whether the mirror
+ * already holds the latest write (either may be NULL). Host only. */
+int cb_filter_host_mirror_info(const cb_filter* f, int* on, int* current);
 
 /* ---- persistence (to_proto / from_proto / to_bytes / from_bytes) ---- */
 /* Vec<bool> layout: m bytes of 0/1. */
@@ -375,14 +387,37 @@ int cb_hits_expand(const uint32_t* packs, uint32_t nranks, uint64_t cap, const u
  *     (a device uint32 holding 1) nothing is read back: ok is cleared when a
  *     rank overflowed, and the caller redoes that batch with CB_XCHG_DENSE.
  *     *sparse_used (nullable) = 1 when the map came from the packs.
- *   One exchange at a time per communicator; exchanges on one communicator
- *   must be issued in the same order on every rank. */
+ *   Exchanges on one communicator must be issued in the same order on every
+ *   rank. They may come from several streams (pipelined batches): the
+ *   library keeps a buffer set per stream and runs a communicator's
+ *   collectives one after another in issue order (each waits for an event
+ *   recorded after the previous one), so at most one collective of a
+ *   communicator is in flight and no two communicators' collectives need to
+ *   interleave. Use ONE communicator per rank. */
 #define CB_COMM_ID_BYTES 128
 #define CB_XCHG_DENSE 0
 #define CB_XCHG_SPARSE 1
 typedef struct cb_comm cb_comm;
 int cb_comm_unique_id(uint8_t* id /* CB_COMM_ID_BYTES */);
 int cb_comm_init(int rank, int world, const uint8_t* id, int device, cb_comm** out);
+/* Two more transports under the same collectives (every host and device step
+ * of cb_hits_allgather / cb_set_probe_allgather_fixed is shared; only the
+ * all-gather of bytes differs):
+ *   cb_comm_init_loopback: `world` ranks in ONE process on one device;
+ *     ranks[r] (an array of world handles) is rank r's communicator. Each
+ *     rank's collectives must be issued from its own host thread: a call
+ *     returns once every rank has issued it. The all-gather is device copies
+ *     between the ranks' buffers, ordered by events on each caller's stream.
+ *     For tests of world > 1 on one GPU.
+ *   cb_comm_init_host: the caller moves the bytes (its own RPC, MPI, gloo ...):
+ *     the library synchronises the stream, copies this rank's `bytes` of send
+ *     data to host memory, calls fn(user, send, recv, bytes) — fn must leave
+ *     rank r's bytes at recv + r * bytes for every rank and return 0 — and
+ *     copies recv back to the device. Not collective at init. */
+typedef int (*cb_host_allgather_fn)(void* user, const void* send, void* recv, uint64_t bytes);
+int cb_comm_init_loopback(int world, int device, cb_comm** ranks);
+int cb_comm_init_host(int rank, int world, int device, cb_host_allgather_fn fn, void* user,
+                      cb_comm** out);
 int cb_comm_destroy(cb_comm* c);
 int cb_comm_info(const cb_comm* c, int* rank, int* world, int* device);
 int cb_comm_shard(uint64_t total_rows, int world, int rank, uint64_t* first_row, uint64_t* rows);
@@ -420,7 +455,8 @@ int cb_hits_expand_set(const uint32_t* packs, uint32_t nranks, uint64_t cap, con
  * 2 = force tiled (LDS-staged filter tiles). Process-wide. */
 int cb_set_path(int path);
 /* Path the last insert/probe on this thread used (1 direct, 2 tiled, 3 FilterSet,
- * 4 FilterSet zero-copy: pinned host keys and hits read/written by the kernel). */
+ * 4 FilterSet zero-copy: pinned host keys and hits read/written by the kernel,
+ * 5 cb_may_contain answered from the host mirror). */
 int cb_last_path(void);
 /* Per-kernel timing with HIP events recorded on each launch's own stream
  * (off by default). Kernel names: "k_insert_direct", "k_probe_direct",

@@ -27,6 +27,9 @@ CB_EUTF8 = -7
 PATH_AUTO, PATH_DIRECT, PATH_TILED = 0, 1, 2
 XCHG_DENSE, XCHG_SPARSE = 0, 1
 COMM_ID_BYTES = 128
+# cb_host_allgather_fn (include/cassbloom.h): int (*)(void* user, const void* send, void* recv, uint64_t bytes)
+HOST_ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_uint64)
 
 _lib = None
 
@@ -86,6 +89,8 @@ def load():
         "cb_hits_pack_words": ([u64, u64, u64, pu64], i32),
         "cb_comm_unique_id": ([P], i32),
         "cb_comm_init": ([i32, i32, P, i32, pp], i32),
+        "cb_comm_init_loopback": ([i32, i32, P], i32),
+        "cb_comm_init_host": ([i32, i32, i32, HOST_ALLGATHER_FN, P, pp], i32),
         "cb_comm_destroy": ([P], i32),
         "cb_comm_info": ([P, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
         "cb_comm_shard": ([u64, i32, i32, pu64, pu64], i32),
@@ -107,6 +112,8 @@ def load():
         "cb_probe_fixed": ([P, u32, u8p, u32, u64, P, P], i32),
         "cb_probe_var": ([P, u32, u8p, P, u64, P, P], i32),
         "cb_may_contain": ([P, u8p, u64, ctypes.POINTER(ctypes.c_int)], i32),
+        "cb_filter_host_mirror": ([P, i32], i32),
+        "cb_filter_host_mirror_info": ([P, ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
         "cb_filter_export_bools": ([P, u8p, P], i32),
         "cb_filter_import_bools": ([P, u8p, u64, P], i32),
         "cb_filter_export_packed": ([P, P, P], i32),

@@ -335,13 +335,26 @@ class BloomFilter:
 
     # ---- probe -------------------------------------------------------------
     def may_contain(self, item) -> bool:
-        """src/bloom.rs:48-51 for one key (synchronous)."""
+        """src/bloom.rs:48-51 for one key (synchronous; answered from the
+        host mirror of the words when it is on, see host_mirror)."""
         self.flush()
         key = item.encode() if isinstance(item, str) else bytes(item)
         buf = ctypes.create_string_buffer(key, max(len(key), 1))
         out = ctypes.c_int(0)
         _raise(_L().cb_may_contain(self._h, ctypes.cast(buf, ctypes.c_void_p), len(key), ctypes.byref(out)))
         return bool(out.value)
+
+    def host_mirror(self, mode: int = 1) -> None:
+        """Single-key may_contain source (cb_filter_host_mirror): 1 the host
+        mirror of the words (refreshed by one copy after each write), 0 a
+        one-key GPU probe per call, -1 auto (mirror when m <= 2^28)."""
+        check(_L().cb_filter_host_mirror(self._h, int(mode)))
+
+    def host_mirror_info(self) -> tuple[bool, bool]:
+        """(mirror on, mirror holds the latest write)."""
+        on, cur = ctypes.c_int(), ctypes.c_int()
+        check(_L().cb_filter_host_mirror_info(self._h, ctypes.byref(on), ctypes.byref(cur)))
+        return bool(on.value), bool(cur.value)
 
     def may_contain_batch(self, keys, stream=None) -> np.ndarray:
         hits = probe([self], keys, stream=stream)
@@ -846,13 +859,14 @@ def _pack_blocks(nw: int) -> int:
     return -(-int(nw) // PACK_BLOCK_WORDS)
 
 
-def hits_compress(hits, pack, cap=None, stream=None) -> None:
+def hits_compress(hits, pack, cap: int, stream=None) -> None:
     """pack (int32 device tensor) := {count, 0, set-bit positions[cap],
     directory} of hits ([rows][words] int64 device tensor): cb_hits_compress.
-    cap defaults to what the pack holds after its directory."""
+    cap is required: packs that are all-gathered share one stride (the
+    largest shard's, cb_hits_pack_words), so every rank must pass the same cap
+    and no rank may derive it from its own pack size."""
     rows, words = hits.shape
-    if cap is None:
-        cap = int(pack.numel()) - 2 - 2 * _pack_blocks(rows * words)
+    cap = int(cap)
     if cap < 0 or int(pack.numel()) < 2 + cap + 2 * _pack_blocks(rows * words):
         raise ValueError("pack too small for cap positions and the directory")
     hp, k1 = _ptr_of(hits)
@@ -860,22 +874,22 @@ def hits_compress(hits, pack, cap=None, stream=None) -> None:
     _raise(_L().cb_hits_compress(hp, rows, words, pp, cap, _stream(stream)))
 
 
-def hits_expand(packs, world: int, row_off, full, ok=None, stream=None, cap=None) -> None:
+def hits_expand(packs, world: int, row_off, full, cap: int, ok=None, stream=None) -> None:
     """full ([total_rows][words] int64 device tensor) := the OR of every
     rank's positions (packs: the all-gathered int32 [world * stride], stride
-    = cb_hits_pack_words of the largest shard). ok: optional int32 device
-    tensor, cleared to 0 when some rank's count exceeds cap (that rank's rows
-    are then zeros in full)."""
+    = cb_hits_pack_words of the largest shard, every pack compressed with this
+    same cap). ok: optional int32 device tensor, cleared to 0 when some rank's
+    count exceeds cap (that rank's rows are then zeros in full)."""
     total_rows, words = full.shape
     bounds = [int(x) for x in row_off] + [int(total_rows)]
     max_rows = max(bounds[r + 1] - bounds[r] for r in range(world))
-    if cap is None:
-        cap = int(packs.numel()) // world - 2 - 2 * _pack_blocks(max_rows * words)
+    if int(packs.numel()) < world * (2 + int(cap) + 2 * _pack_blocks(max_rows * words)):
+        raise ValueError("packs too small for world packs of the largest shard's stride")
     off = (ctypes.c_uint64 * world)(*bounds[:world])
     pp, k1 = _ptr_of(packs)
     fp, k2 = _ptr_of(full)
     op, k3 = _ptr_of(ok)
-    _raise(_L().cb_hits_expand(pp, world, cap, off, words, total_rows, fp, op, _stream(stream)))
+    _raise(_L().cb_hits_expand(pp, world, int(cap), off, words, total_rows, fp, op, _stream(stream)))
 
 
 def hits_expand_set(packs, world: int, row_off, n: int, full, cap: int, ok=None, stream=None) -> None:

@@ -158,11 +158,19 @@ hipError_t ensure_pad_zeroed(const cb_filter* cf, hipStream_t s) {
   return hipSuccess;
 }
 
+// The pending lazy clear, issued on s by whichever operation needs the words
+// first (readers may race: zero_mu makes the exchange, the memset and the
+// event that orders the host mirror's refresh after it one step).
 hipError_t ensure_zeroed(const cb_filter* cf, hipStream_t s) {
   cb_filter* f = const_cast<cb_filter*>(cf);
+  if (!f->needs_zero.load()) return hipSuccess;
+  std::lock_guard<std::mutex> lk(f->zero_mu);
   if (f->needs_zero.exchange(false)) {
     f->needs_pad_zero.store(false);
-    return hipMemsetAsync(f->words, 0, f->nwords_alloc * 4, s);
+    hipError_t e = hipMemsetAsync(f->words, 0, f->nwords_alloc * 4, s);
+    if (e == hipSuccess && !f->wev) e = hipEventCreateWithFlags(&f->wev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(f->wev, s);
+    return e;
   }
   return hipSuccess;
 }
@@ -289,7 +297,16 @@ int insert_locked(Workspace& ws, cb_filter* f, const uint8_t* keys, const uint64
     }
   }
   f->known_zero = false;
+  int mrc = mark_written(f, s);
+  if (mrc) return mrc;
   if (sk.staged) HIP_TRY(hipStreamSynchronize(s));
+  return CB_OK;
+}
+
+int mark_written(cb_filter* f, hipStream_t s) {
+  if (!f->wev) HIP_TRY(hipEventCreateWithFlags(&f->wev, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(f->wev, s));
+  f->gen.fetch_add(1, std::memory_order_acq_rel);
   return CB_OK;
 }
 
@@ -438,7 +455,7 @@ int set_probe_zero_copy(const cb_filterset* set, const uint8_t* keys, uint32_t k
   cb::KeySrc ks{(const uint8_t*)dk, nullptr, key_len};
   HIP_TRY(cb::launch_set_probe(keyk, set->mode, set->width, set->words, set->any, set->used, ks, n,
                                set->mp, zv, (uint64_t*)dh, (n + 63) / 64, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(hipStreamSynchronize(s));  // the table is no longer read: no reader event needed
   return CB_OK;
 }
 
@@ -470,6 +487,10 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
   HIP_TRY(cb::launch_set_probe(sk.keyk, set->mode, set->width, set->words, set->any, set->used,
                                sk.ks, n, set->mp, (gated && set->zgated) ? &zv : nullptr, dhits,
                                hwords, s));
+  if (gated && set->zgated) {
+    int zr = note_zone_read(set, s);
+    if (zr) return zr;
+  }
   g_last_path = 3;
   if (host_hits) {
     HIP_TRY(hipMemcpyAsync(hits, dhits, (size_t)set->used * hwords * 8, hipMemcpyDeviceToHost, s));
@@ -499,8 +520,8 @@ int set_probe_device(const cb_filterset* set, const uint8_t* keys, uint32_t key_
   if (!is_device_ptr(hits) || (key_len && !is_device_ptr(keys)) || (sink_pack && !is_device_ptr(sink_pack)))
     return fail(CB_EINVAL, "keys, hits and pack must be device memory");
   const uint64_t hwords = (n + 63) / 64;
-  if (sink_pack && (uint64_t)set->used * hwords * 64 > (1ull << 32))
-    return fail(CB_EINVAL, "used * ceil(n/64) * 64 must not exceed 2^32 (u32 positions)");
+  if (sink_pack && (uint64_t)set->used * hwords * 64 >= (1ull << 32))
+    return fail(CB_EINVAL, "used * ceil(n/64) * 64 must be below 2^32 (u32 positions and counts)");
   DeviceGuard dg(set->device);
   Workspace& ws = workspace(set->device, s);
   std::lock_guard<std::mutex> lk(ws.mu);
@@ -514,10 +535,26 @@ int set_probe_device(const cb_filterset* set, const uint8_t* keys, uint32_t key_
     if (rc) return rc;
     sink = cb::PackSink{sink_pack, cap, reinterpret_cast<unsigned long long*>(st->ctl), st->parity};
   }
-  HIP_TRY(cb::launch_set_probe(keyk, set->mode, set->width, set->words, set->any, set->used, ks, n, set->mp,
-                               (gated && set->zgated) ? &zv : nullptr, hits, hwords, s, sink_pack ? &sink : nullptr));
+  const hipError_t e = cb::launch_set_probe(keyk, set->mode, set->width, set->words, set->any, set->used, ks, n,
+                                            set->mp, (gated && set->zgated) ? &zv : nullptr, hits, hwords, s,
+                                            sink_pack ? &sink : nullptr);
+  if (e != hipSuccess) {
+    // the kernel may still have been queued (an earlier sticky error): clear
+    // both claim words behind it, so the next launch never reuses a dirty one
+    if (st) (void)hipMemsetAsync(st->ctl, 0, 16, s);
+    return hip_fail(e, "launch_set_probe");
+  }
   if (st) st->parity ^= 1u;  // the launch cleared the other claim word for the next one
   g_last_path = 3;
+  if (gated && set->zgated) return note_zone_read(set, s);
+  return CB_OK;
+}
+
+int note_zone_read(const cb_filterset* set, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(set->zmu);
+  hipEvent_t& ev = set->zread[s];
+  if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(ev, s));
   return CB_OK;
 }
 
@@ -561,12 +598,16 @@ int upload_zones(cb_filterset* set, hipStream_t s) {
   memcpy(tab.data() + cb_zone_hdr_bytes, pre, cb_zone_pre_bytes);
   if (!blob.empty()) memcpy(tab.data() + cb_zone_blob_off, blob.data(), blob.size());
   if (!set->zgated) return CB_OK;
-  // A gated probe queued on ANY stream may still read the old table: wait for
-  // the whole device before freeing or overwriting it (zone updates happen
-  // once per table flush, so a device-wide sync is cheap here).
-  HIP_TRY(hipDeviceSynchronize());
+  // A gated probe or fused read queued on another stream may still read the
+  // old table: wait for every stream's last reader (their events), not the
+  // whole device, before overwriting it. An outgrown table is retired, not
+  // freed (hipFree would synchronise the device), until cb_set_destroy.
+  {
+    std::lock_guard<std::mutex> lk(set->zmu);
+    for (auto& kv : set->zread) HIP_TRY(hipEventSynchronize(kv.second));
+  }
   if (tab.size() > set->zcap) {
-    if (set->zdev) (void)hipFree(set->zdev);
+    if (set->zdev) set->zretired.push_back(set->zdev);
     set->zdev = nullptr;
     set->zcap = 0;
     const size_t want = (tab.size() * 2 + 4095) & ~size_t(4095);
@@ -993,6 +1034,7 @@ int cb_filter_destroy(cb_filter* f) {
   {
     DeviceGuard dg(f->device);
     pool_release(f->device, f->words, f->words_cap);
+    if (f->wev) (void)hipEventDestroy(f->wev);
   }
   delete f;
   return CB_OK;
@@ -1027,6 +1069,22 @@ int cb_filter_clear(cb_filter* f, void* stream) {
   (void)stream;
   f->known_zero = true;
   f->needs_zero.store(true);
+  f->gen.fetch_add(1, std::memory_order_acq_rel);  // the mirror refresh sees needs_zero: all-zero words
+  return CB_OK;
+}
+
+int cb_filter_host_mirror(cb_filter* f, int mode) {
+  if (!f) return fail(CB_EINVAL, "null filter");
+  if (mode < -1 || mode > 1) return fail(CB_EINVAL, "mode must be -1 (auto), 0 (off) or 1 (on)");
+  f->mirror = mode;
+  return CB_OK;
+}
+
+int cb_filter_host_mirror_info(const cb_filter* f, int* on, int* current) {
+  if (!f) return fail(CB_EINVAL, "null filter");
+  if (on) *on = f->mirror == 1 || (f->mirror == -1 && f->m <= kMirrorAutoBits);
+  if (current)
+    *current = f->host_gen.load(std::memory_order_acquire) == f->gen.load(std::memory_order_acquire);
   return CB_OK;
 }
 
@@ -1052,9 +1110,59 @@ int cb_probe_var(const cb_filter* const* filters, uint32_t nf, const uint8_t* by
   return probe_impl(filters, nf, bytes, offsets, 0, n, hits, (hipStream_t)stream);
 }
 
+namespace {
+
+// Refresh the host mirror if a write happened since it was taken: wait for
+// the last write's event (on its own stream: no device-wide sync), then copy
+// the words back once. Readers race only on the flag (acquire/release).
+int refresh_mirror(const cb_filter* cf) {
+  cb_filter* f = const_cast<cb_filter*>(cf);
+  const uint64_t g = f->gen.load(std::memory_order_acquire);
+  if (f->host_gen.load(std::memory_order_acquire) == g) return CB_OK;
+  std::lock_guard<std::mutex> lk(f->host_mu);
+  const uint64_t g2 = f->gen.load(std::memory_order_acquire);
+  if (f->host_gen.load(std::memory_order_acquire) == g2) return CB_OK;
+  const uint64_t nw = (f->m + 31) / 32;
+  f->host.resize(nw);
+  {
+    std::lock_guard<std::mutex> zl(f->zero_mu);  // a racing reader's lazy clear is issued and recorded, or not yet
+    if (f->needs_zero.load()) {  // cleared, nothing on the device yet: all zero
+      std::fill(f->host.begin(), f->host.end(), 0u);
+    } else {
+      DeviceGuard dg(f->device);
+      if (f->wev) HIP_TRY(hipEventSynchronize(f->wev));
+      HIP_TRY(hipMemcpy(f->host.data(), f->words, nw * 4, hipMemcpyDeviceToHost));
+    }
+  }
+  f->host_gen.store(g2, std::memory_order_release);
+  return CB_OK;
+}
+
+// BloomFilter::hashes + may_contain (src/bloom.rs:26-37,48-51) on the mirror:
+// u64 wrapping x33 / x31 folds, h % m, and bit b read only when bit a is set.
+int mirror_contains(const cb_filter* f, const uint8_t* key, uint64_t len) {
+  uint64_t h1 = 5381, h2 = 0;
+  for (uint64_t i = 0; i < len; ++i) {
+    h1 = (h1 << 5) + h1 + key[i];
+    h2 = h2 * 31 + key[i];
+  }
+  const uint64_t a = h1 % f->m, b = h2 % f->m;
+  const uint32_t* w = f->host.data();
+  return ((w[a >> 5] >> (a & 31)) & 1u) && ((w[b >> 5] >> (b & 31)) & 1u);
+}
+
+}  // namespace
+
 int cb_may_contain(const cb_filter* f, const uint8_t* key, uint64_t len, int* out) {
   if (!f || !out || (!key && len)) return fail(CB_EINVAL, "null argument");
   if (f->m == 0) return fail(CB_EZEROM, "attempt to calculate the remainder with a divisor of zero");
+  if (f->mirror == 1 || (f->mirror == -1 && f->m <= kMirrorAutoBits)) {
+    int rc = refresh_mirror(f);
+    if (rc) return rc;
+    *out = mirror_contains(f, key, len);
+    g_last_path = 5;
+    return CB_OK;
+  }
   uint64_t offs[2] = {0, len};
   uint64_t hit = 0;
   const cb_filter* fs[1] = {f};
@@ -1104,7 +1212,7 @@ int cb_filter_import_bools(cb_filter* f, const uint8_t* in, uint64_t m, void* st
   if (f->needs_zero.exchange(false)) f->needs_pad_zero.store(true);
   HIP_TRY(ensure_pad_zeroed(f, s));  // every word < ceil(m/32) was rewritten
   f->known_zero = false;
-  return CB_OK;
+  return mark_written(f, s);
 }
 
 int cb_filter_export_packed(const cb_filter* f, uint32_t* out, void* stream) {
@@ -1138,7 +1246,7 @@ int cb_filter_import_packed(cb_filter* f, const uint32_t* in, uint64_t nwords, v
   HIP_TRY(ensure_pad_zeroed(f, s));
   if (!dev) HIP_TRY(hipStreamSynchronize(s));
   f->known_zero = false;
-  return CB_OK;
+  return mark_written(f, s);
 }
 
 int cb_filter_to_bytes(const cb_filter* f, uint8_t* out, uint64_t cap, uint64_t* len_out) {
@@ -1390,6 +1498,8 @@ int cb_set_destroy(cb_filterset* set) {
     if (set->words) (void)hipFree(set->words);
     if (set->any) (void)hipFree(set->any);
     if (set->zdev) (void)hipFree(set->zdev);
+    for (void* z : set->zretired) (void)hipFree(z);
+    for (auto& kv : set->zread) (void)hipEventDestroy(kv.second);
   }
   delete set;
   return CB_OK;
@@ -1645,8 +1755,11 @@ int cb_filter_insert_fixed_many(cb_filter* const* filters, uint32_t nf, const ui
     HIP_TRY(ws.ent.reserve(cb::build_ent_bytes(p) * nb, s));
     HIP_TRY(cb::launch_build_batch(keyk, f0->mode, bb, nb, f0->mp, p, (uint32_t*)ws.seg.p,
                                    (uint32_t*)ws.ent.p, s));
-    for (uint32_t j = 0; j < nb; ++j)
+    for (uint32_t j = 0; j < nb; ++j) {
       if (n[b0 + j]) filters[b0 + j]->known_zero = false;
+      int rc = mark_written(filters[b0 + j], s);
+      if (rc) return rc;
+    }
   }
   g_last_path = PATH_TILED;
   if (staged) HIP_TRY(hipStreamSynchronize(s));

@@ -40,7 +40,22 @@ struct cb_filter {
   std::atomic<bool> needs_pad_zero{false};
   int mode = 0;
   cb::ModP mp{};
+  // Host mirror of the packed words for single-key may_contain (DESIGN §2,
+  // SURVEY §7 hard part 8): a per-key GPU round trip costs ~10 us, a host
+  // probe of the mirror two word loads. Every write to `words` bumps `gen`
+  // and records `wev` on its stream; the first cb_may_contain after a write
+  // waits for that event and copies ceil(m/32) words back once (128 B at the
+  // product's m = 1024), later ones read the mirror.
+  std::atomic<uint64_t> gen{1};       // bumped by every write to words
+  std::atomic<uint64_t> host_gen{0};  // the gen `host` holds
+  std::mutex host_mu;                 // one refresh at a time
+  std::mutex zero_mu;                 // the lazy clear's issue vs. a refresh (capi.cpp ensure_zeroed)
+  std::vector<uint32_t> host;         // ceil(m/32) words
+  hipEvent_t wev = nullptr;           // recorded after the last device write
+  int mirror = -1;                    // -1 auto (m <= kMirrorAutoBits), 0 off, 1 on
 };
+
+constexpr uint64_t kMirrorAutoBits = 1ull << 28;  // auto mirror up to 32 MiB of host words
 
 struct cb_filterset {
   uint64_t m = 0;
@@ -59,6 +74,13 @@ struct cb_filterset {
   void* zdev = nullptr;
   size_t zcap = 0;
   uint64_t zgated = 0;  // slots with both bounds
+  // Readers of the device zone table: one event per stream, recorded after
+  // every launch that reads it (gated probes, the fused read path). A zone
+  // update waits for these events — the streams' last readers — instead of
+  // the whole device, then rewrites the table (capi.cpp upload_zones).
+  mutable std::mutex zmu;
+  mutable std::map<hipStream_t, hipEvent_t> zread;
+  std::vector<void*> zretired;  // outgrown tables, freed by cb_set_destroy
 };
 
 // The device zone table of a set (capi.cpp upload_zones): 64 cb::ZoneView
@@ -168,6 +190,9 @@ int compress_state(Workspace& ws, hipStream_t s, cb::CompressState** out);
 int set_probe_device(const cb_filterset* set, const uint8_t* keys, uint32_t key_len, uint64_t n, bool gated,
                      uint64_t* hits, uint32_t* sink_pack, uint64_t cap, hipStream_t s);
 
+// A launch that reads set's device zone table was enqueued on s (capi.cpp).
+int note_zone_read(const cb_filterset* set, hipStream_t s);
+
 // Device-accessible memory (hipMalloc, managed) is used in place; anything
 // else (pageable or pinned host memory) is staged by the library.
 bool is_device_ptr(const void* p);
@@ -199,6 +224,9 @@ int insert_locked(Workspace& ws, cb_filter* f, const uint8_t* keys, const uint64
                   uint32_t key_len, uint64_t n, hipStream_t s);
 // Host bytes into an output buffer that may be host or device memory.
 int put_bytes(uint8_t* dst, const void* src, size_t n);
+// A write to f's words was enqueued on s (build, import): the host mirror is
+// stale from here, and its refresh waits for this point of s.
+int mark_written(cb_filter* f, hipStream_t s);
 
 // Device output: used in place when device-resident, else a workspace buffer
 // copied back at the end.

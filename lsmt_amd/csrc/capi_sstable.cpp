@@ -134,6 +134,7 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
     HIP_TRY(cb::launch_set_get_many(sk.keyk, set->mode, set->width, set->words, set->mp,
                                     set->zgated ? &zv : nullptr, dviews, nt, drows, sk.ks, n, dwhich,
                                     (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, tsum, s));
+    if (set->zgated && (rc = note_zone_read(set, s))) return rc;
   } else {
     HIP_TRY(cb::launch_get_many(sk.keyk, dviews, nt, dhits, drows, hwords, sk.ks, n, dwhich,
                                 (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, tsum, s));
@@ -415,29 +416,14 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   }
   if (!sorted) {
     // stable sort by key (memtable flushes arrive sorted and skip this)
-    HIP_TRY(ws.f_sk.reserve(n * sizeof(cb::SortKey), s));
     HIP_TRY(ws.f_sk2.reserve(n * sizeof(cb::SortKey), s));
-    cb::SortKey* a0 = (cb::SortKey*)ws.f_sk.p;
     cb::SortKey* a1 = (cb::SortKey*)ws.f_sk2.p;
-    static const bool use_rocprim = [] {
-      const char* v = getenv("CB_SORT");
-      return v && std::strcmp(v, "rocprim") == 0;
-    }();
-    if (use_rocprim) {  // rocPRIM's merge sort, for comparison (same order)
-      HIP_TRY(cb::launch_sort_keys(dk, dko, n, a0, s));
-      size_t tmp_bytes = 0;
-      HIP_TRY(cb::entry_sort(nullptr, tmp_bytes, a0, a1, n, dk, dko, s));
-      HIP_TRY(ws.f_sort.reserve(tmp_bytes + 16, s));
-      HIP_TRY(cb::entry_sort(ws.f_sort.p, tmp_bytes, a0, a1, n, dk, dko, s));
-      HIP_TRY(cb::launch_line_sums(a1, dko, dvo, n, tsum, s));
-    } else {
-      // records built inside the block sort; the last round also leaves the
-      // value spans and the line tiles in sorted order for k_format
-      HIP_TRY(ws.f_sort.reserve(cb::entry_sort_tmp_bytes(n), s));
-      HIP_TRY(ws.f_vsp.reserve(n * sizeof(ulonglong2), s));
-      vsp = (ulonglong2*)ws.f_vsp.p;
-      HIP_TRY(cb::launch_entry_sort(nullptr, a1, (cb::SortKey*)ws.f_sort.p, n, dk, dko, s, dvo, vsp, tsum));
-    }
+    // records built inside the block sort; the last round also leaves the
+    // value spans and the line tiles in sorted order for k_format
+    HIP_TRY(ws.f_sort.reserve(cb::entry_sort_tmp_bytes(n), s));
+    HIP_TRY(ws.f_vsp.reserve(n * sizeof(ulonglong2), s));
+    vsp = (ulonglong2*)ws.f_vsp.p;
+    HIP_TRY(cb::launch_entry_sort(nullptr, a1, (cb::SortKey*)ws.f_sort.p, n, dk, dko, s, dvo, vsp, tsum));
     order = a1;
   }
   HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));

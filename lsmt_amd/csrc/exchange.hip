@@ -205,7 +205,13 @@ hipError_t launch_hits_compress(const uint64_t* hits, uint64_t rows, uint64_t wo
   hipLaunchKernelGGL(k_hits_compress, dim3(g), dim3(kCT), 0, s, hits, nw, pack, cap,
                      reinterpret_cast<unsigned long long*>(st.ctl), st.parity);
   const hipError_t e = hipGetLastError();
-  if (e == hipSuccess) st.parity ^= 1u;  // the launch cleared the other pair for the next one
+  if (e == hipSuccess) {
+    st.parity ^= 1u;  // the launch cleared the other pair for the next one
+  } else {
+    // the kernel may still have been queued (an earlier sticky error): clear
+    // both claim words behind it, so the next launch never reuses a dirty one
+    (void)hipMemsetAsync(st.ctl, 0, 16, s);
+  }
   return e;
 }
 
@@ -248,7 +254,7 @@ hipError_t launch_hits_expand_blocks(const uint32_t* packs, uint32_t nranks, uin
   for (uint32_t r = 0; r < nranks; ++r) {
     const uint64_t end = r + 1 < nranks ? rr.row_off[r + 1] : total_rows;
     // a rank's rows fit one workgroup's chunk, and its positions fit 32 bits
-    if (end < rr.row_off[r] || end - rr.row_off[r] > kBlkRows || (end - rr.row_off[r]) * hwords * 64 > (1ull << 32))
+    if (end < rr.row_off[r] || end - rr.row_off[r] > kBlkRows || (end - rr.row_off[r]) * hwords * 64 >= (1ull << 32))
       return hipErrorInvalidValue;
     plan.row_off[r] = rr.row_off[r];
   }

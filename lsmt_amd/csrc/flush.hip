@@ -11,7 +11,6 @@
 // exclusive scan gives every line's offset and one lane formats each line.
 #include <hip/hip_runtime.h>
 
-#include <rocprim/device/device_merge_sort.hpp>
 
 #include "blockscan.hpp"
 #include "flush.hpp"
@@ -126,20 +125,6 @@ __global__ __launch_bounds__(kNT) void k_sorted_check(const uint8_t* __restrict_
   if (__syncthreads_or(bad) && threadIdx.x == 0 && *(volatile uint32_t*)ok) atomicAnd(ok, 0u);
 }
 
-// Rust str order on the records: the 16-byte zero-padded prefixes, then (when
-// either key fits in 16 bytes) the length, else the bytes past 16. Equal keys
-// compare equal, so the merge sort's stability keeps their input order.
-struct KeyLess {
-  const uint8_t* kb;
-  const uint64_t* ko;
-  __device__ bool operator()(const SortKey& a, const SortKey& b) const {
-    if (a.w0 != b.w0) return a.w0 < b.w0;
-    if (a.w1 != b.w1) return a.w1 < b.w1;
-    if (a.len <= 16 || b.len <= 16) return a.len < b.len;
-    const uint64_t al = ko[a.idx + 1] - ko[a.idx], bl = ko[b.idx + 1] - ko[b.idx];
-    return bytes_cmp(kb + ko[a.idx] + 16, al - 16, kb + ko[b.idx] + 16, bl - 16) < 0;
-  }
-};
 
 
 // One bound of the ZoneMap (the file's first or last key, w = 0 / 1) into r:
@@ -501,12 +486,6 @@ hipError_t launch_line_sums(const SortKey* order, const uint64_t* ko, const uint
   return hipGetLastError();
 }
 
-hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* out, uint64_t n,
-                      const uint8_t* kb, const uint64_t* ko, hipStream_t s) {
-  if (!tmp) return rocprim::merge_sort(tmp, tmp_bytes, in, out, (size_t)n, KeyLess{kb, ko}, s);
-  ProfScope ps("rocprim_merge_sort", s);
-  return rocprim::merge_sort(tmp, tmp_bytes, in, out, (size_t)n, KeyLess{kb, ko}, s);
-}
 
 
 

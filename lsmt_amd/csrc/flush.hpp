@@ -91,10 +91,6 @@ uint64_t entry_sort_tmp_bytes(uint64_t n);
 hipError_t launch_entry_sort(const SortKey* in, SortKey* out, SortKey* tmp, uint64_t n, const uint8_t* kb,
                              const uint64_t* ko, hipStream_t s, const uint64_t* vo = nullptr,
                              ulonglong2* vsp = nullptr, uint64_t* tsum = nullptr);
-// The same order through rocPRIM's merge sort (kept for comparison,
-// CB_SORT=rocprim). tmp == nullptr: only writes the scratch size to tmp_bytes.
-hipError_t entry_sort(void* tmp, size_t& tmp_bytes, const SortKey* in, SortKey* out, uint64_t n,
-                      const uint8_t* kb, const uint64_t* ko, hipStream_t s);
 // The file (lines at the offsets tsum and the line lengths give, then 16
 // zero bytes of slack), its
 // line index without re-reading it (sstable.hpp layout: entry p is line p),

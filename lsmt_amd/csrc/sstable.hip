@@ -16,9 +16,6 @@
 #include <cstddef>
 #include <cstdlib>
 #include <cstring>
-#include <rocprim/device/device_scan.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "blockscan.hpp"
 #include "profile.hpp"
@@ -331,11 +328,6 @@ __global__ __launch_bounds__(kNT) void k_rebuild_gather(const uint8_t* __restric
 
 // ---- exclusive scan of uint64: one rocPRIM look-back scan over n + 1 items
 // (the last reads as 0, so out[n] = total) ----
-struct TailZero {
-  const uint64_t* in;
-  uint64_t n;
-  __host__ __device__ uint64_t operator()(uint64_t p) const { return p < n ? in[p] : 0; }
-};
 
 // ---- search ----
 
@@ -1007,24 +999,62 @@ hipError_t launch_rebuild_gather(const uint8_t* data, const LineRec* rec, uint64
   return hipGetLastError();
 }
 
-static hipError_t scan_u64(void* tmp, size_t& bytes, const uint64_t* in, uint64_t* out, uint64_t n,
-                           hipStream_t s) {
-  auto it = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint64_t>(0), TailZero{in, n});
-  return rocprim::exclusive_scan(tmp, bytes, it, out, (uint64_t)0, (size_t)n + 1,
-                                 rocprim::plus<uint64_t>(), s);
+// Exclusive scan of n uint64 (out[n] = total) in three launches: each block
+// of 4096 values reduces to one partial, k_tile_scan scans the partials in
+// place (and writes the total to out[n]), and each block rescans its values
+// from its partial. 16 B of traffic per value; used by the line index
+// (per-4-KiB-block line counts) and SsTable::load's rebuild (per-line flags
+// and key lengths).
+constexpr uint64_t kScanPer = 4, kScanChunk = 1024 * kScanPer;
+
+__global__ __launch_bounds__(1024) void k_scan_reduce(const uint64_t* __restrict__ in, uint64_t n,
+                                                      uint64_t* __restrict__ part) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * kScanChunk + threadIdx.x * kScanPer;
+  uint64_t sum = 0;
+#pragma unroll
+  for (uint64_t j = 0; j < kScanPer; ++j) sum += i0 + j < n ? in[i0 + j] : 0;
+  uint64_t total;
+  (void)block_scan<1024>(sum, &total);
+  if (threadIdx.x == 0) part[blockIdx.x] = total;
 }
 
-uint64_t scan_tmp_words(uint64_t n) {
-  size_t bytes = 0;
-  (void)scan_u64(nullptr, bytes, nullptr, nullptr, n, 0);
-  return bytes / 8 + 1;
+__global__ __launch_bounds__(1024) void k_scan_apply(const uint64_t* __restrict__ in, uint64_t n,
+                                                     const uint64_t* __restrict__ part,
+                                                     uint64_t* __restrict__ out) {
+  const uint64_t i0 = (uint64_t)blockIdx.x * kScanChunk + threadIdx.x * kScanPer;
+  uint64_t v[kScanPer], sum = 0;
+#pragma unroll
+  for (uint64_t j = 0; j < kScanPer; ++j) {
+    v[j] = i0 + j < n ? in[i0 + j] : 0;
+    sum += v[j];
+  }
+  const uint64_t base = part[blockIdx.x];
+  uint64_t total;
+  uint64_t p = base + block_scan<1024>(sum, &total);
+#pragma unroll
+  for (uint64_t j = 0; j < kScanPer; ++j) {
+    if (i0 + j < n) out[i0 + j] = p;
+    p += v[j];
+  }
 }
+
+uint64_t scan_tmp_words(uint64_t n) { return (n + kScanChunk - 1) / kScanChunk + 1; }
 
 hipError_t launch_scan_u64(const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* tmp,
                            hipStream_t s) {
-  size_t bytes = scan_tmp_words(n) * 8;
-  ProfScope ps("k_scan_u64", s);
-  return scan_u64(tmp, bytes, in, out, n, s);
+  if (!n) return hipMemsetAsync(out, 0, 8, s);
+  const uint64_t nb = (n + kScanChunk - 1) / kScanChunk;
+  {
+    ProfScope ps("k_scan_reduce", s);
+    hipLaunchKernelGGL(k_scan_reduce, dim3((uint32_t)nb), dim3(1024), 0, s, in, n, tmp);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = launch_tile_scan(tmp, nb, out + n, s);
+  if (e != hipSuccess) return e;
+  ProfScope ps("k_scan_apply", s);
+  hipLaunchKernelGGL(k_scan_apply, dim3((uint32_t)nb), dim3(1024), 0, s, in, n, tmp, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_table_search(int keyk, const TableView& t, const KeySrc& ks, uint64_t n,

@@ -5,16 +5,15 @@ Every rank holds a contiguous subset of the SSTable filters (Database::get's
 tables, /root/reference/src/lib.rs:129-134) and probes the full, replicated
 key batch against it, producing hit rows [F_local][ceil(n/64)]. Because the
 layout is filter-major, rank r's rows are one contiguous slice of the global
-[F][ceil(n/64)] bitmap, so the exchange is a plain concatenation:
-``all_gather_into_tensor`` over RCCL/xGMI on GPUs (gloo on CPU in the tests).
-Uneven shards are padded to the largest shard and sliced back.
-
-The rows are sparse at BASELINE densities (one table per present key, false
-positives ~(1.55 %)^2 per (key, table)), so ``gather_hits_sparse`` ships each
-rank's set-bit positions instead (cb_hits_compress -> all-gather of fixed-size
-packs -> cb_hits_expand) and rebuilds the identical map; if any rank has more
-set bits than the pack holds, every rank sees that in the gathered counts and
-all of them take the dense path for that step.
+[F][ceil(n/64)] bitmap, so the exchange is a plain concatenation. The
+exchange itself is the C ABI's (lsmt_amd/csrc/comm.cpp: cb_hits_allgather,
+cb_set_probe_allgather_fixed): dense rows, or at BASELINE densities the
+set-bit positions of each rank's rows (fixed-size packs) expanded back into
+the identical map, with a dense redo on every rank when some rank's pack
+overflows. ``Comm`` binds it over one of three transports: RCCL (one process
+per GPU, the product path), loopback (every rank in one process, one thread
+per rank: tests at world > 1 on one GPU) and a caller-supplied host
+all-gather (``Comm.host``: e.g. gloo between processes sharing one GPU).
 """
 from __future__ import annotations
 
@@ -26,37 +25,6 @@ def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
     base, extra = divmod(n_total, world)
     lo = rank * base + min(rank, extra)
     return lo, lo + base + (1 if rank < extra else 0)
-
-
-def gather_hits(local_hits, n_total: int, group=None, out=None):
-    """All-gather every rank's hit rows into the global [n_total][words] bitmap
-    (rows in global filter order). local_hits: [F_local][words] int64 tensor."""
-    import torch
-    import torch.distributed as dist
-
-    world = dist.get_world_size(group)
-    rows = max(shard_range(n_total, world, r)[1] - shard_range(n_total, world, r)[0] for r in range(world))
-    words = local_hits.shape[1]
-    even = all(shard_range(n_total, world, r)[1] - shard_range(n_total, world, r)[0] == rows
-               for r in range(world))
-    if even:
-        full = out if out is not None else torch.empty((n_total, words), dtype=local_hits.dtype,
-                                                       device=local_hits.device)
-        dist.all_gather_into_tensor(full, local_hits.contiguous(), group=group)
-        return full
-    pad = torch.zeros((rows, words), dtype=local_hits.dtype, device=local_hits.device)
-    pad[: local_hits.shape[0]] = local_hits
-    buf = torch.empty((world * rows, words), dtype=local_hits.dtype, device=local_hits.device)
-    dist.all_gather_into_tensor(buf, pad, group=group)
-    parts = []
-    for r in range(world):
-        lo, hi = shard_range(n_total, world, r)
-        parts.append(buf[r * rows: r * rows + (hi - lo)])
-    full = torch.cat(parts, 0)
-    if out is not None:
-        out.copy_(full)
-        return out
-    return full
 
 
 def sparse_cap(n_keys: int, f_total: int, world: int) -> int:
@@ -80,50 +48,6 @@ def pack_words(nw: int, cap: int) -> int:
     return 2 + cap + 2 * -(-nw // PACK_BLOCK_WORDS)
 
 
-def gather_hits_sparse(local_hits, n_total: int, cap: int, compress, expand, group=None, out=None,
-                       stats=None, ok=None):
-    """Same result as gather_hits; cap must be equal on every rank
-    (sparse_cap). compress(local_hits, pack, cap) fills an int32 pack of
-    pack_words(largest shard's words, cap) {count, 0, positions, directory};
-    expand(packs, world, row_off, full, ok, cap) rebuilds the global map
-    (lsmt_amd.hits_compress / hits_expand on GPUs).
-
-    Synchronous (ok=None): the gathered counts are read on the host; if some
-    rank overflowed (the same decision on every rank) all ranks then run the
-    dense all-gather, so the result is always complete. stats (a dict,
-    optional) receives "sparse" (whether the packs sufficed) and "max_count".
-
-    Asynchronous (ok = an int32 device tensor holding 1): no host round trip;
-    expand clears ok if some rank overflowed, and the caller must check ok
-    before using the map and redo that batch with gather_hits if it is 0."""
-    import torch
-    import torch.distributed as dist
-
-    world = dist.get_world_size(group)
-    words = local_hits.shape[1]
-    stride = pack_words(-(-n_total // world) * words, cap)  # the largest shard's pack, on every rank
-    pack = torch.zeros(stride, dtype=torch.int32, device=local_hits.device)
-    compress(local_hits, pack, cap)
-    packs = torch.empty(world * stride, dtype=torch.int32, device=local_hits.device)
-    dist.all_gather_into_tensor(packs, pack, group=group)
-    row_off = [shard_range(n_total, world, r)[0] for r in range(world)]
-    if ok is not None:
-        full = out if out is not None else torch.empty((n_total, words), dtype=local_hits.dtype,
-                                                       device=local_hits.device)
-        expand(packs, world, row_off, full, ok, cap)
-        return full
-    counts = packs.view(world, stride)[:, 0].cpu().numpy().astype("int64") & 0xFFFFFFFF
-    if stats is not None:
-        stats["sparse"] = bool((counts <= cap).all())
-        stats["max_count"] = int(counts.max())
-    if (counts > cap).any():
-        return gather_hits(local_hits, n_total, group=group, out=out)
-    full = out if out is not None else torch.empty((n_total, words), dtype=local_hits.dtype,
-                                                   device=local_hits.device)
-    expand(packs, world, row_off, full, None, cap)
-    return full
-
-
 def comm_shard(n_total: int, world: int, rank: int) -> tuple[int, int]:
     """The C ABI's split (cb_comm_shard): must equal shard_range."""
     import ctypes
@@ -135,13 +59,18 @@ def comm_shard(n_total: int, world: int, rank: int) -> tuple[int, int]:
 
 
 class Comm:
-    """An RCCL communicator of the C ABI (cb_comm, lsmt_amd/csrc/comm.cpp):
-    the exchange a Rust ``Database::get`` would call over ``extern "C"``
-    (INTEGRATION.md), driven here from Python. One process per GPU.
+    """A communicator of the C ABI (cb_comm, lsmt_amd/csrc/comm.cpp): the
+    exchange a Rust ``Database::get`` would call over ``extern "C"``
+    (INTEGRATION.md), driven here from Python. One process per GPU, ONE
+    communicator per rank (pipelined lanes on several streams share it; the
+    library runs its collectives in issue order).
 
-    ``Comm.from_process_group(device)`` makes the 128-byte id on rank 0 and
-    hands it to the other ranks over the torch.distributed group (any
-    channel works: it is only bytes)."""
+    ``Comm.from_process_group(device)`` makes the 128-byte RCCL id on rank 0
+    and hands it to the other ranks over the torch.distributed group (any
+    channel works: it is only bytes). ``Comm.loopback(world, device)`` gives
+    `world` ranks in this process (drive each from its own thread);
+    ``Comm.host(rank, world, device, allgather)`` moves the bytes with a
+    Python all-gather of host buffers."""
 
     def __init__(self, rank: int, world: int, device: int, uid: bytes):
         import ctypes
@@ -154,6 +83,63 @@ class Comm:
         buf = (ctypes.c_uint8 * len(uid)).from_buffer_copy(uid)
         _lib.check(self._L.cb_comm_init(rank, world, ctypes.addressof(buf), device, ctypes.byref(self._h)))
         self.rank, self.world, self.device = rank, world, device
+        self._keep = None
+
+    @classmethod
+    def _adopt(cls, handle: int, keep=None) -> "Comm":
+        import ctypes
+
+        from . import _lib
+        c = cls.__new__(cls)
+        c._L = _lib.load()
+        c._h = ctypes.c_void_p(handle)
+        r, w, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.check(c._L.cb_comm_info(c._h, ctypes.byref(r), ctypes.byref(w), ctypes.byref(d)))
+        c.rank, c.world, c.device = r.value, w.value, d.value
+        c._keep = keep
+        return c
+
+    @classmethod
+    def loopback(cls, world: int, device: int = 0) -> "list[Comm]":
+        """`world` ranks in this process on `device` (cb_comm_init_loopback).
+        Rank r's collectives must run on a thread of its own, concurrently
+        with the other ranks' (each call returns when every rank made it)."""
+        import ctypes
+
+        from . import _lib
+        arr = (ctypes.c_void_p * world)()
+        _lib.check(_lib.load().cb_comm_init_loopback(world, device, arr))
+        return [cls._adopt(arr[r]) for r in range(world)]
+
+    @classmethod
+    def host(cls, rank: int, world: int, device: int, allgather) -> "Comm":
+        """A communicator whose bytes move through `allgather(send: bytes-like
+        numpy uint8 array, recv: numpy uint8 array of world * len(send))`, a
+        host-side all-gather the caller provides (cb_comm_init_host)."""
+        import ctypes
+
+        import numpy as np
+
+        from . import _lib
+
+        def cb(user, send, recv, nbytes):
+            try:
+                n = int(nbytes)
+                s = np.ctypeslib.as_array((ctypes.c_uint8 * max(n, 1)).from_address(send))[:n] if n else \
+                    np.zeros(0, np.uint8)
+                r = np.ctypeslib.as_array((ctypes.c_uint8 * max(n * world, 1)).from_address(recv))[:n * world] \
+                    if n else np.zeros(0, np.uint8)
+                allgather(s, r)
+                return 0
+            except Exception:  # reported to the library as a failed transport
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        fn = _lib.HOST_ALLGATHER_FN(cb)
+        h = ctypes.c_void_p()
+        _lib.check(_lib.load().cb_comm_init_host(rank, world, device, fn, None, ctypes.byref(h)))
+        return cls._adopt(h.value, keep=fn)
 
     @staticmethod
     def unique_id() -> bytes:
@@ -188,10 +174,10 @@ class Comm:
         """out ([n_total][words] int64 device tensor) := every rank's hit rows
         (cb_hits_allgather). local_hits: this rank's [rows][words] slice
         (rows = its shard_range of n_total). sparse: compress -> all-gather of
-        (2 + cap)-word packs -> expand; with ok=None an overflow is detected
-        on the host and the batch redone densely, with ok (an int32 device
-        tensor holding 1) it is reported there instead. Returns whether the
-        map came from the packs."""
+        fixed-size packs -> expand; with ok=None an overflow is detected on
+        the host and the batch redone densely, with ok (an int32 device tensor
+        holding 1) it is reported there instead. Returns whether the map came
+        from the packs."""
         import ctypes
 
         from . import _lib

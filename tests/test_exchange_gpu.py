@@ -60,7 +60,7 @@ def test_compress_matches_numpy(gpu, rows, words, density):
         h = np.packbits(bits, bitorder="little").view(np.uint64).reshape(rows, words)
         cap = int(bits.sum()) + 5
         pack = torch.full((2 + cap + 2 * (-(-h.size // PACK_BLOCK_WORDS)),), -1, dtype=torch.int32, device="cuda")
-        gpu.hits_compress(torch.from_numpy(h.view(np.int64).copy()).cuda(), pack)
+        gpu.hits_compress(torch.from_numpy(h.view(np.int64).copy()).cuda(), pack, cap)
         check_pack(pack.cpu().numpy().view(np.uint32), h, cap)
 
 
@@ -105,12 +105,12 @@ def test_expand_rebuilds_map(gpu, sizes):
     row_off = list(np.cumsum([0] + sizes[:-1]))
     full = torch.full(dense.shape, -1, dtype=torch.int64, device="cuda")
     ok = torch.ones(1, dtype=torch.int32, device="cuda")
-    gpu.hits_expand(packs, len(sizes), row_off, full, ok=ok)
+    gpu.hits_expand(packs, len(sizes), row_off, full, cap, ok=ok)
     assert np.array_equal(full.cpu().numpy().view(np.uint64), dense) and int(ok.item()) == 1
     # rank 0's count beyond cap: ok cleared, its rows zero, the others intact
     bad = packs.clone()
     bad[0] = cap + 1
-    gpu.hits_expand(bad, len(sizes), row_off, full, ok=ok)
+    gpu.hits_expand(bad, len(sizes), row_off, full, cap, ok=ok)
     got = full.cpu().numpy().view(np.uint64)
     assert int(ok.item()) == 0 and not got[:sizes[0]].any()
     assert np.array_equal(got[sizes[0]:], dense[sizes[0]:])

@@ -248,3 +248,49 @@ def test_zone_gate_fixed16_bound_lengths(gpu, width):
     exp = oracle.probe_gated(refs, [oracle.OracleZone(lo, hi) for lo, hi in zones], d, offs)
     assert np.array_equal(got, exp)
     assert int(np.unpackbits(exp.view(np.uint8)).sum()) > 0
+
+
+def test_zone_update_waits_for_gated_probes_on_other_streams(gpu):
+    """A zone update while gated probes (and the fused read path's gate) are
+    still queued on other streams: the update waits for those streams' last
+    readers (per-stream events, no device-wide sync), so the queued probes see
+    the old zones and the probes after it the new ones, bit-exact."""
+    import torch
+    m = 1 << 22
+    nt = 6
+    g = workload.zone_tables(nt, 4000, 60_000)
+    fs, refs = [], []
+    for t in g:
+        b = gpu.BloomFilter(m)
+        b.insert_batch(t)
+        fs.append(b)
+        o = oracle.OracleFilter(m)
+        o.insert_fixed(t)
+        refs.append(o)
+    s = gpu.FilterSet.from_filters(fs)
+    full = [(bytes(min(bytes(r) for r in t)), bytes(max(bytes(r) for r in t))) for t in g]
+    narrow = []
+    for t in g:
+        srt = sorted(bytes(r) for r in t)
+        narrow.append((srt[len(srt) // 3], srt[2 * len(srt) // 3]))
+    for i, z in enumerate(full):
+        s.set_zone(i, z)
+    lk = workload.zone_lookups(g, 1 << 20)
+    dk = torch.from_numpy(lk).cuda()
+    d = np.ascontiguousarray(lk.reshape(-1))
+    offs = np.arange(0, 16 * (len(lk) + 1), 16, dtype=np.uint64)
+    exp_full = oracle.probe_gated(refs, [oracle.OracleZone(lo, hi) for lo, hi in full], d, offs)
+    exp_narrow = oracle.probe_gated(refs, [oracle.OracleZone(lo, hi) for lo, hi in narrow], d, offs)
+    assert not np.array_equal(exp_full, exp_narrow)
+    words = (len(lk) + 63) // 64
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    before = [torch.zeros((nt, words), dtype=torch.int64, device="cuda") for _ in range(3 * 4)]
+    for i, out in enumerate(before):  # queue a dozen gated probes on three other streams
+        s.probe(gpu.DeviceKeys(dk), out=out, stream=streams[i % 3], gated=True)
+    for i, z in enumerate(narrow):  # update while they are queued or running
+        s.set_zone(i, z)
+    after = s.probe(lk, gated=True)
+    torch.cuda.synchronize()
+    for out in before:
+        assert np.array_equal(out.cpu().numpy().view(np.uint64), exp_full)
+    assert np.array_equal(after, exp_narrow)

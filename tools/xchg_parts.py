@@ -1,5 +1,5 @@
 """Time the pieces of the sparse hit-bitmap exchange (lsmt_amd/shard.py
-gather_hits_sparse) on one GPU at the per-rank shape of C3 on 8 GPUs: a
+cb_hits_allgather) on one GPU at the per-rank shape of C3 on 8 GPUs: a
 [32][16384] rank slice holding ~66K set bits, 8 packs of that size to expand
 into the [256][16384] global map. Prints one JSON line of microseconds per
 piece (HIP events, median of 50), and the whole C-ABI exchange
@@ -14,7 +14,7 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import lsmt_amd  # noqa: E402
-from lsmt_amd.shard import sparse_cap  # noqa: E402
+from lsmt_amd.shard import pack_words, sparse_cap  # noqa: E402
 
 
 def timed(fn, reps=50):
@@ -41,19 +41,20 @@ def main():
     bits[rng.choice(bits.size, 66_000, replace=False)] = 1
     h = torch.from_numpy(np.packbits(bits, bitorder="little").view(np.int64).reshape(rows, words).copy()).to(dev)
     cap = sparse_cap(1 << 20, rows * world, world)
-    pack = torch.empty(2 + cap, dtype=torch.int32, device=dev)
-    packs = torch.empty(world * (2 + cap), dtype=torch.int32, device=dev)
+    stride = pack_words(rows * words, cap)
+    pack = torch.empty(stride, dtype=torch.int32, device=dev)
+    packs = torch.empty(world * stride, dtype=torch.int32, device=dev)
     full = torch.empty((rows * world, words), dtype=torch.int64, device=dev)
-    lsmt_amd.hits_compress(h, pack)
+    lsmt_amd.hits_compress(h, pack, cap)
     for r in range(world):
-        packs[r * (2 + cap):(r + 1) * (2 + cap)] = pack
+        packs[r * stride:(r + 1) * stride] = pack
     row_off = [r * rows for r in range(world)]
     out = {"cap": cap, "bits_per_rank": int(bits.sum())}
-    out["compress_us"] = timed(lambda: lsmt_amd.hits_compress(h, pack))
-    out["expand_8_ranks_us"] = timed(lambda: lsmt_amd.hits_expand(packs, world, row_off, full))
+    out["compress_us"] = timed(lambda: lsmt_amd.hits_compress(h, pack, cap))
+    out["expand_8_ranks_us"] = timed(lambda: lsmt_amd.hits_expand(packs, world, row_off, full, cap))
     out["memset_full_us"] = timed(lambda: full.zero_())
-    out["counts_to_host_us"] = timed(lambda: packs.view(world, 2 + cap)[:, 0].cpu())
-    one = torch.empty(2 + cap, dtype=torch.int32, device=dev)
+    out["counts_to_host_us"] = timed(lambda: packs.view(world, stride)[:, 0].cpu())
+    one = torch.empty(stride, dtype=torch.int32, device=dev)
     out["allgather_pack_world1_us"] = timed(lambda: dist.all_gather_into_tensor(one, pack))
     dense = torch.empty((rows, words), dtype=torch.int64, device=dev)
     out["allgather_dense_world1_us"] = timed(lambda: dist.all_gather_into_tensor(dense, h))
