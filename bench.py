@@ -74,6 +74,10 @@ def parse():
                    help="initialise the process group and run the exchange path even at N=1")
     p.add_argument("--dry-run", action="store_true",
                    help="launch / join the ranks over gloo and report them; no GPU work")
+    p.add_argument("--rehearse-one-gpu", action="store_true",
+                   help="run the N-rank path with every rank on GPU 0: gloo process group and the C ABI's "
+                        "host transport (cb_comm_init_host) instead of RCCL; checks the multi-rank flow on a "
+                        "one-GPU box, its numbers are not a scaling measurement")
     return p.parse_args()
 
 
@@ -153,6 +157,10 @@ def main():
     import torch
     import torch.distributed as dist
 
+    rehearse = args.rehearse_one_gpu
+    local_rank = local
+    if rehearse:
+        local = 0  # every rank on GPU 0 (the one-GPU rehearsal of the N-rank path)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_dist = world > 1 or args.force_dist
@@ -161,7 +169,14 @@ def main():
             os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", "29533"
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    # host-side reductions (timing max, check flags): on the device for RCCL,
+    # on the CPU for the gloo rehearsal
+    red_dev = torch.device("cpu") if rehearse else dev
+    log(f"[rank {rank}] local rank {local_rank} on cuda:{local} of world {world}")
 
     import lsmt_amd
     from lsmt_amd import _lib, workload
@@ -173,7 +188,7 @@ def main():
     sh = stream.cuda_stream
 
     if args.workload == "c4":
-        return run_c4(args, torch, dist, world, rank, local, dev, use_dist, result)
+        return run_c4(args, torch, dist, world, rank, local, dev, use_dist, result, red_dev)
     seed_base, absent_seed = 100, 999
     if args.workload == "c5":  # key(1000+f, i), absent key(9999, i)
         args.n_keys, seed_base, absent_seed = 10_000_000, 1000, 9999
@@ -244,7 +259,17 @@ def main():
     # the lanes: the library keeps each lane's packs apart and runs the
     # collectives in issue order (every rank issues them in the same order),
     # so no two collectives are ever in flight at once.
-    xcomm = Comm.from_process_group(local) if use_dist else None
+    if use_dist and rehearse:
+        def gloo_allgather(send, recv):
+            nb = send.size
+            parts = [torch.empty(nb, dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(parts, torch.from_numpy(send.copy()))
+            for r, part in enumerate(parts):
+                recv[r * nb:(r + 1) * nb] = part.numpy()
+
+        xcomm = Comm.host(rank, world, local, gloo_allgather)
+    else:
+        xcomm = Comm.from_process_group(local) if use_dist else None
     if xcomm is not None and xcomm.world != world:
         raise RuntimeError(f"RCCL communicator has {xcomm.world} ranks, WORLD_SIZE is {world}")
 
@@ -307,7 +332,7 @@ def main():
         el = time.perf_counter() - t0
         region["ms"], region["k"] = e0.elapsed_time(e1), k
         if use_dist:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            t = torch.tensor([el], dtype=torch.float64, device=red_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         return el
@@ -434,6 +459,19 @@ def main():
         sectors, rand_reads = _set_sectors(filters, look_np, m, F)
         alg_bytes = 64 * sectors + 16 * n + F * n / 8
         alg_def = f"64 B x {sectors} distinct sectors + 16n + F*n/8 (SURVEY.md §8d alternative layout)"
+    # the same FilterSet step on ONE lane (every launch on `stream`, none
+    # overlapping): the kernel's own back-to-back duration, so the roofline
+    # does not depend on the lane count (roofline.frac_one_lane)
+    one_lane_us = None
+    if best == "filterset" and not use_dist:
+        def step_one():
+            fset.probe(keys_batch, out=hits_bufs[0], stream=sh)
+
+        for _ in range(args.warmup):
+            step_one()
+        timed(step_one, args.steps)
+        one_lane_us = region["ms"] * 1e3 / region["k"]
+
     roof = None
     if dominant:
         # Kernel duration for the roofline: HIP events recorded on the kernels'
@@ -458,6 +496,9 @@ def main():
                 "kernel_avg_us_per_launch_events": round(kprof[dominant]["avg_us"], 2),
                 "algorithmic_bytes": int(alg_bytes), "algorithmic_def": alg_def,
                 "step_effective_GBps": round(alg_bytes / (el / args.steps) / 1e9, 1)}
+        if one_lane_us:
+            roof["kernel_avg_us_one_lane"] = round(one_lane_us, 2)
+            roof["frac_one_lane"] = round(alg_bytes / (one_lane_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
         if roof["traffic"]:  # the memory-side bytes the kernel moves (PMC), at the same time per launch
             roof["traffic_GBps"] = round(roof["traffic"] / dur_s / 1e9, 1)
             roof["traffic_frac"] = round(roof["traffic"] / dur_s / 1e9 / HBM_PEAK_GBS, 4)
@@ -472,6 +513,8 @@ def main():
                     "reads_per_launch": rand_reads, "achieved_reads_per_s": round(got, 1),
                     "peak_reads_per_s": rr, "frac": round(got / rr, 4),
                     "source": "profiles/ubench_random_r01.json (256 MiB table, hipMalloc)"}
+                if one_lane_us:
+                    roof["random_read_roofline"]["frac_one_lane"] = round(rand_reads / (one_lane_us * 1e-6) / rr, 4)
 
     # maintenance cost of the set on the flush path: one new filter into an
     # empty slot (sparse OR of its set bits)
@@ -783,7 +826,7 @@ def main():
             if world > 1:
                 nlo, nhi = shard_range(nf_total, world, (rank + 1) % world)
                 good &= bool(np.array_equal(full[nlo:nhi], oracle_rows(nlo, nhi)))
-            flag = torch.tensor([1 if good else 0], dtype=torch.int32, device=dev)
+            flag = torch.tensor([1 if good else 0], dtype=torch.int32, device=red_dev)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             good = bool(flag.item())
         assert good, "bench hits differ from the oracle"
@@ -840,6 +883,10 @@ def main():
         }
         if x_fit is False:
             line["valid"] = False
+        if rehearse:
+            line["rehearsal"] = (f"{world} ranks on ONE GPU over the host transport (gloo): checks the N-rank "
+                                 "flow, not a scaling measurement")
+            line["valid"] = False
         print(json.dumps(line), file=result, flush=True)
     if use_dist:
         dist.barrier()
@@ -849,7 +896,7 @@ def main():
         sys.exit(3)
 
 
-def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result):
+def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result, red_dev):
     """C4: 64 concurrent flush builds (256K keys each, m = 2^25), filters
     split one contiguous subset per GPU (strong scaling: total work fixed).
     One step = zero-fill + batched build of this GPU's filters."""
@@ -888,7 +935,7 @@ def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result):
         dist.barrier()
     el = time.perf_counter() - t0
     if use_dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     if args.check and rank == 0:
