@@ -124,6 +124,7 @@ def test_c5_all_ranks_exchanged(gpu, golden, c5_lookups_dev):
     stride = gpu.FilterSet.pack_words(n, cap)
     packs = torch.zeros(world * stride, dtype=torch.int32, device="cuda")
     hits = torch.empty((per, words), dtype=torch.int64, device="cuda")
+    sets = []
     for r in range(world):
         lo, hi = shard_range(nf, world, r)
         s = gpu.FilterSet(m, 32)
@@ -134,7 +135,7 @@ def test_c5_all_ranks_exchanged(gpu, golden, c5_lookups_dev):
             del b
         s.probe_pack(c5_lookups_dev, hits, packs[r * stride:(r + 1) * stride], cap=cap)
         assert sha(hits.cpu().numpy().view(np.uint64).astype("<u8")) == g["rank_slice_hits_sha256"][r], r
-        del s
+        sets.append(s)
     counts = packs.view(world, stride)[:, 0].cpu().numpy()
     assert (counts <= cap).all() and int(counts.sum()) == g["hits_popcount"]
     full = torch.full((nf, words), -1, dtype=torch.int64, device="cuda")
@@ -144,3 +145,44 @@ def test_c5_all_ranks_exchanged(gpu, golden, c5_lookups_dev):
     got = full.cpu().numpy().view(np.uint64)
     for r in range(world):
         assert sha(got[r * per:(r + 1) * per].astype("<u8")) == g["rank_slice_hits_sha256"][r], r
+    del full, got, packs
+
+    # The same C5 exchange as the N = 8 product path runs it: eight ranks of
+    # the C ABI's communicator (loopback transport: one thread and one stream
+    # per rank, all on this GPU), each calling cb_set_probe_allgather_fixed
+    # with its own FilterSet; ranks 0 and 7 check every slice of their map.
+    import threading
+
+    from lsmt_amd.shard import Comm
+    comms = Comm.loopback(world, 0)
+    fulls = {r: torch.full((nf, words), -1, dtype=torch.int64, device="cuda") for r in (0, 7)}
+    errs = []
+
+    def rank(r):
+        try:
+            st = torch.cuda.Stream()
+            loc = torch.empty((per, words), dtype=torch.int64, device="cuda")
+            out = fulls.get(r, None)
+            if out is None:
+                out = torch.empty((nf, words), dtype=torch.int64, device="cuda")
+            ok = torch.ones(1, dtype=torch.int32, device="cuda")
+            comms[r].probe_allgather(sets[r], c5_lookups_dev, nf, loc, out, sparse=True, cap=cap, ok=ok, stream=st)
+            st.synchronize()
+            assert int(ok.item()) == 1
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            errs.append(e)
+
+    ts = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=90)
+    try:
+        assert not any(t.is_alive() for t in ts) and not errs, errs
+        for r0, fm in fulls.items():
+            got = fm.cpu().numpy().view(np.uint64)
+            for r in range(world):
+                assert sha(got[r * per:(r + 1) * per].astype("<u8")) == g["rank_slice_hits_sha256"][r], (r0, r)
+    finally:
+        for c in comms:
+            c.close()
