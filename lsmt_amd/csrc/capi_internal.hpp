@@ -103,15 +103,14 @@ struct cb_table {
   cb::LineRec* rec = nullptr;   // per-line index record
   uint64_t* pfx = nullptr;      // per-line 8-byte key prefix
   uint64_t* fence = nullptr;    // the fence levels above pfx (sstable.hpp)
-  uint32_t* dir = nullptr;      // the radix directory (sstable.hpp; nullptr under 256 lines)
-  uint64_t pfx_first = 0, pfx_last = 0;  // pfx[0], pfx[nlines - 1] (the directory's key)
+  uint32_t* dir = nullptr;      // the byte-rank directory (sstable.hpp; nullptr under 16 lines)
+  cb::DirMap* dmap = nullptr;   // its map (device, in the index allocation)
   bool fast = false;  // well-formed: TAB on every line, keys strictly increasing
   bool has_zone = false;   // made by cb_sstable_create with n >= 1
   std::string zmin, zmax;  // its ZoneMap bounds (first / last key of the file)
   cb::TableView view() const {
     return cb::TableView{data, rec, pfx, fence, nlines, cb::fence_levels(nlines), fast ? 1u : 0u,
-                         dir, dir ? cb::dir_bits(nlines) : 0u,
-                         pfx_first == pfx_last ? 64u : (uint32_t)__builtin_clzll(pfx_first ^ pfx_last), pfx_first};
+                         dmap ? dir : nullptr, dmap};
   }
 };
 
@@ -173,9 +172,11 @@ struct Workspace {
   DevBuf x_ctl;                   // cb_hits_compress: slot / finish counters (zeroed once)
   cb::CompressState xst;
   cb::CreateResult* hres = nullptr;  // pinned host mirror of f_flag (SsTable::create)
-  uint64_t* htot = nullptr;          // pinned, 64 B: get_many's value byte total; index_table's read-backs
+  uint64_t* htot = nullptr;          // pinned, kHostScratch B: get_many's value byte total; index_table's read-backs
   hipEvent_t ev = nullptr;           // marks hres's first copy in the stream
 };
+
+constexpr size_t kHostScratch = 512;  // Workspace::htot bytes
 
 Workspace& workspace(int device, hipStream_t s);
 

@@ -140,7 +140,7 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
                                 (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, tsum, s));
   }
   HIP_TRY(cb::launch_tile_scan(tsum, cb::get_tiles(n), dvoff + n, s));
-  if (!ws.htot) HIP_TRY(hipHostMalloc((void**)&ws.htot, 64, hipHostMallocDefault));
+  if (!ws.htot) HIP_TRY(hipHostMalloc((void**)&ws.htot, kHostScratch, hipHostMallocDefault));
   if (async) {
     HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, vals, vals ? cap : 0, s));
     return CB_OK;
@@ -169,15 +169,23 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
   return CB_OK;
 }
 
-// The index of nl lines is one allocation: rec | pfx | fence | dir.
+// The index of nl lines is one allocation: rec | pfx | fence | dir | dmap.
+size_t dir_bytes(uint64_t nl) { return cb::dir_words(nl) ? ((cb::dir_words(nl) * 4 + 15) & ~15ull) : 0; }
 size_t index_bytes(uint64_t nl) {
-  return nl * sizeof(cb::LineRec) + nl * 8 + cb::fence_words(nl) * 8 + cb::dir_words(nl) * 4;
+  return nl * sizeof(cb::LineRec) + nl * 8 + cb::fence_words(nl) * 8 + 8 + dir_bytes(nl) +
+         (cb::dir_words(nl) ? sizeof(cb::DirMap) : 0);
 }
 void carve_index(cb_table* t) {
   const uint64_t nl = t->nlines;
   t->pfx = (uint64_t*)(t->rec + nl);
   t->fence = t->pfx + nl;
-  t->dir = cb::dir_words(nl) ? (uint32_t*)(t->fence + cb::fence_words(nl)) : nullptr;
+  // 16-B aligned: the read path copies the map into LDS in 16-B words
+  uint8_t* d = (uint8_t*)(((uintptr_t)(t->fence + cb::fence_words(nl)) + 15) & ~(uintptr_t)15);
+  t->dir = cb::dir_words(nl) ? (uint32_t*)d : nullptr;
+  t->dmap = nullptr;  // set once the directory is written (make_dirmap needs every prefix)
+}
+cb::DirMap* dmap_slot(const cb_table* t) {
+  return t->dir ? (cb::DirMap*)((uint8_t*)t->dir + dir_bytes(t->nlines)) : nullptr;
 }
 
 // Line index of t->data[0..t->len) (count -> scan -> emit -> finish -> keys).
@@ -192,7 +200,7 @@ int index_table(cb_table* t, hipStream_t s) {
   HIP_TRY(ws.i_cnt.reserve(nb * 8, s));
   HIP_TRY(ws.i_base.reserve((nb + 1) * 8, s));
   HIP_TRY(ws.i_tmp.reserve(cb::scan_tmp_words(nb) * 8, s));
-  HIP_TRY(ws.i_err.reserve(8, s));
+  HIP_TRY(ws.i_err.reserve(16 + 8 * cb::kDirPos * 4, s));  // error words, then the prefix byte masks
   uint64_t* cnt = (uint64_t*)ws.i_cnt.p;
   uint64_t* base = (uint64_t*)ws.i_base.p;
   uint32_t* err = (uint32_t*)ws.i_err.p;
@@ -220,20 +228,27 @@ int index_table(cb_table* t, hipStream_t s) {
   HIP_TRY(cb::launch_line_finish(t->data, len, nl, start, end, t->rec, err, s));
   // prefix + fence index, value validity and the well-formed check (sstable.hpp)
   HIP_TRY(cb::launch_line_keys(t->data, nl, t->rec, t->pfx, t->fence, err + 1, s));
-  if (t->dir) HIP_TRY(cb::launch_table_dir(t->pfx, nl, t->dir, s));
-  // the error words and the directory's key (first / last prefix) in one
-  // pinned copy set, one wait
-  if (!ws.htot) HIP_TRY(hipHostMalloc((void**)&ws.htot, 64, hipHostMallocDefault));
-  HIP_TRY(hipMemcpyAsync(ws.htot, err, 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(ws.htot + 1, t->pfx, 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(ws.htot + 2, t->pfx + nl - 1, 8, hipMemcpyDeviceToHost, s));
+  // the byte values of every prefix position (the directory's map)
+  uint64_t* dmask = (uint64_t*)(err + 4);
+  if (t->dir) {
+    HIP_TRY(hipMemsetAsync(dmask, 0, sizeof(uint64_t) * cb::kDirPos * 4, s));
+    HIP_TRY(cb::launch_pfx_masks(t->pfx, nl, dmask, s));
+  }
+  // the error words and the masks in one pinned copy, one wait
+  if (!ws.htot) HIP_TRY(hipHostMalloc((void**)&ws.htot, kHostScratch, hipHostMallocDefault));
+  HIP_TRY(hipMemcpyAsync(ws.htot, err, 16 + (t->dir ? 8 * cb::kDirPos * 4 : 0), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   uint32_t e[2];
   memcpy(e, ws.htot, 8);
-  t->pfx_first = ws.htot[1];
-  t->pfx_last = ws.htot[2];
   if (e[0]) return fail(CB_EINVAL, "an SSTable line is 4 GiB or longer");
   t->fast = e[1] != 0 && !g_table_exact;
+  if (t->dir) {
+    uint64_t m[cb::kDirPos][4];
+    memcpy(m, ws.htot + 2, sizeof m);
+    const cb::DirMap dm = cb::make_dirmap(m, nl);
+    t->dmap = dmap_slot(t);
+    HIP_TRY(cb::launch_table_dir(t->pfx, nl, dm, t->dir, t->dmap, s));
+  }
   return CB_OK;
 }
 
@@ -381,6 +396,7 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   hr->flags[2] = 1;
   hr->flags[3] = 0;
   HIP_TRY(hipMemcpyAsync(dr->flags, hr->flags, 16, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(dr->dmask, 0, sizeof(dr->dmask), s));
   HIP_TRY(ws.f_tsum.reserve(cb::format_tiles(n) * 8, s));
   uint64_t* tsum = (uint64_t*)ws.f_tsum.p;
   HIP_TRY(cb::launch_sorted_check(dk, dko, dvo, n, dr, tsum, s));
@@ -434,14 +450,18 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
     return fail(CB_ENOMEM, "device allocation failed for an SSTable index");
   }
   carve_index(t.get());
+  // the directory's map from round trip 1's prefix byte masks (order-free)
+  cb::DirMap dm{};
+  if (t->dir) {
+    dm = cb::make_dirmap(hr->dmask, n);
+    t->dmap = dmap_slot(t.get());
+  }
   HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, tsum, n, t->data, t->rec, t->pfx, t->fence, dr,
-                            cap_bytes, s, vsp, t->dir));
+                            cap_bytes, s, vsp, t->dir, t->dir ? &dm : nullptr, t->dmap));
   // Round trip 2: flags, file length, zone bounds
   HIP_TRY(hipMemcpyAsync(hr, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   t->len = hr->len;
-  t->pfx_first = hr->pfx_lo;
-  t->pfx_last = hr->pfx_hi;
   // zone map: ZoneMap::update over the sorted keys = first / last line
   if (zone_min_idx) *zone_min_idx = hr->idx_min;
   if (zone_max_idx) *zone_max_idx = hr->idx_max;
@@ -466,6 +486,7 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
     t->rec = nullptr;
     t->pfx = t->fence = nullptr;
     t->dir = nullptr;
+    t->dmap = nullptr;
     t->nlines = 0;
     lk.unlock();  // index_table takes the workspace itself
     if ((rc = index_table(t.get(), s))) return rc;

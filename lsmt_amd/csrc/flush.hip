@@ -113,8 +113,7 @@ __global__ __launch_bounds__(kNT) void k_sorted_check(const uint8_t* __restrict_
   }
   uint64_t i = 0, kl = 0, w0 = 0, w1 = 0;
   if (p < n) key_words(nullptr, kb, ko, p, i, kl, w0, w1);
-  if (p == 0) r->pfx_lo = w0;  // the file's first and last prefix if the input is in order
-  if (p + 1 == n) r->pfx_hi = w0;
+  block_pfx_masks(w0, p < n, &r->dmask[0][0]);  // the directory's alphabet (order-free)
   uint64_t pkl = __shfl_up(kl, 1, 64), pw0 = __shfl_up(w0, 1, 64), pw1 = __shfl_up(w1, 1, 64);
   uint64_t pi = p - 1;
   if (p < n && lane == 0 && p > 0) key_words(nullptr, kb, ko, p - 1, pi, pkl, pw0, pw1);
@@ -282,8 +281,9 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
                                                 uint8_t* __restrict__ out, LineRec* __restrict__ rec,
                                                 uint64_t* __restrict__ pfx, uint64_t* __restrict__ fence,
                                                 CreateResult* r, const ulonglong2* __restrict__ vsp,
-                                                uint32_t* __restrict__ dir, uint32_t dbits) {
+                                                uint32_t* __restrict__ dir, DirMap dm, DirMap* dmap_out) {
   __shared__ uint32_t stage32[LDSB / 4];
+  __shared__ DirMap sdm;  // the directory's map, indexed per lane
   uint8_t* stage = reinterpret_cast<uint8_t*>(stage32);
   const uint64_t p0 = (uint64_t)blockIdx.x * kNT;
   const uint64_t p = p0 + threadIdx.x;
@@ -291,12 +291,9 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   const uint64_t pend = p0 + kNT < n ? p0 + kNT : n;
   const bool live = p < n;
   uint64_t i = 0, kl = 0, w0 = 0, w1 = 0;
-  // the directory's key: the file's first and last prefix (sorted records,
-  // or k_sorted_check's for input already in order), loaded up front
-  uint64_t f0 = 0, f1 = 0;
-  if (dir) {
-    f0 = order ? order[0].w0 : r->pfx_lo;
-    f1 = order ? order[n - 1].w0 : r->pfx_hi;
+  if (dir && threadIdx.x == 0) {
+    sdm = dm;
+    if (blockIdx.x == 0) *dmap_out = dm;  // the table's copy, for the read path
   }
   if (live) key_words(order, kb, ko, p, i, kl, w0, w1);
   // the previous entry's key: the neighbour lane's, or loaded by lane 0
@@ -337,21 +334,22 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
     lr.pad = 0;
     rec[p] = lr;
     pfx[p] = w0;
-    if (p == 0) r->pfx_lo = w0;
-    if (p == n - 1) r->pfx_hi = w0;
     fence_put(fence, n, p, w0);
     if (p > 0) not_inc = key_cmp(kb, ko, pi, pkl, pw0, pw1, i, kl, w0, w1) >= 0;
   }
   if (__syncthreads_or(special) && threadIdx.x == 0) atomicOr(&r->flags[1], 1u);
   if (__syncthreads_or(not_inc) && threadIdx.x == 0) atomicAnd(&r->flags[2], 0u);
   if (dir) {
-    // the radix directory (sstable.hpp dir_bits): dir[B] = p for the
+    // the byte-rank directory (sstable.hpp DirMap): dir[B] = p for the
     // buckets B in (bucket(line p-1), bucket(line p)], and n past the last
-    // line's
-    const uint32_t sh = f0 == f1 ? 64u : (uint32_t)__builtin_clzll(f0 ^ f1);
-    if (sh + dbits <= 64) {
-      const uint64_t nb = 1ull << dbits;
-      auto bucket = [&](uint64_t w) { return (w << sh) >> (64 - dbits); };
+    // line's (every line's bytes are in the map: dir_bucket never fails here)
+    {
+      const uint64_t nb = sdm.nbuckets;
+      auto bucket = [&](uint64_t w) {
+        uint64_t b = 0;
+        (void)dir_bucket(sdm, w, &b);
+        return b;
+      };
       uint64_t s0 = 0, c0 = 0, s1 = 0, c1 = 0;
       if (live) {
         const uint64_t b1 = bucket(w0);
@@ -492,16 +490,19 @@ hipError_t launch_line_sums(const SortKey* order, const uint64_t* ko, const uint
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
-                         uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp, uint32_t* dir) {
+                         uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp, uint32_t* dir,
+                         const DirMap* dm, DirMap* dmap_out) {
   if (!n) return hipSuccess;
+  if (dir && (!dm || !dmap_out)) return hipErrorInvalidValue;
+  const DirMap d = dir ? *dm : DirMap{};
   ProfScope ps("k_format", s);
   const dim3 g(blocks_for(n, kNT));
   if (bytes_bound / n * kNT * 5 / 4 <= kFormatLdsSmall)
     hipLaunchKernelGGL(k_format<kFormatLdsSmall>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
-                       rec, pfx, fence, r, order ? vsp : nullptr, dir, dir ? dir_bits(n) : 0u);
+                       rec, pfx, fence, r, order ? vsp : nullptr, dir, d, dmap_out);
   else
     hipLaunchKernelGGL(k_format<kFormatLdsLarge>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
-                       rec, pfx, fence, r, order ? vsp : nullptr, dir, dir ? dir_bits(n) : 0u);
+                       rec, pfx, fence, r, order ? vsp : nullptr, dir, d, dmap_out);
   return hipGetLastError();
 }
 

@@ -58,10 +58,10 @@ constexpr uint32_t kZoneInline = 256;  // zone bound key bytes carried inline
 struct CreateResult {
   uint32_t flags[4];          // [0] input sorted, [1] a key holds '\n' / '\t', [2] strictly increasing
   uint64_t ktot, vtot;        // ko[n], vo[n]
+  uint64_t dmask[kDirPos][4]; // the byte values at each position of the keys' 8-byte prefixes (DirMap)
   uint64_t len;               // the file's length
   uint64_t idx_min, idx_max;  // input indices of the first / last key in file order
   uint32_t zlen[2];           // their full lengths
-  uint64_t pfx_lo, pfx_hi;    // the first and last line's 8-byte prefix (the directory's key)
   uint8_t zkey[2][kZoneInline];
 };
 
@@ -73,7 +73,8 @@ hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, S
 constexpr uint32_t kFormatTile = 256;
 inline uint64_t format_tiles(uint64_t n) { return n ? (n + kFormatTile - 1) / kFormatTile : 1; }
 // r->flags[0] &= (keys already in non-decreasing order); r->ktot = ko[n],
-// r->vtot = vo[n]; tsum = the line tiles in input order (valid if sorted).
+// r->vtot = vo[n]; r->dmask |= every key's prefix bytes (zeroed by the
+// caller); tsum = the line tiles in input order (valid if sorted).
 // Launches for any n, n = 0 included.
 hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, const uint64_t* vo, uint64_t n,
                                CreateResult* r, uint64_t* tsum, hipStream_t s);
@@ -101,12 +102,13 @@ hipError_t launch_entry_sort(const SortKey* in, SortKey* out, SortKey* tmp, uint
 // the well-formed check).
 // vsp (nullable, with order): entry p's {value offset, value length} in
 // sorted order (launch_entry_sort's), read instead of vo[order[p].idx].
-// dir (nullable): the table's radix directory (dir_words(n)), written here
-// from the lines' prefixes (what launch_table_dir would build).
+// dir (nullable, with dm): the table's directory (dm->nbuckets + 1 entries),
+// written here from the lines' prefixes (what launch_table_dir would build);
+// dm is also stored at dmap_out.
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
                          uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp = nullptr,
-                         uint32_t* dir = nullptr);
+                         uint32_t* dir = nullptr, const DirMap* dm = nullptr, DirMap* dmap_out = nullptr);
 
 }  // namespace cb

@@ -497,38 +497,26 @@ __device__ __forceinline__ void level_down(const TableView& t, uint32_t j, uint6
 
 constexpr uint32_t kWin = 8;  // buckets of up to this many lines: one round of prefix loads
 
-// Whether table t's directory applies: the shared prefix bits plus the
-// bucket bits fit the 64-bit prefix (dshift and dp0 set by the kernel).
-__device__ __forceinline__ bool dir_usable(const TableView& t) {
-  return t.dbits && t.dshift + t.dbits <= 64;
-}
-
 // Where x's descent starts: level j and the run [lo, hi) of at most 16
-// entries holding its lower bound (returns false), or the lower bound b itself
-// (returns true) when x lies outside the table's shared prefix bits or in an
-// empty bucket. Lines before dir[B] have smaller buckets (so smaller
-// prefixes) and lines from dir[B+1] on larger ones, so on every level the
-// entries sampled from [dir[B], dir[B+1]] bracket x's lower bound.
-__device__ __forceinline__ bool dir_start(const TableView& t, uint64_t x, uint32_t& j, uint64_t& lo, uint64_t& hi,
-                                          uint64_t& b) {
+// entries holding its lower bound (returns false), or true when x is absent
+// outright: one of its prefix bytes occurs at that position in no line, or
+// its bucket is empty. dm: the table's DirMap (LDS-staged by the read path).
+// Lines before dir[B] have smaller buckets (so smaller prefixes) and lines
+// from dir[B+1] on larger ones, so on every level the entries sampled from
+// [dir[B], dir[B+1]] bracket x's lower bound.
+__device__ __forceinline__ bool dir_start(const TableView& t, const DirMap* dm, uint64_t x, uint32_t& j,
+                                          uint64_t& lo, uint64_t& hi) {
   j = t.nlev;
   lo = 0;
   hi = level_count(t.nlines, j);
-  if (!dir_usable(t)) return false;
-  const uint32_t sh = t.dshift;
-  if (sh && ((x ^ t.dp0) >> (64 - sh))) {
-    b = x < t.dp0 ? 0 : t.nlines;
-    return true;
-  }
-  const uint64_t bk = (x << sh) >> (64 - t.dbits);
+  if (!t.dir) return false;
+  uint64_t bk;
+  if (!dir_bucket(*dm, x, &bk)) return true;
   // dir[B] and dir[B + 1] as one 8-byte load (one L2 request, not two: the
   // search is bound by the requests a CU keeps in flight)
   const u32x2 ae = *(const __attribute__((address_space(1))) u32x2*)(t.dir + bk);
   const uint64_t a = ae.x, e = ae.y;
-  if (a == e) {
-    b = a;
-    return true;
-  }
+  if (a == e) return true;
   for (uint32_t l = 0; l < t.nlev; ++l) {
     const uint64_t l0 = a >> (kFanBits * l);
     const uint64_t c = level_count(t.nlines, l);
@@ -550,11 +538,12 @@ __device__ __forceinline__ bool dir_start(const TableView& t, uint64_t x, uint32
 // then the lines sharing that prefix by a galloping search with record
 // compares: O(log run) for keys that share long prefixes ('user0000...'), one
 // record compare when the prefix is unique.
-__device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& q, LineRec& hit) {
+__device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& q, LineRec& hit,
+                                               const DirMap* dm) {
   uint32_t j;
-  uint64_t lo, hi, b;
-  // outside the lines' shared prefix bits, or an empty bucket: absent
-  if (dir_start(t, q.w0, j, lo, hi, b)) return -1;
+  uint64_t lo, hi;
+  // a prefix byte no line holds at that position, or an empty bucket: absent
+  if (dir_start(t, dm, q.w0, j, lo, hi)) return -1;
   if (j == 0 && hi - lo <= kWin) {
     // [lo, hi) is the key's whole bucket (or the whole table): its prefixes
     // in one round of independent loads, with the record when it is one line
@@ -598,29 +587,56 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
   }
 }
 
-__device__ __forceinline__ int64_t search(const TableView& t, const Query& q, LineRec& hit) {
-  return t.fast ? search_fast(t, q, hit) : search_exact(t, q, hit);
+// dm: the table's DirMap (LDS or global); used only when t.dir is set.
+__device__ __forceinline__ int64_t search(const TableView& t, const Query& q, LineRec& hit, const DirMap* dm) {
+  return t.fast ? search_fast(t, q, hit, dm) : search_exact(t, q, hit);
 }
 
-// dir[B] for B in [0, 2^dbits]: the lower bound of bucket B's smallest prefix.
-__global__ __launch_bounds__(kNT) void k_table_dir(const uint64_t* __restrict__ pfx, uint64_t nl, uint32_t dbits,
-                                                   uint32_t* __restrict__ dir) {
+// The r-th (0-based) set bit of a 256-bit mask.
+__device__ __forceinline__ uint32_t mask_select(const uint64_t (&m)[4], uint32_t r) {
+  uint32_t w = 0;
+  for (; w < 3; ++w) {
+    const uint32_t c = (uint32_t)__popcll(m[w]);
+    if (r < c) break;
+    r -= c;
+  }
+  uint64_t x = m[w];
+  for (uint32_t k = 0; k < r; ++k) x &= x - 1;
+  return 64 * w + (uint32_t)__builtin_ctzll(x);
+}
+
+// dir[B] for B in [0, nbuckets]: the lower bound of bucket B's smallest
+// prefix (its digits' byte values, zero bytes after them). Block 0 also
+// stores the map (the table's device copy).
+__global__ __launch_bounds__(kNT) void k_table_dir(const uint64_t* __restrict__ pfx, uint64_t nl, DirMap dm,
+                                                   uint32_t* __restrict__ dir, DirMap* dmap_out) {
+  __shared__ DirMap sdm;
+  if (threadIdx.x == 0) {
+    sdm = dm;
+    if (blockIdx.x == 0) *dmap_out = dm;
+  }
+  __syncthreads();
   const uint64_t B = (uint64_t)blockIdx.x * kNT + threadIdx.x;
-  const uint64_t nb = 1ull << dbits;
+  const uint64_t nb = sdm.nbuckets;
   if (B > nb) return;
   if (B == nb) {
     dir[B] = (uint32_t)nl;
     return;
   }
-  const uint64_t p0 = pfx[0], p1 = pfx[nl - 1];
-  const uint32_t shared = p0 == p1 ? 64u : (uint32_t)__builtin_clzll(p0 ^ p1);
-  if (shared + dbits > 64) {  // unused (dir_usable is false)
-    dir[B] = 0;
-    return;
+  uint64_t rest = B, w = 0;
+  for (int32_t j = (int32_t)sdm.npos - 1; j >= 0; --j) {
+    const uint64_t d = rest % sdm.radix[j];
+    rest /= sdm.radix[j];
+    const uint32_t rank = (uint32_t)d << ((uint32_t)j + 1 == sdm.npos ? sdm.shift : 0u);
+    w |= (uint64_t)mask_select(sdm.mask[j], rank) << (56 - 8 * j);
   }
-  const uint64_t hi_bits = shared ? p0 & ~(~0ull >> shared) : 0ull;
-  const uint64_t w = hi_bits | ((B << (64 - dbits)) >> shared);
   dir[B] = (uint32_t)lower_bound_u64(pfx, 0, nl, w);
+}
+
+__global__ __launch_bounds__(kNT) void k_pfx_masks(const uint64_t* __restrict__ pfx, uint64_t nl,
+                                                   uint64_t* __restrict__ mask) {
+  const uint64_t l = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  block_pfx_masks(l < nl ? pfx[l] : 0, l < nl, mask);
 }
 
 // A block's views of the first min(nt, 64) tables into LDS. Barrier inside.
@@ -655,6 +671,21 @@ __device__ __forceinline__ void store_views(const ViewRegs& v, uint32_t nt, Tabl
   __syncthreads();
 }
 
+// The first min(nt, 64) tables' DirMaps (their views already in LDS) into
+// LDS, 16 B per thread and step; barrier at the end. The search computes
+// its bucket from these words (sstable.hpp dir_bucket) without a memory
+// round trip.
+constexpr uint32_t kMapWords = sizeof(DirMap) / 16;
+__device__ __forceinline__ void stage_maps(const TableView* stv, uint32_t nt, DirMap* sdm) {
+  const uint32_t nm = (nt < 64 ? nt : 64) * kMapWords;
+  for (uint32_t i = threadIdx.x; i < nm; i += kNT) {
+    const uint32_t t = i / kMapWords, k = i - t * kMapWords;
+    const DirMap* g = stv[t].dmap;
+    if (g) reinterpret_cast<uint4*>(sdm + t)[k] = reinterpret_cast<const uint4*>(g)[k];
+  }
+  __syncthreads();
+}
+
 template <int KEYK>
 __global__ __launch_bounds__(kNT) void k_table_search(TableView t, KeySrc ks, uint64_t n,
                                                       int64_t* __restrict__ line) {
@@ -662,7 +693,7 @@ __global__ __launch_bounds__(kNT) void k_table_search(TableView t, KeySrc ks, ui
   if (k >= n) return;
   const Query q = make_query<KEYK>(ks, k);
   LineRec r;
-  line[k] = search(t, q, r);
+  line[k] = search(t, q, r, t.dmap);
 }
 
 // One group of up to 64 tables (t0 .. t0 + 63): every candidate in cand,
@@ -671,15 +702,15 @@ __global__ __launch_bounds__(kNT) void k_table_search(TableView t, KeySrc ks, ui
 // view fields from LDS where it uses them instead of copying the 56-byte view
 // into registers (88 -> 80 VGPRs: 6 waves per SIMD instead of 5).
 template <bool LDS_VIEWS = false>
-__device__ __forceinline__ bool resolve_group(const TableView* stv, const TableView* __restrict__ tv, uint32_t t0,
-                                              uint64_t cand, const Query& q, int32_t& w, uint64_t& src,
-                                              uint64_t& d) {
+__device__ __forceinline__ bool resolve_group(const TableView* stv, const TableView* __restrict__ tv,
+                                              const DirMap* sdm, uint32_t t0, uint64_t cand, const Query& q,
+                                              int32_t& w, uint64_t& src, uint64_t& d) {
   while (cand) {
     const uint32_t t = t0 + (uint32_t)__builtin_ctzll(cand);
     cand &= cand - 1;
     auto try_table = [&](const TableView& v) {
       LineRec r;
-      if (search(v, q, r) < 0) return false;  // Ok(None)
+      if (search(v, q, r, t < 64 ? &sdm[t] : v.dmap) < 0) return false;  // Ok(None)
       if (r.vdl == kBadValue) return false;   // Err(..) is skipped by `if let Ok(Some(v))`
       w = (int32_t)t;
       src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
@@ -705,8 +736,9 @@ __device__ __forceinline__ bool resolve_group(const TableView* stv, const TableV
 // the first table whose SsTable::get returns Ok(Some), the value's base64
 // bytes and their decoded length.
 template <bool LDS_VIEWS>
-__device__ __forceinline__ void resolve_key(const TableView* stv, const TableView* __restrict__ tv, uint32_t nt,
-                                            uint64_t cand0, const uint64_t* __restrict__ hits,
+__device__ __forceinline__ void resolve_key(const TableView* stv, const TableView* __restrict__ tv,
+                                            const DirMap* sdm, uint32_t nt, uint64_t cand0,
+                                            const uint64_t* __restrict__ hits,
                                             const uint32_t* __restrict__ rows, uint64_t hwords, uint64_t k,
                                             const Query& q, int32_t& w, uint64_t& src, uint64_t& d) {
   for (uint32_t t0 = 0; t0 < nt; t0 += 64) {
@@ -721,7 +753,7 @@ __device__ __forceinline__ void resolve_key(const TableView* stv, const TableVie
         cand |= ((hits[row * hwords + (k >> 6)] >> (k & 63)) & 1) << i;  // the gate
       }
     }
-    if (resolve_group<LDS_VIEWS>(stv, tv, t0, cand, q, w, src, d)) return;
+    if (resolve_group<LDS_VIEWS>(stv, tv, sdm, t0, cand, q, w, src, d)) return;
   }
 }
 
@@ -756,15 +788,17 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
   // the first 64 tables' views, staged once per block: each lane's search
   // reads its table's view from LDS instead of a divergent global gather
   __shared__ TableView stv[64];
+  __shared__ DirMap sdm[64];
   store_views(vr, nt, stv);
+  stage_maps(stv, nt, sdm);
   uint64_t d = 0;
   if (k < n) {
     int32_t w = -1;
     uint64_t src = 0;
     if constexpr (LDS_VIEWS)
-      (void)resolve_group<true>(stv, tv, 0, cand0, q, w, src, d);  // one group
+      (void)resolve_group<true>(stv, tv, sdm, 0, cand0, q, w, src, d);  // one group
     else
-      resolve_key<false>(stv, tv, nt, cand0, hits, rows, hwords, k, q, w, src, d);
+      resolve_key<false>(stv, tv, sdm, nt, cand0, hits, rows, hwords, k, q, w, src, d);
     which[k] = w;
     vsrc[k] = src;
     dlen[k] = d;
@@ -792,6 +826,7 @@ __global__ __launch_bounds__(kNT) void k_set_get_many(const void* __restrict__ s
   __shared__ BoundPrefix zp[2 * W];
   __shared__ uint32_t sslot[64];
   __shared__ TableView stv[64];
+  __shared__ DirMap sdm[64];
   stage_zone_prefixes<KEYK, W>(zv, zp, kNT);
   if (slots && threadIdx.x < nt) sslot[threadIdx.x] = slots[threadIdx.x];
   // the key's loads go out before the barrier (after it, the compiler kept
@@ -805,11 +840,12 @@ __global__ __launch_bounds__(kNT) void k_set_get_many(const void* __restrict__ s
   } else {
     cand0 = (uint64_t)mask & (nt == 64 ? ~0ull : ((1ull << nt) - 1));
   }
+  stage_maps(stv, nt, sdm);
   uint64_t d = 0;
   if (k < n) {
     int32_t w = -1;
     uint64_t src = 0;
-    (void)resolve_group<true>(stv, tv, 0, cand0, q, w, src, d);  // nt <= 64: one group
+    (void)resolve_group<true>(stv, tv, sdm, 0, cand0, q, w, src, d);  // nt <= 64: one group
     which[k] = w;
     vsrc[k] = src;
     dlen[k] = d;
@@ -1071,11 +1107,19 @@ hipError_t launch_table_search(int keyk, const TableView& t, const KeySrc& ks, u
   return hipGetLastError();
 }
 
-hipError_t launch_table_dir(const uint64_t* pfx, uint64_t nlines, uint32_t* dir, hipStream_t s) {
-  const uint32_t db = dir_bits(nlines);
-  if (!db) return hipSuccess;
+hipError_t launch_table_dir(const uint64_t* pfx, uint64_t nlines, const DirMap& dm, uint32_t* dir,
+                            DirMap* dmap_out, hipStream_t s) {
+  if (!nlines || !dir || !dmap_out) return hipErrorInvalidValue;
   ProfScope ps("k_table_dir", s);
-  hipLaunchKernelGGL(k_table_dir, dim3(blocks_for((1ull << db) + 1, kNT)), dim3(kNT), 0, s, pfx, nlines, db, dir);
+  hipLaunchKernelGGL(k_table_dir, dim3(blocks_for(dm.nbuckets + 1, kNT)), dim3(kNT), 0, s, pfx, nlines, dm, dir,
+                     dmap_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pfx_masks(const uint64_t* pfx, uint64_t nlines, uint64_t* mask, hipStream_t s) {
+  if (!nlines) return hipSuccess;
+  ProfScope ps("k_pfx_masks", s);
+  hipLaunchKernelGGL(k_pfx_masks, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, pfx, nlines, mask);
   return hipGetLastError();
 }
 

@@ -52,24 +52,125 @@ __device__ __forceinline__ void fence_put(uint64_t* fence, uint64_t nl, uint64_t
     off += level_count(nl, j);
   }
 }
-// Radix directory of a well-formed table: below the prefix bits every line
-// shares (dshift = clz(pfx[0] ^ pfx[nlines-1])), the next dbits bits of a
-// prefix name its bucket; dir[B] = the first line whose bucket is >= B
-// (dir[2^dbits] = nlines). A lookup reads dir[B], dir[B+1]: a bucket of at
-// most 8 lines (~4 on average) is searched with one round of prefix loads
-// (and its record loaded with them when it holds one line); a larger one
+// Directory of a well-formed table, on a byte-rank radix of the 8-byte
+// prefix (an order-preserving compression of the key alphabet). For each
+// byte position j the table records which byte values its prefixes hold
+// (DirMap::mask); a prefix's digit j is the rank of its byte among them, the
+// bucket the mixed-radix number of its first npos digits (the last one
+// coarsened by `shift`), sized to ~2 lines per bucket. dir[B] = the first
+// line whose bucket is >= B (dir[nbuckets] = nlines). A lookup computes its
+// bucket from a few LDS words — or learns that a prefix byte occurs in no
+// line, so the key is absent — then reads dir[B], dir[B+1]: a bucket of at
+// most 8 lines is searched with one round of prefix loads, a larger one
 // starts the fence descent at the lowest level where it spans at most 16
-// entries. Tables of fewer than 16 lines have none.
-constexpr uint32_t kDirLineBits = 2;
-__host__ __device__ inline uint32_t dir_bits(uint64_t nl) {
-  if (nl < (1ull << (kDirLineBits + 2)) || nl >= (1ull << 32)) return 0;
-  const uint32_t b = 63u - (uint32_t)__builtin_clzll(nl) - kDirLineBits;
-  return b > 24 ? 24 : b;
+// entries. A plain bit radix would leave text keys in a few huge buckets
+// (16-hex-char keys: 512 occupied buckets of ~1000 lines at 512K lines,
+// whatever the bit count); the ranks spread them over every bucket.
+// Tables of fewer than 16 lines have none.
+constexpr uint32_t kDirPos = 8;  // byte positions of the 8-byte prefix
+struct DirMap {
+  uint64_t mask[kDirPos][4];  // byte values at position j: bit v & 63 of word v >> 6
+  uint32_t pre[kDirPos];      // byte w of pre[j] = popcount(mask[j][0 .. w)), w < 4
+  uint16_t radix[kDirPos];    // digit j's radix (1 past npos)
+  uint32_t npos;              // positions whose digits name the bucket
+  uint32_t shift;             // position npos-1's digit is its rank >> shift
+  uint64_t nbuckets;          // product of the radices: dir has nbuckets + 1 entries
+};
+static_assert(sizeof(DirMap) == 320, "DirMap is staged into LDS as 20 x 16 B");
+
+// Directory size for nl lines: ~2 lines per bucket, at most 2^24 buckets.
+__host__ __device__ inline uint64_t dir_target(uint64_t nl) {
+  if (nl < 16 || nl >= (1ull << 32)) return 0;
+  return nl / 2 < (1ull << 24) ? nl / 2 : (1ull << 24);
 }
-inline uint64_t dir_words(uint64_t nl) {  // uint32 words
-  const uint32_t b = dir_bits(nl);
-  return b ? (1ull << b) + 1 : 0;
+inline uint64_t dir_words(uint64_t nl) {  // uint32 words (an upper bound of nbuckets + 1)
+  const uint64_t t = dir_target(nl);
+  return t ? t + 1 : 0;
 }
+
+// The bucket of prefix w, or false when one of its first npos bytes occurs
+// at that position in no line of the table (then no line has prefix w).
+__host__ __device__ inline bool dir_bucket(const DirMap& d, uint64_t w, uint64_t* bucket) {
+  uint64_t b = 0;
+  for (uint32_t j = 0; j < d.npos; ++j) {
+    const uint32_t c = (uint32_t)(w >> (56 - 8 * j)) & 255u;
+    const uint64_t m = d.mask[j][c >> 6];
+    if (!((m >> (c & 63)) & 1ull)) return false;
+    uint32_t r = ((d.pre[j] >> (8 * (c >> 6))) & 255u) + (uint32_t)__builtin_popcountll(m & ((1ull << (c & 63)) - 1));
+    if (j + 1 == d.npos) r >>= d.shift;
+    b = b * d.radix[j] + r;
+  }
+  *bucket = b;
+  return true;
+}
+
+// OR the byte values of every live lane's prefix w into mask[kDirPos][4]
+// (global, OR-accumulated across blocks). 256-thread blocks; call uniformly
+// (barriers inside). Each lane marks its 8 bytes in an LDS byte table, then
+// wave v ballots values 64v..64v+63 of each position: one 64-bit word of the
+// mask per ballot, ORed into global memory only when it adds bits.
+__device__ __forceinline__ void block_pfx_masks(uint64_t w, bool live, uint64_t* mask) {
+  __shared__ uint64_t seen64[kDirPos * 256 / 8];
+  uint8_t* seen = reinterpret_cast<uint8_t*>(seen64);
+  seen64[threadIdx.x] = 0;  // 256 threads x 8 B = the whole table
+  __syncthreads();
+  if (live) {
+#pragma unroll
+    for (uint32_t j = 0; j < kDirPos; ++j) seen[j * 256 + ((w >> (56 - 8 * j)) & 255u)] = 1;
+  }
+  __syncthreads();
+  const uint32_t v = threadIdx.x, wv = v >> 6;
+#pragma unroll
+  for (uint32_t j = 0; j < kDirPos; ++j) {
+    const uint64_t m = __ballot(seen[j * 256 + v] != 0);
+    if ((v & 63u) == 0 && m) {
+      uint64_t* g = mask + j * 4 + wv;
+      if ((*(volatile uint64_t*)g & m) != m) atomicOr((unsigned long long*)g, (unsigned long long)m);
+    }
+  }
+}
+
+// The DirMap of a table whose prefixes hold the byte values `mask` (OR over
+// every line), for nl lines (host).
+inline DirMap make_dirmap(const uint64_t (&mask)[kDirPos][4], uint64_t nl) {
+  DirMap d{};
+  const uint64_t target = dir_target(nl);
+  uint64_t D = 1;
+  for (uint32_t j = 0; j < kDirPos; ++j) {
+    uint32_t pre = 0, acc = 0;
+    for (uint32_t w = 0; w < 4; ++w) {
+      d.mask[j][w] = mask[j][w];
+      pre |= acc << (8 * w);
+      acc += (uint32_t)__builtin_popcountll(mask[j][w]);
+    }
+    d.pre[j] = pre;
+    d.radix[j] = 1;
+  }
+  for (uint32_t j = 0; j < kDirPos && target; ++j) {
+    uint64_t c = 0;
+    for (uint32_t w = 0; w < 4; ++w) c += (uint64_t)__builtin_popcountll(mask[j][w]);
+    if (!c) break;
+    if (D * c <= target) {
+      D *= c;
+      d.radix[j] = (uint16_t)c;
+      d.npos = j + 1;
+      continue;
+    }
+    uint32_t sh = 0;
+    while (D * (((c - 1) >> sh) + 1) > target) ++sh;
+    const uint64_t r = ((c - 1) >> sh) + 1;
+    if (r > 1) {
+      D *= r;
+      d.radix[j] = (uint16_t)r;
+      d.npos = j + 1;
+      d.shift = sh;
+    }
+    break;
+  }
+  d.nbuckets = D;
+  return d;
+}
+
 constexpr uint32_t kBadValue = 0xFFFFFFFFu;  // value that STANDARD.decode rejects
 
 // Per-line index record (32 B, one load). vdl is computed once at index
@@ -102,10 +203,8 @@ struct TableView {
   uint64_t nlines;
   uint32_t nlev;          // fence_levels(nlines)
   uint32_t fast;
-  const uint32_t* dir;    // dir_words(nlines) (nullptr: none)
-  uint32_t dbits;         // dir_bits(nlines)
-  uint32_t dshift;        // prefix bits every line shares (64: directory unused)
-  uint64_t dp0;           // pfx[0]
+  const uint32_t* dir;    // dmap->nbuckets + 1 entries (nullptr: none)
+  const DirMap* dmap;     // the directory's map (device; staged into LDS by the read path)
 };
 
 // ---- line index build: count -> scan -> emit -> finish ----
@@ -126,9 +225,14 @@ hipError_t launch_line_finish(const uint8_t* data, uint64_t len, uint64_t nlines
 hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, LineRec* rec, uint64_t* pfx,
                             uint64_t* fence, uint32_t* ok, hipStream_t s);
 
-// dir[0 .. dir_words(nlines)) of a table whose pfx is sorted (built for every
-// table; used only when the table is well-formed).
-hipError_t launch_table_dir(const uint64_t* pfx, uint64_t nlines, uint32_t* dir, hipStream_t s);
+// dir[0 .. dm.nbuckets] of a table whose pfx is sorted (built for every
+// table; used only when the table is well-formed); block 0 also stores dm at
+// dmap_out (the table's device copy).
+hipError_t launch_table_dir(const uint64_t* pfx, uint64_t nlines, const DirMap& dm, uint32_t* dir,
+                            DirMap* dmap_out, hipStream_t s);
+// mask[j][w] |= the byte values at position j of every prefix (OR; the
+// caller zeroes mask first).
+hipError_t launch_pfx_masks(const uint64_t* pfx, uint64_t nlines, uint64_t* mask, hipStream_t s);
 
 // Exclusive scan of n uint64 (out[n] = total). tmp: scan_tmp_words(n) words.
 uint64_t scan_tmp_words(uint64_t n);
