@@ -176,7 +176,7 @@ struct Workspace {
   hipEvent_t ev = nullptr;           // marks hres's first copy in the stream
 };
 
-constexpr size_t kHostScratch = 512;  // Workspace::htot bytes
+constexpr size_t kHostScratch = 16 + sizeof(uint64_t) * cb::kDirPos * 4;  // Workspace::htot bytes
 
 Workspace& workspace(int device, hipStream_t s);
 

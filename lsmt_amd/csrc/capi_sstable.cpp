@@ -200,7 +200,7 @@ int index_table(cb_table* t, hipStream_t s) {
   HIP_TRY(ws.i_cnt.reserve(nb * 8, s));
   HIP_TRY(ws.i_base.reserve((nb + 1) * 8, s));
   HIP_TRY(ws.i_tmp.reserve(cb::scan_tmp_words(nb) * 8, s));
-  HIP_TRY(ws.i_err.reserve(16 + 8 * cb::kDirPos * 4, s));  // error words, then the prefix byte masks
+  HIP_TRY(ws.i_err.reserve(16 + sizeof(uint64_t) * cb::kDirPos * 4, s));  // error words, then the prefix byte masks
   uint64_t* cnt = (uint64_t*)ws.i_cnt.p;
   uint64_t* base = (uint64_t*)ws.i_base.p;
   uint32_t* err = (uint32_t*)ws.i_err.p;
@@ -230,19 +230,17 @@ int index_table(cb_table* t, hipStream_t s) {
   HIP_TRY(cb::launch_line_keys(t->data, nl, t->rec, t->pfx, t->fence, err + 1, s));
   // the byte values of every prefix position (the directory's map)
   uint64_t* dmask = (uint64_t*)(err + 4);
-  if (t->dir) {
-    HIP_TRY(hipMemsetAsync(dmask, 0, sizeof(uint64_t) * cb::kDirPos * 4, s));
-    HIP_TRY(cb::launch_pfx_masks(t->pfx, nl, dmask, s));
-  }
+  if (t->dir) HIP_TRY(cb::launch_pfx_masks(t->pfx, nl, dmask, s));
   // the error words and the masks in one pinned copy, one wait
   if (!ws.htot) HIP_TRY(hipHostMalloc((void**)&ws.htot, kHostScratch, hipHostMallocDefault));
-  HIP_TRY(hipMemcpyAsync(ws.htot, err, 16 + (t->dir ? 8 * cb::kDirPos * 4 : 0), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(ws.htot, err, 16 + (t->dir ? sizeof(uint64_t) * cb::kDirPos * 4 : 0),
+                         hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   uint32_t e[2];
   memcpy(e, ws.htot, 8);
   if (e[0]) return fail(CB_EINVAL, "an SSTable line is 4 GiB or longer");
   t->fast = e[1] != 0 && !g_table_exact;
-  if (t->dir) {
+  if (t->dir && e[1]) {  // well-formed (sorted prefixes): the directory applies
     uint64_t m[cb::kDirPos][4];
     memcpy(m, ws.htot + 2, sizeof m);
     const cb::DirMap dm = cb::make_dirmap(m, nl);
@@ -396,7 +394,6 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   hr->flags[2] = 1;
   hr->flags[3] = 0;
   HIP_TRY(hipMemcpyAsync(dr->flags, hr->flags, 16, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemsetAsync(dr->dmask, 0, sizeof(dr->dmask), s));
   HIP_TRY(ws.f_tsum.reserve(cb::format_tiles(n) * 8, s));
   uint64_t* tsum = (uint64_t*)ws.f_tsum.p;
   HIP_TRY(cb::launch_sorted_check(dk, dko, dvo, n, dr, tsum, s));

@@ -113,7 +113,12 @@ __global__ __launch_bounds__(kNT) void k_sorted_check(const uint8_t* __restrict_
   }
   uint64_t i = 0, kl = 0, w0 = 0, w1 = 0;
   if (p < n) key_words(nullptr, kb, ko, p, i, kl, w0, w1);
-  block_pfx_masks(w0, p < n, &r->dmask[0][0]);  // the directory's alphabet (order-free)
+  if (blockIdx.x == 0)  // the directory's alphabet, from evenly spaced keys (order-free)
+    sample_pfx_masks(n, [&](uint64_t q) {
+      uint64_t a, b;
+      load16(kb + ko[q], ko[q + 1] - ko[q], a, b);
+      return a;
+    }, &r->dmask[0][0]);
   uint64_t pkl = __shfl_up(kl, 1, 64), pw0 = __shfl_up(w0, 1, 64), pw1 = __shfl_up(w1, 1, 64);
   uint64_t pi = p - 1;
   if (p < n && lane == 0 && p > 0) key_words(nullptr, kb, ko, p - 1, pi, pkl, pw0, pw1);
@@ -223,34 +228,6 @@ __device__ __forceinline__ uint32_t line16(uint64_t w0, uint64_t w1, uint32_t kl
   return kl + 2 + 4 * g;
 }
 
-// Wave-cooperative fill: every lane holds a range dir[s, s + c) to set to v.
-// The wave walks the non-empty ranges one by one, all 64 lanes storing each,
-// so one long range (a wide gap between two lines' buckets: keys whose bytes
-// leave many buckets empty) costs its length / 64 stores per lane instead of
-// one lane's serial loop. Whole wave.
-__device__ __forceinline__ void wave_fill(uint32_t* dir, uint64_t s, uint64_t c, uint32_t v) {
-  const uint32_t lane = threadIdx.x & 63u;
-  uint64_t m = __ballot(c != 0);
-  while (m) {
-    const int L = __builtin_ctzll(m);
-    m &= m - 1;
-    const uint64_t ls = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)s, L) |
-                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(s >> 32), L) << 32;
-    const uint64_t lc = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)c, L) |
-                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(c >> 32), L) << 32;
-    const uint32_t lv = (uint32_t)__builtin_amdgcn_readlane((int)v, L);
-    uint32_t* d = dir + ls;
-    uint64_t j = lane;
-    for (; j + 192 < lc; j += 256) {  // 4 contiguous 256-B stores per round
-      d[j] = lv;
-      d[j + 64] = lv;
-      d[j + 128] = lv;
-      d[j + 192] = lv;
-    }
-    for (; j < lc; j += 64) d[j] = lv;
-  }
-}
-
 // Staged output bytes per block: 16 KiB (more resident blocks) when the
 // average line is short, else 32 KiB; a block whose lines exceed the stage
 // writes its bytes directly.
@@ -340,65 +317,12 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   if (__syncthreads_or(special) && threadIdx.x == 0) atomicOr(&r->flags[1], 1u);
   if (__syncthreads_or(not_inc) && threadIdx.x == 0) atomicAnd(&r->flags[2], 0u);
   if (dir) {
-    // the byte-rank directory (sstable.hpp DirMap): dir[B] = p for the
-    // buckets B in (bucket(line p-1), bucket(line p)], and n past the last
-    // line's (every line's bytes are in the map: dir_bucket never fails here)
-    {
-      const uint64_t nb = sdm.nbuckets;
-      auto bucket = [&](uint64_t w) {
-        uint64_t b = 0;
-        (void)dir_bucket(sdm, w, &b);
-        return b;
-      };
-      uint64_t s0 = 0, c0 = 0, s1 = 0, c1 = 0;
-      if (live) {
-        const uint64_t b1 = bucket(w0);
-        s0 = p ? bucket(pw0) + 1 : 0;
-        c0 = b1 + 1 - s0;
-        if (p == n - 1) {
-          s1 = b1 + 1;
-          c1 = nb + 1 - s1;
-        }
-      }
-      // ranges longer than a wave's store go to the block's list, which all
-      // kNT threads fill together (a wide gap in the keys is one line's
-      // range: spread over the block, not one wave)
-      // (a short list: LDS per block sets how many blocks share a CU; a range
-      // that finds the list full stays with its wave)
-      constexpr uint32_t kBig = 64;
-      __shared__ uint64_t big_s[kBig], big_c[kBig];
-      __shared__ uint32_t big_v[kBig], nbig;
-      if (threadIdx.x == 0) nbig = 0;
-      __syncthreads();
-      auto defer = [&](uint64_t st, uint64_t& c, uint32_t v) {
-        if (c <= 64) return;
-        const uint32_t k = atomicAdd(&nbig, 1u);
-        if (k >= kBig) return;
-        big_s[k] = st;
-        big_c[k] = c;
-        big_v[k] = v;
-        c = 0;
-      };
-      defer(s0, c0, (uint32_t)p);
-      defer(s1, c1, (uint32_t)n);
-      wave_fill(dir, s0, c0, (uint32_t)p);
-      wave_fill(dir, s1, c1, (uint32_t)n);
-      __syncthreads();
-      const uint32_t nb_ = nbig < kBig ? nbig : kBig;
-      for (uint32_t k = 0; k < nb_; ++k) {
-        uint32_t* d = dir + big_s[k];
-        const uint64_t c = big_c[k];
-        const uint32_t v = big_v[k];
-        uint64_t j = threadIdx.x;
-        for (; j + 3 * kNT < c; j += 4 * kNT) {
-          d[j] = v;
-          d[j + kNT] = v;
-          d[j + 2 * kNT] = v;
-          d[j + 3 * kNT] = v;
-        }
-        for (; j < c; j += kNT) d[j] = v;
-      }
-    }
+    // the byte-rank directory (sstable.hpp DirMap, dir_fill): line p owns
+    // dir[B] for the buckets B in (bucket(line p-1), bucket(line p)]
+    const uint64_t b1 = live ? dir_bucket(sdm, w0) : 0;
+    uint64_t bp = __shfl_up(b1, 1, 64);  // the previous line's bucket: the neighbour lane's
+    if (live && lane == 0 && p > 0) bp = dir_bucket(sdm, pw0);
+    dir_fill(dir, sdm.nbuckets, n, p, live, b1, bp);
   }
   if (blockIdx.x == 0) zone_bound(order, kb, ko, 0, 0, r);
   if (pend == n) {

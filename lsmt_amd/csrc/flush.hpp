@@ -58,7 +58,7 @@ constexpr uint32_t kZoneInline = 256;  // zone bound key bytes carried inline
 struct CreateResult {
   uint32_t flags[4];          // [0] input sorted, [1] a key holds '\n' / '\t', [2] strictly increasing
   uint64_t ktot, vtot;        // ko[n], vo[n]
-  uint64_t dmask[kDirPos][4]; // the byte values at each position of the keys' 8-byte prefixes (DirMap)
+  uint64_t dmask[kDirPos][4]; // byte values at each position of sampled keys' 8-byte prefixes (DirMap)
   uint64_t len;               // the file's length
   uint64_t idx_min, idx_max;  // input indices of the first / last key in file order
   uint32_t zlen[2];           // their full lengths
@@ -73,8 +73,8 @@ hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, S
 constexpr uint32_t kFormatTile = 256;
 inline uint64_t format_tiles(uint64_t n) { return n ? (n + kFormatTile - 1) / kFormatTile : 1; }
 // r->flags[0] &= (keys already in non-decreasing order); r->ktot = ko[n],
-// r->vtot = vo[n]; r->dmask |= every key's prefix bytes (zeroed by the
-// caller); tsum = the line tiles in input order (valid if sorted).
+// r->vtot = vo[n]; r->dmask = the prefix bytes of kDirSample evenly spaced
+// keys; tsum = the line tiles in input order (valid if sorted).
 // Launches for any n, n = 0 included.
 hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, const uint64_t* vo, uint64_t n,
                                CreateResult* r, uint64_t* tsum, hipStream_t s);

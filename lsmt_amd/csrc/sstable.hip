@@ -499,8 +499,7 @@ constexpr uint32_t kWin = 8;  // buckets of up to this many lines: one round of 
 
 // Where x's descent starts: level j and the run [lo, hi) of at most 16
 // entries holding its lower bound (returns false), or true when x is absent
-// outright: one of its prefix bytes occurs at that position in no line, or
-// its bucket is empty. dm: the table's DirMap (LDS-staged by the read path).
+// outright: its bucket is empty. dm: the table's DirMap (LDS-staged by the read path).
 // Lines before dir[B] have smaller buckets (so smaller prefixes) and lines
 // from dir[B+1] on larger ones, so on every level the entries sampled from
 // [dir[B], dir[B+1]] bracket x's lower bound.
@@ -510,8 +509,7 @@ __device__ __forceinline__ bool dir_start(const TableView& t, const DirMap* dm, 
   lo = 0;
   hi = level_count(t.nlines, j);
   if (!t.dir) return false;
-  uint64_t bk;
-  if (!dir_bucket(*dm, x, &bk)) return true;
+  const uint64_t bk = dir_bucket(*dm, x);
   // dir[B] and dir[B + 1] as one 8-byte load (one L2 request, not two: the
   // search is bound by the requests a CU keeps in flight)
   const u32x2 ae = *(const __attribute__((address_space(1))) u32x2*)(t.dir + bk);
@@ -542,7 +540,7 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
                                                const DirMap* dm) {
   uint32_t j;
   uint64_t lo, hi;
-  // a prefix byte no line holds at that position, or an empty bucket: absent
+  // an empty bucket: absent
   if (dir_start(t, dm, q.w0, j, lo, hi)) return -1;
   if (j == 0 && hi - lo <= kWin) {
     // [lo, hi) is the key's whole bucket (or the whole table): its prefixes
@@ -592,21 +590,7 @@ __device__ __forceinline__ int64_t search(const TableView& t, const Query& q, Li
   return t.fast ? search_fast(t, q, hit, dm) : search_exact(t, q, hit);
 }
 
-// The r-th (0-based) set bit of a 256-bit mask.
-__device__ __forceinline__ uint32_t mask_select(const uint64_t (&m)[4], uint32_t r) {
-  uint32_t w = 0;
-  for (; w < 3; ++w) {
-    const uint32_t c = (uint32_t)__popcll(m[w]);
-    if (r < c) break;
-    r -= c;
-  }
-  uint64_t x = m[w];
-  for (uint32_t k = 0; k < r; ++k) x &= x - 1;
-  return 64 * w + (uint32_t)__builtin_ctzll(x);
-}
-
-// dir[B] for B in [0, nbuckets]: the lower bound of bucket B's smallest
-// prefix (its digits' byte values, zero bytes after them). Block 0 also
+// dir from the sorted prefixes, one lane per line (dir_fill). Block 0 also
 // stores the map (the table's device copy).
 __global__ __launch_bounds__(kNT) void k_table_dir(const uint64_t* __restrict__ pfx, uint64_t nl, DirMap dm,
                                                    uint32_t* __restrict__ dir, DirMap* dmap_out) {
@@ -616,27 +600,18 @@ __global__ __launch_bounds__(kNT) void k_table_dir(const uint64_t* __restrict__ 
     if (blockIdx.x == 0) *dmap_out = dm;
   }
   __syncthreads();
-  const uint64_t B = (uint64_t)blockIdx.x * kNT + threadIdx.x;
-  const uint64_t nb = sdm.nbuckets;
-  if (B > nb) return;
-  if (B == nb) {
-    dir[B] = (uint32_t)nl;
-    return;
-  }
-  uint64_t rest = B, w = 0;
-  for (int32_t j = (int32_t)sdm.npos - 1; j >= 0; --j) {
-    const uint64_t d = rest % sdm.radix[j];
-    rest /= sdm.radix[j];
-    const uint32_t rank = (uint32_t)d << ((uint32_t)j + 1 == sdm.npos ? sdm.shift : 0u);
-    w |= (uint64_t)mask_select(sdm.mask[j], rank) << (56 - 8 * j);
-  }
-  dir[B] = (uint32_t)lower_bound_u64(pfx, 0, nl, w);
+  const uint64_t p = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  const bool live = p < nl;
+  const uint64_t w = live ? pfx[p] : 0;
+  const uint64_t b = live ? dir_bucket(sdm, w) : 0;
+  uint64_t bp = __shfl_up(b, 1, 64);
+  if (live && (threadIdx.x & 63u) == 0 && p > 0) bp = dir_bucket(sdm, pfx[p - 1]);
+  dir_fill(dir, sdm.nbuckets, nl, p, live, b, bp);
 }
 
 __global__ __launch_bounds__(kNT) void k_pfx_masks(const uint64_t* __restrict__ pfx, uint64_t nl,
                                                    uint64_t* __restrict__ mask) {
-  const uint64_t l = (uint64_t)blockIdx.x * kNT + threadIdx.x;
-  block_pfx_masks(l < nl ? pfx[l] : 0, l < nl, mask);
+  sample_pfx_masks(nl, [&](uint64_t q) { return pfx[q]; }, mask);
 }
 
 // A block's views of the first min(nt, 64) tables into LDS. Barrier inside.
@@ -1111,15 +1086,14 @@ hipError_t launch_table_dir(const uint64_t* pfx, uint64_t nlines, const DirMap& 
                             DirMap* dmap_out, hipStream_t s) {
   if (!nlines || !dir || !dmap_out) return hipErrorInvalidValue;
   ProfScope ps("k_table_dir", s);
-  hipLaunchKernelGGL(k_table_dir, dim3(blocks_for(dm.nbuckets + 1, kNT)), dim3(kNT), 0, s, pfx, nlines, dm, dir,
-                     dmap_out);
+  hipLaunchKernelGGL(k_table_dir, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, pfx, nlines, dm, dir, dmap_out);
   return hipGetLastError();
 }
 
 hipError_t launch_pfx_masks(const uint64_t* pfx, uint64_t nlines, uint64_t* mask, hipStream_t s) {
   if (!nlines) return hipSuccess;
   ProfScope ps("k_pfx_masks", s);
-  hipLaunchKernelGGL(k_pfx_masks, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, pfx, nlines, mask);
+  hipLaunchKernelGGL(k_pfx_masks, dim3(1), dim3(kNT), 0, s, pfx, nlines, mask);
   return hipGetLastError();
 }
 

@@ -54,20 +54,29 @@ __device__ __forceinline__ void fence_put(uint64_t* fence, uint64_t nl, uint64_t
 }
 // Directory of a well-formed table, on a byte-rank radix of the 8-byte
 // prefix (an order-preserving compression of the key alphabet). For each
-// byte position j the table records which byte values its prefixes hold
-// (DirMap::mask); a prefix's digit j is the rank of its byte among them, the
-// bucket the mixed-radix number of its first npos digits (the last one
-// coarsened by `shift`), sized to ~2 lines per bucket. dir[B] = the first
-// line whose bucket is >= B (dir[nbuckets] = nlines). A lookup computes its
-// bucket from a few LDS words — or learns that a prefix byte occurs in no
-// line, so the key is absent — then reads dir[B], dir[B+1]: a bucket of at
-// most 8 lines is searched with one round of prefix loads, a larger one
-// starts the fence descent at the lowest level where it spans at most 16
-// entries. A plain bit radix would leave text keys in a few huge buckets
-// (16-hex-char keys: 512 occupied buckets of ~1000 lines at 512K lines,
-// whatever the bit count); the ranks spread them over every bucket.
-// Tables of fewer than 16 lines have none.
+// byte position j a DirMap records byte values the table's prefixes hold
+// (mask: from a sample of the lines); a prefix's digit j is the rank of its
+// byte among them, the bucket the mixed-radix number of its first npos
+// digits (the last one coarsened by `shift`), sized to ~2 lines per bucket.
+// dir[B] = the first line whose bucket is >= B (dir[nbuckets] = nlines). A
+// lookup computes its bucket from a few LDS words, then reads dir[B],
+// dir[B+1]: a bucket of at most 8 lines is searched with one round of prefix
+// loads, a larger one starts the fence descent at the lowest level where it
+// spans at most 16 entries. A plain bit radix leaves text keys in a few huge
+// buckets (16-hex-char keys: 512 occupied buckets of ~1000 lines at 512K
+// lines, whatever the bit count); the ranks spread them over every bucket.
+//
+// The bucket must only be monotone (x < y => bucket(x) <= bucket(y)) for
+// any prefix, sampled byte values or not: then lines before dir[B] are below
+// every key of bucket B and lines from dir[B+1] on above it, so a key's lower
+// bound lies in its bucket's window. A byte v missing from the mask at
+// position j takes the rank of the next larger value and forces the later
+// digits to 0 (v sorts before every prefix of that digit); a byte above the
+// largest value takes the last digit and forces the later digits to their
+// maximum. The sample therefore only shapes the buckets' sizes, never the
+// answers. Tables of fewer than 16 lines have none.
 constexpr uint32_t kDirPos = 8;  // byte positions of the 8-byte prefix
+constexpr uint32_t kDirSample = 8192;  // lines sampled (evenly spaced) for the masks
 struct DirMap {
   uint64_t mask[kDirPos][4];  // byte values at position j: bit v & 63 of word v >> 6
   uint32_t pre[kDirPos];      // byte w of pre[j] = popcount(mask[j][0 .. w)), w < 4
@@ -88,50 +97,37 @@ inline uint64_t dir_words(uint64_t nl) {  // uint32 words (an upper bound of nbu
   return t ? t + 1 : 0;
 }
 
-// The bucket of prefix w, or false when one of its first npos bytes occurs
-// at that position in no line of the table (then no line has prefix w).
-__host__ __device__ inline bool dir_bucket(const DirMap& d, uint64_t w, uint64_t* bucket) {
+// The bucket of prefix w (monotone in w; see above).
+__host__ __device__ inline uint64_t dir_bucket(const DirMap& d, uint64_t w) {
   uint64_t b = 0;
+  int force = 0;  // 0: exact digits; -1: later digits 0; +1: later digits at their maximum
   for (uint32_t j = 0; j < d.npos; ++j) {
-    const uint32_t c = (uint32_t)(w >> (56 - 8 * j)) & 255u;
-    const uint64_t m = d.mask[j][c >> 6];
-    if (!((m >> (c & 63)) & 1ull)) return false;
-    uint32_t r = ((d.pre[j] >> (8 * (c >> 6))) & 255u) + (uint32_t)__builtin_popcountll(m & ((1ull << (c & 63)) - 1));
-    if (j + 1 == d.npos) r >>= d.shift;
-    b = b * d.radix[j] + r;
-  }
-  *bucket = b;
-  return true;
-}
-
-// OR the byte values of every live lane's prefix w into mask[kDirPos][4]
-// (global, OR-accumulated across blocks). 256-thread blocks; call uniformly
-// (barriers inside). Each lane marks its 8 bytes in an LDS byte table, then
-// wave v ballots values 64v..64v+63 of each position: one 64-bit word of the
-// mask per ballot, ORed into global memory only when it adds bits.
-__device__ __forceinline__ void block_pfx_masks(uint64_t w, bool live, uint64_t* mask) {
-  __shared__ uint64_t seen64[kDirPos * 256 / 8];
-  uint8_t* seen = reinterpret_cast<uint8_t*>(seen64);
-  seen64[threadIdx.x] = 0;  // 256 threads x 8 B = the whole table
-  __syncthreads();
-  if (live) {
-#pragma unroll
-    for (uint32_t j = 0; j < kDirPos; ++j) seen[j * 256 + ((w >> (56 - 8 * j)) & 255u)] = 1;
-  }
-  __syncthreads();
-  const uint32_t v = threadIdx.x, wv = v >> 6;
-#pragma unroll
-  for (uint32_t j = 0; j < kDirPos; ++j) {
-    const uint64_t m = __ballot(seen[j * 256 + v] != 0);
-    if ((v & 63u) == 0 && m) {
-      uint64_t* g = mask + j * 4 + wv;
-      if ((*(volatile uint64_t*)g & m) != m) atomicOr((unsigned long long*)g, (unsigned long long)m);
+    const uint32_t R = d.radix[j];
+    uint32_t r;
+    if (force) {
+      r = force < 0 ? 0u : R - 1;
+    } else {
+      const uint32_t c = (uint32_t)(w >> (56 - 8 * j)) & 255u;
+      const uint64_t m = d.mask[j][c >> 6];
+      const uint32_t cnt = ((d.pre[j] >> 24) & 255u) + (uint32_t)__builtin_popcountll(d.mask[j][3]);
+      r = ((d.pre[j] >> (8 * (c >> 6))) & 255u) + (uint32_t)__builtin_popcountll(m & ((1ull << (c & 63)) - 1));
+      if (!((m >> (c & 63)) & 1ull)) {
+        if (r >= cnt) {  // above every sampled value: the last digit, later digits at their maximum
+          r = cnt - 1;
+          force = 1;
+        } else {  // before the next sampled value: its digit, later digits 0
+          force = -1;
+        }
+      }
+      if (j + 1 == d.npos) r >>= d.shift;
     }
+    b = b * R + r;
   }
+  return b;
 }
 
-// The DirMap of a table whose prefixes hold the byte values `mask` (OR over
-// every line), for nl lines (host).
+// The DirMap of a table whose sampled prefixes hold the byte values `mask`,
+// for nl lines (host).
 inline DirMap make_dirmap(const uint64_t (&mask)[kDirPos][4], uint64_t nl) {
   DirMap d{};
   const uint64_t target = dir_target(nl);
@@ -169,6 +165,87 @@ inline DirMap make_dirmap(const uint64_t (&mask)[kDirPos][4], uint64_t nl) {
   }
   d.nbuckets = D;
   return d;
+}
+
+// mask[kDirPos][4] := the byte values of the prefixes pfx_of(i) of kDirSample
+// evenly spaced items i of [0, n) (all of them when n is smaller). One
+// 256-thread block; each lane marks its items' bytes in an LDS byte table,
+// then wave v ballots values 64v..64v+63 of each position: one mask word per
+// ballot, stored by lane 0.
+template <class PfxOf>
+__device__ __forceinline__ void sample_pfx_masks(uint64_t n, PfxOf pfx_of, uint64_t* mask) {
+  __shared__ uint64_t seen64[kDirPos * 256 / 8];
+  uint8_t* seen = reinterpret_cast<uint8_t*>(seen64);
+  seen64[threadIdx.x] = 0;  // 256 threads x 8 B = the whole table
+  __syncthreads();
+  const uint64_t S = n < kDirSample ? n : kDirSample;
+  for (uint64_t s = threadIdx.x; s < S; s += 256) {
+    const uint64_t w = pfx_of(S == n ? s : s * n / S);
+#pragma unroll
+    for (uint32_t j = 0; j < kDirPos; ++j) seen[j * 256 + ((w >> (56 - 8 * j)) & 255u)] = 1;
+  }
+  __syncthreads();
+  const uint32_t v = threadIdx.x, wv = v >> 6;
+#pragma unroll
+  for (uint32_t j = 0; j < kDirPos; ++j) {
+    const uint64_t m = __ballot(seen[j * 256 + v] != 0);
+    if ((v & 63u) == 0) mask[j * 4 + wv] = m;
+  }
+}
+
+// Wave-cooperative fill: every lane holds a range dir[s, s + c) to set to v.
+// The wave walks the non-empty ranges one by one, all 64 lanes storing each,
+// so one long range (a wide gap between two lines' buckets) costs its length
+// / 64 stores per lane instead of one lane's serial loop. Whole wave.
+__device__ __forceinline__ void wave_fill(uint32_t* dir, uint64_t s, uint64_t c, uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t m = __ballot(c != 0);
+  while (m) {
+    const int L = __builtin_ctzll(m);
+    m &= m - 1;
+    const uint64_t ls = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)s, L) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(s >> 32), L) << 32;
+    const uint64_t lc = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)c, L) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(c >> 32), L) << 32;
+    const uint32_t lv = (uint32_t)__builtin_amdgcn_readlane((int)v, L);
+    uint32_t* d = dir + ls;
+    uint64_t j = lane;
+    for (; j + 192 < lc; j += 256) {  // 4 contiguous 256-B stores per round
+      d[j] = lv;
+      d[j + 64] = lv;
+      d[j + 128] = lv;
+      d[j + 192] = lv;
+    }
+    for (; j < lc; j += 64) d[j] = lv;
+  }
+}
+
+// The directory entries line p of nl owns, given its bucket b and the
+// previous line's bp: dir[B] = p for B in (bp, b] ([0, b] for line 0), and
+// dir[B] = nl for B in (b, nb] after the last line. Short ranges (~2 lines
+// per bucket: the common case) each lane stores itself, long ones go to
+// wave_fill. Whole wave; only live lanes own entries.
+__device__ __forceinline__ void dir_fill(uint32_t* dir, uint64_t nb, uint64_t nl, uint64_t p, bool live,
+                                         uint64_t b, uint64_t bp) {
+  uint64_t s0 = 0, c0 = 0, s1 = 0, c1 = 0;
+  if (live) {
+    s0 = p ? bp + 1 : 0;
+    c0 = b + 1 >= s0 ? b + 1 - s0 : 0;  // (prefixes are sorted: never negative)
+    if (p == nl - 1) {
+      s1 = b + 1;
+      c1 = nb + 1 - s1;
+    }
+  }
+  if (c0 && c0 <= 8) {
+    for (uint32_t k = 0; k < (uint32_t)c0; ++k) dir[s0 + k] = (uint32_t)p;
+    c0 = 0;
+  }
+  if (c1 && c1 <= 8) {
+    for (uint32_t k = 0; k < (uint32_t)c1; ++k) dir[s1 + k] = (uint32_t)nl;
+    c1 = 0;
+  }
+  wave_fill(dir, s0, c0, (uint32_t)p);
+  wave_fill(dir, s1, c1, (uint32_t)nl);
 }
 
 constexpr uint32_t kBadValue = 0xFFFFFFFFu;  // value that STANDARD.decode rejects
@@ -225,13 +302,13 @@ hipError_t launch_line_finish(const uint8_t* data, uint64_t len, uint64_t nlines
 hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, LineRec* rec, uint64_t* pfx,
                             uint64_t* fence, uint32_t* ok, hipStream_t s);
 
-// dir[0 .. dm.nbuckets] of a table whose pfx is sorted (built for every
-// table; used only when the table is well-formed); block 0 also stores dm at
-// dmap_out (the table's device copy).
+// dir[0 .. dm.nbuckets] of a table whose pfx is sorted, one lane per line
+// (dir_fill; built for every table, used only when the table is
+// well-formed); block 0 also stores dm at dmap_out (the table's device copy).
 hipError_t launch_table_dir(const uint64_t* pfx, uint64_t nlines, const DirMap& dm, uint32_t* dir,
                             DirMap* dmap_out, hipStream_t s);
-// mask[j][w] |= the byte values at position j of every prefix (OR; the
-// caller zeroes mask first).
+// mask[kDirPos][4] := the byte values of kDirSample evenly spaced prefixes
+// (sample_pfx_masks; one block).
 hipError_t launch_pfx_masks(const uint64_t* pfx, uint64_t nlines, uint64_t* mask, hipStream_t s);
 
 // Exclusive scan of n uint64 (out[n] = total). tmp: scan_tmp_words(n) words.

@@ -478,16 +478,20 @@ def _keys_hi(hi: np.ndarray, seed: int) -> np.ndarray:
     return np.unique(b, axis=0)
 
 
-@pytest.mark.parametrize("shape", ["uniform", "shared20", "shared60", "clustered", "equal"])
+@pytest.mark.parametrize("shape", ["uniform", "shared20", "shared60", "clustered", "equal", "hex", "rare", "text"])
 def test_search_directory_vs_oracle(gpu, shape):
-    """The radix directory (sstable.hpp dir_bits / dir_start) under prefix
-    distributions that move its bucket bits: uniform prefixes, 20 and 60
-    shared leading bits (the latter leaves no room: directory unused), a
-    clustered set with long runs of empty buckets, and one equal prefix.
-    Probes: present keys, absent keys, prefixes at bucket edges and prefixes
-    outside the shared bits on both sides. t.search, get_many (the staged
-    kernel, <= 64 tables) and the exact trajectory agree with the oracle."""
-    rng = np.random.default_rng({"uniform": 1, "shared20": 2, "shared60": 3, "clustered": 4, "equal": 5}[shape])
+    """The byte-rank directory (sstable.hpp DirMap / dir_bucket / dir_start)
+    under prefix distributions that move its digits: uniform prefixes, 20 and
+    60 shared leading bits, a clustered set with long runs of empty buckets,
+    one equal prefix, 16-hex-char text keys (the bench's), hex keys with a few
+    rare bytes the 8192-line sample misses ('rare': their digits are forced,
+    sstable.hpp), and 'user'+digits keys. Probes: present keys, absent keys,
+    prefixes at bucket edges, outside the key range on both sides, and keys
+    with a byte just outside the alphabet at each position. t.search,
+    get_many (the staged kernel, <= 64 tables) and the exact trajectory agree
+    with the oracle."""
+    rng = np.random.default_rng({"uniform": 1, "shared20": 2, "shared60": 3, "clustered": 4, "equal": 5,
+                                 "hex": 6, "rare": 7, "text": 8}[shape])
     for n in (255, 256, 257, 5000, 70_001):
         keys = _dir_keys(shape, n, rng)
         data = workload.sstable_bytes(keys, workload.table_value(keys, 2)).tobytes()
@@ -501,7 +505,23 @@ def test_search_directory_vs_oracle(gpu, shape):
             _check_dir_table(gpu, t2, ot, keys, rng, n)
 
 
+def _text_keys(shape, n, rng):
+    if shape == "hex":
+        return workload.sort_keys16(workload.key_range(int(rng.integers(1, 1 << 20)), n))
+    if shape == "rare":
+        k = workload.key_range(int(rng.integers(1, 1 << 20)), n).copy()
+        pick = rng.choice(n, max(1, n // 300), replace=False)
+        k[pick, rng.integers(0, 8, len(pick))] = rng.choice(np.frombuffer(b"GHXYZ~!%" + bytes(range(0xC0, 0xC8)),
+                                                                          np.uint8), len(pick))
+        return np.unique(k, axis=0)
+    d = rng.integers(0, 10, (n, 12), dtype=np.uint8) + ord("0")  # "user" + 12 digits
+    k = np.concatenate([np.frombuffer(b"user", np.uint8)[None, :].repeat(n, 0), d], 1)
+    return np.unique(k, axis=0)
+
+
 def _dir_keys(shape, n, rng):
+    if shape in ("hex", "rare", "text"):
+        return _text_keys(shape, n, rng)
     if shape == "uniform":
         hi = rng.integers(0, 1 << 64, n, dtype=np.uint64)
     elif shape == "shared20":
@@ -528,7 +548,12 @@ def _check_dir_table(gpu, t, ot, keys, rng, n):
     edges += [0, (1 << 64) - 1, int(h.min()) - 1 if h.min() else 0, int(h.max()) + 1 if h.max() < (1 << 64) - 1 else 0]
     eh = np.array(edges, dtype=np.uint64)
     absent = _keys_hi(np.concatenate([eh, rng.integers(0, 1 << 64, 2000, dtype=np.uint64)]), 7)
-    look = np.concatenate([keys[rng.integers(0, len(keys), 3000)], absent, keys[:1], keys[-1:]])
+    # present keys with one prefix byte moved just outside / inside the
+    # alphabet at each position (bytes the directory's sample never saw)
+    near = keys[rng.integers(0, len(keys), 400)].copy()
+    pos = rng.integers(0, 8, len(near))
+    near[np.arange(len(near)), pos] = rng.choice(np.frombuffer(b"/:@`gG\x00\xff\x7f0af9", np.uint8), len(near))
+    look = np.concatenate([keys[rng.integers(0, len(keys), 3000)], absent, near, keys[:1], keys[-1:]])
     exp = [ot.search(bytes(k))[0] for k in look]
     assert list(t.search(look)) == exp, n
     which, voff, vals = gpu.get_many([t], look)
