@@ -230,7 +230,10 @@ int index_table(cb_table* t, hipStream_t s) {
   HIP_TRY(cb::launch_line_keys(t->data, nl, t->rec, t->pfx, t->fence, err + 1, s));
   // the byte values of every prefix position (the directory's map)
   uint64_t* dmask = (uint64_t*)(err + 4);
-  if (t->dir) HIP_TRY(cb::launch_pfx_masks(t->pfx, nl, dmask, s));
+  if (t->dir) {
+    HIP_TRY(hipMemsetAsync(dmask, 0, sizeof(uint64_t) * cb::kDirPos * 4, s));
+    HIP_TRY(cb::launch_pfx_masks(t->pfx, nl, dmask, s));
+  }
   // the error words and the masks in one pinned copy, one wait
   if (!ws.htot) HIP_TRY(hipHostMalloc((void**)&ws.htot, kHostScratch, hipHostMallocDefault));
   HIP_TRY(hipMemcpyAsync(ws.htot, err, 16 + (t->dir ? sizeof(uint64_t) * cb::kDirPos * 4 : 0),
@@ -394,6 +397,7 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   hr->flags[2] = 1;
   hr->flags[3] = 0;
   HIP_TRY(hipMemcpyAsync(dr->flags, hr->flags, 16, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(dr->dmask, 0, sizeof(dr->dmask), s));
   HIP_TRY(ws.f_tsum.reserve(cb::format_tiles(n) * 8, s));
   uint64_t* tsum = (uint64_t*)ws.f_tsum.p;
   HIP_TRY(cb::launch_sorted_check(dk, dko, dvo, n, dr, tsum, s));

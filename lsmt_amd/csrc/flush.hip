@@ -113,7 +113,7 @@ __global__ __launch_bounds__(kNT) void k_sorted_check(const uint8_t* __restrict_
   }
   uint64_t i = 0, kl = 0, w0 = 0, w1 = 0;
   if (p < n) key_words(nullptr, kb, ko, p, i, kl, w0, w1);
-  if (blockIdx.x == 0)  // the directory's alphabet, from evenly spaced keys (order-free)
+  if (blockIdx.x < kSampleBlocks)  // the directory's alphabet, from evenly spaced keys (order-free)
     sample_pfx_masks(n, [&](uint64_t q) {
       uint64_t a, b;
       load16(kb + ko[q], ko[q + 1] - ko[q], a, b);

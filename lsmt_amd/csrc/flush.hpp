@@ -73,8 +73,9 @@ hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, S
 constexpr uint32_t kFormatTile = 256;
 inline uint64_t format_tiles(uint64_t n) { return n ? (n + kFormatTile - 1) / kFormatTile : 1; }
 // r->flags[0] &= (keys already in non-decreasing order); r->ktot = ko[n],
-// r->vtot = vo[n]; r->dmask = the prefix bytes of kDirSample evenly spaced
-// keys; tsum = the line tiles in input order (valid if sorted).
+// r->vtot = vo[n]; r->dmask |= the prefix bytes of kDirSample evenly spaced
+// keys (zeroed by the caller); tsum = the line tiles in input order (valid
+// if sorted).
 // Launches for any n, n = 0 included.
 hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, const uint64_t* vo, uint64_t n,
                                CreateResult* r, uint64_t* tsum, hipStream_t s);

@@ -1093,7 +1093,7 @@ hipError_t launch_table_dir(const uint64_t* pfx, uint64_t nlines, const DirMap& 
 hipError_t launch_pfx_masks(const uint64_t* pfx, uint64_t nlines, uint64_t* mask, hipStream_t s) {
   if (!nlines) return hipSuccess;
   ProfScope ps("k_pfx_masks", s);
-  hipLaunchKernelGGL(k_pfx_masks, dim3(1), dim3(kNT), 0, s, pfx, nlines, mask);
+  hipLaunchKernelGGL(k_pfx_masks, dim3(kSampleBlocks), dim3(kNT), 0, s, pfx, nlines, mask);
   return hipGetLastError();
 }
 

@@ -167,29 +167,43 @@ inline DirMap make_dirmap(const uint64_t (&mask)[kDirPos][4], uint64_t nl) {
   return d;
 }
 
-// mask[kDirPos][4] := the byte values of the prefixes pfx_of(i) of kDirSample
-// evenly spaced items i of [0, n) (all of them when n is smaller). One
-// 256-thread block; each lane marks its items' bytes in an LDS byte table,
-// then wave v ballots values 64v..64v+63 of each position: one mask word per
-// ballot, stored by lane 0.
+// mask[kDirPos][4] |= the byte values of the prefixes pfx_of(i) of
+// kDirSample evenly spaced items i of [0, n) (all of them when n is
+// smaller), over the first kSampleBlocks 256-thread blocks of a launch (the
+// caller zeroes mask; other blocks return at once). Each lane loads its
+// kSamplePer items together, marks their bytes in an LDS byte table, then
+// wave v ballots values 64v..64v+63 of each position: one mask word per
+// ballot, ORed into global memory by lane 0 (8 blocks x 32 atomics).
+constexpr uint32_t kSampleBlocks = 8, kSamplePer = 4;
+static_assert(kSampleBlocks * 256 * kSamplePer == kDirSample, "sample size");
 template <class PfxOf>
 __device__ __forceinline__ void sample_pfx_masks(uint64_t n, PfxOf pfx_of, uint64_t* mask) {
+  if (blockIdx.x >= kSampleBlocks) return;
   __shared__ uint64_t seen64[kDirPos * 256 / 8];
   uint8_t* seen = reinterpret_cast<uint8_t*>(seen64);
   seen64[threadIdx.x] = 0;  // 256 threads x 8 B = the whole table
-  __syncthreads();
   const uint64_t S = n < kDirSample ? n : kDirSample;
-  for (uint64_t s = threadIdx.x; s < S; s += 256) {
-    const uint64_t w = pfx_of(S == n ? s : s * n / S);
+  uint64_t w[kSamplePer];
 #pragma unroll
-    for (uint32_t j = 0; j < kDirPos; ++j) seen[j * 256 + ((w >> (56 - 8 * j)) & 255u)] = 1;
+  for (uint32_t k = 0; k < kSamplePer; ++k) {  // every load in flight together
+    const uint64_t sidx = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * kSamplePer + k;
+    w[k] = sidx < S ? pfx_of(S == n ? sidx : sidx * n / S) : 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < kSamplePer; ++k) {
+    const uint64_t sidx = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * kSamplePer + k;
+    if (sidx < S) {
+#pragma unroll
+      for (uint32_t j = 0; j < kDirPos; ++j) seen[j * 256 + ((w[k] >> (56 - 8 * j)) & 255u)] = 1;
+    }
   }
   __syncthreads();
   const uint32_t v = threadIdx.x, wv = v >> 6;
 #pragma unroll
   for (uint32_t j = 0; j < kDirPos; ++j) {
     const uint64_t m = __ballot(seen[j * 256 + v] != 0);
-    if ((v & 63u) == 0) mask[j * 4 + wv] = m;
+    if ((v & 63u) == 0 && m) atomicOr((unsigned long long*)(mask + j * 4 + wv), (unsigned long long)m);
   }
 }
 
@@ -307,8 +321,8 @@ hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, LineRec* rec, 
 // well-formed); block 0 also stores dm at dmap_out (the table's device copy).
 hipError_t launch_table_dir(const uint64_t* pfx, uint64_t nlines, const DirMap& dm, uint32_t* dir,
                             DirMap* dmap_out, hipStream_t s);
-// mask[kDirPos][4] := the byte values of kDirSample evenly spaced prefixes
-// (sample_pfx_masks; one block).
+// mask[kDirPos][4] |= the byte values of kDirSample evenly spaced prefixes
+// (sample_pfx_masks; kSampleBlocks blocks; the caller zeroes mask).
 hipError_t launch_pfx_masks(const uint64_t* pfx, uint64_t nlines, uint64_t* mask, hipStream_t s);
 
 // Exclusive scan of n uint64 (out[n] = total). tmp: scan_tmp_words(n) words.
