@@ -431,17 +431,38 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
     *table_out = t.release();
     return CB_OK;
   }
-  if (!sorted) {
-    // stable sort by key (memtable flushes arrive sorted and skip this)
-    HIP_TRY(ws.f_sk2.reserve(n * sizeof(cb::SortKey), s));
-    cb::SortKey* a1 = (cb::SortKey*)ws.f_sk2.p;
-    // records built inside the block sort; the last round also leaves the
-    // value spans and the line tiles in sorted order for k_format
+  // stable sort by key (memtable flushes arrive sorted and skip this). Both
+  // sorts leave the value spans and the line tiles in sorted order for
+  // k_format. merge: LDS block sorts, then merge-path rounds; bin: one
+  // binning pass over the directory map's buckets and one LDS sort per
+  // group (sort.hip), falling back to the merge sort when a group outgrows
+  // an LDS tile (flags[3], read at round trip 2).
+  bool binned = false;
+  auto merge_sort = [&]() -> int {
     HIP_TRY(ws.f_sort.reserve(cb::entry_sort_tmp_bytes(n), s));
+    HIP_TRY(cb::launch_entry_sort(nullptr, (cb::SortKey*)ws.f_sk2.p, (cb::SortKey*)ws.f_sort.p, n, dk, dko, s,
+                                  dvo, vsp, tsum));
+    return CB_OK;
+  };
+  if (!sorted) {
+    HIP_TRY(ws.f_sk2.reserve(n * sizeof(cb::SortKey), s));
     HIP_TRY(ws.f_vsp.reserve(n * sizeof(ulonglong2), s));
     vsp = (ulonglong2*)ws.f_vsp.p;
-    HIP_TRY(cb::launch_entry_sort(nullptr, a1, (cb::SortKey*)ws.f_sort.p, n, dk, dko, s, dvo, vsp, tsum));
-    order = a1;
+    order = (cb::SortKey*)ws.f_sk2.p;
+    static const uint32_t bin_T = [] {
+      const char* v = getenv("CB_BIN_T");  // group size target (tests, tuning); 0 disables the bin sort
+      return v && *v ? (uint32_t)atoi(v) : 1536u;
+    }();
+    if (bin_T && bin_T <= cb::bin_sort_max_group() && n > 4096 && n <= (1ull << 24)) {
+      const cb::DirMap bm = cb::make_dirmap(hr->dmask, n, cb::bin_sort_max_bins());
+      if (bm.nbuckets >= 2) {
+        HIP_TRY(ws.f_sort.reserve(cb::bin_sort_tmp_bytes(n, bm.nbuckets, bin_T), s));
+        HIP_TRY(cb::launch_bin_sort(dk, dko, n, bm, bin_T, (cb::SortKey*)ws.f_sk2.p, ws.f_sort.p, s, dvo, vsp,
+                                    tsum, &dr->flags[3]));
+        binned = true;
+      }
+    }
+    if (!binned && (rc = merge_sort())) return rc;
   }
   HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
   // the line index straight from the entries (entry p is line p), no re-read of the file
@@ -457,11 +478,27 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
     dm = cb::make_dirmap(hr->dmask, n);
     t->dmap = dmap_slot(t.get());
   }
-  HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, tsum, n, t->data, t->rec, t->pfx, t->fence, dr,
-                            cap_bytes, s, vsp, t->dir, t->dir ? &dm : nullptr, t->dmap));
-  // Round trip 2: flags, file length, zone bounds
-  HIP_TRY(hipMemcpyAsync(hr, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  auto format = [&]() -> int {
+    HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, tsum, n, t->data, t->rec, t->pfx, t->fence, dr,
+                              cap_bytes, s, vsp, t->dir, t->dir ? &dm : nullptr, t->dmap));
+    // Round trip 2: flags, file length, zone bounds
+    HIP_TRY(hipMemcpyAsync(hr, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return CB_OK;
+  };
+  if ((rc = format())) return rc;
+  if (binned && hr->flags[3]) {
+    // the bin sort overflowed (a bin of more than an LDS tile: keys sharing a
+    // long prefix): the merge sort, then the file again from clean flags
+    hr->flags[0] = 0;
+    hr->flags[1] = 0;
+    hr->flags[2] = 1;
+    hr->flags[3] = 0;
+    HIP_TRY(hipMemcpyAsync(dr->flags, hr->flags, 16, hipMemcpyHostToDevice, s));
+    if ((rc = merge_sort())) return rc;
+    HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
+    if ((rc = format())) return rc;
+  }
   t->len = hr->len;
   // zone map: ZoneMap::update over the sorted keys = first / last line
   if (zone_min_idx) *zone_min_idx = hr->idx_min;

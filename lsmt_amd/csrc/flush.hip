@@ -123,10 +123,10 @@ __global__ __launch_bounds__(kNT) void k_sorted_check(const uint8_t* __restrict_
   uint64_t pi = p - 1;
   if (p < n && lane == 0 && p > 0) key_words(nullptr, kb, ko, p - 1, pi, pkl, pw0, pw1);
   const bool bad = p < n && p > 0 && key_cmp(kb, ko, p - 1, pkl, pw0, pw1, p, kl, w0, w1) > 0;
-  // one atomic per block, and none once the flag is down: a fully unsorted
-  // batch would otherwise serialise up to a million atomics on one word
-  uint32_t* ok = &r->flags[0];
-  if (__syncthreads_or(bad) && threadIdx.x == 0 && *(volatile uint32_t*)ok) atomicAnd(ok, 0u);
+  // one plain store of 0 per block holding an inversion (every writer
+  // writes the same value): a fully unsorted batch would otherwise queue a
+  // returning load and an atomic per block on one word
+  if (__syncthreads_or(bad) && threadIdx.x == 0) r->flags[0] = 0u;
 }
 
 

@@ -20,6 +20,12 @@ struct SortKey {
 // these loads stay inside mapped memory however src is aligned).
 __device__ __forceinline__ void load16(const uint8_t* src, uint64_t len, uint64_t& w0, uint64_t& w1) {
   const uint64_t m = len < 16 ? len : 16;
+  if (m == 16 && !((uintptr_t)src & 15)) {  // an aligned 16-byte key (fixed-length batches): one dwordx4
+    const uint4 v = *reinterpret_cast<const uint4*>(src);
+    w0 = (uint64_t)__builtin_bswap32(v.x) << 32 | __builtin_bswap32(v.y);
+    w1 = (uint64_t)__builtin_bswap32(v.z) << 32 | __builtin_bswap32(v.w);
+    return;
+  }
   uint32_t d[5] = {0, 0, 0, 0, 0};
   const uint64_t a0 = (uint64_t)(uintptr_t)src;
   const uint32_t* base = reinterpret_cast<const uint32_t*>((uintptr_t)(a0 & ~3ull));
@@ -56,7 +62,8 @@ __host__ __device__ inline uint64_t line_len(uint64_t kl, uint64_t vl) { return 
 // each of its two host round trips is one copy into pinned memory.
 constexpr uint32_t kZoneInline = 256;  // zone bound key bytes carried inline
 struct CreateResult {
-  uint32_t flags[4];          // [0] input sorted, [1] a key holds '\n' / '\t', [2] strictly increasing
+  uint32_t flags[4];          // [0] input sorted, [1] a key holds '\n' / '\t', [2] strictly increasing,
+                              // [3] the bin sort overflowed (redo with the merge sort)
   uint64_t ktot, vtot;        // ko[n], vo[n]
   uint64_t dmask[kDirPos][4]; // byte values at each position of sampled keys' 8-byte prefixes (DirMap)
   uint64_t len;               // the file's length
@@ -93,6 +100,17 @@ uint64_t entry_sort_tmp_bytes(uint64_t n);
 hipError_t launch_entry_sort(const SortKey* in, SortKey* out, SortKey* tmp, uint64_t n, const uint8_t* kb,
                              const uint64_t* ko, hipStream_t s, const uint64_t* vo = nullptr,
                              ulonglong2* vsp = nullptr, uint64_t* tsum = nullptr);
+// The same order by binning (sort.hip "bin sort"): dm's buckets over the
+// keys' prefixes as bins (monotone in the key), groups of ~T records sorted
+// in LDS; out = the sorted records, vsp / tsum as launch_entry_sort's tail.
+// tmp: bin_sort_tmp_bytes. *overflow |= 1 when a group outgrew an LDS tile
+// (out is then incomplete: redo with launch_entry_sort).
+uint64_t bin_sort_tmp_bytes(uint64_t n, uint64_t nbins, uint32_t T);
+uint32_t bin_sort_max_bins();   // dm.nbuckets at most
+uint32_t bin_sort_max_group();  // T at most (one LDS tile)
+hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, const DirMap& dm, uint32_t T,
+                           SortKey* out, void* tmp, hipStream_t s, const uint64_t* vo, ulonglong2* vsp,
+                           uint64_t* tsum, uint32_t* overflow);
 // The file (lines at the offsets tsum and the line lengths give, then 16
 // zero bytes of slack), its
 // line index without re-reading it (sstable.hpp layout: entry p is line p),

@@ -21,11 +21,13 @@
 //       of up to 2^20 records), stages the two input pieces in LDS and merges
 //       them as in the block sort; loads and stores are coalesced through LDS.
 // Records make (1 + rounds) round trips through HBM: 48 MB per round at 1M
-// entries. The last launch also writes what k_format needs in sorted order
+// entries. cb_sstable_create uses it for batches the bin sort below cannot
+// take (a bin larger than one LDS tile, or too few entries). The last launch also writes what k_format needs in sorted order
 // (value spans and line-tile sums), from the records in its registers, so
 // no separate pass gathers them through the permutation.
 #include <hip/hip_runtime.h>
 
+#include "blockscan.hpp"
 #include "flush.hpp"
 #include "profile.hpp"
 #include "zone.hpp"
@@ -77,16 +79,18 @@ __device__ __forceinline__ SortKey sentinel() {
 // different banks (record i sits at word i + i/8 of each array).
 constexpr uint32_t kPadBits = 3;
 constexpr uint32_t kPadded = kTile + (kTile >> kPadBits);
-__device__ __forceinline__ uint32_t pad(uint32_t i) { return i + (i >> kPadBits); }
 
-struct LdsTile {
-  uint64_t* w;  // 3 * kPadded words
+// P: words per field array; PAD: record i at word i + i / 8 (else i).
+template <uint32_t P, bool PAD>
+struct LdsTileT {
+  uint64_t* w;  // 3 * P words
+  static __device__ __forceinline__ uint32_t pad(uint32_t i) { return PAD ? i + (i >> kPadBits) : i; }
   __device__ __forceinline__ SortKey get(uint32_t i) const {
     const uint32_t j = pad(i);
-    const uint64_t li = w[2 * kPadded + j];
+    const uint64_t li = w[2 * P + j];
     SortKey r;
     r.w0 = w[j];
-    r.w1 = w[kPadded + j];
+    r.w1 = w[P + j];
     r.len = (uint32_t)li;
     r.idx = (uint32_t)(li >> 32);
     return r;
@@ -94,13 +98,14 @@ struct LdsTile {
   __device__ __forceinline__ void set(uint32_t i, const SortKey& r) const {
     const uint32_t j = pad(i);
     w[j] = r.w0;
-    w[kPadded + j] = r.w1;
-    w[2 * kPadded + j] = (uint64_t)r.len | (uint64_t)r.idx << 32;
+    w[P + j] = r.w1;
+    w[2 * P + j] = (uint64_t)r.len | (uint64_t)r.idx << 32;
   }
   // global record words -> LDS: word g of the records is field g % 3 of record g / 3
-  __device__ __forceinline__ void put_word(uint32_t g, uint64_t v) const { w[(g % 3) * kPadded + pad(g / 3)] = v; }
-  __device__ __forceinline__ uint64_t word(uint32_t g) const { return w[(g % 3) * kPadded + pad(g / 3)]; }
+  __device__ __forceinline__ void put_word(uint32_t g, uint64_t v) const { w[(g % 3) * P + pad(g / 3)] = v; }
+  __device__ __forceinline__ uint64_t word(uint32_t g) const { return w[(g % 3) * P + pad(g / 3)]; }
 };
+using LdsTile = LdsTileT<kPadded, true>;
 
 // What the last launch of a sort also writes (vo == nullptr: nothing): per
 // output p, vsp[p] = {value offset, value length} of its entry, and per
@@ -141,15 +146,17 @@ __device__ __forceinline__ void emit_tail(const SortTail& tl, const SortKey (&r)
 // Records move between global memory and LDS as 8-byte words (3 per record),
 // consecutive threads on consecutive words; past cnt the tile holds
 // sentinels (greater than every record).
-__device__ __forceinline__ void tile_load(const SortKey* __restrict__ g, uint32_t cnt, const LdsTile& t) {
+template <uint32_t NT = kST, uint32_t TILE = kTile, class Tile = LdsTile>
+__device__ __forceinline__ void tile_load(const SortKey* __restrict__ g, uint32_t cnt, const Tile& t) {
   const uint64_t* gw = reinterpret_cast<const uint64_t*>(g);
-  for (uint32_t i = threadIdx.x; i < 3 * cnt; i += kST) t.put_word(i, gw[i]);
-  for (uint32_t i = cnt + threadIdx.x; i < kTile; i += kST) t.set(i, sentinel());
+  for (uint32_t i = threadIdx.x; i < 3 * cnt; i += NT) t.put_word(i, gw[i]);
+  for (uint32_t i = cnt + threadIdx.x; i < TILE; i += NT) t.set(i, sentinel());
 }
 
-__device__ __forceinline__ void tile_store(const LdsTile& t, SortKey* __restrict__ g, uint32_t cnt) {
+template <uint32_t NT = kST, class Tile = LdsTile>
+__device__ __forceinline__ void tile_store(const Tile& t, SortKey* __restrict__ g, uint32_t cnt) {
   uint64_t* gw = reinterpret_cast<uint64_t*>(g);
-  for (uint32_t i = threadIdx.x; i < 3 * cnt; i += kST) gw[i] = t.word(i);
+  for (uint32_t i = threadIdx.x; i < 3 * cnt; i += NT) gw[i] = t.word(i);
 }
 
 // Merge-path split of diagonal d between sorted a[0..la) and b[0..lb): the
@@ -161,7 +168,10 @@ __device__ __forceinline__ uint32_t merge_split(const A& a, uint32_t la, const B
   uint32_t lo = d > lb ? d - lb : 0, hi = d < la ? d : la;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (less(b[d - mid - 1], a[mid]))
+    // the first key words decide almost every step: the rest of the two
+    // records is read only on a tie (a third of the LDS reads)
+    const uint64_t x = b.w0(d - mid - 1), y = a.w0(mid);
+    if (x != y ? x < y : less(b[d - mid - 1], a[mid]))
       hi = mid;
     else
       lo = mid + 1;
@@ -170,11 +180,14 @@ __device__ __forceinline__ uint32_t merge_split(const A& a, uint32_t la, const B
 }
 
 // A run of records inside the LDS tile, starting at record `base`.
-struct LdsRun {
-  LdsTile t;
+template <class Tile = LdsTile>
+struct LdsRunT {
+  Tile t;
   uint32_t base;
   __device__ __forceinline__ SortKey operator[](uint32_t i) const { return t.get(base + i); }
+  __device__ __forceinline__ uint64_t w0(uint32_t i) const { return t.w[Tile::pad(base + i)]; }
 };
+using LdsRun = LdsRunT<>;
 
 // Up to kIPT outputs from a[i..la) and b[j..lb), in order; sentinels once
 // both are exhausted.
@@ -322,9 +335,294 @@ __global__ __launch_bounds__(kST) void k_sort_merge(const SortKey* __restrict__ 
   tile_store(tile, out + o0, tot);
 }
 
+// ---- bin sort: one pass to bin the records, one LDS sort per group of bins ----
+//
+// The bins are the buckets of a DirMap over the keys' 8-byte prefixes (its
+// byte masks sampled by k_sorted_check; sstable.hpp), at most kBins of them:
+// a monotone function of the key, so every record of bin b sorts before
+// every record of bin b + 1. As in a radix sort pass, without global
+// atomics: k_bin_count leaves each block's bin histogram (LDS) in cnt;
+// k_bin_offsets turns every bin's column into the blocks' exclusive offsets
+// and the bin's total; k_bin_plan scans the totals (start[b]) and cuts the
+// bins into groups of ~T records (group g starts at the first bin starting
+// at or after g * T); k_bin_scatter writes each record into its bin's range
+// (LDS cursors; any order inside a bin); k_bin_sort sorts one group in LDS by
+// the full record order (index last: the stable order) and writes what
+// k_format needs. A group larger than an LDS tile (a bin holding more than
+// kBinTile - T records: keys sharing a long prefix) sets
+// CreateResult::flags[3] and the caller redoes the sort with the merge sort.
+// Records make 2 round trips through HBM instead of 9, and the group sorts
+// (2048-record tiles, three blocks per CU) run as one wave at 1M entries.
+
+constexpr uint32_t kBins = 4096;         // bins at most (one 16-KiB LDS histogram)
+constexpr uint32_t kBinNT = 1024;        // count / scatter threads (16 waves: loads in flight)
+constexpr uint32_t kBinPer = 4;          // records per count / scatter thread
+constexpr uint32_t kBinChunk = kBinNT * kBinPer;  // records per count / scatter block
+constexpr uint32_t kBinST = 512;         // group-sort threads
+constexpr uint32_t kBinTile = kBinST * kIPT;      // records per group sort
+// padded by 1/16 (record i at word i + i / 16): 3 x 2176 x 8 B = 51 KiB, so
+// three blocks share a CU (1/8 padding would leave room for two)
+template <uint32_t TILE>
+struct LdsTile16 {
+  static constexpr uint32_t P = TILE + TILE / 16;
+  uint64_t* w;
+  static __device__ __forceinline__ uint32_t pad(uint32_t i) { return i + (i >> 4); }
+  __device__ __forceinline__ SortKey get(uint32_t i) const {
+    const uint32_t j = pad(i);
+    const uint64_t li = w[2 * P + j];
+    SortKey r;
+    r.w0 = w[j];
+    r.w1 = w[P + j];
+    r.len = (uint32_t)li;
+    r.idx = (uint32_t)(li >> 32);
+    return r;
+  }
+  __device__ __forceinline__ void set(uint32_t i, const SortKey& r) const {
+    const uint32_t j = pad(i);
+    w[j] = r.w0;
+    w[P + j] = r.w1;
+    w[2 * P + j] = (uint64_t)r.len | (uint64_t)r.idx << 32;
+  }
+  __device__ __forceinline__ void put_word(uint32_t g, uint64_t v) const { w[(g % 3) * P + pad(g / 3)] = v; }
+  __device__ __forceinline__ uint64_t word(uint32_t g) const { return w[(g % 3) * P + pad(g / 3)]; }
+};
+using BinTile = LdsTile16<kBinTile>;
+
+__global__ __launch_bounds__(kBinNT) void k_bin_count(const uint8_t* __restrict__ kb, const uint64_t* __restrict__ ko,
+                                                      uint64_t n, DirMap dm, uint32_t* __restrict__ cnt) {
+  __shared__ DirMap sdm;
+  __shared__ uint32_t hist[kBins];
+  const uint64_t p0 = (uint64_t)blockIdx.x * kBinChunk + threadIdx.x;
+  uint64_t w0[kBinPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kBinPer; ++k) {  // every key load in flight together
+    const uint64_t p = p0 + (uint64_t)k * kBinNT;
+    uint64_t w1;
+    w0[k] = 0;
+    if (p < n) load16(kb + ko[p], ko[p + 1] - ko[p], w0[k], w1);
+  }
+  if (threadIdx.x == 0) sdm = dm;
+  for (uint32_t b = threadIdx.x; b < kBins; b += kBinNT) hist[b] = 0;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < kBinPer; ++k)
+    if (p0 + (uint64_t)k * kBinNT < n) atomicAdd(&hist[dir_bucket(sdm, w0[k])], 1u);
+  __syncthreads();
+  const uint32_t nb = (uint32_t)sdm.nbuckets;
+  for (uint32_t b = threadIdx.x; b < nb; b += kBinNT) cnt[(uint64_t)blockIdx.x * nb + b] = hist[b];
+}
+
+// cnt[blk][b] := the blocks' exclusive offsets inside bin b; total[b] = its
+// size. A block takes 64 bins (the lanes: each row of cnt is read 256 B at a
+// time) and splits the nblk rows among its 16 waves; the waves' row sums are
+// joined in LDS.
+constexpr uint32_t kOffW = 16;  // waves per k_bin_offsets block
+__global__ __launch_bounds__(kOffW * 64) void k_bin_offsets(uint32_t* __restrict__ cnt, uint32_t nblk, uint32_t nb,
+                                                            uint32_t* __restrict__ total) {
+  __shared__ uint32_t part[kOffW][64];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, b = blockIdx.x * 64 + lane;
+  const uint32_t per = (nblk + kOffW - 1) / kOffW, k0 = wv * per, k1 = k0 + per < nblk ? k0 + per : nblk;
+  uint32_t sum = 0;
+  if (b < nb)
+    for (uint32_t k = k0; k < k1; ++k) sum += cnt[(uint64_t)k * nb + b];
+  part[wv][lane] = sum;
+  __syncthreads();
+  uint32_t run = 0, tot = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kOffW; ++w) {
+    const uint32_t v = part[w][lane];
+    run += w < wv ? v : 0u;
+    tot += v;
+  }
+  if (b >= nb) return;
+  for (uint32_t k = k0; k < k1; ++k) {
+    const uint32_t v = cnt[(uint64_t)k * nb + b];
+    cnt[(uint64_t)k * nb + b] = run;
+    run += v;
+  }
+  if (wv == 0) total[b] = tot;
+}
+
+// One block: start[b] = exclusive scan of total (start[nb] = n),
+// gstart[g] = the start of the first bin starting at or after g * T
+// (gstart[0] = 0, gstart[G] = n).
+__global__ __launch_bounds__(1024) void k_bin_plan(const uint32_t* __restrict__ total, uint32_t nb, uint64_t n,
+                                                   uint32_t T, uint32_t G, uint32_t* __restrict__ start,
+                                                   uint32_t* __restrict__ gstart) {
+  constexpr uint32_t kPer = kBins / 1024;
+  const uint32_t i0 = threadIdx.x * kPer;
+  uint32_t v[kPer];
+  uint64_t sum = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) {
+    v[j] = i0 + j < nb ? total[i0 + j] : 0u;
+    sum += v[j];
+  }
+  uint64_t tot;
+  uint64_t pre = block_scan<1024>(sum, &tot);
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) {
+    if (i0 + j < nb) {
+      const uint64_t st = pre, e = pre + v[j];
+      start[i0 + j] = (uint32_t)st;
+      // the non-empty bins' ranges (st, e] tile (0, n]: a multiple g * T in
+      // this one means the first bin starting at or after it starts at e
+      for (uint64_t g = st / T + 1; g * T <= e && g < G; ++g) gstart[g] = (uint32_t)e;
+    }
+    pre += v[j];
+  }
+  if (threadIdx.x == 0) {
+    start[nb] = (uint32_t)n;
+    gstart[0] = 0;
+    gstart[G] = (uint32_t)n;
+  }
+}
+
+__global__ __launch_bounds__(kBinNT) void k_bin_scatter(const uint8_t* __restrict__ kb,
+                                                        const uint64_t* __restrict__ ko, uint64_t n, DirMap dm,
+                                                        const uint32_t* __restrict__ cnt,
+                                                        const uint32_t* __restrict__ start,
+                                                        SortKey* __restrict__ out) {
+  __shared__ DirMap sdm;
+  __shared__ uint32_t cur[kBins];
+  const uint64_t p0 = (uint64_t)blockIdx.x * kBinChunk + threadIdx.x;
+  SortKey r[kBinPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kBinPer; ++k) {
+    const uint64_t p = p0 + (uint64_t)k * kBinNT;
+    if (p < n) r[k] = sort_record(kb, ko, p);
+  }
+  if (threadIdx.x == 0) sdm = dm;
+  const uint32_t nb = (uint32_t)dm.nbuckets;
+  for (uint32_t b = threadIdx.x; b < nb; b += kBinNT) cur[b] = start[b] + cnt[(uint64_t)blockIdx.x * nb + b];
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < kBinPer; ++k)
+    if (p0 + (uint64_t)k * kBinNT < n) out[atomicAdd(&cur[dir_bucket(sdm, r[k].w0)], 1u)] = r[k];
+}
+
+// One group [gstart[g], gstart[g + 1]) per block: the k_sort_block network
+// on the group's records, then vsp / tsum for k_format (tsum zeroed by the
+// caller: a group's outputs are not aligned to format tiles, so each wave
+// adds its share of the (at most two) tiles its 256 outputs touch) and the
+// sorted records.
+__global__ __launch_bounds__(kBinST) void k_bin_sort(const SortKey* __restrict__ in, SortKey* __restrict__ out,
+                                                     const uint32_t* __restrict__ gstart, RecLess less,
+                                                     const uint64_t* __restrict__ vo, ulonglong2* __restrict__ vsp,
+                                                     uint64_t* __restrict__ tsum, uint32_t* __restrict__ overflow) {
+  static_assert(kFormatTile == 64 * kIPT, "a wave's outputs span at most two format tiles");
+  __shared__ uint64_t lds[3 * BinTile::P];
+  const BinTile tile{lds};
+  const uint64_t beg = gstart[blockIdx.x], end = gstart[blockIdx.x + 1];
+  if (end <= beg) return;
+  if (end - beg > kBinTile) {  // a bin too large for one tile: the caller falls back to the merge sort
+    if (threadIdx.x == 0) atomicOr(overflow, 1u);
+    return;
+  }
+  const uint32_t cnt = (uint32_t)(end - beg);
+  tile_load<kBinST, kBinTile>(in + beg, cnt, tile);
+  __syncthreads();
+  SortKey r[kIPT];
+  const uint32_t t0 = threadIdx.x * kIPT;
+#pragma unroll
+  for (uint32_t k = 0; k < kIPT; ++k) r[k] = tile.get(t0 + k);
+#pragma unroll
+  for (uint32_t q = 0; q < kIPT; ++q) {
+#pragma unroll
+    for (uint32_t k = q & 1; k + 1 < kIPT; k += 2) cas(r[k], r[k + 1], less);
+  }
+  uint32_t span = kIPT;  // the network only as wide as the group
+  while (span < cnt) span <<= 1;
+  for (uint32_t w = kIPT; w < span; w <<= 1) {
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kIPT; ++k) tile.set(t0 + k, r[k]);
+    __syncthreads();
+    const uint32_t pb = t0 & ~(2 * w - 1), d = t0 - pb;
+    const LdsRunT<BinTile> a{tile, pb}, b{tile, pb + w};
+    const uint32_t i = merge_split(a, w, b, w, d, less);
+    merge_seq(a, w, b, w, i, d - i, r, less);
+  }
+  // value spans, and the line lengths of this wave's outputs into the two
+  // format tiles they can touch
+  const uint64_t wbase = beg + (uint64_t)(threadIdx.x & ~63u) * kIPT;
+  const uint64_t tlo = wbase / kFormatTile;
+  uint64_t s_lo = 0, s_hi = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kIPT; ++k) {
+    if (t0 + k < cnt) {
+      const uint32_t i = r[k].idx;
+      const uint64_t v0 = vo[i], vl = vo[i + 1] - v0;
+      const uint64_t kl = r[k].len != 0xFFFFFFFFu ? r[k].len : less.ko[i + 1] - less.ko[i];
+      const uint64_t p = beg + t0 + k;
+      vsp[p] = make_ulonglong2(v0, vl);
+      (p / kFormatTile == tlo ? s_lo : s_hi) += line_len(kl, vl);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    s_lo += __shfl_xor(s_lo, o, 64);
+    s_hi += __shfl_xor(s_hi, o, 64);
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    if (s_lo) atomicAdd((unsigned long long*)&tsum[tlo], (unsigned long long)s_lo);
+    if (s_hi) atomicAdd((unsigned long long*)&tsum[tlo + 1], (unsigned long long)s_hi);
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < kIPT; ++k) tile.set(t0 + k, r[k]);
+  __syncthreads();
+  tile_store<kBinST>(tile, out + beg, cnt);
+}
+
 }  // namespace
 
 uint64_t entry_sort_tmp_bytes(uint64_t n) { return n * sizeof(SortKey); }
+
+uint64_t bin_sort_tmp_bytes(uint64_t n, uint64_t nbins, uint32_t T) {
+  const uint64_t G = (n + T - 1) / T, nblk = (n + kBinChunk - 1) / kBinChunk;
+  return n * sizeof(SortKey) + (nblk * nbins + 2 * (nbins + 1) + G + 1) * 4;
+}
+
+uint32_t bin_sort_max_bins() { return kBins; }
+uint32_t bin_sort_max_group() { return kBinTile; }
+
+hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, const DirMap& dm, uint32_t T,
+                           SortKey* out, void* tmp, hipStream_t s, const uint64_t* vo, ulonglong2* vsp,
+                           uint64_t* tsum, uint32_t* overflow) {
+  if (!n) return hipSuccess;
+  const uint32_t nb = (uint32_t)dm.nbuckets;
+  if (nb < 1 || nb > kBins || !T || T > kBinTile) return hipErrorInvalidValue;
+  const uint32_t G = (uint32_t)((n + T - 1) / T);
+  const uint32_t nblk = (uint32_t)((n + kBinChunk - 1) / kBinChunk);
+  SortKey* binned = (SortKey*)tmp;
+  uint32_t* cnt = (uint32_t*)(binned + n);         // nblk x nb
+  uint32_t* total = cnt + (uint64_t)nblk * nb;      // nb + 1
+  uint32_t* start = total + nb + 1;                 // nb + 1
+  uint32_t* gstart = start + nb + 1;                // G + 1
+  hipError_t e = hipMemsetAsync(tsum, 0, format_tiles(n) * 8, s);
+  if (e != hipSuccess) return e;
+  {
+    ProfScope ps("k_bin_count", s);
+    hipLaunchKernelGGL(k_bin_count, dim3(nblk), dim3(kBinNT), 0, s, kb, ko, n, dm, cnt);
+  }
+  {
+    ProfScope ps("k_bin_offsets", s);
+    hipLaunchKernelGGL(k_bin_offsets, dim3((nb + 63) / 64), dim3(kOffW * 64), 0, s, cnt, nblk, nb, total);
+  }
+  {
+    ProfScope ps("k_bin_plan", s);
+    hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(1024), 0, s, total, nb, n, T, G, start, gstart);
+  }
+  {
+    ProfScope ps("k_bin_scatter", s);
+    hipLaunchKernelGGL(k_bin_scatter, dim3(nblk), dim3(kBinNT), 0, s, kb, ko, n, dm, cnt, start, binned);
+  }
+  ProfScope ps("k_bin_sort", s);
+  hipLaunchKernelGGL(k_bin_sort, dim3(G), dim3(kBinST), 0, s, binned, out, gstart, RecLess{kb, ko}, vo, vsp, tsum,
+                     overflow);
+  return hipGetLastError();
+}
 
 hipError_t launch_entry_sort(const SortKey* in, SortKey* out, SortKey* tmp, uint64_t n, const uint8_t* kb,
                              const uint64_t* ko, hipStream_t s, const uint64_t* vo, ulonglong2* vsp,

@@ -127,10 +127,10 @@ __host__ __device__ inline uint64_t dir_bucket(const DirMap& d, uint64_t w) {
 }
 
 // The DirMap of a table whose sampled prefixes hold the byte values `mask`,
-// for nl lines (host).
-inline DirMap make_dirmap(const uint64_t (&mask)[kDirPos][4], uint64_t nl) {
+// for nl lines: ~target buckets (default dir_target(nl)) (host).
+inline DirMap make_dirmap(const uint64_t (&mask)[kDirPos][4], uint64_t nl, uint64_t target = ~0ull) {
   DirMap d{};
-  const uint64_t target = dir_target(nl);
+  if (target == ~0ull) target = dir_target(nl);
   uint64_t D = 1;
   for (uint32_t j = 0; j < kDirPos; ++j) {
     uint32_t pre = 0, acc = 0;

@@ -183,16 +183,32 @@ def test_table_zone_only_for_created_tables(gpu):
 @pytest.mark.parametrize("n,shape", [(2, "random"), (2047, "random"), (2048, "descending"), (2049, "random"),
                                      (4095, "random"), (4096, "descending"), (4097, "equal"), (8193, "random"),
                                      (6145, "equal"), (70_001, "long"), (300_001, "random"),
-                                     (1 << 20, "descending")])
+                                     (1 << 20, "descending"), (20_000, "hot"), (100_000, "skew"),
+                                     (50_000, "text")])
 def test_create_sort_sizes(gpu, n, shape):
-    """The hand-written stable sort of unsorted flush batches (sort.hip: LDS
-    block sorts of 4096 records, then merge-path rounds) across tile and
-    round boundaries: random keys, reversed keys, all-equal keys (pure
-    stability) and long keys sharing 16-byte prefixes; the file must equal
-    the oracle's stable sort + format (src/sstable.rs:57-72)."""
+    """The hand-written stable sorts of unsorted flush batches (sort.hip):
+    the bin sort for n > 4096 (one binning pass over the directory map's
+    buckets, one LDS sort per group) and, below that or when a group outgrows
+    an LDS tile, the merge sort (LDS block sorts of 4096 records, then
+    merge-path rounds). Random keys, reversed keys, all-equal keys (pure
+    stability; one bin: the fallback), long keys sharing 16-byte prefixes
+    (the fallback), one key repeated 6000 times among random ones (a hot bin:
+    the fallback), 90 % of the keys under one 4-byte prefix (skewed bins) and
+    'user'+digits text keys; the file must equal the oracle's stable sort +
+    format (src/sstable.rs:57-72)."""
     rng = np.random.default_rng(n)
     if shape == "equal":
         keys = [b"same-key"] * n
+    elif shape == "hot":
+        keys = [bytes(r) for r in workload.key_range(6000 + n, n)]
+        for i in rng.choice(n, 6000, replace=False):
+            keys[i] = b"0123456789abcdef"
+    elif shape == "skew":
+        keys = [bytes(r) for r in workload.key_range(7000 + n, n)]
+        for i in rng.choice(n, 9 * n // 10, replace=False):
+            keys[i] = b"aaaa" + keys[i][4:]
+    elif shape == "text":
+        keys = [b"user%012d" % int(x) for x in rng.integers(0, 10 ** 9, n)]
     elif shape == "long":
         pre = [bytes(rng.integers(97, 100, 16, dtype=np.uint8)) for _ in range(7)]
         keys = [pre[i % 7] + bytes(rng.integers(97, 99, rng.integers(0, 12), dtype=np.uint8)) for i in range(n)]
