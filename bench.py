@@ -50,6 +50,9 @@ def parse():
                         "(m=2^25) split over the GPUs")
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--leg-steps", type=int, default=200,
+                   help="steps of each secondary leg (build, read path, zone, flush/4, rotating, one lane): "
+                        "at least --steps; the headline leg times exactly --steps")
     p.add_argument("--n-keys", type=int, default=1 << 20)
     p.add_argument("--filters", type=int, default=32, help="filters per GPU")
     p.add_argument("--m-bits", type=int, default=1 << 26)
@@ -318,9 +321,11 @@ def main():
         torch.cuda.synchronize(dev)  # all streams: every exchange of the K steps is inside
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        # every stream is idle here, so the lanes' first steps (issued after
+        # e0) cannot start before it; no cross-stream wait is issued: each
+        # wait_stream costs ~9 us of host time, which at K = 20 delays the
+        # first step (and every step after it) by ~19 us
         e0.record(stream)
-        for st in lane_streams[1:]:
-            st.wait_stream(stream)  # the other lanes start after e0
         for _ in range(k):
             fn()
         for st in lane_streams[1:]:
@@ -337,6 +342,9 @@ def main():
             el = float(t.item())
         return el
 
+    # secondary legs time LK steps: a sub-0.1 ms step timed 20 times is mostly
+    # the region's fill and drain (the headline leg keeps exactly --steps)
+    LK = max(args.steps, args.leg_steps)
     probes_per_step = n * nf_total
     legs = {}
     for name, fn in (("tiled", step_tiled), ("filterset", step_set)):
@@ -437,10 +445,10 @@ def main():
 
         for _ in range(args.warmup):
             step_rot()
-        rel = timed(step_rot, args.steps)
-        rprof = kernel_ms(probe_kernels, step_rot, args.steps)
-        rot = {"value": round(probes_per_step / (rel / args.steps), 1),
-               "ms_per_step": round(rel / args.steps * 1e3, 4),
+        rel = timed(step_rot, LK)
+        rprof = kernel_ms(probe_kernels, step_rot, LK)
+        rot = {"value": round(probes_per_step / (rel / LK), 1),
+               "ms_per_step": round(rel / LK * 1e3, 4), "steps": LK,
                "kernels_us": {k: round(v["avg_us"], 2) for k, v in rprof.items()},
                "batches": nrot}
         del rot_keys
@@ -469,7 +477,7 @@ def main():
 
         for _ in range(args.warmup):
             step_one()
-        timed(step_one, args.steps)
+        timed(step_one, LK)
         one_lane_us = region["ms"] * 1e3 / region["k"]
 
     roof = None
@@ -545,11 +553,11 @@ def main():
 
         for _ in range(args.warmup):
             step_gated()
-        gel = timed(step_gated, args.steps)
-        gprof = kernel_ms(["k_set_probe_gated"], step_gated, args.steps)
+        gel = timed(step_gated, LK)
+        gprof = kernel_ms(["k_set_probe_gated"], step_gated, LK)
         gated_hits = int(np.unpackbits(hits_bufs[(step_no[0] - 1) % P].cpu().numpy().view(np.uint8)).sum())
-        zone = {"value": round(probes_per_step / (gel / args.steps), 1), "unit": "gated probes/s",
-                "ms_per_step": round(gel / args.steps * 1e3, 4),
+        zone = {"value": round(probes_per_step / (gel / LK), 1), "unit": "gated probes/s",
+                "ms_per_step": round(gel / LK * 1e3, 4), "steps": LK,
                 "kernels_us": {k: round(v["avg_us"], 2) for k, v in gprof.items()},
                 "zone_build_keys_per_s": round(F * kpf / zone_build_s, 1),
                 "gated_hits_last_step": gated_hits,
@@ -611,10 +619,10 @@ def main():
                              ("fused", step_fused, ["k_set_get_many", "k_tile_scan", "k_b64_decode"])):
             for _ in range(args.warmup):
                 fn()
-            el_r = timed(fn, args.steps)
-            rprof = kernel_ms(kn, fn, args.steps)
+            el_r = timed(fn, LK)
+            rprof = kernel_ms(kn, fn, LK)
             torch.cuda.synchronize(dev)
-            rforms[name] = {"value": round(n / (el_r / args.steps), 1), "ms_per_step": round(el_r / args.steps * 1e3, 4),
+            rforms[name] = {"value": round(n / (el_r / LK), 1), "ms_per_step": round(el_r / LK * 1e3, 4), "steps": LK,
                             "kernels_us": {k: round(v["avg_us"], 2) for k, v in rprof.items()},
                             "which": which_l[0].clone(), "voff": voff_l[0].clone()}
             assert all(torch.equal(which_l[0], w) and torch.equal(voff_l[0], v) for w, v in zip(which_l, voff_l))
@@ -681,7 +689,7 @@ def main():
 
             for _ in range(max(1, args.warmup)):
                 step_flush()
-            k_fl = max(3, args.steps // 4)
+            k_fl = max(3, LK // 4)
             fel = timed(step_flush, k_fl)
             fprof = kernel_ms(["k_sorted_check", "k_entry_sort", "k_bin_count", "k_bin_offsets", "k_bin_plan", "k_bin_scatter", "k_bin_sort", "k_tile_scan",
                                "k_format", "k_line_count", "k_line_emit", "k_line_finish", "k_line_keys",
@@ -690,6 +698,7 @@ def main():
             if label == "unsorted" and rank == 0 and world == 1 and not args.no_cpu:
                 flush_file = made[-1][0].data()  # checked against the oracle below
             res[label] = {"entries_per_s": round(nf_e / (fel / k_fl), 1), "ms_per_flush": round(fel / k_fl * 1e3, 3),
+                          "flushes": k_fl,
                           "file_bytes": out_bytes, "file_GBps": round(out_bytes / (fel / k_fl) / 1e9, 2),
                           "kernels_us": {k: round(v["avg_us"], 2) for k, v in fprof.items()}}
             del made, kd, vd, ko
@@ -724,8 +733,8 @@ def main():
 
     for _ in range(args.warmup):
         build_step()
-    bel = timed(build_step, args.steps)
-    bprof = kernel_ms(["k_build_part", "k_build_tile", "k_insert_direct"], build_step, args.steps)
+    bel = timed(build_step, LK)
+    bprof = kernel_ms(["k_build_part", "k_build_tile", "k_insert_direct"], build_step, LK)
     bcold = None
     if not args.no_cold:
         bcold_ms, bcold_k = cold_run(["k_build_part", "k_build_tile", "k_insert_direct"], build_step)
@@ -742,11 +751,11 @@ def main():
         del o
     b_alg = 16 * args.build_keys + args.build_m_bits / 8
     build = {"metric": "build keys/s (C2: 1M 16-B keys -> one 16 MiB filter, m=2^27)",
-             "value": round(args.build_keys * world / (bel / args.steps), 1), "unit": "keys/s",
-             "ms_per_step": round(bel / args.steps * 1e3, 4), "path": int(L.cb_last_path()),
+             "value": round(args.build_keys * world / (bel / LK), 1), "unit": "keys/s",
+             "ms_per_step": round(bel / LK * 1e3, 4), "steps": LK, "path": int(L.cb_last_path()),
              "kernels": {k: round(v["avg_us"], 2) for k, v in bprof.items()},
              "algorithmic_bytes": int(b_alg),
-             "step_effective_GBps": round(b_alg / (bel / args.steps) / 1e9, 1),
+             "step_effective_GBps": round(b_alg / (bel / LK) / 1e9, 1),
              "pipeline_lanes": P, "cold": bcold}
 
     # ---- PCIe-inclusive end-to-end probe (pinned host keys -> host hits)
@@ -996,17 +1005,18 @@ def zone_partitioned_leg(args, torch, dev, local, sh, F, m, kpf, n, timed, kerne
     def step():
         fset.probe(keys, out=gated, stream=sh, gated=True)
 
+    LK = max(args.steps, args.leg_steps)
     for _ in range(args.warmup):
         step()
-    el = timed(step, args.steps)
-    prof = kernel_ms(["k_set_probe_gated"], step, args.steps)
+    el = timed(step, LK)
+    prof = kernel_ms(["k_set_probe_gated"], step, LK)
     torch.cuda.synchronize(dev)
     g = gated.cpu().numpy().view(np.uint64)
     pl = plain.cpu().numpy().view(np.uint64)
     bits = lambda a: int(np.unpackbits(a.view(np.uint8)).sum())
     bloom_pass, gate_pass = bits(pl), bits(g)
-    out = {"value": round(probes_per_step / (el / args.steps), 1), "unit": "gated probes/s",
-           "ms_per_step": round(el / args.steps * 1e3, 4),
+    out = {"value": round(probes_per_step / (el / LK), 1), "unit": "gated probes/s",
+           "ms_per_step": round(el / LK * 1e3, 4), "steps": LK,
            "kernels_us": {k: round(v["avg_us"], 2) for k, v in prof.items()},
            "bloom_pass_pairs": bloom_pass, "gate_pass_pairs": gate_pass,
            "zone_rejected_fraction_of_bloom_pass": round(1 - gate_pass / max(bloom_pass, 1), 4),
