@@ -449,10 +449,14 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
     HIP_TRY(ws.f_vsp.reserve(n * sizeof(ulonglong2), s));
     vsp = (ulonglong2*)ws.f_vsp.p;
     order = (cb::SortKey*)ws.f_sk2.p;
-    static const uint32_t bin_T = [] {
+    static const int bin_T_env = [] {
       const char* v = getenv("CB_BIN_T");  // group size target (tests, tuning); 0 disables the bin sort
-      return v && *v ? (uint32_t)atoi(v) : 1536u;
+      return v && *v ? atoi(v) : -1;
     }();
+    // groups of ~n / 1536 records (six 1024-record group sorts per CU on 256
+    // CUs, one wave), at least 640, at most 1536 (2048-record group sorts)
+    const uint32_t bin_T = bin_T_env >= 0 ? (uint32_t)bin_T_env
+                                          : (uint32_t)std::min<uint64_t>(1536, std::max<uint64_t>(640, (n + 1535) / 1536));
     if (bin_T && bin_T <= cb::bin_sort_max_group() && n > 4096 && n <= (1ull << 24)) {
       const cb::DirMap bm = cb::make_dirmap(hr->dmask, n, cb::bin_sort_max_bins());
       if (bm.nbuckets >= 2) {

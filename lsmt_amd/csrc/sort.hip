@@ -349,19 +349,24 @@ __global__ __launch_bounds__(kST) void k_sort_merge(const SortKey* __restrict__ 
 // (LDS cursors; any order inside a bin); k_bin_sort sorts one group in LDS by
 // the full record order (index last: the stable order) and writes what
 // k_format needs. A group larger than an LDS tile (a bin holding more than
-// kBinTile - T records: keys sharing a long prefix) sets
+// tile - T records: keys sharing a long prefix) sets
 // CreateResult::flags[3] and the caller redoes the sort with the merge sort.
 // Records make 2 round trips through HBM instead of 9, and the group sorts
-// (2048-record tiles, three blocks per CU) run as one wave at 1M entries.
+// run as one wave at 1M entries.
 
-constexpr uint32_t kBins = 4096;         // bins at most (one 16-KiB LDS histogram)
+constexpr uint32_t kBins = 8192;         // bins at most (one 32-KiB LDS histogram)
 constexpr uint32_t kBinNT = 1024;        // count / scatter threads (16 waves: loads in flight)
 constexpr uint32_t kBinPer = 4;          // records per count / scatter thread
 constexpr uint32_t kBinChunk = kBinNT * kBinPer;  // records per count / scatter block
-constexpr uint32_t kBinST = 512;         // group-sort threads
-constexpr uint32_t kBinTile = kBinST * kIPT;      // records per group sort
-// padded by 1/16 (record i at word i + i / 16): 3 x 2176 x 8 B = 51 KiB, so
-// three blocks share a CU (1/8 padding would leave room for two)
+// Group sorts: 256 threads x 4 records (26 KiB of LDS, six blocks per CU)
+// for groups of <= 1024 records, 512 x 4 (51 KiB, three per CU) up to 2048.
+// A CU's share of the sort is what sets the time (the blocks all run in one
+// wave): at 1M entries 1536 groups of ~683 fill 6 x 256 slots evenly, where
+// 683 groups of ~1536 left a third of the CUs with two groups and the rest
+// with three.
+constexpr uint32_t kBinTileMax = 2048;    // records per group sort, at most
+// LDS tiles padded by 1/16 (record i at word i + i / 16): 3 x 2176 x 8 B =
+// 51 KiB for 2048 records (1/8 padding would leave room for two per CU)
 template <uint32_t TILE>
 struct LdsTile16 {
   static constexpr uint32_t P = TILE + TILE / 16;
@@ -386,7 +391,6 @@ struct LdsTile16 {
   __device__ __forceinline__ void put_word(uint32_t g, uint64_t v) const { w[(g % 3) * P + pad(g / 3)] = v; }
   __device__ __forceinline__ uint64_t word(uint32_t g) const { return w[(g % 3) * P + pad(g / 3)]; }
 };
-using BinTile = LdsTile16<kBinTile>;
 
 __global__ __launch_bounds__(kBinNT) void k_bin_count(const uint8_t* __restrict__ kb, const uint64_t* __restrict__ ko,
                                                       uint64_t n, DirMap dm, uint32_t* __restrict__ cnt) {
@@ -446,35 +450,35 @@ __global__ __launch_bounds__(kOffW * 64) void k_bin_offsets(uint32_t* __restrict
 // One block: start[b] = exclusive scan of total (start[nb] = n),
 // gstart[g] = the start of the first bin starting at or after g * T
 // (gstart[0] = 0, gstart[G] = n).
-__global__ __launch_bounds__(1024) void k_bin_plan(const uint32_t* __restrict__ total, uint32_t nb, uint64_t n,
+__global__ __launch_bounds__(1024) void k_bin_plan(const uint32_t* __restrict__ total, uint32_t nb, uint32_t n,
                                                    uint32_t T, uint32_t G, uint32_t* __restrict__ start,
                                                    uint32_t* __restrict__ gstart) {
-  constexpr uint32_t kPer = kBins / 1024;
+  constexpr uint32_t kPer = kBins / 1024;  // n < 2^32 here: 32-bit sums and divisions
   const uint32_t i0 = threadIdx.x * kPer;
-  uint32_t v[kPer];
-  uint64_t sum = 0;
+  uint32_t v[kPer], sum = 0;
 #pragma unroll
   for (uint32_t j = 0; j < kPer; ++j) {
     v[j] = i0 + j < nb ? total[i0 + j] : 0u;
     sum += v[j];
   }
   uint64_t tot;
-  uint64_t pre = block_scan<1024>(sum, &tot);
+  uint32_t pre = (uint32_t)block_scan<1024>(sum, &tot);
+  uint32_t g = pre / T + 1;  // the next group start to place
 #pragma unroll
   for (uint32_t j = 0; j < kPer; ++j) {
     if (i0 + j < nb) {
-      const uint64_t st = pre, e = pre + v[j];
-      start[i0 + j] = (uint32_t)st;
-      // the non-empty bins' ranges (st, e] tile (0, n]: a multiple g * T in
+      const uint32_t e = pre + v[j];
+      start[i0 + j] = pre;
+      // the non-empty bins' ranges (pre, e] tile (0, n]: a multiple g * T in
       // this one means the first bin starting at or after it starts at e
-      for (uint64_t g = st / T + 1; g * T <= e && g < G; ++g) gstart[g] = (uint32_t)e;
+      for (; (uint64_t)g * T <= e && g < G; ++g) gstart[g] = e;
     }
     pre += v[j];
   }
   if (threadIdx.x == 0) {
-    start[nb] = (uint32_t)n;
+    start[nb] = n;
     gstart[0] = 0;
-    gstart[G] = (uint32_t)n;
+    gstart[G] = n;
   }
 }
 
@@ -506,21 +510,24 @@ __global__ __launch_bounds__(kBinNT) void k_bin_scatter(const uint8_t* __restric
 // caller: a group's outputs are not aligned to format tiles, so each wave
 // adds its share of the (at most two) tiles its 256 outputs touch) and the
 // sorted records.
-__global__ __launch_bounds__(kBinST) void k_bin_sort(const SortKey* __restrict__ in, SortKey* __restrict__ out,
+template <uint32_t NT>
+__global__ __launch_bounds__(NT) void k_bin_sort(const SortKey* __restrict__ in, SortKey* __restrict__ out,
                                                      const uint32_t* __restrict__ gstart, RecLess less,
                                                      const uint64_t* __restrict__ vo, ulonglong2* __restrict__ vsp,
                                                      uint64_t* __restrict__ tsum, uint32_t* __restrict__ overflow) {
   static_assert(kFormatTile == 64 * kIPT, "a wave's outputs span at most two format tiles");
+  constexpr uint32_t TILE = NT * kIPT;
+  using BinTile = LdsTile16<TILE>;
   __shared__ uint64_t lds[3 * BinTile::P];
   const BinTile tile{lds};
   const uint64_t beg = gstart[blockIdx.x], end = gstart[blockIdx.x + 1];
   if (end <= beg) return;
-  if (end - beg > kBinTile) {  // a bin too large for one tile: the caller falls back to the merge sort
+  if (end - beg > TILE) {  // a bin too large for one tile: the caller falls back to the merge sort
     if (threadIdx.x == 0) atomicOr(overflow, 1u);
     return;
   }
   const uint32_t cnt = (uint32_t)(end - beg);
-  tile_load<kBinST, kBinTile>(in + beg, cnt, tile);
+  tile_load<NT, TILE>(in + beg, cnt, tile);
   __syncthreads();
   SortKey r[kIPT];
   const uint32_t t0 = threadIdx.x * kIPT;
@@ -572,7 +579,7 @@ __global__ __launch_bounds__(kBinST) void k_bin_sort(const SortKey* __restrict__
 #pragma unroll
   for (uint32_t k = 0; k < kIPT; ++k) tile.set(t0 + k, r[k]);
   __syncthreads();
-  tile_store<kBinST>(tile, out + beg, cnt);
+  tile_store<NT>(tile, out + beg, cnt);
 }
 
 }  // namespace
@@ -585,14 +592,14 @@ uint64_t bin_sort_tmp_bytes(uint64_t n, uint64_t nbins, uint32_t T) {
 }
 
 uint32_t bin_sort_max_bins() { return kBins; }
-uint32_t bin_sort_max_group() { return kBinTile; }
+uint32_t bin_sort_max_group() { return kBinTileMax; }
 
 hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, const DirMap& dm, uint32_t T,
                            SortKey* out, void* tmp, hipStream_t s, const uint64_t* vo, ulonglong2* vsp,
                            uint64_t* tsum, uint32_t* overflow) {
   if (!n) return hipSuccess;
   const uint32_t nb = (uint32_t)dm.nbuckets;
-  if (nb < 1 || nb > kBins || !T || T > kBinTile) return hipErrorInvalidValue;
+  if (nb < 1 || nb > kBins || !T || T > kBinTileMax) return hipErrorInvalidValue;
   const uint32_t G = (uint32_t)((n + T - 1) / T);
   const uint32_t nblk = (uint32_t)((n + kBinChunk - 1) / kBinChunk);
   SortKey* binned = (SortKey*)tmp;
@@ -612,15 +619,19 @@ hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, co
   }
   {
     ProfScope ps("k_bin_plan", s);
-    hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(1024), 0, s, total, nb, n, T, G, start, gstart);
+    hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(1024), 0, s, total, nb, (uint32_t)n, T, G, start, gstart);
   }
   {
     ProfScope ps("k_bin_scatter", s);
     hipLaunchKernelGGL(k_bin_scatter, dim3(nblk), dim3(kBinNT), 0, s, kb, ko, n, dm, cnt, start, binned);
   }
   ProfScope ps("k_bin_sort", s);
-  hipLaunchKernelGGL(k_bin_sort, dim3(G), dim3(kBinST), 0, s, binned, out, gstart, RecLess{kb, ko}, vo, vsp, tsum,
-                     overflow);
+  if (T <= 768)  // 1024-record tiles: room for bins of up to 1024 - T records past the target
+    hipLaunchKernelGGL(k_bin_sort<256>, dim3(G), dim3(256), 0, s, binned, out, gstart, RecLess{kb, ko}, vo, vsp,
+                       tsum, overflow);
+  else
+    hipLaunchKernelGGL(k_bin_sort<512>, dim3(G), dim3(512), 0, s, binned, out, gstart, RecLess{kb, ko}, vo, vsp,
+                       tsum, overflow);
   return hipGetLastError();
 }
 

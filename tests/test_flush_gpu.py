@@ -183,12 +183,14 @@ def test_table_zone_only_for_created_tables(gpu):
 @pytest.mark.parametrize("n,shape", [(2, "random"), (2047, "random"), (2048, "descending"), (2049, "random"),
                                      (4095, "random"), (4096, "descending"), (4097, "equal"), (8193, "random"),
                                      (6145, "equal"), (70_001, "long"), (300_001, "random"),
-                                     (1 << 20, "descending"), (20_000, "hot"), (100_000, "skew"),
+                                     (1 << 20, "descending"), (1_300_000, "random"), (20_000, "hot"),
+                                     (100_000, "skew"),
                                      (50_000, "text")])
 def test_create_sort_sizes(gpu, n, shape):
     """The hand-written stable sorts of unsorted flush batches (sort.hip):
     the bin sort for n > 4096 (one binning pass over the directory map's
-    buckets, one LDS sort per group) and, below that or when a group outgrows
+    buckets, one LDS sort per group: 1024-record group sorts up to ~1.18M
+    entries, 2048-record ones above) and, below that or when a group outgrows
     an LDS tile, the merge sort (LDS block sorts of 4096 records, then
     merge-path rounds). Random keys, reversed keys, all-equal keys (pure
     stability; one bin: the fallback), long keys sharing 16-byte prefixes
