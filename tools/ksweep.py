@@ -13,7 +13,9 @@ import lsmt_amd  # noqa: E402
 from lsmt_amd import workload  # noqa: E402
 
 dev = torch.device("cuda:0")
-F, m, kpf, n, P = 32, 1 << 26, 1 << 19, 1 << 20, 3
+import os
+F, m, kpf, n = 32, 1 << 26, 1 << 19, 1 << 20
+P = int(os.environ.get("LANES", "3"))
 stream = torch.cuda.current_stream(dev)
 filters = []
 for f in range(F):
@@ -64,7 +66,7 @@ def region(k, warm, per_step=False, waits=True):
     e1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    out = {"k": k, "waits": waits, "wall_us_per_step": round(wall / k * 1e6, 2),
+    out = {"lanes": P, "k": k, "waits": waits, "wall_us_per_step": round(wall / k * 1e6, 2),
            "region_us_per_step": round(e0.elapsed_time(e1) * 1e3 / k, 2),
            "issue_us_per_step": round(t_issue / k * 1e6, 2)}
     if per_step:
@@ -74,27 +76,8 @@ def region(k, warm, per_step=False, waits=True):
 
 
 res = []
-for k in (20, 200, 20):
-    res.append(region(k, 5))
+for k in (20, 200, 20, 20, 20):
     res.append(region(k, 5, waits=False))
-res.append(region(20, 5, per_step=True))
 res.append(region(20, 5, per_step=True, waits=False))
-# host cost of the region's first calls
-torch.cuda.synchronize(dev)
-t = [time.perf_counter()]
-e0 = torch.cuda.Event(enable_timing=True)
-e0.record(stream)
-t.append(time.perf_counter())
-lanes[1].wait_stream(stream)
-t.append(time.perf_counter())
-lanes[2].wait_stream(stream)
-t.append(time.perf_counter())
-step()
-t.append(time.perf_counter())
-step()
-t.append(time.perf_counter())
-torch.cuda.synchronize(dev)
-print(json.dumps({"host_us": [round((b - a) * 1e6, 1) for a, b in zip(t, t[1:])],
-                  "labels": ["e0.record", "wait_stream", "wait_stream", "step", "step"]}))
 for r in res:
     print(json.dumps(r))
