@@ -4,7 +4,10 @@
 // Database::get's newest-first walk (cb_get_many_*).
 //
 // Reference: /root/reference/src/sstable.rs:51-179, src/lib.rs:125-136.
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <cstring>
 
 #include "capi_internal.hpp"
@@ -318,6 +321,20 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   if (bloom_out) *bloom_out = nullptr;
   if (zone_min_idx) *zone_min_idx = ~0ull;
   if (zone_max_idx) *zone_max_idx = ~0ull;
+  static const bool trace = getenv("CB_FLUSH_TRACE") != nullptr;  // diagnostic: host timeline to stderr
+  struct Marks {
+    bool on;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    std::string line;
+    void operator()(const char* what) {
+      if (!on) return;
+      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      line += std::string(what) + "=" + std::to_string((int)us) + " ";
+    }
+    ~Marks() {
+      if (on) fprintf(stderr, "[flush] %s\n", line.c_str());
+    }
+  } mark{trace};
   int rc = cb_init(device);
   if (rc) return rc;
   if (bloom_out && n && m_bits == 0)  // BloomFilter::insert's `% 0` (src/bloom.rs:36)
@@ -400,9 +417,15 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   HIP_TRY(hipMemsetAsync(dr->dmask, 0, sizeof(dr->dmask), s));
   HIP_TRY(ws.f_tsum.reserve(cb::format_tiles(n) * 8, s));
   uint64_t* tsum = (uint64_t*)ws.f_tsum.p;
+  mark("staged");
   HIP_TRY(cb::launch_sorted_check(dk, dko, dvo, n, dr, tsum, s));
   HIP_TRY(hipMemcpyAsync(hr, dr, offsetof(cb::CreateResult, len), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipEventRecord(ws.ev, s));
+  // The Bloom build fills the GPU while the host waits for round trip 1: it
+  // needs neither the order nor the totals (OR is order-free). Measured
+  // slower elsewhere: on a side stream beside the sort and the format (the
+  // kernels contend; unsorted 0.236 -> 0.262 ms), and after the format's
+  // enqueue (the same).
   auto build_bloom = [&]() -> int {  // (keys are non-null or all empty here)
     if (!bloom_out) return CB_OK;
     cb_filter* fp = nullptr;
@@ -412,7 +435,9 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
     return n ? insert_locked(ws, fp, dk, dko, 0, n, s) : CB_OK;
   };
   if ((rc = build_bloom())) return rc;
+  mark("bloom_enq");
   HIP_TRY(hipEventSynchronize(ws.ev));
+  mark("rt1");
   if (kdev) ktot = hr->ktot;
   if (vdev) vtot = hr->vtot;
   const bool sorted = hr->flags[0] != 0;
@@ -468,6 +493,7 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
     }
     if (!binned && (rc = merge_sort())) return rc;
   }
+  mark("sort_enq");
   HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
   // the line index straight from the entries (entry p is line p), no re-read of the file
   t->nlines = n;
@@ -487,7 +513,9 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
                               cap_bytes, s, vsp, t->dir, t->dir ? &dm : nullptr, t->dmap));
     // Round trip 2: flags, file length, zone bounds
     HIP_TRY(hipMemcpyAsync(hr, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
+    mark("fmt_enq");
     HIP_TRY(hipStreamSynchronize(s));
+    mark("rt2");
     return CB_OK;
   };
   if ((rc = format())) return rc;
@@ -537,6 +565,7 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
   }
   if (bloom_out) *bloom_out = f.release();
   *table_out = t.release();
+  mark("end");
   return CB_OK;
 }
 
