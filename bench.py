@@ -691,7 +691,7 @@ def main():
                 step_flush()
             k_fl = max(3, LK // 4)
             fel = timed(step_flush, k_fl)
-            fprof = kernel_ms(["k_sorted_check", "k_entry_sort", "k_bin_count", "k_bin_offsets", "k_bin_plan", "k_bin_scatter", "k_bin_sort", "k_tile_scan",
+            fprof = kernel_ms(["k_sorted_check", "k_entry_sort", "k_bin_count", "k_bin_offsets", "k_bin_scatter", "k_bin_sort", "k_tile_scan",
                                "k_format", "k_line_count", "k_line_emit", "k_line_finish", "k_line_keys",
                                "k_build_part", "k_build_tile", "k_insert_direct"], step_flush, k_fl)
             out_bytes = made[-1][0].nbytes

@@ -343,12 +343,13 @@ __global__ __launch_bounds__(kST) void k_sort_merge(const SortKey* __restrict__ 
 // every record of bin b + 1. As in a radix sort pass, without global
 // atomics: k_bin_count leaves each block's bin histogram (LDS) in cnt;
 // k_bin_offsets turns every bin's column into the blocks' exclusive offsets
-// and the bin's total; k_bin_plan scans the totals (start[b]) and cuts the
-// bins into groups of ~T records (group g starts at the first bin starting
-// at or after g * T); k_bin_scatter writes each record into its bin's range
-// (LDS cursors; any order inside a bin); k_bin_sort sorts one group in LDS by
+// and the bins' starts inside 64-bin blocks plus each block's sum;
+// k_bin_scatter writes each record into its bin's range (LDS cursors; any
+// order inside a bin); k_bin_sort sorts one group of ~T records in LDS by
 // the full record order (index last: the stable order) and writes what
-// k_format needs. A group larger than an LDS tile (a bin holding more than
+// k_format needs. Groups are cut at bin boundaries: group g starts at the
+// first bin starting at or after g * T, which each group-sort block finds
+// itself from the 64-bin blocks' sums. A group larger than an LDS tile (a bin holding more than
 // tile - T records: keys sharing a long prefix) sets
 // CreateResult::flags[3] and the caller redoes the sort with the merge sort.
 // Records make 2 round trips through HBM instead of 9, and the group sorts
@@ -416,79 +417,95 @@ __global__ __launch_bounds__(kBinNT) void k_bin_count(const uint8_t* __restrict_
   for (uint32_t b = threadIdx.x; b < nb; b += kBinNT) cnt[(uint64_t)blockIdx.x * nb + b] = hist[b];
 }
 
-// cnt[blk][b] := the blocks' exclusive offsets inside bin b; total[b] = its
-// size. A block takes 64 bins (the lanes: each row of cnt is read 256 B at a
-// time) and splits the nblk rows among its 16 waves; the waves' row sums are
-// joined in LDS.
+// cnt[blk][b] := the blocks' exclusive offsets inside bin b; lstart[b] :=
+// the exclusive prefix of the bin totals inside its 64-bin block; bsum[j] :=
+// block j's total. A block takes 64 bins (the lanes: each row of cnt is read
+// 256 B at a time) and splits the nblk rows among its 16 waves, each wave
+// loading its first 16 rows together and keeping them for the rewrite; the
+// waves' row sums are joined in LDS. The bins' global starts are never
+// written: k_bin_scatter and k_bin_sort add the 64-bin blocks' prefix (a
+// wave scan of <= 128 sums) to lstart themselves, so no single-block plan
+// launch sits between the passes (one took 9 us).
 constexpr uint32_t kOffW = 16;  // waves per k_bin_offsets block
+constexpr uint32_t kOffR = 16;  // rows per wave held in registers
+constexpr uint32_t kBinBlocks = kBins / 64;  // 64-bin blocks at most
 __global__ __launch_bounds__(kOffW * 64) void k_bin_offsets(uint32_t* __restrict__ cnt, uint32_t nblk, uint32_t nb,
-                                                            uint32_t* __restrict__ total) {
+                                                            uint32_t* __restrict__ lstart,
+                                                            uint32_t* __restrict__ bsum) {
   __shared__ uint32_t part[kOffW][64];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, b = blockIdx.x * 64 + lane;
-  const uint32_t per = (nblk + kOffW - 1) / kOffW, k0 = wv * per, k1 = k0 + per < nblk ? k0 + per : nblk;
-  uint32_t sum = 0;
-  if (b < nb)
-    for (uint32_t k = k0; k < k1; ++k) sum += cnt[(uint64_t)k * nb + b];
+  const uint32_t per = (nblk + kOffW - 1) / kOffW, k0 = min(wv * per, nblk), k1 = min(k0 + per, nblk);
+  const bool live = b < nb;
+  uint32_t v[kOffR], sum = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kOffR; ++j) {  // every load in flight together
+    v[j] = live && k0 + j < k1 ? cnt[(uint64_t)(k0 + j) * nb + b] : 0u;
+    sum += v[j];
+  }
+  for (uint32_t k = k0 + kOffR; k < k1; ++k) sum += live ? cnt[(uint64_t)k * nb + b] : 0u;  // > 4M entries
   part[wv][lane] = sum;
   __syncthreads();
   uint32_t run = 0, tot = 0;
 #pragma unroll
   for (uint32_t w = 0; w < kOffW; ++w) {
-    const uint32_t v = part[w][lane];
-    run += w < wv ? v : 0u;
-    tot += v;
+    const uint32_t x = part[w][lane];
+    run += w < wv ? x : 0u;
+    tot += x;
   }
-  if (b >= nb) return;
-  for (uint32_t k = k0; k < k1; ++k) {
-    const uint32_t v = cnt[(uint64_t)k * nb + b];
+  if (wv == 0) {  // the bins' prefix inside this 64-bin block, and its total
+    uint32_t x = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if ((int)lane >= d) x += y;
+    }
+    if (live) lstart[b] = x - tot;
+    if (lane == 63) bsum[blockIdx.x] = x;
+  }
+  if (!live) return;
+#pragma unroll
+  for (uint32_t j = 0; j < kOffR; ++j) {
+    if (k0 + j < k1) {
+      cnt[(uint64_t)(k0 + j) * nb + b] = run;
+      run += v[j];
+    }
+  }
+  for (uint32_t k = k0 + kOffR; k < k1; ++k) {
+    const uint32_t x = cnt[(uint64_t)k * nb + b];
     cnt[(uint64_t)k * nb + b] = run;
-    run += v;
+    run += x;
   }
-  if (wv == 0) total[b] = tot;
 }
 
-// One block: start[b] = exclusive scan of total (start[nb] = n),
-// gstart[g] = the start of the first bin starting at or after g * T
-// (gstart[0] = 0, gstart[G] = n).
-__global__ __launch_bounds__(1024) void k_bin_plan(const uint32_t* __restrict__ total, uint32_t nb, uint32_t n,
-                                                   uint32_t T, uint32_t G, uint32_t* __restrict__ start,
-                                                   uint32_t* __restrict__ gstart) {
-  constexpr uint32_t kPer = kBins / 1024;  // n < 2^32 here: 32-bit sums and divisions
-  const uint32_t i0 = threadIdx.x * kPer;
-  uint32_t v[kPer], sum = 0;
+// One wave (all 64 lanes): the 64-bin blocks' exclusive prefix from bsum
+// (nbb <= 128 blocks, two per lane). Lane l gets pre0 = prefix of block 2l
+// and a0 = its sum, so block 2l spans [pre0, pre0 + a0) and block 2l + 1
+// [pre0 + a0, pre0 + s).
+struct BinPrefix {
+  uint32_t pre0, a0, s;
+};
+__device__ __forceinline__ BinPrefix bin_block_prefix(const uint32_t* __restrict__ bsum, uint32_t nbb) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t a = 2 * lane < nbb ? bsum[2 * lane] : 0u, c = 2 * lane + 1 < nbb ? bsum[2 * lane + 1] : 0u;
+  const uint32_t s = a + c;
+  uint32_t x = s;
 #pragma unroll
-  for (uint32_t j = 0; j < kPer; ++j) {
-    v[j] = i0 + j < nb ? total[i0 + j] : 0u;
-    sum += v[j];
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if ((int)lane >= d) x += y;
   }
-  uint64_t tot;
-  uint32_t pre = (uint32_t)block_scan<1024>(sum, &tot);
-  uint32_t g = pre / T + 1;  // the next group start to place
-#pragma unroll
-  for (uint32_t j = 0; j < kPer; ++j) {
-    if (i0 + j < nb) {
-      const uint32_t e = pre + v[j];
-      start[i0 + j] = pre;
-      // the non-empty bins' ranges (pre, e] tile (0, n]: a multiple g * T in
-      // this one means the first bin starting at or after it starts at e
-      for (; (uint64_t)g * T <= e && g < G; ++g) gstart[g] = e;
-    }
-    pre += v[j];
-  }
-  if (threadIdx.x == 0) {
-    start[nb] = n;
-    gstart[0] = 0;
-    gstart[G] = n;
-  }
+  return BinPrefix{x - s, a, s};
 }
 
 __global__ __launch_bounds__(kBinNT) void k_bin_scatter(const uint8_t* __restrict__ kb,
                                                         const uint64_t* __restrict__ ko, uint64_t n, DirMap dm,
                                                         const uint32_t* __restrict__ cnt,
-                                                        const uint32_t* __restrict__ start,
+                                                        const uint32_t* __restrict__ lstart,
+                                                        const uint32_t* __restrict__ bsum, uint32_t nbb,
                                                         SortKey* __restrict__ out) {
   __shared__ DirMap sdm;
   __shared__ uint32_t cur[kBins];
+  __shared__ uint32_t bpre[kBinBlocks];
   const uint64_t p0 = (uint64_t)blockIdx.x * kBinChunk + threadIdx.x;
   SortKey r[kBinPer];
 #pragma unroll
@@ -497,30 +514,73 @@ __global__ __launch_bounds__(kBinNT) void k_bin_scatter(const uint8_t* __restric
     if (p < n) r[k] = sort_record(kb, ko, p);
   }
   if (threadIdx.x == 0) sdm = dm;
+  if (threadIdx.x < 64) {
+    const BinPrefix bp = bin_block_prefix(bsum, nbb);
+    const uint32_t l = threadIdx.x;
+    if (2 * l < nbb) bpre[2 * l] = bp.pre0;
+    if (2 * l + 1 < nbb) bpre[2 * l + 1] = bp.pre0 + bp.a0;
+  }
+  __syncthreads();
   const uint32_t nb = (uint32_t)dm.nbuckets;
-  for (uint32_t b = threadIdx.x; b < nb; b += kBinNT) cur[b] = start[b] + cnt[(uint64_t)blockIdx.x * nb + b];
+  for (uint32_t b = threadIdx.x; b < nb; b += kBinNT)
+    cur[b] = bpre[b >> 6] + lstart[b] + cnt[(uint64_t)blockIdx.x * nb + b];
   __syncthreads();
 #pragma unroll
   for (uint32_t k = 0; k < kBinPer; ++k)
     if (p0 + (uint64_t)k * kBinNT < n) out[atomicAdd(&cur[dir_bucket(sdm, r[k].w0)], 1u)] = r[k];
 }
 
-// One group [gstart[g], gstart[g + 1]) per block: the k_sort_block network
+// The start of group g: 0 for g = 0, n for g >= G, else the start of the
+// first bin starting at or after g * T (bins never split). One wave: the
+// first 64-bin block j whose end reaches g * T, then the first of its bins
+// starting there (or, if its last bin straddles g * T, the next block's
+// start).
+__device__ __forceinline__ uint32_t bin_group_start(uint32_t g, uint32_t G, uint32_t T, uint32_t n,
+                                                    const uint32_t* __restrict__ lstart,
+                                                    const uint32_t* __restrict__ bsum, uint32_t nb,
+                                                    uint32_t nbb) {
+  if (g == 0) return 0;
+  if (g >= G) return n;
+  const uint32_t X = g * T, lane = threadIdx.x & 63u;
+  const BinPrefix bp = bin_block_prefix(bsum, nbb);
+  const uint32_t e0 = bp.pre0 + bp.a0, e1 = bp.pre0 + bp.s;  // ends of blocks 2l, 2l + 1
+  const uint64_t m0 = __ballot(2 * lane < nbb && e0 >= X), m1 = __ballot(2 * lane + 1 < nbb && e1 >= X);
+  // block nbb - 1 ends at n > X, so one of the masks is non-zero
+  const uint32_t j0 = m0 ? 2 * (uint32_t)__builtin_ctzll(m0) : ~0u;
+  const uint32_t j1 = m1 ? 2 * (uint32_t)__builtin_ctzll(m1) + 1 : ~0u;
+  const uint32_t j = min(j0, j1), src = j >> 1;
+  const uint32_t p = __shfl(bp.pre0, src, 64), a = __shfl(bp.a0, src, 64), sj = __shfl(bp.s, src, 64);
+  const uint32_t bj = (j & 1) ? p + a : p, ej = (j & 1) ? p + sj : p + a;
+  const uint32_t b = j * 64 + lane;
+  const uint32_t st = b < nb ? bj + lstart[b] : ej;
+  const uint64_t m = __ballot(st >= X);
+  return m ? __shfl(st, (int)__builtin_ctzll(m), 64) : ej;
+}
+
+// One group [start(g), start(g + 1)) per block (bin_group_start): the k_sort_block network
 // on the group's records, then vsp / tsum for k_format (tsum zeroed by the
 // caller: a group's outputs are not aligned to format tiles, so each wave
 // adds its share of the (at most two) tiles its 256 outputs touch) and the
 // sorted records.
 template <uint32_t NT>
 __global__ __launch_bounds__(NT) void k_bin_sort(const SortKey* __restrict__ in, SortKey* __restrict__ out,
-                                                     const uint32_t* __restrict__ gstart, RecLess less,
-                                                     const uint64_t* __restrict__ vo, ulonglong2* __restrict__ vsp,
-                                                     uint64_t* __restrict__ tsum, uint32_t* __restrict__ overflow) {
+                                                 const uint32_t* __restrict__ lstart,
+                                                 const uint32_t* __restrict__ bsum, uint32_t nb, uint32_t nbb,
+                                                 uint32_t T, uint32_t G, uint32_t n, RecLess less,
+                                                 const uint64_t* __restrict__ vo, ulonglong2* __restrict__ vsp,
+                                                 uint64_t* __restrict__ tsum, uint32_t* __restrict__ overflow) {
   static_assert(kFormatTile == 64 * kIPT, "a wave's outputs span at most two format tiles");
   constexpr uint32_t TILE = NT * kIPT;
   using BinTile = LdsTile16<TILE>;
   __shared__ uint64_t lds[3 * BinTile::P];
   const BinTile tile{lds};
-  const uint64_t beg = gstart[blockIdx.x], end = gstart[blockIdx.x + 1];
+  __shared__ uint32_t gb[2];
+  if (threadIdx.x < 128) {  // waves 0 and 1: the group's start and end
+    const uint32_t v = bin_group_start(blockIdx.x + (threadIdx.x >> 6), G, T, n, lstart, bsum, nb, nbb);
+    if ((threadIdx.x & 63u) == 0) gb[threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  const uint64_t beg = gb[0], end = gb[1];
   if (end <= beg) return;
   if (end - beg > TILE) {  // a bin too large for one tile: the caller falls back to the merge sort
     if (threadIdx.x == 0) atomicOr(overflow, 1u);
@@ -588,7 +648,8 @@ uint64_t entry_sort_tmp_bytes(uint64_t n) { return n * sizeof(SortKey); }
 
 uint64_t bin_sort_tmp_bytes(uint64_t n, uint64_t nbins, uint32_t T) {
   const uint64_t G = (n + T - 1) / T, nblk = (n + kBinChunk - 1) / kBinChunk;
-  return n * sizeof(SortKey) + (nblk * nbins + 2 * (nbins + 1) + G + 1) * 4;
+  (void)G;
+  return n * sizeof(SortKey) + (nblk * nbins + nbins + kBinBlocks) * 4;
 }
 
 uint32_t bin_sort_max_bins() { return kBins; }
@@ -603,10 +664,10 @@ hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, co
   const uint32_t G = (uint32_t)((n + T - 1) / T);
   const uint32_t nblk = (uint32_t)((n + kBinChunk - 1) / kBinChunk);
   SortKey* binned = (SortKey*)tmp;
-  uint32_t* cnt = (uint32_t*)(binned + n);         // nblk x nb
-  uint32_t* total = cnt + (uint64_t)nblk * nb;      // nb + 1
-  uint32_t* start = total + nb + 1;                 // nb + 1
-  uint32_t* gstart = start + nb + 1;                // G + 1
+  uint32_t* cnt = (uint32_t*)(binned + n);          // nblk x nb
+  uint32_t* lstart = cnt + (uint64_t)nblk * nb;      // nb
+  uint32_t* bsum = lstart + nb;                      // nbb
+  const uint32_t nbb = (nb + 63) / 64;
   hipError_t e = hipMemsetAsync(tsum, 0, format_tiles(n) * 8, s);
   if (e != hipSuccess) return e;
   {
@@ -615,23 +676,20 @@ hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, co
   }
   {
     ProfScope ps("k_bin_offsets", s);
-    hipLaunchKernelGGL(k_bin_offsets, dim3((nb + 63) / 64), dim3(kOffW * 64), 0, s, cnt, nblk, nb, total);
-  }
-  {
-    ProfScope ps("k_bin_plan", s);
-    hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(1024), 0, s, total, nb, (uint32_t)n, T, G, start, gstart);
+    hipLaunchKernelGGL(k_bin_offsets, dim3(nbb), dim3(kOffW * 64), 0, s, cnt, nblk, nb, lstart, bsum);
   }
   {
     ProfScope ps("k_bin_scatter", s);
-    hipLaunchKernelGGL(k_bin_scatter, dim3(nblk), dim3(kBinNT), 0, s, kb, ko, n, dm, cnt, start, binned);
+    hipLaunchKernelGGL(k_bin_scatter, dim3(nblk), dim3(kBinNT), 0, s, kb, ko, n, dm, cnt, lstart, bsum, nbb,
+                       binned);
   }
   ProfScope ps("k_bin_sort", s);
   if (T <= 768)  // 1024-record tiles: room for bins of up to 1024 - T records past the target
-    hipLaunchKernelGGL(k_bin_sort<256>, dim3(G), dim3(256), 0, s, binned, out, gstart, RecLess{kb, ko}, vo, vsp,
-                       tsum, overflow);
+    hipLaunchKernelGGL(k_bin_sort<256>, dim3(G), dim3(256), 0, s, binned, out, lstart, bsum, nb, nbb, T, G,
+                       (uint32_t)n, RecLess{kb, ko}, vo, vsp, tsum, overflow);
   else
-    hipLaunchKernelGGL(k_bin_sort<512>, dim3(G), dim3(512), 0, s, binned, out, gstart, RecLess{kb, ko}, vo, vsp,
-                       tsum, overflow);
+    hipLaunchKernelGGL(k_bin_sort<512>, dim3(G), dim3(512), 0, s, binned, out, lstart, bsum, nb, nbb, T, G,
+                       (uint32_t)n, RecLess{kb, ko}, vo, vsp, tsum, overflow);
   return hipGetLastError();
 }
 
