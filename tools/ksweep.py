@@ -3,9 +3,13 @@ where the per-step cost at small K (the driver runs K = 20) goes. Per-step
 HIP events on each lane show whether the first steps of a region run slower
 than the steady state, or whether the region's ends (fill, drain) cost it."""
 import json
+import os
 import sys
 import time
 
+if os.environ.get("SPIN") == "1":  # hipDeviceScheduleSpin before the runtime creates its context
+    import ctypes
+    ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(1)
 import torch
 
 sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
@@ -66,7 +70,7 @@ def region(k, warm, per_step=False, waits=True):
     e1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    out = {"lanes": P, "k": k, "waits": waits, "wall_us_per_step": round(wall / k * 1e6, 2),
+    out = {"spin": os.environ.get("SPIN") == "1", "lanes": P, "k": k, "waits": waits, "wall_us_per_step": round(wall / k * 1e6, 2),
            "region_us_per_step": round(e0.elapsed_time(e1) * 1e3 / k, 2),
            "issue_us_per_step": round(t_issue / k * 1e6, 2)}
     if per_step:
