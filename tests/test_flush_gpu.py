@@ -226,3 +226,31 @@ def test_create_sort_sizes(gpu, n, shape):
     t, _, zone = gpu.sstable_create(list(zip(keys, vals)))
     assert t.data() == oracle.sstable_create(list(zip(keys, vals)))
     assert (zone.min, zone.max) == (min(keys), max(keys))
+
+
+@pytest.mark.parametrize("n", [1 << 22, 1 << 24])
+def test_create_unsorted_large(gpu, n):
+    """Unsorted flushes at 4M entries and at 2^24, the largest batch the bin
+    sort takes (10923 groups of 2048-record sorts, 4096 count blocks), with
+    BASELINE's 16-B keys and values: the whole file against a numpy
+    restatement of the sort + format (workload.sstable_bytes; the keys are
+    distinct, so the stable order is the key order), the zone bounds, and a
+    sample of keys through the read path (src/sstable.rs:57-72,133-179)."""
+    keys = workload.key_range(8000 + n, n)
+    vals = workload.table_value(keys, 3)
+    koff = np.arange(0, 16 * (n + 1), 16, dtype=np.uint64)
+    kb = gpu.KeyBatch(n=n, data=np.ascontiguousarray(keys.reshape(-1)), offsets=koff)
+    vb = gpu.KeyBatch(n=n, data=np.ascontiguousarray(vals.reshape(-1)), offsets=koff)
+    t, _, zone = gpu.sstable_create((kb, vb), m=1 << 20)
+    want = workload.sstable_bytes(keys, vals)
+    got = np.frombuffer(t.data(), np.uint8)
+    assert got.size == want.size and np.array_equal(got, want)
+    w = keys.view(">u8").reshape(n, 2)
+    lo, hi = np.lexsort((w[:, 1], w[:, 0]))[[0, -1]]
+    assert (zone.min, zone.max) == (bytes(keys[lo]), bytes(keys[hi]))
+    rng = np.random.default_rng(n)
+    idx = rng.integers(0, n, 4096)
+    which, voffs, out = gpu.get_many([t], keys[idx])
+    assert (np.asarray(which) == 0).all()
+    got_vals = np.frombuffer(bytes(out), np.uint8).reshape(-1, 16)
+    assert np.array_equal(got_vals, vals[idx])
