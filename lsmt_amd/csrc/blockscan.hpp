@@ -5,6 +5,21 @@
 
 namespace cb {
 
+// Inclusive wave64 scan in DPP moves (no LDS crossbar): row_shr 1/2/4/8 scan
+// each row of 16 lanes, row_bcast:15 adds row 0's total to row 1 and row 2's
+// to row 3, row_bcast:31 adds rows 0-1's total to rows 2-3. A lane whose
+// source is outside its row, or whose row the row mask leaves out, takes the
+// `old` operand, 0. Six VALU ops against six ds_bpermute round trips.
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+
 // Block-wide exclusive scan of one uint64 per thread (NT threads). Returns the
 // thread's prefix; *total = block sum. Contains barriers: call uniformly.
 template <int NT>

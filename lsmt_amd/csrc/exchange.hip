@@ -25,6 +25,7 @@
 // The expanded map is bit-identical to the dense all-gather's.
 #include <hip/hip_runtime.h>
 
+#include "blockscan.hpp"
 #include "exchange.hpp"
 #include "profile.hpp"
 
@@ -40,12 +41,7 @@ constexpr uint32_t kXT = 256;           // expand: threads per block (one chunk 
 template <uint32_t NT>
 __device__ __forceinline__ uint32_t block_incl_scan(uint32_t c, uint32_t* wsum, uint32_t* total) {
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  uint32_t x = c;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= (uint32_t)d) x += y;
-  }
+  const uint32_t x = wave_inclusive_scan(c);
   __syncthreads();  // wsum may still be read by a previous call
   if (lane == 63) wsum[wid] = x;
   __syncthreads();

@@ -23,6 +23,7 @@
 
 #include <cstdlib>
 
+#include "blockscan.hpp"
 #include "kernels.hpp"
 #include "profile.hpp"
 
@@ -64,12 +65,7 @@ __device__ uint32_t block_exclusive_scan(uint32_t* arr, uint32_t len, uint32_t* 
   const uint32_t beg = min(tid * per, len), end = min(beg + per, len);
   uint32_t s = 0;
   for (uint32_t i = beg; i < end; ++i) s += arr[i];
-  uint32_t x = s;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= (uint32_t)d) x += y;
-  }
+  const uint32_t x = wave_inclusive_scan(s);
   if (lane == 63) wsum[wid] = x;
   __syncthreads();
   uint32_t wpre = 0, total = 0;
@@ -219,13 +215,7 @@ __device__ __forceinline__ void wave0_exclusive_scan4(uint32_t* arr, uint32_t le
     const uint4 v = a4[i];
     sum += v.x + v.y + v.z + v.w;
   }
-  uint32_t x = sum;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= (uint32_t)d) x += y;
-  }
-  uint32_t run = x - sum;
+  uint32_t run = wave_inclusive_scan(sum) - sum;
   for (uint32_t i = beg; i < end; ++i) {
     const uint4 v = a4[i];
     uint4 o;

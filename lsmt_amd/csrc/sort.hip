@@ -453,12 +453,7 @@ __global__ __launch_bounds__(kOffW * 64) void k_bin_offsets(uint32_t* __restrict
     tot += x;
   }
   if (wv == 0) {  // the bins' prefix inside this 64-bin block, and its total
-    uint32_t x = tot;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(x, d, 64);
-      if ((int)lane >= d) x += y;
-    }
+    const uint32_t x = wave_inclusive_scan(tot);
     if (live) lstart[b] = x - tot;
     if (lane == 63) bsum[blockIdx.x] = x;
   }
@@ -488,12 +483,7 @@ __device__ __forceinline__ BinPrefix bin_block_prefix(const uint32_t* __restrict
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t a = 2 * lane < nbb ? bsum[2 * lane] : 0u, c = 2 * lane + 1 < nbb ? bsum[2 * lane + 1] : 0u;
   const uint32_t s = a + c;
-  uint32_t x = s;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if ((int)lane >= d) x += y;
-  }
+  const uint32_t x = wave_inclusive_scan(s);
   return BinPrefix{x - s, a, s};
 }
 

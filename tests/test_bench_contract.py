@@ -29,7 +29,7 @@ def test_defaults_are_the_c3_single_gpu_run():
     assert (a.n_keys, a.filters, a.m_bits, a.keys_per_filter) == (1 << 20, 32, 1 << 26, 1 << 19)
     assert (a.build_keys, a.build_m_bits) == (1 << 20, 1 << 27)  # C2
     assert a.steps > 0 and a.warmup >= 0
-    assert a.probe_streams in (1, 2, 3, 4)
+    assert a.probe_streams in (1, 2, 3, 4) and a.build_streams in (1, 2, 3, 4)
 
 
 def test_driver_flags_parse():
@@ -37,6 +37,8 @@ def test_driver_flags_parse():
     assert (a.gpus, a.steps, a.warmup) == (8, 20, 3)
     with pytest.raises(SystemExit):
         _parse(["--probe-streams", "5"])
+    with pytest.raises(SystemExit):
+        _parse(["--build-streams", "5"])  # GPU_MAX_HW_QUEUES is 4 on the box
 
 
 def test_metric_names_the_baseline_metric():

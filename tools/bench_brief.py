@@ -1,0 +1,21 @@
+"""One-screen summary of a bench.py JSON line (the legs a round compares)."""
+import json
+import sys
+
+d = json.load(open(sys.argv[1]))
+r = d["roofline"]
+print(f"probe C3 {d['value'] / 1e12:.3f} T/s {d['ms_per_step'] * 1e3:.1f} us/step  frac {r['frac']} "
+      f"one-lane {r.get('frac_one_lane')} ({r.get('kernel_avg_us_one_lane')} us)  "
+      f"rr {r['random_read_roofline']['frac']}")
+b = d.get("build")
+if b:
+    print(f"build C2 {b['value'] / 1e9:.1f} G keys/s {b['ms_per_step'] * 1e3:.2f} us/step lanes {b['pipeline_lanes']} "
+          f"{b['kernels']}")
+rp = d.get("read_path")
+if rp:
+    print(f"read path {rp['value'] / 1e9:.2f} G gets/s")
+f = d.get("flush")
+if f:
+    for k in ("sorted_input", "unsorted_input"):
+        if k in f:
+            print(f"flush {k}: {f[k]['ms_per_flush']} ms  {f[k]['kernels_us']}")
