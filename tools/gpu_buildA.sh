@@ -1,18 +1,18 @@
 #!/bin/bash
-# Build-path A/B on one GPU: build parity tests (fused build, then the two
-# launches), the phase-stamped ubench, and the bench's C2 leg for both.
+# Build-path A/B on one GPU: build parity tests, the phase-stamped ubench, and
+# the bench's C2 leg, for partition blocks of 512 and of 1024 threads.
 set -o pipefail
 mkdir -p gpurun_out
 K="build or insert or golden or c4 or create or rebuild"
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$K" > gpurun_out/pytest_build.log 2>&1 || { tail -30 gpurun_out/pytest_build.log; exit 1; }
 tail -1 gpurun_out/pytest_build.log
-timeout -k 10 60 ./build/tools/ubench_build > gpurun_out/ubench_build.json || exit 1
-cat gpurun_out/ubench_build.json
-for C in 1 0; do
-for P in 3 4 1; do
-CB_BUILD_FUSED=$C timeout -k 10 200 python bench.py --no-cpu --no-e2e --no-zone --no-flush --no-cold --steps 50 --probe-streams $P > gpurun_out/b_c2_$C$P.json 2>gpurun_out/b_c2.err || { tail gpurun_out/b_c2.err; exit 1; }
-python -c "import json;d=json.load(open('gpurun_out/b_c2_$C$P.json'))['build'];print('C2 fused=$C lanes=$P',round(d['value']/1e9,2),'Gkeys/s',d['ms_per_step'],d['kernels'])"
+for V in 512 1024; do
+CB_BUILD_PNT=$V timeout -k 10 60 ./build/tools/ubench_build > gpurun_out/ubench_build_$V.json || exit 1
+cat gpurun_out/ubench_build_$V.json
+for P in 4 3 2 1; do
+CB_BUILD_PNT=$V timeout -k 10 200 python bench.py --no-cpu --no-e2e --no-zone --no-flush --no-cold --steps 50 --build-streams $P > gpurun_out/b_c2_$V$P.json 2>gpurun_out/b_c2.err || { tail gpurun_out/b_c2.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/b_c2_$V$P.json'))['build'];print('C2 pnt=$V lanes=$P',round(d['value']/1e9,2),'Gkeys/s',d['ms_per_step'],d['kernels'])"
 done
 done
-CB_BUILD_FUSED=0 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$K" > gpurun_out/pytest_build0.log 2>&1 || { tail -30 gpurun_out/pytest_build0.log; exit 1; }
+CB_BUILD_PNT=1024 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$K" > gpurun_out/pytest_build0.log 2>&1 || { tail -30 gpurun_out/pytest_build0.log; exit 1; }
 tail -1 gpurun_out/pytest_build0.log
