@@ -246,31 +246,31 @@ __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp,
   const uint64_t kbase = (uint64_t)blockIdx.x * C;
   CB_STAMP(0);
 
-  // positions first: every key load of the thread is in flight together
-  uint64_t pa[KPT], pb[KPT];
-  bool ok[KPT];
+  // positions first: every key load of the thread is in flight together.
+  // Each entry is kept packed as (tile << 20) | offset in the tile (tiles <
+  // kMaxTiles = 2^12, offsets < 2^kMaxTileBits <= 2^20), 0xFFFFFFFF for none:
+  // one register per entry instead of a 64-bit position and a tile.
+  static_assert(kMaxTiles <= 4096 && kMaxTileBits <= 20, "packed entry");
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  const uint32_t tmask = (1u << tb) - 1u;
+  uint32_t q[2 * KPT], er[2 * KPT];
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     const uint64_t k = kbase + (uint64_t)j * NT + tid;
-    ok[j] = k < n;
-    pa[j] = pb[j] = 0;
-    if (ok[j]) key_positions<KEYK, MODE>(ks, k, mp, pa[j], pb[j]);
+    q[2 * j] = q[2 * j + 1] = kNone;
+    if (k < n) {
+      uint64_t a, b;
+      key_positions<KEYK, MODE>(ks, k, mp, a, b);
+      q[2 * j] = ((uint32_t)(a >> tb) << 20) | ((uint32_t)a & tmask);
+      q[2 * j + 1] = ((uint32_t)(b >> tb) << 20) | ((uint32_t)b & tmask);
+    }
   }
   for (uint32_t i = tid; i < Tp; i += NT) hist[i] = 0;
   __syncthreads();
   CB_STAMP(1);
-  const uint32_t tmask = (1u << tb) - 1u;
-  uint32_t et[2 * KPT], er[2 * KPT];
 #pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    et[2 * j] = et[2 * j + 1] = 0xFFFFFFFFu;
-    if (ok[j]) {
-      et[2 * j] = (uint32_t)(pa[j] >> tb);
-      et[2 * j + 1] = (uint32_t)(pb[j] >> tb);
-      er[2 * j] = atomicAdd(&hist[et[2 * j]], 1u);
-      er[2 * j + 1] = atomicAdd(&hist[et[2 * j + 1]], 1u);
-    }
-  }
+  for (int e = 0; e < 2 * KPT; ++e)
+    if (q[e] != kNone) er[e] = atomicAdd(&hist[q[e] >> 20], 1u);
   __syncthreads();
   CB_STAMP(2);
   wave0_exclusive_scan4(hist, Tp);  // Tp >= T + 1: hist[T] = the total
@@ -280,12 +280,8 @@ __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp,
   uint32_t* srow = seg + (size_t)blockIdx.x * (T + 1);
   for (uint32_t t = tid; t <= T; t += NT) srow[t] = hist[t];
 #pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    if (et[2 * j] != 0xFFFFFFFFu) {
-      stage[hist[et[2 * j]] + er[2 * j]] = (uint32_t)pa[j] & tmask;
-      stage[hist[et[2 * j + 1]] + er[2 * j + 1]] = (uint32_t)pb[j] & tmask;
-    }
-  }
+  for (int e = 0; e < 2 * KPT; ++e)
+    if (q[e] != kNone) stage[hist[q[e] >> 20] + er[e]] = q[e] & 0xFFFFFu;
   __syncthreads();
   CB_STAMP(4);
   uint32_t* out = ent + (size_t)blockIdx.x * (2 * C);  // 16-B aligned, as is stage

@@ -115,12 +115,13 @@ int main() {
   const float e1 = per_launch_us([&] { hipLaunchKernelGGL(k_empty, dim3(p.nblk), dim3(1024), lds1, 0, dummy); }, 50);
   const float e2 = per_launch_us([&] { hipLaunchKernelGGL(k_empty, dim3(p.T), dim3(1024), lds2, 0, dummy); }, 50);
   const float full = per_launch_us([&] { CHECK(launch_build_batch(KEY_FIXED16, mode, bb, 1, mp, p, seg, ent, 0)); }, 50);
-  allow_lds(k_build_part<KEY_FIXED16, MOD_POW2_32, 4>, lds1);
   allow_lds(k_build_tile<16>, lds2);
-  const float part = per_launch_us([&] {
-    hipLaunchKernelGGL((k_build_part<KEY_FIXED16, MOD_POW2_32, 4>), dim3(p.nblk, 1), dim3(1024), lds1, 0, bb,
-                       mp, p.tb, p.T, seg, ent);
-  }, 50);
+  allow_lds(k_build_part<KEY_FIXED16, MOD_POW2_32, 4>, lds1);
+  auto launch_part = [&] {
+    hipLaunchKernelGGL((k_build_part<KEY_FIXED16, MOD_POW2_32, 4>), dim3(p.nblk, 1), dim3(1024), lds1, 0, bb, mp,
+                       p.tb, p.T, seg, ent);
+  };
+  const float part = per_launch_us(launch_part, 50);
   const float tile = per_launch_us([&] {
     hipLaunchKernelGGL(k_build_tile<16>, dim3(p.T, 1), dim3(1024), lds2, 0, bb, p.tb, p.T, seg, p.nblk, ent,
                        2 * p.C);
@@ -134,8 +135,7 @@ int main() {
   CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st)));
   std::vector<uint64_t> h((size_t)nst_blocks * 8);
   CHECK(hipMemset(st, 0, (size_t)nst_blocks * 64));
-  hipLaunchKernelGGL((k_build_part<KEY_FIXED16, MOD_POW2_32, 4>), dim3(p.nblk, 1), dim3(1024), lds1, 0, bb, mp,
-                     p.tb, p.T, seg, ent);
+  launch_part();
   CHECK(hipDeviceSynchronize());
   CHECK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
   phases("part_stamps", h, p.nblk, 6, false);
