@@ -63,6 +63,13 @@ __device__ __forceinline__ void store16_nt(uint4* p, const uint4& v) {
   __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
 }
 
+// Write-through (sc1) 16-B store at byte offset off of a buffer resource.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store16_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& v) {
+  const i32x4 w = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 16);
+}
+
 // Exclusive scan of arr[0..len) in LDS by a whole NT-thread block; returns the
 // total. wsum: NT/64 words of LDS scratch. Contains barriers: all threads call.
 template <uint32_t NT>
@@ -293,8 +300,12 @@ __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp,
   CB_STAMP(4);
   uint32_t* out = ent + (size_t)blockIdx.x * (2 * C);  // 16-B aligned, as is stage
   const uint32_t n4 = total / 4;
-  for (uint32_t i = tid; i < n4; i += NT)
-    reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(stage)[i];
+  // write-through (sc1): the entries go on to the memory side at once, so the
+  // kernel's end has no dirty L2 lines to write back, and the tile pass (on
+  // other XCDs) still finds them there; C2 on four lanes 101 -> 105-107 G
+  // keys/s (non-temporal stores instead made the tile pass's reads slower)
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, 2 * C * 4, 0x00020000);
+  for (uint32_t i = tid; i < n4; i += NT) store16_wt(r, i * 16, reinterpret_cast<const uint4*>(stage)[i]);
   for (uint32_t i = 4 * n4 + tid; i < total; i += NT) out[i] = stage[i];
   CB_STAMP(5);
 }
@@ -378,8 +389,8 @@ __global__ __launch_bounds__(kBuildNT) void k_build_tile(BuildBatch bb, uint32_t
   CB_STAMP(3);
   // non-temporal: the filter is written once and read by other launches, so
   // no L2 lines to write back at the kernel's end (tile pass alone 8.8 ->
-  // 7.5 us, C2 on four lanes 97.8 -> 101 G keys/s; non-temporal entry
-  // stores in k_build_part made the tile pass's reads of them slower)
+  // 7.5 us, C2 on four lanes 97.8 -> 101 G keys/s; write-through measured
+  // the same here)
   for (uint32_t i = tid; i < tw / 4; i += NT) store16_nt(gt + i, lt[i]);
   CB_STAMP(4);
 }
