@@ -158,6 +158,20 @@ hipError_t ensure_pad_zeroed(const cb_filter* cf, hipStream_t s) {
   return hipSuccess;
 }
 
+// Record f's write mark on s: its own mark again when no one else holds it
+// (no batch shares it, no mirror refresh is waiting on it), else a new one.
+hipError_t record_own_mark(cb_filter* f, hipStream_t s) {
+  std::shared_ptr<WriteMark> m = std::atomic_load(&f->wmark);
+  if (!m || m.use_count() > 2) {  // (2: f's reference and this copy)
+    m = std::make_shared<WriteMark>();
+    const hipError_t e = hipEventCreateWithFlags(&m->ev, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  const hipError_t e = hipEventRecord(m->ev, s);
+  if (e == hipSuccess) std::atomic_store(&f->wmark, m);
+  return e;
+}
+
 // The pending lazy clear, issued on s by whichever operation needs the words
 // first (readers may race: zero_mu makes the exchange, the memset and the
 // event that orders the host mirror's refresh after it one step).
@@ -168,8 +182,7 @@ hipError_t ensure_zeroed(const cb_filter* cf, hipStream_t s) {
   if (f->needs_zero.exchange(false)) {
     f->needs_pad_zero.store(false);
     hipError_t e = hipMemsetAsync(f->words, 0, f->nwords_alloc * 4, s);
-    if (e == hipSuccess && !f->wev) e = hipEventCreateWithFlags(&f->wev, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventRecord(f->wev, s);
+    if (e == hipSuccess) e = record_own_mark(f, s);
     return e;
   }
   return hipSuccess;
@@ -304,9 +317,29 @@ int insert_locked(Workspace& ws, cb_filter* f, const uint8_t* keys, const uint64
 }
 
 int mark_written(cb_filter* f, hipStream_t s) {
-  if (!f->wev) HIP_TRY(hipEventCreateWithFlags(&f->wev, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(f->wev, s));
+  HIP_TRY(record_own_mark(f, s));
   f->gen.fetch_add(1, std::memory_order_acq_rel);
+  return CB_OK;
+}
+
+int mark_written_many(Workspace& ws, cb_filter* const* fs, uint32_t nf, hipStream_t s) {
+  if (!nf) return CB_OK;
+  std::shared_ptr<WriteMark> m;
+  for (auto& c : ws.marks)
+    if (c.use_count() == 1) {  // only the pool holds it: no filter, no waiting refresh
+      m = c;
+      break;
+    }
+  if (!m) {
+    m = std::make_shared<WriteMark>();
+    HIP_TRY(hipEventCreateWithFlags(&m->ev, hipEventDisableTiming));
+    ws.marks.push_back(m);
+  }
+  HIP_TRY(hipEventRecord(m->ev, s));
+  for (uint32_t i = 0; i < nf; ++i) {
+    std::atomic_store(&fs[i]->wmark, m);
+    fs[i]->gen.fetch_add(1, std::memory_order_acq_rel);
+  }
   return CB_OK;
 }
 
@@ -1034,7 +1067,7 @@ int cb_filter_destroy(cb_filter* f) {
   {
     DeviceGuard dg(f->device);
     pool_release(f->device, f->words, f->words_cap);
-    if (f->wev) (void)hipEventDestroy(f->wev);
+    std::atomic_store(&f->wmark, std::shared_ptr<WriteMark>());
   }
   delete f;
   return CB_OK;
@@ -1130,7 +1163,8 @@ int refresh_mirror(const cb_filter* cf) {
       std::fill(f->host.begin(), f->host.end(), 0u);
     } else {
       DeviceGuard dg(f->device);
-      if (f->wev) HIP_TRY(hipEventSynchronize(f->wev));
+      const std::shared_ptr<WriteMark> m = std::atomic_load(&f->wmark);
+      if (m) HIP_TRY(hipEventSynchronize(m->ev));
       HIP_TRY(hipMemcpy(f->host.data(), f->words, nw * 4, hipMemcpyDeviceToHost));
     }
   }
@@ -1755,11 +1789,9 @@ int cb_filter_insert_fixed_many(cb_filter* const* filters, uint32_t nf, const ui
     HIP_TRY(ws.ent.reserve(cb::build_ent_bytes(p) * nb, s));
     HIP_TRY(cb::launch_build_batch(keyk, f0->mode, bb, nb, f0->mp, p, (uint32_t*)ws.seg.p,
                                    (uint32_t*)ws.ent.p, s));
-    for (uint32_t j = 0; j < nb; ++j) {
+    for (uint32_t j = 0; j < nb; ++j)
       if (n[b0 + j]) filters[b0 + j]->known_zero = false;
-      int rc = mark_written(filters[b0 + j], s);
-      if (rc) return rc;
-    }
+    if (int rc = mark_written_many(ws, filters + b0, nb, s)) return rc;  // one event for the batch
   }
   g_last_path = PATH_TILED;
   if (staged) HIP_TRY(hipStreamSynchronize(s));

@@ -24,6 +24,16 @@
 #include "sstable.hpp"
 #include "zone.hpp"
 
+// An event recorded after a device write to one or more filters (a batched
+// build shares one among all its filters: one hipEventRecord per call, not
+// per filter).
+struct WriteMark {
+  hipEvent_t ev = nullptr;
+  ~WriteMark() {
+    if (ev) (void)hipEventDestroy(ev);
+  }
+};
+
 struct cb_filter {
   uint64_t m = 0;
   int device = 0;
@@ -43,7 +53,7 @@ struct cb_filter {
   // Host mirror of the packed words for single-key may_contain (DESIGN §2,
   // SURVEY §7 hard part 8): a per-key GPU round trip costs ~10 us, a host
   // probe of the mirror two word loads. Every write to `words` bumps `gen`
-  // and records `wev` on its stream; the first cb_may_contain after a write
+  // and records `wmark` on its stream; the first cb_may_contain after a write
   // waits for that event and copies ceil(m/32) words back once (128 B at the
   // product's m = 1024), later ones read the mirror.
   std::atomic<uint64_t> gen{1};       // bumped by every write to words
@@ -51,7 +61,7 @@ struct cb_filter {
   std::mutex host_mu;                 // one refresh at a time
   std::mutex zero_mu;                 // the lazy clear's issue vs. a refresh (capi.cpp ensure_zeroed)
   std::vector<uint32_t> host;         // ceil(m/32) words
-  hipEvent_t wev = nullptr;           // recorded after the last device write
+  std::shared_ptr<WriteMark> wmark;   // recorded after the last device write (atomic_load / atomic_store)
   int mirror = -1;                    // -1 auto (m <= kMirrorAutoBits), 0 off, 1 on
 };
 
@@ -170,6 +180,7 @@ struct Workspace {
   DevBuf i_cnt, i_base, i_tmp, i_end, i_err, i_start;                 // line indexing
   DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_tsum, f_flag, f_vsp;  // SsTable::create
   DevBuf x_ctl;                   // cb_hits_compress: slot / finish counters (zeroed once)
+  std::vector<std::shared_ptr<WriteMark>> marks;  // write marks, reused once no filter holds them
   cb::CompressState xst;
   cb::CreateResult* hres = nullptr;  // pinned host mirror of f_flag (SsTable::create)
   uint64_t* htot = nullptr;          // pinned, kHostScratch B: get_many's value byte total; index_table's read-backs
@@ -228,6 +239,8 @@ int put_bytes(uint8_t* dst, const void* src, size_t n);
 // A write to f's words was enqueued on s (build, import): the host mirror is
 // stale from here, and its refresh waits for this point of s.
 int mark_written(cb_filter* f, hipStream_t s);
+// One write mark recorded on s for filters fs[0..nf) (ws.mu held).
+int mark_written_many(Workspace& ws, cb_filter* const* fs, uint32_t nf, hipStream_t s);
 
 // Device output: used in place when device-resident, else a workspace buffer
 // copied back at the end.

@@ -246,7 +246,7 @@ template <int KEYK, int MODE, int KPT>
 __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp, uint32_t tb,
                                                          uint32_t T,
                                                          uint32_t* __restrict__ seg_all,
-                                                         uint32_t* __restrict__ ent_all) {
+                                                         uint32_t* __restrict__ ent_all, uint32_t pol) {
   constexpr uint32_t NT = kBuildNT, C = NT * KPT;
   const KeySrc ks = bb.ks[blockIdx.y];
   const uint64_t n = bb.n[blockIdx.y];
@@ -304,8 +304,13 @@ __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp,
   // kernel's end has no dirty L2 lines to write back, and the tile pass (on
   // other XCDs) still finds them there; C2 on four lanes 101 -> 105-107 G
   // keys/s (non-temporal stores instead made the tile pass's reads slower)
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, 2 * C * 4, 0x00020000);
-  for (uint32_t i = tid; i < n4; i += NT) store16_wt(r, i * 16, reinterpret_cast<const uint4*>(stage)[i]);
+  if (pol & 1u) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, 2 * C * 4, 0x00020000);
+    for (uint32_t i = tid; i < n4; i += NT) store16_wt(r, i * 16, reinterpret_cast<const uint4*>(stage)[i]);
+  } else {
+    for (uint32_t i = tid; i < n4; i += NT)
+      reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(stage)[i];
+  }
   for (uint32_t i = 4 * n4 + tid; i < total; i += NT) out[i] = stage[i];
   CB_STAMP(5);
 }
@@ -320,7 +325,7 @@ __global__ __launch_bounds__(kBuildNT) void k_build_tile(BuildBatch bb, uint32_t
                                                          const uint32_t* __restrict__ seg_all,
                                                          uint32_t nblk,
                                                          const uint32_t* __restrict__ ent_all,
-                                                         uint32_t estride) {
+                                                         uint32_t estride, uint32_t pol) {
   constexpr uint32_t NT = kBuildNT, NW = NT / 64;
   static_assert(G <= 64, "one lane per run bound");
   uint32_t* __restrict__ words = bb.words[blockIdx.y];
@@ -391,7 +396,10 @@ __global__ __launch_bounds__(kBuildNT) void k_build_tile(BuildBatch bb, uint32_t
   // no L2 lines to write back at the kernel's end (tile pass alone 8.8 ->
   // 7.5 us, C2 on four lanes 97.8 -> 101 G keys/s; write-through measured
   // the same here)
-  for (uint32_t i = tid; i < tw / 4; i += NT) store16_nt(gt + i, lt[i]);
+  if (pol & 2u)
+    for (uint32_t i = tid; i < tw / 4; i += NT) store16_nt(gt + i, lt[i]);
+  else
+    for (uint32_t i = tid; i < tw / 4; i += NT) gt[i] = lt[i];
   CB_STAMP(4);
 }
 
@@ -850,12 +858,20 @@ static void part_probe(const TilePlan& p, const KeySrc& ks, uint64_t n, const Mo
                      mp, p.tb, p.T, seg, ent, lkey);
 }
 
+// Store cache policy of the build's two outputs (CB_BUILD_STORES, default
+// 3): bit 0 write-through partition entries, bit 1 non-temporal tile
+// write-back.
+static uint32_t build_stores() {
+  static const uint32_t v = (uint32_t)env_int("CB_BUILD_STORES", 3);
+  return v;
+}
+
 template <int KK, int MM, int KPT>
 static void build_part(const TilePlan& p, const BuildBatch& bb, uint32_t nb, const ModP& mp,
                        uint32_t* seg, uint32_t* ent, size_t lds, hipStream_t s) {
   allow_lds(k_build_part<KK, MM, KPT>, lds);
   hipLaunchKernelGGL((k_build_part<KK, MM, KPT>), dim3(p.nblk, nb), dim3(kBuildNT), lds, s, bb, mp,
-                     p.tb, p.T, seg, ent);
+                     p.tb, p.T, seg, ent, build_stores());
 }
 
 hipError_t launch_build_batch(int keyk, int mode, const BuildBatch& bb, uint32_t nb,
@@ -880,7 +896,7 @@ hipError_t launch_build_batch(int keyk, int mode, const BuildBatch& bb, uint32_t
   allow_lds(k_build_tile<16>, lds2);
   ProfScope ps("k_build_tile", s);
   hipLaunchKernelGGL(k_build_tile<16>, dim3(p.T, nb), dim3(kBuildNT), lds2, s, bb, p.tb, p.T, seg,
-                     p.nblk, ent, 2 * p.C);
+                     p.nblk, ent, 2 * p.C, build_stores());
   return hipGetLastError();
 }
 

@@ -119,12 +119,12 @@ int main() {
   allow_lds(k_build_part<KEY_FIXED16, MOD_POW2_32, 4>, lds1);
   auto launch_part = [&] {
     hipLaunchKernelGGL((k_build_part<KEY_FIXED16, MOD_POW2_32, 4>), dim3(p.nblk, 1), dim3(1024), lds1, 0, bb, mp,
-                       p.tb, p.T, seg, ent);
+                       p.tb, p.T, seg, ent, build_stores());
   };
   const float part = per_launch_us(launch_part, 50);
   const float tile = per_launch_us([&] {
     hipLaunchKernelGGL(k_build_tile<16>, dim3(p.T, 1), dim3(1024), lds2, 0, bb, p.tb, p.T, seg, p.nblk, ent,
-                       2 * p.C);
+                       2 * p.C, build_stores());
   }, 50);
   printf("\"empty_part_grid_us\": %.2f, \"empty_tile_grid_us\": %.2f, \"build_step_us\": %.2f, "
          "\"part_alone_us\": %.2f, \"tile_alone_us\": %.2f, ", e1, e2, full, part, tile);
@@ -141,7 +141,7 @@ int main() {
   phases("part_stamps", h, p.nblk, 6, false);
   CHECK(hipMemset(st, 0, (size_t)nst_blocks * 64));
   hipLaunchKernelGGL(k_build_tile<16>, dim3(p.T, 1), dim3(1024), lds2, 0, bb, p.tb, p.T, seg, p.nblk, ent,
-                     2 * p.C);
+                     2 * p.C, build_stores());
   CHECK(hipDeviceSynchronize());
   CHECK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
   phases("tile_stamps", h, p.T, 5, true);
