@@ -119,8 +119,9 @@ int cb_probe_var(const cb_filter* const* filters, uint32_t nf, const uint8_t* by
  * round trip. With the mirror off every call is a one-key GPU probe.
  * Reentrant: concurrent callers may share a filter (`&self`). */
 int cb_may_contain(const cb_filter* f, const uint8_t* key, uint64_t len, int* out);
-/* Host mirror policy: 1 on, 0 off, -1 auto (the default: on when m <= 2^28,
- * i.e. up to 32 MiB of host words). */
+/* Host mirror policy: 1 on, 0 off, -1 auto (the default: on when m <= 2^24,
+ * i.e. up to 2 MiB of host words; past that a write records no event, and
+ * the first refresh after the mirror is turned on synchronises the device). */
 int cb_filter_host_mirror(cb_filter* f, int mode);
 /* *on = whether cb_may_contain uses the mirror; *current = whether the mirror
  * already holds the latest write (either may be NULL). Host only. */

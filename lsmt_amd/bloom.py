@@ -347,7 +347,7 @@ class BloomFilter:
     def host_mirror(self, mode: int = 1) -> None:
         """Single-key may_contain source (cb_filter_host_mirror): 1 the host
         mirror of the words (refreshed by one copy after each write), 0 a
-        one-key GPU probe per call, -1 auto (mirror when m <= 2^28)."""
+        one-key GPU probe per call, -1 auto (mirror when m <= 2^24)."""
         check(_L().cb_filter_host_mirror(self._h, int(mode)))
 
     def host_mirror_info(self) -> tuple[bool, bool]:

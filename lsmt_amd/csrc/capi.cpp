@@ -161,6 +161,10 @@ hipError_t ensure_pad_zeroed(const cb_filter* cf, hipStream_t s) {
 // Record f's write mark on s: its own mark again when no one else holds it
 // (no batch shares it, no mirror refresh is waiting on it), else a new one.
 hipError_t record_own_mark(cb_filter* f, hipStream_t s) {
+  if (!mirror_on(f)) {  // no mirror to order: the next refresh (mirror turned on) syncs the device
+    f->unmarked.store(true, std::memory_order_release);
+    return hipSuccess;
+  }
   std::shared_ptr<WriteMark> m = std::atomic_load(&f->wmark);
   if (!m || m.use_count() > 2) {  // (2: f's reference and this copy)
     m = std::make_shared<WriteMark>();
@@ -324,6 +328,15 @@ int mark_written(cb_filter* f, hipStream_t s) {
 
 int mark_written_many(Workspace& ws, cb_filter* const* fs, uint32_t nf, hipStream_t s) {
   if (!nf) return CB_OK;
+  bool any_on = false;
+  for (uint32_t i = 0; i < nf; ++i) any_on |= mirror_on(fs[i]);
+  if (!any_on) {  // no mirror to order (see record_own_mark)
+    for (uint32_t i = 0; i < nf; ++i) {
+      fs[i]->unmarked.store(true, std::memory_order_release);
+      fs[i]->gen.fetch_add(1, std::memory_order_acq_rel);
+    }
+    return CB_OK;
+  }
   std::shared_ptr<WriteMark> m;
   for (auto& c : ws.marks)
     if (c.use_count() == 1) {  // only the pool holds it: no filter, no waiting refresh
@@ -1115,7 +1128,7 @@ int cb_filter_host_mirror(cb_filter* f, int mode) {
 
 int cb_filter_host_mirror_info(const cb_filter* f, int* on, int* current) {
   if (!f) return fail(CB_EINVAL, "null filter");
-  if (on) *on = f->mirror == 1 || (f->mirror == -1 && f->m <= kMirrorAutoBits);
+  if (on) *on = mirror_on(f);
   if (current)
     *current = f->host_gen.load(std::memory_order_acquire) == f->gen.load(std::memory_order_acquire);
   return CB_OK;
@@ -1163,8 +1176,12 @@ int refresh_mirror(const cb_filter* cf) {
       std::fill(f->host.begin(), f->host.end(), 0u);
     } else {
       DeviceGuard dg(f->device);
-      const std::shared_ptr<WriteMark> m = std::atomic_load(&f->wmark);
-      if (m) HIP_TRY(hipEventSynchronize(m->ev));
+      if (f->unmarked.exchange(false, std::memory_order_acq_rel)) {
+        HIP_TRY(hipDeviceSynchronize());  // a write made while the mirror was off recorded no event
+      } else {
+        const std::shared_ptr<WriteMark> m = std::atomic_load(&f->wmark);
+        if (m) HIP_TRY(hipEventSynchronize(m->ev));
+      }
       HIP_TRY(hipMemcpy(f->host.data(), f->words, nw * 4, hipMemcpyDeviceToHost));
     }
   }
@@ -1190,7 +1207,7 @@ int mirror_contains(const cb_filter* f, const uint8_t* key, uint64_t len) {
 int cb_may_contain(const cb_filter* f, const uint8_t* key, uint64_t len, int* out) {
   if (!f || !out || (!key && len)) return fail(CB_EINVAL, "null argument");
   if (f->m == 0) return fail(CB_EZEROM, "attempt to calculate the remainder with a divisor of zero");
-  if (f->mirror == 1 || (f->mirror == -1 && f->m <= kMirrorAutoBits)) {
+  if (mirror_on(f)) {
     int rc = refresh_mirror(f);
     if (rc) return rc;
     *out = mirror_contains(f, key, len);

@@ -62,10 +62,16 @@ struct cb_filter {
   std::mutex zero_mu;                 // the lazy clear's issue vs. a refresh (capi.cpp ensure_zeroed)
   std::vector<uint32_t> host;         // ceil(m/32) words
   std::shared_ptr<WriteMark> wmark;   // recorded after the last device write (atomic_load / atomic_store)
+  std::atomic<bool> unmarked{false};  // a write went unrecorded (mirror off): the refresh syncs the device
   int mirror = -1;                    // -1 auto (m <= kMirrorAutoBits), 0 off, 1 on
 };
 
-constexpr uint64_t kMirrorAutoBits = 1ull << 28;  // auto mirror up to 32 MiB of host words
+// auto mirror up to 2 MiB of host words: past that, the first per-key call
+// after every build copies megabytes, and each write would pay an event
+// record only for it (SSTable filters are m = 1024, src/sstable.rs:44)
+constexpr uint64_t kMirrorAutoBits = 1ull << 24;
+
+inline bool mirror_on(const cb_filter* f) { return f->mirror == 1 || (f->mirror == -1 && f->m <= kMirrorAutoBits); }
 
 struct cb_filterset {
   uint64_t m = 0;

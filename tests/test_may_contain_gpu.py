@@ -128,6 +128,45 @@ def test_concurrent_readers_race_the_refresh(gpu):
             assert np.array_equal(res[t], expect[t::8]), (rep, t)
 
 
+def test_mirror_turned_on_after_unrecorded_writes(gpu):
+    """m = 2^26 is past the auto mirror (m <= 2^24), so builds record no
+    write event; turning the mirror on afterwards, while a build on a side
+    stream may still run, must still give the oracle's answers (the first
+    refresh syncs the device), and so must a batched build of two filters."""
+    import torch
+    m = 1 << 26
+    keys = workload.key_range(51, 200_000)
+    probe = np.concatenate([keys[:3000], workload.key_range(52, 3000)])
+    o = oracle.OracleFilter(m)
+    o.insert_fixed(keys)
+    expect = oracle_hits(o, probe)
+    b = gpu.BloomFilter(m)
+    assert b.host_mirror_info()[0] is False  # auto: off past 2^24
+    st = torch.cuda.Stream()
+    b.insert_batch(gpu.DeviceKeys(torch.from_numpy(keys).cuda()), stream=st)  # async on st
+    b.host_mirror(1)
+    assert np.array_equal(np.array([b.may_contain(bytes(k)) for k in probe]), expect)
+    # on, a write (marked), off, a write (unrecorded), on again
+    more = workload.key_range(53, 50_000)
+    b.insert_batch(more)
+    b.host_mirror(0)
+    extra = workload.key_range(54, 50_000)
+    b.insert_batch(gpu.DeviceKeys(torch.from_numpy(extra).cuda()), stream=st)
+    b.host_mirror(1)
+    o.insert_fixed(more)
+    o.insert_fixed(extra)
+    assert np.array_equal(np.array([b.may_contain(bytes(k)) for k in probe]), oracle_hits(o, probe))
+    # a batched build (one launch pair for both filters), then the mirror
+    fs = [gpu.BloomFilter(m) for _ in range(2)]
+    dk = [torch.from_numpy(keys).cuda(), torch.from_numpy(extra).cuda()]
+    gpu.insert_many(fs, dk, stream=st)
+    for f, ks in zip(fs, (keys, extra)):
+        f.host_mirror(1)
+        of = oracle.OracleFilter(m)
+        of.insert_fixed(ks)
+        assert np.array_equal(np.array([f.may_contain(bytes(k)) for k in probe]), oracle_hits(of, probe))
+
+
 def test_latency_tool_mirror_under_1us(gpu):
     """The C-ABI per-key call (no Python in the loop) at the product's m =
     1024 and at the C3 filter size: the mirror agrees with the GPU probe on
