@@ -242,6 +242,7 @@ __device__ __forceinline__ void wave0_exclusive_scan4(uint32_t* arr, uint32_t le
   }
 }
 
+// pol: the store policy bits (build_stores(): bit 0 write-through entries).
 template <int KEYK, int MODE, int KPT>
 __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp, uint32_t tb,
                                                          uint32_t T,
@@ -320,6 +321,7 @@ __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp,
 // run's start and length to the whole wave, and the wave issues the 16 run
 // loads back to back (lane i = entry i): two dependent memory round trips per
 // group and no LDS run table or barrier before the ORs.
+// pol: the store policy bits (build_stores(): bit 1 non-temporal write-back).
 template <int G>
 __global__ __launch_bounds__(kBuildNT) void k_build_tile(BuildBatch bb, uint32_t tb, uint32_t T,
                                                          const uint32_t* __restrict__ seg_all,
