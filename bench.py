@@ -53,7 +53,8 @@ def parse():
     p.add_argument("--leg-steps", type=int, default=200,
                    help="steps of each secondary leg (build, read path, zone, flush/4, rotating, one lane): "
                         "at least --steps; the headline leg times exactly --steps")
-    p.add_argument("--n-keys", type=int, default=1 << 20)
+    p.add_argument("--n-keys", type=int, default=None,
+                   help="lookup keys per step (default: 2^20 for c3, 10,000,000 for c5)")
     p.add_argument("--filters", type=int, default=32, help="filters per GPU")
     p.add_argument("--m-bits", type=int, default=1 << 26)
     p.add_argument("--keys-per-filter", type=int, default=1 << 19)
@@ -69,6 +70,8 @@ def parse():
     p.add_argument("--no-cold", action="store_true",
                    help="skip the cold-cache legs (profiles: keeps every k_set_probe launch warm, so "
                         "rocprofv3's average matches the bench line's warm kernel time)")
+    p.add_argument("--no-c4", action="store_true", help="skip the C4 leg (64 concurrent builds) of the default line")
+    p.add_argument("--no-c5", action="store_true", help="skip the C5 rank-slice leg (10M keys x 32 filters)")
     p.add_argument("--flush-entries", type=int, default=1 << 20)
     p.add_argument("--build-streams", type=int, default=4, choices=[1, 2, 3, 4],
                    help="pipeline lanes of the C2 build leg (independent flushes in flight)")
@@ -83,7 +86,10 @@ def parse():
                    help="run the N-rank path with every rank on GPU 0: gloo process group and the C ABI's "
                         "host transport (cb_comm_init_host) instead of RCCL; checks the multi-rank flow on a "
                         "one-GPU box, its numbers are not a scaling measurement")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.n_keys is None:
+        a.n_keys = 10_000_000 if a.workload == "c5" else 1 << 20
+    return a
 
 
 def launch_ranks(args) -> int:
@@ -196,7 +202,7 @@ def main():
         return run_c4(args, torch, dist, world, rank, local, dev, use_dist, result, red_dev)
     seed_base, absent_seed = 100, 999
     if args.workload == "c5":  # key(1000+f, i), absent key(9999, i)
-        args.n_keys, seed_base, absent_seed = 10_000_000, 1000, 9999
+        seed_base, absent_seed = 1000, 9999
     F, n, m, kpf = args.filters, args.n_keys, args.m_bits, args.keys_per_filter
     nf_total = F * world  # weak scaling: F filters per GPU
     f_lo, f_hi = shard_range(nf_total, world, rank)
@@ -820,6 +826,24 @@ def main():
     if rank == 0 and world == 1:
         may_contain = may_contain_latency()
 
+    # ---- BASELINE C4 and C5 in the same line (HIP-event timed, roofline,
+    # golden + oracle checks): C4's 64 builds split over the ranks (strong
+    # scaling); C5's per-GPU slice (rank r: filters 32(r mod 8) .. +31 of 256)
+    c4 = c5 = None
+    if args.workload == "c3" and not args.no_c4:
+        c4 = c4_leg(args, torch, dist, world, rank, local, dev, use_dist, red_dev, LK, args.warmup,
+                    args.probe_streams, check=True, oracle_sample=0 if args.no_cpu else 4)
+        c4["roofline"] = c4_roofline(c4, world)
+        if rank == 0 and world == 1 and not args.no_cpu:
+            c4["cpu_baseline"] = c4_cpu_baseline(64, 1 << 18, 1 << 25)
+        log(f"[c4] {c4['value'] / 1e9:.1f} G keys/s, {c4['region_us_per_step']} us/step, "
+            f"frac {c4['roofline']['frac']}, golden {c4.get('golden_all_filters_bit_exact')}")
+    if args.workload == "c3" and not args.no_c5:
+        c5 = c5_leg(args, torch, dev, local, world, rank, max(args.steps, LK // 4), args.warmup,
+                    args.probe_streams, True, red_dev, dist, use_dist)
+        log(f"[c5] {c5['value'] / 1e12:.3f} T probes/s, {c5['region_us_per_step']} us/step, "
+            f"frac {c5['roofline']['frac']}, golden {c5.get('golden_slice_bit_exact')}")
+
     if args.check:
         # Every rank checks its own rows and, in the exchanged map, the rows
         # of the next rank, so each rank's slice is verified as received by
@@ -899,6 +923,7 @@ def main():
                           "bytes": m * (4 if F <= 32 else 8)},
             "cold": cold, "rotating_batches": rot, "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e,
             "zone_gate": zone, "read_path": read, "flush": flush, "may_contain": may_contain,
+            "c4": c4, "c5": c5,
         }
         if x_fit is False:
             line["valid"] = False
@@ -915,18 +940,86 @@ def main():
         sys.exit(3)
 
 
-def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result, red_dev):
-    """C4: 64 concurrent flush builds (256K keys each, m = 2^25), filters
-    split one contiguous subset per GPU (strong scaling: total work fixed).
-    One step = zero-fill + batched build of this GPU's filters."""
+def _golden():
+    with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as fh:
+        return json.load(fh)
+
+
+def _sha(a) -> str:
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes, fn, k):
+    """K steps of fn between a barrier + device sync on both sides; HIP events
+    on lanes[0] around them (every other lane joined into the end event).
+    Returns (wall seconds, event ms), each the max over ranks."""
+    if use_dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(lanes[0])
+    for _ in range(k):
+        fn()
+    for st in lanes[1:]:
+        lanes[0].wait_stream(st)
+    e1.record(lanes[0])
+    torch.cuda.synchronize(dev)
+    if use_dist:
+        dist.barrier()
+    el, ev = time.perf_counter() - t0, e0.elapsed_time(e1)
+    if use_dist:
+        t = torch.tensor([el, ev], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, ev = float(t[0].item()), float(t[1].item())
+    return el, ev
+
+
+def _all_ranks_true(torch, dist, use_dist, red_dev, ok: bool) -> bool:
+    if not use_dist:
+        return ok
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=red_dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item())
+
+
+def _kernel_us(L, torch, dev, names, fn, k):
+    """Per-launch durations from the library's own HIP events (cb_profile)."""
+    import ctypes
+    L.cb_profile_reset()
+    L.cb_profile_enable(1)
+    for _ in range(k):
+        fn()
+    torch.cuda.synchronize(dev)
+    L.cb_profile_enable(0)
+    out = {}
+    for nm in names:
+        tot, cnt = ctypes.c_double(), ctypes.c_uint64()
+        L.cb_profile_read(nm.encode(), ctypes.byref(tot), ctypes.byref(cnt))
+        if cnt.value:
+            out[nm] = {"avg_us": round(tot.value * 1e3 / cnt.value, 2), "launches": int(cnt.value)}
+    return out
+
+
+def c4_leg(args, torch, dist, world, rank, local, dev, use_dist, red_dev, steps, warmup, lanes_n, check, oracle_sample):
+    """BASELINE C4: 64 concurrent flush builds (2^18 keys each -> m = 2^25),
+    the filters split one contiguous subset per GPU (src/lib.rs:96-109,195-210:
+    each flush builds its table's filter, src/sstable.rs:62-65). One step =
+    clear + one batched build of this GPU's filters (cb_filter_insert_fixed_many:
+    one partition and one tile launch for all of them); consecutive steps go
+    round-robin to lanes_n lanes, each with its own filters and stream.
+    Timed with HIP events over the region (max over ranks). check: every
+    filter of every rank against the golden SHA-256s (tests/golden, made by an
+    independent numpy restatement) and, for oracle_sample filters per rank,
+    the C oracle's bits."""
     import lsmt_amd
-    from lsmt_amd import workload
+    from lsmt_amd import _lib, workload
     from lsmt_amd.shard import shard_range
+    L = _lib.load()
     nf_total, kpf, m = 64, 1 << 18, 1 << 25
     lo, hi = shard_range(nf_total, world, rank)
-    # pipeline lanes as in the probe: consecutive steps alternate between P
-    # sets of this GPU's filters, each set on its own stream
-    P = args.probe_streams
+    P = lanes_n
     lanes = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(P - 1)]
     keys = [torch.from_numpy(workload.c4_filter_keys(f, kpf)).to(dev) for f in range(lo, hi)]
     fsets = [[lsmt_amd.BloomFilter(m, device=local) for _ in range(lo, hi)] for _ in range(P)]
@@ -941,41 +1034,189 @@ def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result, red_dev
             f.clear(stream=sh)
         lsmt_amd.insert_many(fsets[i], batches, stream=sh)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
-    if use_dist:
-        dist.barrier()
+    el, ev_ms = _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes, step, steps)
+    # one lane: each batched build alone on the chip (its own duration)
+    nstep[0] = 0
+    P_saved, P = P, 1
+    _, ev1_ms = _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes[:1], step, steps)
+    P = P_saved
+    kus = _kernel_us(L, torch, dev, ["k_build_part", "k_build_tile"], step, min(steps, 50))
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
+    out = {"filters_total": nf_total, "filters_this_gpu": hi - lo, "keys_per_filter": kpf, "m_bits": m,
+           "steps": steps, "warmup": warmup, "pipeline_lanes": P,
+           "ms_per_step": round(el / steps * 1e3, 4),
+           "region_us_per_step": round(ev_ms * 1e3 / steps, 2),
+           "one_lane_us_per_step": round(ev1_ms * 1e3 / steps, 2),
+           "value": round(nf_total * kpf / (el / steps), 1), "unit": "keys/s (all GPUs)",
+           "kernels_us": kus}
+    if check:
+        g = _golden()["c4"]
+        good = True
+        for i, f in enumerate(range(lo, hi)):
+            for fl in fsets:
+                good &= _sha(fl[i].packed().view(np.uint8)) == g["packed_sha256"][f]
+        out["golden_all_filters_bit_exact"] = _all_ranks_true(torch, dist, use_dist, red_dev, good)
+        if oracle_sample:
+            from oracle import oracle
+            picks = sorted({0, (hi - lo) // 3, 2 * (hi - lo) // 3, hi - lo - 1})[:oracle_sample]
+            good = True
+            for i in picks:
+                o = oracle.OracleFilter(m)
+                o.insert_fixed(workload.c4_filter_keys(lo + i, kpf))
+                good &= all(np.array_equal(fl[i].bools(), o.bools()) for fl in fsets)
+                del o
+            out["oracle_sample_bit_exact"] = _all_ranks_true(torch, dist, use_dist, red_dev, good)
+            out["oracle_sample"] = f"filters {[lo + i for i in picks]} of each rank vs the C oracle (byte-per-bit)"
+    del fsets, keys, batches
+    torch.cuda.synchronize(dev)
+    return out
+
+
+def c4_roofline(leg, world):
+    """C4's roofline: SURVEY.md §8d's algorithmic bytes (16 B per key read +
+    the filter written once) per GPU per step over the HIP-event step time;
+    traffic from the committed C4 PMC summary (profiles/pmc_c4_r*.json)."""
+    per_gpu = leg["filters_this_gpu"] * (16 * leg["keys_per_filter"] + leg["m_bits"] / 8)
+    us = leg["region_us_per_step"]
+    ach = per_gpu / (us * 1e-6) / 1e9
+    r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(ach / HBM_PEAK_GBS, 4), "kernel": "k_build_part+k_build_tile",
+         "kernel_avg_us": us, "kernel_avg_source": "HIP events around the timed region / K (lanes overlap)",
+         "algorithmic_bytes": int(per_gpu),
+         "algorithmic_def": "filters_this_gpu x (16 B x 2^18 keys + 2^25/8 B) (SURVEY.md §8d C4 row)",
+         "frac_one_lane": round(per_gpu / (leg["one_lane_us_per_step"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+    t = 0
+    for k in ("k_build_part", "k_build_tile"):
+        v = _pmc_traffic(k, "pmc_c4_r[0-9]*.json")
+        t = t + v if (v and t is not None) else None
+    r["traffic"] = t if world == 1 else None
+    if r["traffic"]:
+        r["traffic_over_algorithmic"] = round(t / per_gpu, 3)
+    return r
+
+
+def c5_leg(args, torch, dev, local, world, rank, steps, warmup, lanes_n, check, red_dev, dist, use_dist):
+    """BASELINE C5, one rank's slice of the read fan-out (src/lib.rs:129-134
+    over 256 tables, 32 per GPU at 8 GPUs): 10M lookups (SURVEY.md §8d C5
+    batch over all 256 tables) probed against this rank's 32 filters of
+    m = 2^26 (filters 32r .. 32r+31, key(1000 + f, i < 2^19)) through the
+    FilterSet, one [32][156250] hit map per step, lanes_n lanes. The
+    all-gather that completes C5 at 8 GPUs runs in `--workload c5 --gpus 8`;
+    here the step is the per-GPU probe. check: the rank's whole slice against
+    the golden SHA-256, and filter 32r's row against the C oracle."""
+    import lsmt_amd
+    from lsmt_amd import workload
+    g = _golden()["c5"] if check else None
+    F, m, kpf, n, nf = 32, 1 << 26, 1 << 19, 10_000_000, 256
+    r = rank % 8
+    filters = []
+    for f in range(32 * r, 32 * r + F):
+        b = lsmt_amd.BloomFilter(m, device=local)
+        b.insert_batch(lsmt_amd.DeviceKeys(torch.from_numpy(workload.c5_filter_keys(f, kpf)).to(dev)))
+        filters.append(b)
+    look_np = workload.c5_lookups(n, nf, kpf)
+    look = torch.from_numpy(look_np).to(dev)
+    keys = lsmt_amd.DeviceKeys(look)
+    fset = lsmt_amd.FilterSet(m, width=32, device=local)
+    fset.assign_all(filters)
+    words = (n + 63) // 64
+    P = lanes_n
+    lanes = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(P - 1)]
+    hits = [torch.zeros((F, words), dtype=torch.int64, device=dev) for _ in range(P)]
+    nstep = [0]
+
+    def step():
+        i = nstep[0] % P
+        nstep[0] += 1
+        fset.probe(keys, out=hits[i], stream=lanes[i].cuda_stream)
+
+    for _ in range(warmup):
         step()
-    torch.cuda.synchronize(dev)  # every lane
-    if use_dist:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if use_dist:
-        t = torch.tensor([el], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    if args.check and rank == 0:
+    el, ev_ms = _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes, step, steps)
+    nstep[0] = 0
+    Psaved, P = P, 1
+    _, ev1_ms = _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes[:1], step, steps)
+    P = Psaved
+    sectors, rand_reads = _set_sectors(filters, look_np, m, F)
+    alg = 64 * sectors + 16 * n + F * n / 8
+    us = ev_ms * 1e3 / steps
+    ach = alg / (us * 1e-6) / 1e9
+    out = {"slice": f"rank {r} of 8: filters {32 * r}..{32 * r + F - 1} of {nf}", "n_keys": n,
+           "filters": F, "m_bits": m, "steps": steps, "pipeline_lanes": lanes_n,
+           "ms_per_step": round(el / steps * 1e3, 4), "region_us_per_step": round(us, 2),
+           "one_lane_us_per_step": round(ev1_ms * 1e3 / steps, 2),
+           "value": round(n * F * world / (el / steps), 1), "unit": "probes/s (all GPUs)",
+           "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4),
+                        "frac_one_lane": round(alg / (ev1_ms * 1e-3 / steps) / 1e9 / HBM_PEAK_GBS, 4),
+                        "kernel": "k_set_probe", "kernel_avg_us": round(us, 2),
+                        "algorithmic_bytes": int(alg),
+                        "algorithmic_def": f"64 B x {sectors} distinct sectors + 16n + F*n/8 "
+                                           "(SURVEY.md §8d alternative layout)",
+                        "traffic": _pmc_traffic("k_set_probe", "pmc_c5_r[0-9]*.json")}}
+    rr = _random_read_roofline()
+    if rr:
+        out["roofline"]["random_read_frac"] = round(rand_reads / (us * 1e-6) / rr, 4)
+    if check:
+        torch.cuda.synchronize(dev)
+        got = hits[0].cpu().numpy().view(np.uint64)
+        good = _sha(got.astype("<u8")) == g["rank_slice_hits_sha256"][r]
+        out["golden_slice_bit_exact"] = _all_ranks_true(torch, dist, use_dist, red_dev, good)
         from oracle import oracle
-        for i in range(min(4, hi - lo)):
-            o = oracle.OracleFilter(m)
-            o.insert_fixed(workload.c4_filter_keys(lo + i, kpf))
-            assert all(np.array_equal(fl[i].bools(), o.bools()) for fl in fsets), "C4 build differs from the oracle"
-        log("[check] C4 filters bit-exact vs oracle")
+        o = oracle.OracleFilter(m)
+        o.insert_fixed(workload.c5_filter_keys(32 * r, kpf))
+        row = oracle.probe_fixed([o], look_np, threads=8)
+        out["oracle_row_bit_exact"] = _all_ranks_true(torch, dist, use_dist, red_dev,
+                                                      bool(np.array_equal(got[0], row[0])))
+        out["oracle_sample"] = f"row of filter {32 * r} (all {n} lookups) vs the C oracle"
+        del o
+        if rank == 0 and world == 1 and not args.no_cpu:
+            # the C oracle (byte-per-bit src/bloom.rs, short-circuit) on one
+            # thread over a bounded sample of the same batch: the first 2^20
+            # lookups against all 32 filters
+            refs = []
+            for f in range(32 * r, 32 * r + F):
+                o = oracle.OracleFilter(m)
+                o.insert_fixed(workload.c5_filter_keys(f, kpf))
+                refs.append(o)
+            smp = 1 << 20
+            t0 = time.perf_counter()
+            oracle.probe_fixed(refs, look_np[:smp], threads=1)
+            tc = time.perf_counter() - t0
+            del refs
+            out["cpu_baseline"] = {"value": round(smp * F / tc, 1), "unit": "probes/s", "cores": 1, "kind": "port",
+                                   "sample": f"first {smp} of the {n} C5 lookups x {F} filters on 1 thread, "
+                                             f"{tc:.2f}s"}
+    del filters, fset, hits, look, keys
+    torch.cuda.synchronize(dev)
+    return out
+
+
+def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result, red_dev):
+    """`--workload c4`: the C4 leg alone (strong scaling: 64 filters split over
+    the GPUs), one JSON line from rank 0."""
+    leg = c4_leg(args, torch, dist, world, rank, local, dev, use_dist, red_dev, args.steps, args.warmup,
+                 args.probe_streams, check=args.check, oracle_sample=4 if args.check else 0)
     if rank == 0:
+        nf_total, kpf, m = 64, 1 << 18, 1 << 25
         alg = nf_total * (16 * kpf + m / 8)
+        el_step = leg["ms_per_step"] * 1e-3
         line = {"metric": "build keys/s (C4: 64 concurrent flush builds x 256K keys, m=2^25)",
-                "value": round(nf_total * kpf / (el / args.steps), 1), "unit": "keys/s", "n_gpus": world,
-                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
+                "value": leg["value"], "unit": "keys/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": leg["ms_per_step"],
                 "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
                 "data": "synthetic (splitmix64 hex keys, SURVEY.md §8d)",
                 "config": {"workload": "C4: 64 filters x 2^18 keys -> m=2^25 each, one subset per GPU",
-                           "parallelism": "filter-sharded, no collective", "pipeline_lanes": P},
+                           "parallelism": "filter-sharded, no collective", "pipeline_lanes": args.probe_streams},
                 "algorithmic_bytes_total": int(alg),
-                "step_effective_GBps_all_gpus": round(alg / (el / args.steps) / 1e9, 1),
+                "step_effective_GBps_all_gpus": round(alg / el_step / 1e9, 1),
+                "roofline": c4_roofline(leg, world), "c4": leg,
                 "cpu_baseline": c4_cpu_baseline(nf_total, kpf, m) if world == 1 and not args.no_cpu else None}
+        if args.rehearse_one_gpu:
+            line["rehearsal"] = f"{world} ranks on ONE GPU (gloo): checks the N-rank flow, not a scaling measurement"
+            line["valid"] = False
         print(json.dumps(line), file=result, flush=True)
     if use_dist:
         dist.barrier()
@@ -1112,12 +1353,13 @@ def _random_read_roofline():
     return None
 
 
-def _pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/pmc_rNN.json, FETCH_SIZE/WRITE_SIZE with the gfx950 corrections), or
-    None when no PMC run has been recorded for the current kernels."""
+def _pmc_traffic(kernel, pattern="pmc_r[0-9]*.json"):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
+    summary matching `pattern` under profiles/ (FETCH_SIZE/WRITE_SIZE with the
+    gfx950 corrections; C3 by default, pmc_c4_r*/pmc_c5_r* for those shapes),
+    or None when no PMC run has been recorded for it."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r[0-9]*.json")))  # the round summaries
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))  # the round summaries
     if not files:
         return None
     try:

@@ -161,7 +161,8 @@ hipError_t ensure_pad_zeroed(const cb_filter* cf, hipStream_t s) {
 // Record f's write mark on s: its own mark again when no one else holds it
 // (no batch shares it, no mirror refresh is waiting on it), else a new one.
 hipError_t record_own_mark(cb_filter* f, hipStream_t s) {
-  if (!mirror_on(f)) {  // no mirror to order: the next refresh (mirror turned on) syncs the device
+  if (!mirror_on(f)) {  // no mirror to order: the next refresh (mirror turned on) syncs this stream
+    f->unmarked_stream.store(s, std::memory_order_relaxed);
     f->unmarked.store(true, std::memory_order_release);
     return hipSuccess;
   }
@@ -332,6 +333,7 @@ int mark_written_many(Workspace& ws, cb_filter* const* fs, uint32_t nf, hipStrea
   for (uint32_t i = 0; i < nf; ++i) any_on |= mirror_on(fs[i]);
   if (!any_on) {  // no mirror to order (see record_own_mark)
     for (uint32_t i = 0; i < nf; ++i) {
+      fs[i]->unmarked_stream.store(s, std::memory_order_relaxed);
       fs[i]->unmarked.store(true, std::memory_order_release);
       fs[i]->gen.fetch_add(1, std::memory_order_acq_rel);
     }
@@ -1125,7 +1127,7 @@ int cb_filter_clear(cb_filter* f, void* stream) {
 int cb_filter_host_mirror(cb_filter* f, int mode) {
   if (!f) return fail(CB_EINVAL, "null filter");
   if (mode < -1 || mode > 1) return fail(CB_EINVAL, "mode must be -1 (auto), 0 (off) or 1 (on)");
-  f->mirror = mode;
+  f->mirror.store(mode, std::memory_order_relaxed);
   return CB_OK;
 }
 
@@ -1180,11 +1182,14 @@ int refresh_mirror(const cb_filter* cf) {
     } else {
       DeviceGuard dg(f->device);
       if (f->unmarked.exchange(false, std::memory_order_acq_rel)) {
-        HIP_TRY(hipDeviceSynchronize());  // a write made while the mirror was off recorded no event
-      } else {
-        const std::shared_ptr<WriteMark> m = std::atomic_load(&f->wmark);
-        if (m) HIP_TRY(hipEventSynchronize(m->ev));
+        // a write made while the mirror was off recorded no event: wait for
+        // the stream it was issued on (every write to one filter is ordered
+        // by its exclusive writer, so that stream's tail covers them all)
+        HIP_TRY(hipStreamSynchronize(f->unmarked_stream.load(std::memory_order_relaxed)));
       }
+      // and the last recorded write (a write made after the mirror came on)
+      const std::shared_ptr<WriteMark> m = std::atomic_load(&f->wmark);
+      if (m) HIP_TRY(hipEventSynchronize(m->ev));
       HIP_TRY(hipMemcpy(f->host.data(), f->words, nw * 4, hipMemcpyDeviceToHost));
     }
   }

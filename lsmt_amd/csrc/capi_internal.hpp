@@ -62,8 +62,16 @@ struct cb_filter {
   std::mutex zero_mu;                 // the lazy clear's issue vs. a refresh (capi.cpp ensure_zeroed)
   std::vector<uint32_t> host;         // ceil(m/32) words
   std::shared_ptr<WriteMark> wmark;   // recorded after the last device write (atomic_load / atomic_store)
-  std::atomic<bool> unmarked{false};  // a write went unrecorded (mirror off): the refresh syncs the device
-  int mirror = -1;                    // -1 auto (m <= kMirrorAutoBits), 0 off, 1 on
+  // a write went unrecorded (mirror off): the refresh synchronises the stream
+  // of the last such write (unmarked_stream; hipStreamSynchronize on it, not
+  // the whole device). Writes from several streams while unrecorded keep the
+  // last stream only when each write was ordered after the previous one (the
+  // reference's `&mut self` insert: exclusive, so ordered by the caller).
+  std::atomic<bool> unmarked{false};
+  std::atomic<hipStream_t> unmarked_stream{nullptr};
+  // -1 auto (m <= kMirrorAutoBits), 0 off, 1 on; read by concurrent `&self`
+  // callers (cb_may_contain, probes) while cb_filter_host_mirror may write it
+  std::atomic<int> mirror{-1};
 };
 
 // auto mirror up to 2 MiB of host words: past that, the first per-key call
@@ -71,7 +79,10 @@ struct cb_filter {
 // record only for it (SSTable filters are m = 1024, src/sstable.rs:44)
 constexpr uint64_t kMirrorAutoBits = 1ull << 24;
 
-inline bool mirror_on(const cb_filter* f) { return f->mirror == 1 || (f->mirror == -1 && f->m <= kMirrorAutoBits); }
+inline bool mirror_on(const cb_filter* f) {
+  const int mode = f->mirror.load(std::memory_order_relaxed);
+  return mode == 1 || (mode == -1 && f->m <= kMirrorAutoBits);
+}
 
 struct cb_filterset {
   uint64_t m = 0;

@@ -474,10 +474,14 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
     HIP_TRY(ws.f_vsp.reserve(n * sizeof(ulonglong2), s));
     vsp = (ulonglong2*)ws.f_vsp.p;
     order = (cb::SortKey*)ws.f_sk2.p;
+#ifdef CB_EXPERIMENTS
     static const int bin_T_env = [] {
-      const char* v = getenv("CB_BIN_T");  // group size target (tests, tuning); 0 disables the bin sort
+      const char* v = getenv("CB_BIN_T");  // group size target (tuning); 0 disables the bin sort
       return v && *v ? atoi(v) : -1;
     }();
+#else
+    const int bin_T_env = -1;
+#endif
     // groups of ~n / 1536 records (six 1024-record group sorts per CU on 256
     // CUs, one wave), at least 640, at most 1536 (2048-record group sorts)
     const uint32_t bin_T = bin_T_env >= 0 ? (uint32_t)bin_T_env

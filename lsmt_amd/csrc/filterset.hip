@@ -166,8 +166,10 @@ __global__ __launch_bounds__(256) void k_set_put_slot(const uint32_t* __restrict
 }
 
 constexpr uint32_t kSetProbeThreads = 64 * kSetWords;  // one 64-key hit word per wave
+#ifdef CB_EXPERIMENTS
 constexpr uint32_t kFlowThreads = 256;  // k_set_probe_flow: 4 waves per block
 constexpr uint32_t kFlowWaves = kFlowThreads / 64;
+#endif
 
 // set_key_mask for a 16-byte key already in registers (no union pre-test).
 template <int MODE, int W, bool SC>
@@ -282,6 +284,7 @@ __global__ __launch_bounds__(kSetProbeThreads) void k_set_probe(const void* __re
   if (sink.pack) emit_positions(sink, hb, used, wbase, hwords);
 }
 
+#ifdef CB_EXPERIMENTS
 // Persistent form: a grid sized to the chip (blocks per CU x CUs), each wave
 // striding over 64-key hit words on its own, with no block barrier after the
 // start: a wave whose random reads came back early starts its next word at
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(kFlowThreads) void k_set_probe_flow(const void* __r
     }
   }
 }
-
+#endif  // CB_EXPERIMENTS
 
 inline uint32_t grid_cap(uint64_t items, uint32_t cap) {
   uint64_t g = (items + 255) / 256;
@@ -380,26 +383,24 @@ hipError_t launch_set_put_slot(const uint32_t* words, uint64_t m, uint32_t slot,
 }
 
 template <int KK, int MM, int WW>
-static void set_probe(bool sc, bool flow, const void* set, const uint32_t* any, uint32_t used,
-                      const KeySrc& ks, uint64_t n, const ModP& mp, const ZoneView& zv,
-                      uint64_t* hits, uint64_t hwords, uint32_t grid, hipStream_t s, const PackSink& sink) {
+static void set_probe(bool flow, const void* set, const uint32_t* any, uint32_t used, const KeySrc& ks,
+                      uint64_t n, const ModP& mp, const ZoneView& zv, uint64_t* hits, uint64_t hwords,
+                      uint32_t grid, hipStream_t s, const PackSink& sink) {
+#ifdef CB_EXPERIMENTS
   if (flow) {
-    if (sc)
-      hipLaunchKernelGGL((k_set_probe_flow<KK, MM, WW, true>), dim3(grid), dim3(kFlowThreads), 0, s,
-                         set, any, used, ks, n, mp, zv, hits, hwords);
-    else
-      hipLaunchKernelGGL((k_set_probe_flow<KK, MM, WW, false>), dim3(grid), dim3(kFlowThreads), 0, s,
-                         set, any, used, ks, n, mp, zv, hits, hwords);
+    hipLaunchKernelGGL((k_set_probe_flow<KK, MM, WW, true>), dim3(grid), dim3(kFlowThreads), 0, s, set, any,
+                       used, ks, n, mp, zv, hits, hwords);
     return;
   }
-  if (sc)
-    hipLaunchKernelGGL((k_set_probe<KK, MM, WW, true>), dim3(grid), dim3(kSetProbeThreads), 0, s,
-                       set, any, used, ks, n, mp, zv, hits, hwords, sink);
-  else
-    hipLaunchKernelGGL((k_set_probe<KK, MM, WW, false>), dim3(grid), dim3(kSetProbeThreads), 0, s,
-                       set, any, used, ks, n, mp, zv, hits, hwords, sink);
+#else
+  (void)flow;
+#endif
+  // the reference's short-circuit (src/bloom.rs:50): set[b] only where set[a] != 0
+  hipLaunchKernelGGL((k_set_probe<KK, MM, WW, true>), dim3(grid), dim3(kSetProbeThreads), 0, s, set, any, used,
+                     ks, n, mp, zv, hits, hwords, sink);
 }
 
+#ifdef CB_EXPERIMENTS
 // Compute units of the current device (cached per device).
 static uint32_t device_cus() {
   static uint32_t cus[64] = {};
@@ -412,6 +413,7 @@ static uint32_t device_cus() {
   }
   return cus[dev];
 }
+#endif
 
 hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
                             const uint32_t* any, uint32_t used, const KeySrc& ks, uint64_t n,
@@ -419,41 +421,38 @@ hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
                             uint64_t hwords, hipStream_t s, const PackSink* sink) {
   if (!n || !used) return hipSuccess;
   const PackSink nosink{nullptr, 0, nullptr, 0};
-  // CB_SET_SC=0 reads set[b] unconditionally (one latency, more bytes);
-  // default keeps the reference's short-circuit.
-  static const bool sc = [] {
-    const char* v = getenv("CB_SET_SC");
-    return !(v && v[0] == '0');
-  }();
-  // CB_SET_ANY=1 enables the union pre-test. Off by default: measured on C3
-  // it costs more than it saves (52.8 vs 40.0 us), because the 2 extra random
-  // reads per key into any[] cost as much random-read throughput as the set
-  // reads they avoid, and half of C3's keys are present in some slot. It pays
-  // only when most lookups miss every table.
-  static const bool use_any = [] {
+  const ZoneView zv = zones ? *zones : ZoneView{nullptr, nullptr, nullptr, 0};
+  const uint64_t nw = (n + 63) / 64;
+  uint32_t grid = (uint32_t)((nw + kSetWords - 1) / kSetWords);
+  bool use_any = false, flow = false;
+#ifdef CB_EXPERIMENTS
+  // A/B knobs, compiled only into experiment builds (make EXTRA=-DCB_EXPERIMENTS):
+  // CB_SET_ANY=1 the union pre-test (measured on C3: 52.8 vs 40.0 us, the 2
+  // extra random reads per key into any[] cost as much as the set reads they
+  // avoid); CB_SET_FLOW=1 the persistent k_set_probe_flow (38.6-39.3 us, no
+  // better; slower at the C5 shape), CB_SET_FLOW_BPC its blocks per CU.
+  static const bool env_any = [] {
     const char* v = getenv("CB_SET_ANY");
     return v && v[0] == '1';
   }();
-  const ZoneView zv = zones ? *zones : ZoneView{nullptr, nullptr, nullptr, 0};
-  const uint64_t nw = (n + 63) / 64;
-  // CB_SET_FLOW=1: the persistent k_set_probe_flow; CB_SET_FLOW_BPC: its
-  // blocks per CU (default 8: 32 waves per CU). Read per launch (tuning).
-  const char* fv = getenv("CB_SET_FLOW");
-  const bool flow = fv && fv[0] == '1' && !use_any && !sink;  // no union pre-test or pack in the flow form
-  uint32_t grid;
+  static const int env_flow_bpc = [] {
+    const char* v = getenv("CB_SET_FLOW");
+    if (!(v && v[0] == '1')) return 0;
+    const char* b = getenv("CB_SET_FLOW_BPC");
+    return b && atoi(b) > 0 ? atoi(b) : 8;
+  }();
+  use_any = env_any;
+  flow = env_flow_bpc && !use_any && !sink;  // no union pre-test or pack in the flow form
   if (flow) {
-    const char* bv = getenv("CB_SET_FLOW_BPC");
-    const uint32_t bpc = bv ? (uint32_t)atoi(bv) : 8u;
     const uint64_t want = (nw + kFlowWaves - 1) / kFlowWaves;
-    const uint64_t cap = (uint64_t)device_cus() * (bpc ? bpc : 8u);
+    const uint64_t cap = (uint64_t)device_cus() * (uint32_t)env_flow_bpc;
     grid = (uint32_t)(want < cap ? want : cap);
-  } else {
-    grid = (uint32_t)((nw + kSetWords - 1) / kSetWords);
   }
+#endif
   ProfScope ps(zv.gated ? "k_set_probe_gated" : "k_set_probe", s);
   CB_SET_DISPATCH(keyk, mode, width,
-                  (set_probe<KK, MM, WW>(sc, flow, set, use_any ? any : nullptr, used, ks, n, mp, zv,
-                                         hits, hwords, grid, s, sink ? *sink : nosink)));
+                  (set_probe<KK, MM, WW>(flow, set, use_any ? any : nullptr, used, ks, n, mp, zv, hits, hwords,
+                                         grid, s, sink ? *sink : nosink)));
   return hipGetLastError();
 }
 

@@ -262,6 +262,10 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   __shared__ uint32_t stage32[LDSB / 4];
   __shared__ DirMap sdm;  // the directory's map, indexed per lane
   uint8_t* stage = reinterpret_cast<uint8_t*>(stage32);
+  // the bin sort overflowed (a group outgrew its LDS tile and left its slice
+  // of `order` / `vsp` unwritten): nothing here may read those stale records
+  // or write at offsets derived from them; the caller redoes the sort
+  if (r->flags[3]) return;
   const uint64_t p0 = (uint64_t)blockIdx.x * kNT;
   const uint64_t p = p0 + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;

@@ -766,11 +766,19 @@ static uint32_t fit_tiles(uint64_t m, int64_t tb, int64_t hi) {
   return (uint32_t)tb;
 }
 
-// Tuning overrides for experiments (unset in production): CB_PROBE_TB / CB_BUILD_TB
-// fix the tile bits, CB_PROBE_KPT / CB_BUILD_KPT the partition keys per thread.
+// Tuning overrides, compiled only into experiment builds (make
+// EXTRA=-DCB_EXPERIMENTS): CB_PROBE_TB / CB_BUILD_TB fix the tile bits,
+// CB_PROBE_KPT / CB_BUILD_KPT the partition keys per thread, CB_BUILD_STORES
+// the build's store policy, CB_PROBE_XFLAGS the tile probe's variant bits.
+// The shipped library always takes the defaults.
 static int env_int(const char* name, int dflt) {
+#ifdef CB_EXPERIMENTS
   const char* v = getenv(name);
   return v && *v ? atoi(v) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
 }
 
 TilePlan plan_build(uint64_t m, uint64_t n, uint32_t nb) {

@@ -23,12 +23,15 @@ def splitmix64(x: np.ndarray) -> np.ndarray:
     return z ^ (z >> np.uint64(31))
 
 
+# byte b -> its two lowercase hex chars, high nibble first in memory
+_HEX2 = (_HEX[np.arange(256) >> 4].astype(np.uint16) | (_HEX[np.arange(256) & 15].astype(np.uint16) << 8))
+
+
 def hex16(v: np.ndarray) -> np.ndarray:
-    """uint64[n] -> uint8[n,16] lowercase hex, most-significant nibble first."""
-    v = v.astype(np.uint64, copy=False)
-    shifts = np.arange(60, -4, -4, dtype=np.uint64)  # 60, 56, ..., 0
-    nib = (v[:, None] >> shifts[None, :]) & np.uint64(15)
-    return _HEX[nib.astype(np.intp)]
+    """uint64[n] -> uint8[n,16] lowercase hex, most-significant nibble first
+    (one 2-char table lookup per byte of the big-endian value)."""
+    be = np.ascontiguousarray(v, dtype=np.uint64).astype(">u8").view(np.uint8).reshape(-1, 8)
+    return _HEX2[be].view(np.uint8).reshape(-1, 16)
 
 
 def keys(seed: int, idx) -> np.ndarray:
@@ -57,15 +60,11 @@ def probe_lookups(n: int, nf: int, keys_per_filter: int, seed_base: int, absent_
     filters (bench.py's rotating-batch leg)."""
     i = np.arange(n, dtype=np.uint64)
     out = np.empty((n, 16), np.uint8)
-    even = i[0::2]
-    j = even // np.uint64(2)
-    f = (j % np.uint64(nf)).astype(np.int64)
+    j = i[0::2] // np.uint64(2)
+    seed = np.uint64(seed_base) + j % np.uint64(nf)
     kidx = (j // np.uint64(nf) + np.uint64(shift)) % np.uint64(keys_per_filter)
-    ev = np.empty((len(even), 16), np.uint8)
-    for fs in np.unique(f):
-        sel = f == fs
-        ev[sel] = keys(seed_base + int(fs), kidx[sel])
-    out[0::2] = ev
+    with np.errstate(over="ignore"):
+        out[0::2] = hex16(splitmix64(((seed << np.uint64(32)) & np.uint64(_M64)) + kidx))
     out[1::2] = keys(absent_seed, i[1::2])
     return out
 

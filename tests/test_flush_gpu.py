@@ -228,6 +228,31 @@ def test_create_sort_sizes(gpu, n, shape):
     assert (zone.min, zone.max) == (min(keys), max(keys))
 
 
+def test_create_bin_overflow_over_stale_workspace(gpu):
+    """A bin sort that overflows (two 8-byte key prefixes, 100K keys each: a
+    bin far larger than an LDS tile) right after a larger flush on the same
+    stream, whose sort records and value spans (longer values, other offsets)
+    still sit in the workspace. The overflowed groups leave their slice of
+    those buffers unwritten, so the first k_format must not run over them
+    (ADVICE r3): the file must equal the oracle's, and a table made before it
+    must be untouched (src/sstable.rs:57-72)."""
+    rng = np.random.default_rng(77)
+    big = [bytes(r) for r in workload.key_range(9100, 300_000)]
+    big_vals = [bytes(rng.integers(0, 256, 60, dtype=np.uint8)) for _ in big]
+    t_big, _, _ = gpu.sstable_create(list(zip(big, big_vals)))
+    neighbour = [(bytes(r), b"v%d" % i) for i, r in enumerate(workload.key_range(9200, 5000))]
+    t_nb, _, _ = gpu.sstable_create(neighbour)
+    nb_file = t_nb.data()
+    tail = workload.key_range(9300, 200_000)
+    keys = [(b"aaaaaaaa" if i % 2 else b"bbbbbbbb") + bytes(r[:8]) for i, r in enumerate(tail)]
+    vals = [(i % 251).to_bytes(1, "little") for i in range(len(keys))]
+    t, _, zone = gpu.sstable_create(list(zip(keys, vals)))
+    assert t.data() == oracle.sstable_create(list(zip(keys, vals)))
+    assert (zone.min, zone.max) == (min(keys), max(keys))
+    assert t_nb.data() == nb_file == oracle.sstable_create(neighbour)
+    assert t_big.nlines == len(big)
+
+
 @pytest.mark.parametrize("n", [1 << 22, 1 << 24])
 def test_create_unsorted_large(gpu, n):
     """Unsorted flushes at 4M entries and at 2^24, the largest batch the bin

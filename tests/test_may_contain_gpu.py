@@ -167,6 +167,34 @@ def test_mirror_turned_on_after_unrecorded_writes(gpu):
         assert np.array_equal(np.array([f.may_contain(bytes(k)) for k in probe]), oracle_hits(of, probe))
 
 
+def test_unrecorded_refresh_waits_for_its_stream_only(gpu):
+    """A write made while the mirror was off records no event; the first
+    refresh after the mirror comes on waits for the stream that write was
+    issued on, not the whole device: a long kernel on another stream (a
+    ~1 s spin) is still running when the refresh has returned the oracle's
+    answers (the refresh used to call hipDeviceSynchronize)."""
+    import torch
+    m = 1 << 26
+    keys = workload.key_range(61, 100_000)
+    probe = np.concatenate([keys[:500], workload.key_range(62, 500)])
+    o = oracle.OracleFilter(m)
+    o.insert_fixed(keys)
+    b = gpu.BloomFilter(m)
+    b.host_mirror(0)
+    wr, busy = torch.cuda.Stream(), torch.cuda.Stream()
+    b.insert_batch(gpu.DeviceKeys(torch.from_numpy(keys).cuda()), stream=wr)  # unrecorded
+    with torch.cuda.stream(busy):
+        torch.cuda._sleep(2_000_000_000)  # ~1 s of spinning on the other stream
+        done = torch.cuda.Event()
+        done.record(busy)
+    b.host_mirror(1)
+    got = np.array([b.may_contain(bytes(k)) for k in probe])
+    still_busy = not done.query()
+    busy.synchronize()
+    assert np.array_equal(got, oracle_hits(o, probe))
+    assert still_busy, "the mirror refresh waited for an unrelated stream"
+
+
 def test_latency_tool_mirror_under_1us(gpu):
     """The C-ABI per-key call (no Python in the loop) at the product's m =
     1024 and at the C3 filter size: the mirror agrees with the GPU probe on

@@ -5,7 +5,7 @@
 # Usage: bash tools/profile_round.sh [extra bench.py args]
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p $OUT
 # the trace pass runs the bench as configured (three pipeline lanes: launches
 # overlap, so per-dispatch durations are ~2x the per-step share; pmc_summary
