@@ -181,12 +181,20 @@ int cb_set_load_meta(cb_filterset* set, uint32_t slot, const uint8_t* in, uint64
                      void* stream);
 
 /* ---- bit-sliced filter sets (the read-path fan-out) ---- */
-/* A FilterSet holds up to `width` (32 or 64) filters of one size m in a
- * position-major layout: word p (uint32 / uint64) has bit s = bit p of the
- * filter in slot s. Probing it answers may_contain for every slot with two
- * word reads per key (Database::get's per-table loop, src/lib.rs:129-134,
- * collapsed; m is uniform across SSTables, src/sstable.rs:44,59). The set is a
- * derived copy: the cb_filter handles stay the source of truth. */
+/* A FilterSet holds up to `width` filters of one size m in a position-major
+ * layout: word p (uint32 / uint64) has bit s = bit p of the filter in slot s.
+ * Probing it answers may_contain for every slot with two word reads per key
+ * (Database::get's per-table loop, src/lib.rs:129-134, collapsed; m is
+ * uniform across SSTables, src/sstable.rs:44,59). The set is a derived copy:
+ * the cb_filter handles stay the source of truth.
+ * width is 32, 64, or a multiple of 64 up to 4096 (a "wide" set: row p is
+ * width/64 uint64 words, 128 B per row at 1024 slots; at the product's
+ * m = 1024 the whole set is 128 KiB). A wide set serves the reference's
+ * real shape — a table per 1024 inserts (src/lib.rs:72,105), hundreds of
+ * m = 1024 filters — in one launch: cb_set_get_many_* take up to `width`
+ * tables. Its probe reads row b's word only where row a's is non-zero (the
+ * reference's `&&`, src/bloom.rs:50). cb_set_probe_pack_fixed and
+ * cb_set_probe_allgather_fixed take sets of at most 64 slots. */
 int cb_set_create(uint64_t m_bits, uint32_t width, int device, cb_filterset** out);
 int cb_set_destroy(cb_filterset* set);
 /* used = 1 + the highest slot assigned so far (the number of hit rows). */
@@ -325,8 +333,11 @@ int cb_get_many_var(const cb_table* const* tables, uint32_t nt, const uint64_t* 
  * (key, table) gate — zone_map.contains && bloom.may_contain, exactly
  * cb_set_probe_gated_*'s bit — computed from the FilterSet inside the search
  * kernel instead of read from hit rows. Table t is set slot slots[t]
- * (slots NULL = slot t); nt <= the set's width; tables and set on one device.
- * Same async contract (total = NULL). */
+ * (slots NULL = slot t); nt <= the set's width (up to 4096 with a wide set;
+ * runs of ascending or descending slots, e.g. slot = the table's position in
+ * Vec<SsTable> walked newest first, take each group of 64 tables' gate from
+ * one window of the set's rows, other mappings one bit per table); tables and
+ * set on one device. Same async contract (total = NULL). */
 int cb_set_get_many_fixed(const cb_filterset* set, const cb_table* const* tables, uint32_t nt,
                           const uint32_t* slots, const uint8_t* keys, uint32_t key_len, uint64_t n,
                           int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap, uint64_t* total,

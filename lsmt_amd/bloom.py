@@ -469,10 +469,13 @@ def probe(filters: Sequence[BloomFilter], keys, out=None, stream=None) -> np.nda
 
 
 class FilterSet:
-    """Up to ``width`` (32 or 64) filters of one size m, bit-sliced in HBM for
-    the read-path fan-out (Database::get, src/lib.rs:129-134): one probe call
-    answers may_contain for every slot with two word reads per key. A derived
-    copy — the BloomFilter handles remain the source of truth."""
+    """Up to ``width`` filters of one size m, bit-sliced in HBM for the
+    read-path fan-out (Database::get, src/lib.rs:129-134): one probe call
+    answers may_contain for every slot with two word (or row) reads per key.
+    width 32 or 64, or a wide set of any multiple of 64 up to 4096 slots
+    (rows of width/64 uint64 words: the reference's real shape of hundreds of
+    m = 1024 tables, src/sstable.rs:44,59, src/lib.rs:72,105). A derived copy —
+    the BloomFilter handles remain the source of truth."""
 
     def __init__(self, m: int, width: int = 32, device: int = 0):
         self._h = ctypes.c_void_p()
@@ -484,7 +487,8 @@ class FilterSet:
                      stream=None) -> "FilterSet":
         if not filters:
             raise ValueError("need at least one filter")
-        width = width or (32 if len(filters) <= 32 else 64)
+        width = width or (32 if len(filters) <= 32 else 64 if len(filters) <= 64 else
+                          (len(filters) + 63) // 64 * 64)
         s = cls(filters[0].m, width, device=filters[0].device)
         s.assign_all(filters, stream=stream)
         return s
@@ -790,7 +794,8 @@ def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=Non
     table's gate (its slot's ZoneMap and Bloom bits, as
     FilterSet.probe(gated=True)) is computed inside the search kernel, so no
     hit rows exist; hit_rows then names each table's slot (default t) and
-    hits must be None. At most the set's width tables."""
+    hits must be None. At most the set's width tables (a wide set: up to 4096
+    in one launch)."""
     if filterset is not None and hits is not None:
         raise ValueError("filterset= computes the gate itself: pass hits=None")
     b = as_batch(keys)

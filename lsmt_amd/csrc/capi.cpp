@@ -501,8 +501,14 @@ int set_probe_zero_copy(const cb_filterset* set, const uint8_t* keys, uint32_t k
   HIP_TRY(hipHostGetDevicePointer(&dh, hits, 0));
   const int keyk = (key_len == 16 && !((uintptr_t)dk & 15)) ? cb::KEY_FIXED16 : cb::KEY_FIXED;
   cb::KeySrc ks{(const uint8_t*)dk, nullptr, key_len};
-  HIP_TRY(cb::launch_set_probe(keyk, set->mode, set->width, set->words, set->any, set->used, ks, n,
-                               set->mp, zv, (uint64_t*)dh, (n + 63) / 64, s));
+  if (set_is_wide(set)) {
+    const cb::WideZone wz = wide_zone_view(set);
+    HIP_TRY(cb::launch_wide_probe(keyk, set->mode, set->R, (const uint64_t*)set->words, set->used, ks, n, set->mp,
+                                  zv ? &wz : nullptr, (uint64_t*)dh, (n + 63) / 64, s));
+  } else {
+    HIP_TRY(cb::launch_set_probe(keyk, set->mode, set->width, set->words, set->any, set->used, ks, n,
+                                 set->mp, zv, (uint64_t*)dh, (n + 63) / 64, s));
+  }
   HIP_TRY(hipStreamSynchronize(s));  // the table is no longer read: no reader event needed
   return CB_OK;
 }
@@ -519,7 +525,7 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
   const cb::ZoneView zv = set_zone_view(set);
   if (!offsets && key_len && is_pinned_host(keys) && is_pinned_host(hits)) {
     g_last_path = 4;
-    return set_probe_zero_copy(set, keys, key_len, n, hits, s, (gated && set->zgated) ? &zv : nullptr);
+    return set_probe_zero_copy(set, keys, key_len, n, hits, s, (gated && set->zany) ? &zv : nullptr);
   }
   StagedKeys sk;
   int rc = offsets ? stage_var(ws, keys, offsets, n, s, sk)
@@ -532,10 +538,16 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
     HIP_TRY(ws.hits.reserve((size_t)set->used * hwords * 8, s));
     dhits = (uint64_t*)ws.hits.p;
   }
-  HIP_TRY(cb::launch_set_probe(sk.keyk, set->mode, set->width, set->words, set->any, set->used,
-                               sk.ks, n, set->mp, (gated && set->zgated) ? &zv : nullptr, dhits,
-                               hwords, s));
-  if (gated && set->zgated) {
+  if (set_is_wide(set)) {
+    const cb::WideZone wz = wide_zone_view(set);
+    HIP_TRY(cb::launch_wide_probe(sk.keyk, set->mode, set->R, (const uint64_t*)set->words, set->used, sk.ks, n,
+                                  set->mp, (gated && set->zany) ? &wz : nullptr, dhits, hwords, s));
+  } else {
+    HIP_TRY(cb::launch_set_probe(sk.keyk, set->mode, set->width, set->words, set->any, set->used,
+                                 sk.ks, n, set->mp, (gated && set->zany) ? &zv : nullptr, dhits,
+                                 hwords, s));
+  }
+  if (gated && set->zany) {
     int zr = note_zone_read(set, s);
     if (zr) return zr;
   }
@@ -568,6 +580,8 @@ int set_probe_device(const cb_filterset* set, const uint8_t* keys, uint32_t key_
   if (!is_device_ptr(hits) || (key_len && !is_device_ptr(keys)) || (sink_pack && !is_device_ptr(sink_pack)))
     return fail(CB_EINVAL, "keys, hits and pack must be device memory");
   const uint64_t hwords = (n + 63) / 64;
+  if (sink_pack && set_is_wide(set))
+    return fail(CB_EINVAL, "the fused probe + pack takes sets of at most 64 slots");
   if (sink_pack && (uint64_t)set->used * hwords * 64 >= (1ull << 32))
     return fail(CB_EINVAL, "used * ceil(n/64) * 64 must be below 2^32 (u32 positions and counts)");
   DeviceGuard dg(set->device);
@@ -583,9 +597,15 @@ int set_probe_device(const cb_filterset* set, const uint8_t* keys, uint32_t key_
     if (rc) return rc;
     sink = cb::PackSink{sink_pack, cap, reinterpret_cast<unsigned long long*>(st->ctl), st->parity};
   }
-  const hipError_t e = cb::launch_set_probe(keyk, set->mode, set->width, set->words, set->any, set->used, ks, n,
-                                            set->mp, (gated && set->zgated) ? &zv : nullptr, hits, hwords, s,
-                                            sink_pack ? &sink : nullptr);
+  hipError_t e;
+  if (set_is_wide(set)) {
+    const cb::WideZone wz = wide_zone_view(set);
+    e = cb::launch_wide_probe(keyk, set->mode, set->R, (const uint64_t*)set->words, set->used, ks, n, set->mp,
+                              (gated && set->zany) ? &wz : nullptr, hits, hwords, s);
+  } else {
+    e = cb::launch_set_probe(keyk, set->mode, set->width, set->words, set->any, set->used, ks, n, set->mp,
+                             (gated && set->zany) ? &zv : nullptr, hits, hwords, s, sink_pack ? &sink : nullptr);
+  }
   if (e != hipSuccess) {
     // the kernel may still have been queued (an earlier sticky error): clear
     // both claim words behind it, so the next launch never reuses a dirty one
@@ -594,7 +614,7 @@ int set_probe_device(const cb_filterset* set, const uint8_t* keys, uint32_t key_
   }
   if (st) st->parity ^= 1u;  // the launch cleared the other claim word for the next one
   g_last_path = 3;
-  if (gated && set->zgated) return note_zone_read(set, s);
+  if (gated && set->zany) return note_zone_read(set, s);
   return CB_OK;
 }
 
@@ -617,38 +637,45 @@ namespace {
 // zone updates, which happen once per table flush: the upload is ordered on
 // stream s and waited for, so the host staging vector can be reused.
 int upload_zones(cb_filterset* set, hipStream_t s) {
-  uint32_t hdr[64 * 4] = {};
+  // layout: 32/64-slot sets cb::ZoneView (64 headers, 128 prefixes, blob);
+  // wide sets cb::WideZone (W headers, 2 W prefixes, the gated bits, blob)
+  const bool wide = set_is_wide(set);
+  const uint32_t nslot = wide ? set->width : 64;
+  const size_t hdr_bytes = wide ? wide_zone_hdr_bytes(nslot) : cb_zone_hdr_bytes;
+  const size_t pre_bytes = wide ? wide_zone_pre_bytes(nslot) : cb_zone_pre_bytes;
+  const size_t blob_off = wide ? wide_zone_blob_off(nslot) : cb_zone_blob_off;
+  std::vector<uint32_t> hdr((size_t)nslot * 4, 0u);
+  std::vector<cb::BoundPrefix> pre((size_t)nslot * 2);
+  std::memset(pre.data(), 0, pre.size() * sizeof(cb::BoundPrefix));
   std::vector<uint8_t> blob;
-  set->zgated = 0;
+  set->zg.assign(std::max<uint32_t>(1, set->width / 64), 0ull);
+  set->zany = false;
   for (uint32_t i = 0; i < set->width; ++i) {
     if (!(set->zhas_lo[i] && set->zhas_hi[i])) continue;
-    set->zgated |= 1ull << i;
+    set->zg[i >> 6] |= 1ull << (i & 63);
+    set->zany = true;
     hdr[4 * i + 0] = (uint32_t)blob.size();
     hdr[4 * i + 1] = (uint32_t)set->zlo[i].size();
     blob.insert(blob.end(), set->zlo[i].begin(), set->zlo[i].end());
     hdr[4 * i + 2] = (uint32_t)blob.size();
     hdr[4 * i + 3] = (uint32_t)set->zhi[i].size();
     blob.insert(blob.end(), set->zhi[i].begin(), set->zhi[i].end());
-  }
-  static_assert(sizeof(hdr) == cb_zone_hdr_bytes, "ZoneView header size");
-  // big-endian 16-byte prefixes of every bound (cb::cmp16's operands)
-  cb::BoundPrefix pre[64 * 2] = {};
-  for (uint32_t i = 0; i < set->width; ++i) {
-    if (!((set->zgated >> i) & 1)) continue;
+    // big-endian 16-byte prefixes of both bounds (cb::cmp16's operands)
     for (int j = 0; j < 2; ++j) {
-      const std::string& b = j ? set->zhi[i] : set->zlo[i];
+      const std::string& bnd = j ? set->zhi[i] : set->zlo[i];
       cb::BoundPrefix& p = pre[2 * i + j];
-      for (size_t k = 0; k < b.size() && k < 16; ++k)
-        p.w[k >> 2] |= (uint32_t)(uint8_t)b[k] << (24 - 8 * (k & 3));
-      p.len = (uint32_t)b.size();
+      for (size_t k = 0; k < bnd.size() && k < 16; ++k)
+        p.w[k >> 2] |= (uint32_t)(uint8_t)bnd[k] << (24 - 8 * (k & 3));
+      p.len = (uint32_t)bnd.size();
     }
   }
-  static_assert(sizeof(pre) == cb_zone_pre_bytes, "ZoneView prefix size");
-  std::vector<uint8_t> tab(cb_zone_blob_off + blob.size());
-  memcpy(tab.data(), hdr, cb_zone_hdr_bytes);
-  memcpy(tab.data() + cb_zone_hdr_bytes, pre, cb_zone_pre_bytes);
-  if (!blob.empty()) memcpy(tab.data() + cb_zone_blob_off, blob.data(), blob.size());
-  if (!set->zgated) return CB_OK;
+  set->zgated = wide ? 0 : set->zg[0];
+  std::vector<uint8_t> tab(blob_off + blob.size());
+  memcpy(tab.data(), hdr.data(), hdr_bytes);
+  memcpy(tab.data() + hdr_bytes, pre.data(), pre_bytes);
+  if (wide) memcpy(tab.data() + hdr_bytes + pre_bytes, set->zg.data(), set->zg.size() * 8);
+  if (!blob.empty()) memcpy(tab.data() + blob_off, blob.data(), blob.size());
+  if (!set->zany) return CB_OK;
   // A gated probe or fused read queued on another stream may still read the
   // old table: wait for every stream's last reader (their events), not the
   // whole device, before overwriting it. An outgrown table is retired, not
@@ -665,6 +692,7 @@ int upload_zones(cb_filterset* set, hipStream_t s) {
     if (hipMalloc(&set->zdev, want) != hipSuccess) {
       (void)hipGetLastError();
       set->zgated = 0;
+      set->zany = false;
       return fail(CB_ENOMEM, "hipMalloc failed for zone table");
     }
     set->zcap = want;
@@ -677,12 +705,28 @@ int upload_zones(cb_filterset* set, hipStream_t s) {
 // A slot that receives another table's filter starts with no zone map
 // (accept-all), so a stale zone can never hide a key. Headers of ungated
 // slots are never read, so no upload is needed.
-void reset_zone(cb_filterset* set, uint32_t slot) {
+bool reset_zone(cb_filterset* set, uint32_t slot) {
+  const bool was = (slot >> 6) < set->zg.size() && ((set->zg[slot >> 6] >> (slot & 63)) & 1ull);
   set->zlo[slot].clear();
   set->zhi[slot].clear();
   set->zhas_lo[slot] = set->zhas_hi[slot] = 0;
-  set->zgated &= ~(1ull << slot);
+  if (slot < 64) set->zgated &= ~(1ull << slot);
+  if ((slot >> 6) < set->zg.size()) set->zg[slot >> 6] &= ~(1ull << (slot & 63));
+  bool any = false;
+  for (uint64_t w : set->zg) any |= w != 0;
+  set->zany = any;
+  return was;
 }
+
+// After zone resets: a wide set's kernels read the gated bits from its device
+// table (a 32/64-slot set passes them by value), so a reset slot that was
+// gated needs a new table before the next gated launch.
+int zones_after_reset(cb_filterset* set, bool changed, hipStream_t s) {
+  if (!changed || !set_is_wide(set)) return CB_OK;
+  return upload_zones(set, s);
+}
+
+bool slot_dirty(const cb_filterset* set, uint32_t slot) { return (set->dirty[slot >> 6] >> (slot & 63)) & 1ull; }
 
 // Bytes of key i of a staged batch (device-resident) into out.
 int fetch_key(const StagedKeys& sk, uint64_t i, std::string& out, hipStream_t s) {
@@ -1516,7 +1560,8 @@ int cb_set_load_meta(cb_filterset* set, uint32_t slot, const uint8_t* in, uint64
 int cb_set_create(uint64_t m_bits, uint32_t width, int device, cb_filterset** out) {
   if (!out) return fail(CB_EINVAL, "null out");
   *out = nullptr;
-  if (width != 32 && width != 64) return fail(CB_EINVAL, "set width must be 32 or 64");
+  if (!(width == 32 || width == 64 || (width % 64 == 0 && width <= cb::kWideMax)))
+    return fail(CB_EINVAL, "set width must be 32, 64 or a multiple of 64 up to 4096");
   if (m_bits == 0) return fail(CB_EZEROM, "attempt to calculate the remainder with a divisor of zero");
   int rc = cb_init(device);
   if (rc) return rc;
@@ -1530,13 +1575,21 @@ int cb_set_create(uint64_t m_bits, uint32_t width, int device, cb_filterset** ou
   set->zhi.assign(width, std::string());
   set->zhas_lo.assign(width, 0);
   set->zhas_hi.assign(width, 0);
-  const size_t bytes = (size_t)((m_bits + 31) / 32 * 32) * (width / 8);
+  set->dirty.assign(std::max<uint32_t>(1, width / 64), 0ull);
+  set->zg.assign(std::max<uint32_t>(1, width / 64), 0ull);
+  set->R = width > 64 ? width / 64 : 0;
+  const size_t bytes = width > 64 ? (size_t)m_bits * (width / 8) : (size_t)((m_bits + 31) / 32 * 32) * (width / 8);
   hipError_t e = hipMalloc(&set->words, bytes);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     return fail(CB_ENOMEM, "hipMalloc failed for filter set words");
   }
   HIP_TRY(hipMemsetAsync(set->words, 0, bytes, nullptr));
+  if (width > 64) {  // wide sets keep no union words (the pre-test is a 32/64-slot experiment)
+    HIP_TRY(hipStreamSynchronize(nullptr));
+    *out = set.release();
+    return CB_OK;
+  }
   const size_t any_bytes = (size_t)((m_bits + 31) / 32) * 4;
   e = hipMalloc(&set->any, any_bytes);
   if (e != hipSuccess) {
@@ -1557,6 +1610,7 @@ int cb_set_destroy(cb_filterset* set) {
     if (set->words) (void)hipFree(set->words);
     if (set->any) (void)hipFree(set->any);
     if (set->zdev) (void)hipFree(set->zdev);
+    if (set->wfw) (void)hipFree(set->wfw);
     for (void* z : set->zretired) (void)hipFree(z);
     for (auto& kv : set->zread) (void)hipEventDestroy(kv.second);
   }
@@ -1580,14 +1634,20 @@ int cb_set_assign(cb_filterset* set, uint32_t slot, const cb_filter* f, void* st
   hipStream_t s = (hipStream_t)stream;
   DeviceGuard dg(set->device);
   HIP_TRY(ensure_zeroed(f, s));
-  if (set->dirty >> slot & 1)
+  if (set_is_wide(set)) {
+    uint64_t* w = (uint64_t*)set->words;
+    if (slot_dirty(set, slot))
+      HIP_TRY(cb::launch_wide_put_slot(f->words, set->m, slot, set->R, w, s));
+    else
+      HIP_TRY(cb::launch_wide_or_slot(f->words, set->m, slot, set->R, w, s));
+  } else if (slot_dirty(set, slot)) {
     HIP_TRY(cb::launch_set_put_slot(f->words, set->m, slot, set->width, set->words, set->any, s));
-  else
+  } else {
     HIP_TRY(cb::launch_set_or_slot(f->words, set->m, slot, set->width, set->words, set->any, s));
-  set->dirty |= 1ull << slot;
+  }
+  set->dirty[slot >> 6] |= 1ull << (slot & 63);
   set->used = std::max(set->used, slot + 1);
-  reset_zone(set, slot);
-  return CB_OK;
+  return zones_after_reset(set, reset_zone(set, slot), s);
 }
 
 int cb_set_assign_all(cb_filterset* set, const cb_filter* const* filters, uint32_t nf, void* stream) {
@@ -1597,31 +1657,58 @@ int cb_set_assign_all(cb_filterset* set, const cb_filter* const* filters, uint32
   hipStream_t s = (hipStream_t)stream;
   DeviceGuard dg(set->device);
   FilterPtrs fp{};
+  std::vector<const uint32_t*> ptrs(nf);
   for (uint32_t i = 0; i < nf; ++i) {
     const cb_filter* f = filters[i];
     if (!f) return fail(CB_EINVAL, "null filter");
     if (f->m != set->m) return fail(CB_EINVAL, "filter size differs from the set's m");
     if (f->device != set->device) return fail(CB_EINVAL, "filter and set live on different devices");
     HIP_TRY(ensure_zeroed(f, s));
-    fp.w[i] = f->words;
-    fp.row[i] = i;
+    ptrs[i] = f->words;
+    if (i < 64) {
+      fp.w[i] = f->words;
+      fp.row[i] = i;
+    }
   }
-  HIP_TRY(cb::launch_set_build(fp, nf, set->m, set->width, set->words, set->any, s));
+  if (set_is_wide(set)) {
+    // the filters' word pointers in device memory for the one-launch build
+    const size_t pb = std::max<size_t>(8, (size_t)nf * sizeof(void*));
+    if (pb > set->wfw_cap) {
+      HIP_TRY(hipStreamSynchronize(s));  // an earlier build may still read the old array
+      if (set->wfw) HIP_TRY(hipFree(set->wfw));
+      set->wfw = nullptr;
+      set->wfw_cap = 0;
+      HIP_TRY(hipMalloc(&set->wfw, pb));
+      set->wfw_cap = pb;
+    }
+    if (nf) HIP_TRY(hipMemcpyAsync(set->wfw, ptrs.data(), (size_t)nf * sizeof(void*), hipMemcpyHostToDevice, s));
+    HIP_TRY(cb::launch_wide_build((const uint32_t* const*)set->wfw, nf, set->m, set->R, (uint64_t*)set->words, s));
+    HIP_TRY(hipStreamSynchronize(s));  // the pageable pointer array is copied, and wfw is reused
+  } else {
+    HIP_TRY(cb::launch_set_build(fp, nf, set->m, set->width, set->words, set->any, s));
+  }
   set->used = nf;
-  set->dirty = nf >= 64 ? ~0ull : ((1ull << nf) - 1);
-  for (uint32_t i = 0; i < set->width; ++i) reset_zone(set, i);
-  return CB_OK;
+  for (size_t j = 0; j < set->dirty.size(); ++j) {
+    const uint32_t lo = (uint32_t)j * 64;
+    set->dirty[j] = nf >= lo + 64 ? ~0ull : (nf > lo ? ((1ull << (nf - lo)) - 1) : 0ull);
+  }
+  bool changed = false;
+  for (uint32_t i = 0; i < set->width; ++i) changed |= reset_zone(set, i);
+  return zones_after_reset(set, changed, s);
 }
 
 int cb_set_clear_slot(cb_filterset* set, uint32_t slot, void* stream) {
   if (!set) return fail(CB_EINVAL, "null set");
   if (slot >= set->width) return fail(CB_EINVAL, "slot out of range");
-  reset_zone(set, slot);
-  if (!(set->dirty >> slot & 1)) return CB_OK;
   DeviceGuard dg(set->device);
-  HIP_TRY(cb::launch_set_put_slot(nullptr, set->m, slot, set->width, set->words, set->any,
-                                  (hipStream_t)stream));
-  set->dirty &= ~(1ull << slot);
+  int rc = zones_after_reset(set, reset_zone(set, slot), (hipStream_t)stream);
+  if (rc || !slot_dirty(set, slot)) return rc;
+  if (set_is_wide(set))
+    HIP_TRY(cb::launch_wide_put_slot(nullptr, set->m, slot, set->R, (uint64_t*)set->words, (hipStream_t)stream));
+  else
+    HIP_TRY(cb::launch_set_put_slot(nullptr, set->m, slot, set->width, set->words, set->any,
+                                    (hipStream_t)stream));
+  set->dirty[slot >> 6] &= ~(1ull << (slot & 63));
   return CB_OK;
 }
 

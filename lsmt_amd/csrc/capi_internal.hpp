@@ -22,6 +22,7 @@
 #include "flush.hpp"
 #include "kernels.hpp"
 #include "sstable.hpp"
+#include "wideset.hpp"
 #include "zone.hpp"
 
 // An event recorded after a device write to one or more filters (a batched
@@ -91,16 +92,23 @@ struct cb_filterset {
   void* words = nullptr;  // device, m (rounded up to 32) words of width bits
   uint32_t* any = nullptr;  // device, ceil(m/32) words: bit p = (words[p] != 0)
   uint32_t used = 0;      // 1 + highest assigned slot
-  uint64_t dirty = 0;     // bit s: slot s may hold set bits
+  std::vector<uint64_t> dirty;  // word j bit i: slot 64 j + i may hold set bits
   int mode = 0;
   cb::ModP mp{};
+  // width > 64: a wide set (wideset.hpp), rows of R = width / 64 uint64 words;
+  // wfw is a device array of filter word pointers (cb_set_assign_all's build)
+  uint32_t R = 0;
+  void* wfw = nullptr;
+  size_t wfw_cap = 0;
   // Per-slot ZoneMap (src/zonemap.rs): host copy, and the device table the
   // gated probe reads (cb::ZoneView: 64 x 16-B headers, then the bytes).
   std::vector<std::string> zlo, zhi;
   std::vector<uint8_t> zhas_lo, zhas_hi;
   void* zdev = nullptr;
   size_t zcap = 0;
-  uint64_t zgated = 0;  // slots with both bounds
+  uint64_t zgated = 0;         // slots with both bounds (sets of <= 64 slots: the kernels' mask)
+  std::vector<uint64_t> zg;    // the same for every width: word j bit i = slot 64 j + i
+  bool zany = false;           // any slot gated
   // Readers of the device zone table: one event per stream, recorded after
   // every launch that reads it (gated probes, the fused read path). A zone
   // update waits for these events — the streams' last readers — instead of
@@ -119,6 +127,21 @@ inline cb::ZoneView set_zone_view(const cb_filterset* set) {
   const uint8_t* z = (const uint8_t*)set->zdev;
   return cb::ZoneView{(const uint32_t*)z, (const cb::BoundPrefix*)(z + cb_zone_hdr_bytes), z + cb_zone_blob_off,
                       set->zgated};
+}
+// A wide set's zone table: W 16-B headers, 2 W bound prefixes, the R-word
+// gated bit array, then the bound bytes.
+inline bool set_is_wide(const cb_filterset* set) { return set->width > 64; }
+inline size_t wide_zone_hdr_bytes(uint32_t w) { return (size_t)w * 16; }
+inline size_t wide_zone_pre_bytes(uint32_t w) { return (size_t)w * 2 * sizeof(cb::BoundPrefix); }
+inline size_t wide_zone_blob_off(uint32_t w) {
+  return wide_zone_hdr_bytes(w) + wide_zone_pre_bytes(w) + (size_t)(w / 64) * 8;
+}
+inline cb::WideZone wide_zone_view(const cb_filterset* set) {
+  const uint8_t* z = (const uint8_t*)set->zdev;
+  const uint32_t w = set->width;
+  return cb::WideZone{(const uint32_t*)z, (const cb::BoundPrefix*)(z + wide_zone_hdr_bytes(w)),
+                      z + wide_zone_blob_off(w),
+                      (const uint64_t*)(z + wide_zone_hdr_bytes(w) + wide_zone_pre_bytes(w)), set->zany ? 1u : 0u};
 }
 
 // An SSTable data file resident in HBM with its line index (sstable.hpp).
@@ -194,6 +217,8 @@ struct Workspace {
   // what t_views / t_rows hold (a call with the same tables and rows uploads nothing)
   std::vector<uint8_t> t_views_host;
   std::vector<uint32_t> t_rows_host;
+  DevBuf t_groups;                          // a wide set's table groups (cb::WideGroup)
+  std::vector<uint8_t> t_groups_host;
   DevBuf i_cnt, i_base, i_tmp, i_end, i_err, i_start;                 // line indexing
   DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_tsum, f_flag, f_vsp;  // SsTable::create
   DevBuf x_ctl;                   // cb_hits_compress: slot / finish counters (zeroed once)

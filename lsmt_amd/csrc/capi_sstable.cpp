@@ -132,12 +132,55 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
   const uint64_t* vsrc = (const uint64_t*)ws.t_line.p;
   const uint64_t* dlen = (const uint64_t*)ws.t_dlen.p;
   uint64_t* tsum = (uint64_t*)ws.t_scan.p;
-  if (set) {
+  if (set && set_is_wide(set)) {
+    // the groups of 64 tables (newest first) and how each maps to slots:
+    // ascending or descending runs take their candidate bits from one window
+    // of the rows (wideset.hpp WideGroup), anything else one bit per table
+    const uint32_t ng = (nt + 63) / 64;
+    std::vector<cb::WideGroup> groups(ng);
+    bool need_slots = false;
+    for (uint32_t g = 0; g < ng; ++g) {
+      const uint32_t t0 = 64 * g, gn = std::min<uint32_t>(64, nt - t0);
+      auto slot = [&](uint32_t i) { return rows.empty() ? t0 + i : rows[t0 + i]; };
+      bool asc = true, desc = true;
+      for (uint32_t i = 1; i < gn; ++i) {
+        asc = asc && slot(i) == slot(0) + i;
+        desc = desc && slot(i) + i == slot(0);
+      }
+      cb::WideGroup& gd = groups[g];
+      gd.gn = gn;
+      if (asc) {
+        gd.kind = 0;
+        gd.lo = slot(0);
+      } else if (desc) {
+        gd.kind = 1;
+        gd.lo = slot(gn - 1);
+      } else {
+        gd.kind = 2;
+        gd.lo = 0;
+        need_slots = true;
+      }
+    }
+    const uint8_t* gb = (const uint8_t*)groups.data();
+    const size_t gbytes = ng * sizeof(cb::WideGroup);
+    if (ws.t_groups_host.size() != gbytes || memcmp(ws.t_groups_host.data(), gb, gbytes)) {
+      HIP_TRY(ws.t_groups.reserve(gbytes, s));
+      HIP_TRY(hipMemcpyAsync(ws.t_groups.p, gb, gbytes, hipMemcpyHostToDevice, s));
+      HIP_TRY(hipStreamSynchronize(s));  // the source is pageable
+      ws.t_groups_host.assign(gb, gb + gbytes);
+    }
+    const cb::WideZone wz = wide_zone_view(set);
+    HIP_TRY(cb::launch_wide_get_many(sk.keyk, set->mode, set->R, (const uint64_t*)set->words, set->mp,
+                                     set->zany ? &wz : nullptr, dviews, nt, (const cb::WideGroup*)ws.t_groups.p,
+                                     need_slots ? drows : nullptr, sk.ks, n, dwhich, (uint64_t*)ws.t_line.p,
+                                     (uint64_t*)ws.t_dlen.p, tsum, s));
+    if (set->zany && (rc = note_zone_read(set, s))) return rc;
+  } else if (set) {
     const cb::ZoneView zv = set_zone_view(set);
     HIP_TRY(cb::launch_set_get_many(sk.keyk, set->mode, set->width, set->words, set->mp,
-                                    set->zgated ? &zv : nullptr, dviews, nt, drows, sk.ks, n, dwhich,
+                                    set->zany ? &zv : nullptr, dviews, nt, drows, sk.ks, n, dwhich,
                                     (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, tsum, s));
-    if (set->zgated && (rc = note_zone_read(set, s))) return rc;
+    if (set->zany && (rc = note_zone_read(set, s))) return rc;
   } else {
     HIP_TRY(cb::launch_get_many(sk.keyk, dviews, nt, dhits, drows, hwords, sk.ks, n, dwhich,
                                 (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, tsum, s));

@@ -21,6 +21,7 @@
 #include "profile.hpp"
 #include "setmask.hpp"
 #include "sstable.hpp"
+#include "wideset.hpp"
 #include "zone.hpp"
 
 namespace cb {
@@ -830,6 +831,76 @@ __global__ __launch_bounds__(kNT) void k_set_get_many(const void* __restrict__ s
   if (threadIdx.x == 0) tsum[blockIdx.x] = total;
 }
 
+// Database::get in one launch over a wide set (wideset.hpp): k_set_get_many
+// for more than 64 tables. Per key: rows a and b of the set (h1 % m, h2 % m,
+// src/bloom.rs:26-37); then the tables in groups of 64, newest first
+// (tables.iter().rev(), src/lib.rs:130): the group's candidate bits are a
+// 64-bit window of row a AND the same window of row b, the latter read only
+// when the former is non-zero (src/bloom.rs:50), reordered to table order
+// (groups[g].kind); the zone gate drops gated candidates outside their
+// bounds (src/sstable.rs:138); then resolve_group searches the candidates
+// newest first and the first Ok(Some) ends the walk. Views of tables past
+// the first 64 come from global memory.
+template <int KEYK, int MODE>
+__global__ __launch_bounds__(kNT) void k_wide_get_many(const uint64_t* __restrict__ set, uint32_t R, ModP mp,
+                                                       WideZone z, const TableView* __restrict__ tv, uint32_t nt,
+                                                       const WideGroup* __restrict__ groups,
+                                                       const uint32_t* __restrict__ slots, KeySrc ks, uint64_t n,
+                                                       int32_t* __restrict__ which, uint64_t* __restrict__ vsrc,
+                                                       uint64_t* __restrict__ dlen, uint64_t* __restrict__ tsum) {
+  const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  const bool live = k < n;
+  const ViewRegs vr = load_views(tv, nt);
+  const Query q = make_query<KEYK>(ks, live ? k : 0);
+  uint64_t pa = 0, pb = 0;
+  if (live) key_positions<KEYK, MODE>(ks, k, mp, pa, pb);
+  __shared__ TableView stv[64];
+  __shared__ DirMap sdm[64];
+  store_views(vr, nt, stv);
+  stage_maps(stv, nt, sdm);
+  uint64_t d = 0;
+  if (live) {
+    const uint64_t* ra = set + pa * R;
+    const uint64_t* rb = set + pb * R;
+    const uint32_t kw[4] = {(uint32_t)(q.w0 >> 32), (uint32_t)q.w0, (uint32_t)(q.w1 >> 32), (uint32_t)q.w1};
+    int32_t w = -1;
+    uint64_t src = 0;
+    const uint32_t ng = (nt + 63) / 64;
+    for (uint32_t g = 0; g < ng; ++g) {
+      const WideGroup gd = groups[g];
+      const uint32_t t0 = 64 * g;
+      const uint64_t gmask = gd.gn >= 64 ? ~0ull : ((1ull << gd.gn) - 1);
+      uint64_t cand = 0;
+      if (gd.kind == 2) {  // scattered slots: one bit per table
+        for (uint32_t i = 0; i < gd.gn; ++i) {
+          const uint32_t s = slots[t0 + i];
+          if ((ra[s >> 6] >> (s & 63)) & 1ull) cand |= ((rb[s >> 6] >> (s & 63)) & 1ull) << i;
+        }
+      } else {
+        const uint64_t wa = wide_window(ra, R, gd.lo) & gmask;
+        cand = wa ? (wa & wide_window(rb, R, gd.lo)) : 0ull;
+        if (gd.kind == 1 && cand) cand = __builtin_bitreverse64(cand) >> (64 - gd.gn);  // bit gn-1-i -> i
+      }
+      if (z.any && cand) {
+        uint64_t c = cand;
+        while (c) {
+          const uint32_t i = (uint32_t)__builtin_ctzll(c);
+          c &= c - 1;
+          const uint32_t s = gd.kind == 2 ? slots[t0 + i] : gd.kind == 1 ? gd.lo + gd.gn - 1 - i : gd.lo + i;
+          if (!wide_zone_ok<KEYK>(z, s, kw, q.p, q.len)) cand &= ~(1ull << i);
+        }
+      }
+      if (resolve_group<false>(stv, tv, sdm, t0, cand, q, w, src, d)) break;
+    }
+    which[k] = w;
+    vsrc[k] = src;
+    dlen[k] = d;
+  }
+  uint64_t total;
+  (void)block_scan<kNT>(d, &total);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = total;
+}
+
 // ---- base64 decode of the found values ----
 
 // Decode 4 base64 chars (canonical, validated at index time) to 3 bytes.
@@ -1149,6 +1220,34 @@ hipError_t launch_set_get_many(int keyk, int mode, uint32_t width, const void* s
   ProfScope ps("k_set_get_many", s);
   CB_SET_DISPATCH(keyk, mode, width,
                   (set_get_many<KK, MM, WW>(set, mp, zv, tv, nt, slots, ks, n, which, vsrc, dlen, tsum, s)));
+  return hipGetLastError();
+}
+
+hipError_t launch_wide_get_many(int keyk, int mode, uint32_t R, const uint64_t* set, const ModP& mp,
+                                const WideZone* zones, const TableView* tv, uint32_t nt, const WideGroup* groups,
+                                const uint32_t* slots, const KeySrc& ks, uint64_t n, int32_t* which,
+                                uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum, hipStream_t s) {
+  if (!n) return hipSuccess;
+  if (!nt || nt > 64 * R || R > kWideMax / 64) return hipErrorInvalidValue;
+  const WideZone z = zones ? *zones : WideZone{nullptr, nullptr, nullptr, nullptr, 0};
+  const dim3 g(blocks_for(n, kNT));
+  ProfScope ps("k_wide_get_many", s);
+#define WG(KK, MM)                                                                                                 \
+  hipLaunchKernelGGL((k_wide_get_many<KK, MM>), g, dim3(kNT), 0, s, set, R, mp, z, tv, nt, groups, slots, ks, n, \
+                     which, vsrc, dlen, tsum)
+  switch (keyk * 3 + mode) {
+    case 0: WG(KEY_FIXED16, MOD_POW2_32); break;
+    case 1: WG(KEY_FIXED16, MOD_POW2_64); break;
+    case 2: WG(KEY_FIXED16, MOD_GENERIC); break;
+    case 3: WG(KEY_FIXED, MOD_POW2_32); break;
+    case 4: WG(KEY_FIXED, MOD_POW2_64); break;
+    case 5: WG(KEY_FIXED, MOD_GENERIC); break;
+    case 6: WG(KEY_VAR, MOD_POW2_32); break;
+    case 7: WG(KEY_VAR, MOD_POW2_64); break;
+    case 8: WG(KEY_VAR, MOD_GENERIC); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef WG
   return hipGetLastError();
 }
 

@@ -362,6 +362,17 @@ hipError_t launch_set_get_many(int keyk, int mode, uint32_t width, const void* s
                                const ZoneView* zones, const TableView* tv, uint32_t nt, const uint32_t* slots,
                                const KeySrc& ks, uint64_t n, int32_t* which, uint64_t* vsrc, uint64_t* dlen,
                                uint64_t* tsum, hipStream_t s);
+// Database::get in one launch over a WIDE set (wideset.hpp: more than 64
+// slots, R = W/64 words per row): the groups of 64 tables (newest first)
+// take their candidate bits from windows of rows a and b (groups[g], the
+// slot mapping of tables 64 g ..; slots[t] for kind 2), the zone gate from
+// zones (nullable), then the same walk and outputs as launch_get_many.
+struct WideZone;
+struct WideGroup;
+hipError_t launch_wide_get_many(int keyk, int mode, uint32_t R, const uint64_t* set, const ModP& mp,
+                                const WideZone* zones, const TableView* tv, uint32_t nt, const WideGroup* groups,
+                                const uint32_t* slots, const KeySrc& ks, uint64_t n, int32_t* which,
+                                uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum, hipStream_t s);
 hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uint64_t* hits,
                            const uint32_t* rows, uint64_t hwords, const KeySrc& ks, uint64_t n,
                            int32_t* which, uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum,
