@@ -72,6 +72,8 @@ def parse():
                         "rocprofv3's average matches the bench line's warm kernel time)")
     p.add_argument("--no-c4", action="store_true", help="skip the C4 leg (64 concurrent builds) of the default line")
     p.add_argument("--no-c5", action="store_true", help="skip the C5 rank-slice leg (10M keys x 32 filters)")
+    p.add_argument("--no-wide", action="store_true",
+                   help="skip the wide fan-out leg (300 auto-flush-sized tables of m=1024 in one wide set)")
     p.add_argument("--flush-entries", type=int, default=1 << 20)
     p.add_argument("--build-streams", type=int, default=4, choices=[1, 2, 3, 4],
                    help="pipeline lanes of the C2 build leg (independent flushes in flight)")
@@ -674,6 +676,15 @@ def main():
     if zone is not None:
         fset.assign_all(filters, stream=sh)  # zones reset; the set is unchanged otherwise
 
+    # ---- the reference's own read shape: 300 auto-flushed tables (1024
+    # entries each, m = 1024, src/lib.rs:72,105, src/sstable.rs:44,59) in
+    # one wide FilterSet, Database::get over all of them in one launch
+    wide = None
+    if not args.no_wide and rank == 0 and world == 1:
+        wide = wide_fanout_leg(args, torch, dev, local, sh, LK, timed, kernel_ms, lsmt_amd, workload)
+        log(f"[wide] {wide['value'] / 1e6:.1f} M gets/s over {wide['tables']} tables, "
+            f"oracle {wide.get('oracle_sample_bit_exact')}")
+
     # ---- flush producer: SsTable::create on the device
     # for a 1M-entry memtable (16-B keys, 16-B insert_ts values): data file +
     # line index + Bloom filter (m = 2^26) + zone bounds, inputs in HBM
@@ -923,7 +934,7 @@ def main():
                           "bytes": m * (4 if F <= 32 else 8)},
             "cold": cold, "rotating_batches": rot, "roofline": roof, "cpu_baseline": cpu, "build": build, "e2e": e2e,
             "zone_gate": zone, "read_path": read, "flush": flush, "may_contain": may_contain,
-            "c4": c4, "c5": c5,
+            "c4": c4, "c5": c5, "wide_fanout": wide,
         }
         if x_fit is False:
             line["valid"] = False
@@ -1286,6 +1297,94 @@ def zone_partitioned_leg(args, torch, dev, local, sh, F, m, kpf, n, timed, kerne
         exp = oracle.probe_gated(refs, zones, d, offs)
         out["oracle_sample_bit_exact"] = bool(np.array_equal(g[:, :sample // 64], exp))
         del refs
+    return out
+
+
+def wide_fanout_leg(args, torch, dev, local, sh, LK, timed, kernel_ms, lsmt_amd, workload):
+    """Database::get at the reference's own shape (SURVEY.md §8a a11): 300
+    tables as 300 auto-flushes of 1024 entries leave them (keys from a
+    shared pool, so later flushes rewrite keys; each table's filter m = 1024
+    and its zone map), held in one wide FilterSet (slot = the table's
+    position in Vec<SsTable>), and 2^18 lookups (3/4 present) walked newest
+    first in ONE launch (cb_set_get_many_fixed over a 320-slot set). At
+    m = 1024 with 1024 keys a filter is 86 % ones, so ~75 % of the tables pass
+    the Bloom gate for any key and a lookup searches ~100-225 tables: the
+    reference's own cost model. Oracle: the first 4096 lookups through the
+    CPU restatement of the same gate and walk."""
+    nt, per, n = 300, 1024, 1 << 18
+    rng = np.random.default_rng(300)
+    pool = workload.key_range(4242, 120_000)
+    tables, blooms, zones, ents = [], [], [], []
+    t0 = time.perf_counter()
+    for t in range(nt):
+        idx = np.unique(rng.choice(len(pool), per, replace=False))
+        ks = np.ascontiguousarray(pool[idx])
+        vs = workload.table_value(ks, t)
+        kb = lsmt_amd.KeyBatch(n=len(idx), data=ks.reshape(-1), offsets=np.arange(0, 16 * (len(idx) + 1), 16,
+                                                                                 dtype=np.uint64))
+        vb = lsmt_amd.KeyBatch(n=len(idx), data=np.ascontiguousarray(vs).reshape(-1),
+                               offsets=np.arange(0, 16 * (len(idx) + 1), 16, dtype=np.uint64))
+        tb, bloom, zone = lsmt_amd.sstable_create((kb, vb), m=1024, device=local)
+        tables.append(tb)
+        blooms.append(bloom)
+        zones.append(zone)
+        ents.append((ks, vs))
+    flush_s = time.perf_counter() - t0
+    fset = lsmt_amd.FilterSet(1024, width=320, device=local)
+    for t in range(nt):
+        fset.assign(t, blooms[t])
+        fset.set_zone(t, zones[t])
+    present = pool[rng.integers(0, len(pool), 3 * n // 4)]
+    look_np = np.concatenate([present, workload.key_range(4343, n - len(present))])[rng.permutation(n)]
+    keys = lsmt_amd.DeviceKeys(torch.from_numpy(look_np).to(dev))
+    newest_first = tables[::-1]
+    slots = np.arange(nt, dtype=np.uint32)[::-1].copy()
+    which = torch.empty(n, dtype=torch.int32, device=dev)
+    voff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    vals = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+
+    def step():
+        lsmt_amd.get_many(newest_first, keys, filterset=fset, hit_rows=slots, out=(which, voff, vals), stream=sh,
+                          wait=False)
+
+    for _ in range(2):
+        step()
+    k = max(3, LK // 20)
+    el = timed(step, k, lanes=[torch.cuda.current_stream(dev)])
+    kus = kernel_ms(["k_wide_get_many", "k_tile_scan", "k_b64_decode"], step, k)
+    torch.cuda.synchronize(dev)
+    found = int((which >= 0).sum().item())
+    out = {"metric": f"gets/s: Database::get over {nt} tables of m=1024 (1024 entries each) in one wide set",
+           "value": round(n / (el / k), 1), "unit": "keys/s", "ms_per_step": round(el / k * 1e3, 4), "steps": k,
+           "tables": nt, "set_width": 320, "lookups": n, "found": found,
+           "kernels_us": {kk: round(v["avg_us"], 2) for kk, v in kus.items()},
+           "launches_per_batch": {"search": 1, "tile_scan": 1, "b64_decode": 1},
+           "table_build_s": round(flush_s, 2)}
+    if not args.no_cpu:
+        from oracle import oracle
+        smp = 4096
+        d = np.ascontiguousarray(look_np[:smp].reshape(-1))
+        offs = np.arange(0, 16 * (smp + 1), 16, dtype=np.uint64)
+        ofs, ozs, ots = [], [], []
+        for t in range(nt - 1, -1, -1):
+            o = oracle.OracleFilter(1024)
+            o.insert_fixed(ents[t][0])
+            ofs.append(o)
+            ozs.append(oracle.OracleZone(zones[t].min, zones[t].max))
+            ots.append(oracle.OracleTable(tables[t].data()))
+        t0 = time.perf_counter()
+        gate = oracle.probe_gated(ofs, ozs, d, offs)
+        ow, ovoff, ovals = oracle.get_many(ots, gate, d, offs)
+        tc = time.perf_counter() - t0
+        gvo = voff[: smp + 1].cpu().numpy().astype(np.uint64)
+        out["oracle_sample_bit_exact"] = bool(
+            np.array_equal(which[:smp].cpu().numpy(), ow) and np.array_equal(gvo, ovoff) and
+            bytes(vals[: int(gvo[-1])].cpu().numpy()) == ovals)
+        out["cpu_baseline"] = {"value": round(smp / tc, 1), "unit": "keys/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle gate + newest-first walk over {nt} tables for the first {smp} "
+                                         f"lookups, {tc:.2f}s"}
+    del tables, blooms, fset, keys, which, voff, vals
+    torch.cuda.synchronize(dev)
     return out
 
 

@@ -84,7 +84,7 @@ def test_wide_get_many_300_tables(gpu, lsm300, mapping):
     ow, ovoff, ovals = _oracle_expect(d, newest_first)
     assert np.array_equal(np.asarray(which), ow)
     assert np.array_equal(np.asarray(voff, dtype=np.uint64), ovoff) and vals == ovals
-    assert (np.asarray(which) >= 0).sum() >= 5900  # the present keys resolve (newest copy)
+    assert (np.asarray(which) >= 0).sum() >= 5000  # most present keys live in some table (pool of 120K, 307K draws)
 
 
 def test_wide_probe_rows_match_oracle(gpu, lsm300):

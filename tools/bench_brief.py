@@ -19,3 +19,15 @@ if f:
     for k in ("sorted_input", "unsorted_input"):
         if k in f:
             print(f"flush {k}: {f[k]['ms_per_flush']} ms  {f[k]['kernels_us']}")
+for k in ("c4", "c5"):
+    leg = d.get(k)
+    if leg:
+        rf = leg.get("roofline", {})
+        print(f"{k}: {leg['value'] / (1e9 if k == 'c4' else 1e12):.3f} {'G keys' if k == 'c4' else 'T probes'}/s "
+              f"region {leg['region_us_per_step']} us/step one-lane {leg['one_lane_us_per_step']} us frac {rf.get('frac')} "
+              f"golden {leg.get('golden_all_filters_bit_exact', leg.get('golden_slice_bit_exact'))} "
+              f"oracle {leg.get('oracle_sample_bit_exact', leg.get('oracle_row_bit_exact'))} {leg.get('kernels_us', '')}")
+w = d.get("wide_fanout")
+if w:
+    print(f"wide fan-out: {w['value'] / 1e6:.2f} M gets/s over {w['tables']} tables, oracle {w.get('oracle_sample_bit_exact')} "
+          f"{w['kernels_us']}")

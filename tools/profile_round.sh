@@ -11,7 +11,7 @@ mkdir -p $OUT
 # overlap, so per-dispatch durations are ~2x the per-step share; pmc_summary
 # reports the union of each kernel's busy intervals per launch beside them);
 # the PMC passes run one lane so every dispatch's counters are its own
-BENCH="python bench.py --no-cpu --no-e2e --no-cold --steps 50 --warmup 5 $*"
+BENCH="python bench.py --no-cpu --no-e2e --no-cold --no-c4 --no-c5 --no-wide --steps 50 --warmup 5 $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $BENCH > $OUT/kt_bench.json 2> $OUT/kt.err || exit 1
 BENCH="$BENCH --probe-streams 1"
 # the same with one lane: launches do not overlap, so each dispatch's
