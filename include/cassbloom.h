@@ -268,11 +268,29 @@ int cb_table_copy(const cb_table* t, uint64_t offset, uint64_t len, uint8_t* out
  * STANDARD.encode(value) \n` (*table_out, indexed and searchable), the
  * table's Bloom filter of m_bits (*bloom_out, nullable: BloomFilter::new(1024)
  * + insert per key in the reference) and its zone map as the input indices of
- * a smallest and a largest key (UINT64_MAX when n == 0). */
+ * a smallest and a largest key (UINT64_MAX when n == 0).
+ * The call only ENQUEUES its work on `stream` (the device decides whether the
+ * batch needs a sort) and returns; the table finalises on first use — every
+ * call that reads it (cb_table_*, searches, get_many, cb_table_wait) first
+ * waits for the work and takes its results once. zone_min_idx / zone_max_idx
+ * non-NULL are host results: the call then waits itself. Device offsets cost
+ * one read-back of their totals (cb_sstable_create_bounded takes bounds
+ * instead). Host inputs are staged into memory the table owns; device inputs
+ * must stay valid until the table is finalised (a batch the bin sort cannot
+ * place — keys sharing long prefixes — is sorted again from them then). */
 int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_t* vals,
                       const uint64_t* val_off, uint64_t n, uint64_t m_bits, int device, void* stream,
                       cb_table** table_out, cb_filter** bloom_out, uint64_t* zone_min_idx,
                       uint64_t* zone_max_idx);
+/* The same, enqueue-only for device offsets too: key_bytes / val_bytes bound
+ * key_off[n] / val_off[n] (the file buffer is sized from them). A batch past
+ * its bounds writes no file; its table reports CB_EINVAL when finalised. */
+int cb_sstable_create_bounded(const uint8_t* keys, const uint64_t* key_off, uint64_t key_bytes, const uint8_t* vals,
+                              const uint64_t* val_off, uint64_t val_bytes, uint64_t n, uint64_t m_bits, int device,
+                              void* stream, cb_table** table_out, cb_filter** bloom_out);
+/* Finalise a table from cb_sstable_create*: wait for its work, take its
+ * results; returns its deferred error, if any. Idempotent, thread-safe. */
+int cb_table_wait(const cb_table* t);
 /* The zone map bounds of a table made by cb_sstable_create with n >= 1 (the
  * first / last key of the file: ZoneMap::update over the sorted entries,
  * src/sstable.rs:60-64): which = 0 min, 1 max. *len = the key's length; up to

@@ -147,6 +147,8 @@ def load():
         "cb_table_data": ([P, pp, pu64], i32),
         "cb_table_copy": ([P, u64, u64, u8p], i32),
         "cb_sstable_create": ([u8p, P, u8p, P, u64, u64, i32, P, pp, pp, pu64, pu64], i32),
+        "cb_sstable_create_bounded": ([u8p, P, u64, u8p, P, u64, u64, u64, i32, P, pp, pp], i32),
+        "cb_table_wait": ([P], i32),
         "cb_table_zone": ([P, i32, u8p, u64, pu64], i32),
         "cb_table_rebuild": ([P, u64, P, pp, pu64, pu64], i32),
         "cb_table_well_formed": ([P, ctypes.POINTER(i32)], i32),

@@ -640,6 +640,12 @@ class Table:
     def handle(self) -> ctypes.c_void_p:
         return self._h
 
+    def wait(self) -> None:
+        """Finalise a table from sstable_create(wait=False): wait for its
+        enqueued work, take its results (raises its deferred error, if any)."""
+        _raise(_L().cb_table_wait(self._h))
+        self.__dict__.pop("_inputs", None)
+
     @property
     def nlines(self) -> int:
         n = ctypes.c_uint64()
@@ -738,10 +744,16 @@ class Table:
         return res
 
 
-def sstable_create(entries, m: int = 1024, device: int = 0, stream=None):
+def sstable_create(entries, m: int = 1024, device: int = 0, stream=None, wait: bool = True):
     """SsTable::create (src/sstable.rs:51-87) on the device. entries: a list of
     (key, value) pairs (str/bytes), or a (keys, values) pair of ragged
-    KeyBatches. Returns (Table, BloomFilter of m bits, ZoneMap)."""
+    KeyBatches. Returns (Table, BloomFilter of m bits, ZoneMap).
+
+    The C call only enqueues (cb_sstable_create_bounded: device offsets are
+    sized by their data buffers, no host round trip); the table finalises on
+    first use. wait=False returns (Table, BloomFilter, None) without waiting
+    for the zone bounds (Table.wait() or any read of the table finalises it);
+    the key and value buffers must then stay alive until it has."""
     if isinstance(entries, tuple) and len(entries) == 2 and isinstance(entries[0], KeyBatch):
         kb, vb = entries
     else:
@@ -754,15 +766,26 @@ def sstable_create(entries, m: int = 1024, device: int = 0, stream=None):
     if kb.n != vb.n:
         raise ValueError("keys and values differ in count")
     th, fh = ctypes.c_void_p(), ctypes.c_void_p()
-    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
     kd, k1 = _ptr_of(kb.data)
     ko, k2 = _ptr_of(kb.offsets)
     vd, k3 = _ptr_of(vb.data)
     vo, k4 = _ptr_of(vb.offsets)
-    _raise(_L().cb_sstable_create(kd, ko, vd, vo, kb.n, int(m), int(device), _stream(stream), ctypes.byref(th),
-                                  ctypes.byref(fh), ctypes.byref(lo), ctypes.byref(hi)))
+
+    def nbytes(x):
+        return int(x.numel() * x.element_size()) if hasattr(x, "numel") else int(np.asarray(x).nbytes)
+    if kb.n and hasattr(kb.offsets, "is_cuda") and kb.offsets.is_cuda:
+        # device offsets: their data buffers bound the byte totals
+        _raise(_L().cb_sstable_create_bounded(kd, ko, nbytes(kb.data), vd, vo, nbytes(vb.data), kb.n, int(m),
+                                              int(device), _stream(stream), ctypes.byref(th), ctypes.byref(fh)))
+    else:
+        _raise(_L().cb_sstable_create(kd, ko, vd, vo, kb.n, int(m), int(device), _stream(stream), ctypes.byref(th),
+                                      ctypes.byref(fh), None, None))
     table = Table._adopt(th.value, device)
+    if not wait:
+        table._inputs = (kb, vb)  # the enqueued work (and a fallback sort) reads them until finalised
     bloom = BloomFilter(0, device=device, _handle=fh.value)
+    if not wait:
+        return table, bloom, None
     zone = ZoneMap()
     if kb.n:
         zone = ZoneMap(table._zone(0), table._zone(1))

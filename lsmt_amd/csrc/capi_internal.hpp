@@ -144,6 +144,22 @@ inline cb::WideZone wide_zone_view(const cb_filterset* set) {
                       (const uint64_t*)(z + wide_zone_hdr_bytes(w) + wide_zone_pre_bytes(w)), set->zany ? 1u : 0u};
 }
 
+// What a table made by cb_sstable_create still owes the host until its
+// enqueued work has run (capi_sstable.cpp finalize_table): the event after
+// the result copy, the pinned result block, and what a fallback sort needs
+// (the batch: the caller's device buffers, or the table's own staged copy).
+struct TablePending {
+  hipEvent_t ev = nullptr;
+  cb::CreateResult* hres = nullptr;  // pinned, from the result pool
+  hipStream_t stream = nullptr;      // the creation stream (the fallback runs on it)
+  const uint8_t *dk = nullptr, *dv = nullptr;
+  const uint64_t *dko = nullptr, *dvo = nullptr;
+  uint64_t n = 0, cap_bytes = 0;
+  bool binned = false;                // the bin sort was enqueued (a fallback may be needed)
+  void* staged = nullptr;             // host inputs staged into this pool block
+  size_t staged_cap = 0;
+};
+
 // An SSTable data file resident in HBM with its line index (sstable.hpp).
 struct cb_table {
   int device = 0;
@@ -158,6 +174,16 @@ struct cb_table {
   bool fast = false;  // well-formed: TAB on every line, keys strictly increasing
   bool has_zone = false;   // made by cb_sstable_create with n >= 1
   std::string zmin, zmax;  // its ZoneMap bounds (first / last key of the file)
+  // cb_sstable_create only enqueues: until `ready`, len / fast / zone /
+  // (rarely) the index are still on their way. Every accessor finalises the
+  // table first (waits for its work, reads the results once); ferr keeps a
+  // deferred error (the batch exceeded the byte bounds it was sized from).
+  std::unique_ptr<TablePending> pend;
+  uint64_t zidx[2] = {~0ull, ~0ull};  // input indices of the zone's min / max key
+  std::atomic<bool> ready{true};
+  std::mutex fin_mu;
+  int ferr = 0;
+  std::string ferr_msg;
   cb::TableView view() const {
     return cb::TableView{data, rec, pfx, fence, nlines, cb::fence_levels(nlines), fast ? 1u : 0u,
                          dmap ? dir : nullptr, dmap};
@@ -276,6 +302,10 @@ int stage_var(Workspace& ws, const uint8_t* bytes, const uint64_t* offsets, uint
 // A batched insert with the stream's workspace already locked by the caller.
 int insert_locked(Workspace& ws, cb_filter* f, const uint8_t* keys, const uint64_t* offsets,
                   uint32_t key_len, uint64_t n, hipStream_t s);
+// A table from cb_sstable_create: wait for its enqueued work and take its
+// results (once; thread-safe). Returns the table's deferred error, if any.
+// Every entry point that reads a table calls it first (capi_sstable.cpp).
+int finalize_table(cb_table* t);
 // Host bytes into an output buffer that may be host or device memory.
 int put_bytes(uint8_t* dst, const void* src, size_t n);
 // A write to f's words was enqueued on s (build, import): the host mirror is

@@ -21,6 +21,7 @@ bool g_table_exact = false;  // cb_table_force_exact: index files for the exact-
 int table_search_impl(const cb_table* t, const uint8_t* keys, const uint64_t* offsets,
                       uint32_t key_len, uint64_t n, int64_t* line_out, hipStream_t s) {
   if (!t || !line_out) return fail(CB_EINVAL, "null argument");
+  if (int rc = finalize_table(const_cast<cb_table*>(t))) return rc;
   if (n == 0) return CB_OK;
   if (offsets == nullptr && keys == nullptr && key_len) return fail(CB_EINVAL, "null keys");
   DeviceGuard dg(t->device);
@@ -79,6 +80,7 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
   for (uint32_t i = 0; i < nt; ++i) {
     if (!tables[i]) return fail(CB_EINVAL, "null table");
     if (tables[i]->device != dev) return fail(CB_EINVAL, "tables live on different devices");
+    if (int rc = finalize_table(const_cast<cb_table*>(tables[i]))) return rc;
     views[i] = tables[i]->view();
   }
   if (set && set->device != dev) return fail(CB_EINVAL, "set and tables live on different devices");
@@ -299,6 +301,317 @@ int index_table(cb_table* t, hipStream_t s) {
   return CB_OK;
 }
 
+// ---- SsTable::create: enqueue now, finalise on first use ----
+//
+// cb_sstable_create only enqueues its kernels (sortedness check, Bloom
+// build, the sort the device picks, tile scan, format) and one copy of the
+// CreateResult into a pinned block, followed by an event; nothing waits. The
+// host-side results (file length, zone bounds, the well-formed flag) are read
+// when the table is first used (finalize_table). Two cases need the host
+// there: a batch the bin sort could not place (one bin, or a bin larger than
+// an LDS tile: the merge sort and the format run again, synchronously) and a
+// key holding '\n' or '\t' (the file is re-indexed the way SsTable::get
+// splits it). Until a table is finalised its inputs must stay valid (host
+// inputs are staged into a block the table owns).
+
+// Pinned result blocks and their events, reused across tables.
+struct ResultSlot {
+  cb::CreateResult* h = nullptr;
+  hipEvent_t ev = nullptr;
+};
+std::mutex g_res_mu;
+std::vector<ResultSlot> g_res_free;
+
+int result_slot(ResultSlot* out) {
+  {
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    if (!g_res_free.empty()) {
+      *out = g_res_free.back();
+      g_res_free.pop_back();
+      return CB_OK;
+    }
+  }
+  ResultSlot r;
+  HIP_TRY(hipHostMalloc((void**)&r.h, sizeof(cb::CreateResult), hipHostMallocDefault));
+  // host-waited after a copy into pinned memory: the default (system-scope) release
+  HIP_TRY(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
+  *out = r;
+  return CB_OK;
+}
+
+void result_release(cb::CreateResult* h, hipEvent_t ev) {
+  if (!h) return;
+  std::lock_guard<std::mutex> lk(g_res_mu);
+  g_res_free.push_back(ResultSlot{h, ev});
+}
+
+// Bin-sort group target: ~n / 1536 records (six 1024-record group sorts per
+// CU on 256 CUs, one wave), at least 640, at most 1536 (2048-record sorts).
+uint32_t bin_group_target(uint64_t n) {
+#ifdef CB_EXPERIMENTS
+  static const int env = [] {
+    const char* v = getenv("CB_BIN_T");  // group size target (tuning); 0 disables the bin sort
+    return v && *v ? atoi(v) : -1;
+  }();
+  if (env >= 0) return (uint32_t)env;
+#endif
+  return (uint32_t)std::min<uint64_t>(1536, std::max<uint64_t>(640, (n + 1535) / 1536));
+}
+
+// The format pass and everything after the sort, on s (ws.mu held).
+int enqueue_format(cb_table* t, Workspace& ws, const TablePending& p, cb::CreateResult* dr, hipStream_t s) {
+  const uint64_t n = p.n;
+  uint64_t* tsum = (uint64_t*)ws.f_tsum.p;
+  HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
+  HIP_TRY(cb::launch_format((const cb::SortKey*)ws.f_sk2.p, p.dk, p.dko, p.dv, p.dvo, tsum, n, t->data, t->rec,
+                            t->pfx, t->fence, dr, p.cap_bytes, s, (const ulonglong2*)ws.f_vsp.p, t->dir,
+                            t->dir ? dmap_slot(t) : nullptr));
+  return CB_OK;
+}
+
+int sstable_enqueue(const uint8_t* keys, const uint64_t* key_off, uint64_t kbytes, const uint8_t* vals,
+                    const uint64_t* val_off, uint64_t vbytes, uint64_t n, uint64_t m_bits, int device, hipStream_t s,
+                    cb_table** table_out, cb_filter** bloom_out) {
+  *table_out = nullptr;
+  if (bloom_out) *bloom_out = nullptr;
+  if (n >= 0xFFFFFFFFull) return fail(CB_EINVAL, "too many entries for one table");
+  int rc = cb_init(device);
+  if (rc) return rc;
+  if (bloom_out && n && m_bits == 0)  // BloomFilter::insert's `% 0` (src/bloom.rs:36)
+    return fail(CB_EZEROM, "attempt to calculate the remainder with a divisor of zero");
+  if ((kbytes && !keys) || (vbytes && !vals)) return fail(CB_EINVAL, "null bytes");
+  DeviceGuard dg(device);
+  std::unique_ptr<cb_table, int (*)(cb_table*)> t(new cb_table(), cb_table_destroy);
+  std::unique_ptr<cb_filter, int (*)(cb_filter*)> f(nullptr, cb_filter_destroy);
+  t->device = device;
+  std::unique_ptr<TablePending> pend(new TablePending());
+  TablePending& p = *pend;
+  p.n = n;
+  p.stream = s;
+  // Host inputs go into one block the table owns (the work reads them after
+  // this call returns, and a fallback sort at finalisation reads them again);
+  // device inputs are used in place.
+  const bool ko_h = !is_device_ptr(key_off), vo_h = !is_device_ptr(val_off);
+  const bool kb_h = kbytes && !is_device_ptr(keys), vb_h = vbytes && !is_device_ptr(vals);
+  if (ko_h)
+    for (uint64_t i = 0; i < n; ++i)
+      if (key_off[i + 1] < key_off[i]) return fail(CB_EINVAL, "offsets must be non-decreasing");
+  if (vo_h)
+    for (uint64_t i = 0; i < n; ++i)
+      if (val_off[i + 1] < val_off[i]) return fail(CB_EINVAL, "offsets must be non-decreasing");
+  auto up16 = [](uint64_t x) { return (x + 15) & ~15ull; };
+  const uint64_t offb = up16((n + 1) * 8);
+  const uint64_t stage = (ko_h ? offb : 0) + (vo_h ? offb : 0) + (kb_h ? up16(kbytes) : 0) + (vb_h ? up16(vbytes) : 0);
+  if (stage) {
+    if (pool_alloc(device, stage, &p.staged, &p.staged_cap) != hipSuccess) {
+      p.staged = nullptr;
+      return fail(CB_ENOMEM, "device allocation failed for a staged flush batch");
+    }
+    uint8_t* at = (uint8_t*)p.staged;
+    auto put = [&](const void* src, uint64_t bytes) -> uint8_t* {
+      uint8_t* d = at;
+      at += up16(bytes);
+      return d;
+    };
+    if (ko_h) {
+      uint8_t* d = put(key_off, (n + 1) * 8);
+      HIP_TRY(hipMemcpyAsync(d, key_off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+      key_off = (const uint64_t*)d;
+    }
+    if (vo_h) {
+      uint8_t* d = put(val_off, (n + 1) * 8);
+      HIP_TRY(hipMemcpyAsync(d, val_off, (n + 1) * 8, hipMemcpyHostToDevice, s));
+      val_off = (const uint64_t*)d;
+    }
+    if (kb_h) {
+      uint8_t* d = put(keys, kbytes);
+      HIP_TRY(hipMemcpyAsync(d, keys, kbytes, hipMemcpyHostToDevice, s));
+      keys = d;
+    }
+    if (vb_h) {
+      uint8_t* d = put(vals, vbytes);
+      HIP_TRY(hipMemcpyAsync(d, vals, vbytes, hipMemcpyHostToDevice, s));
+      vals = d;
+    }
+  }
+  p.dk = keys;
+  p.dko = key_off;
+  p.dv = vals;
+  p.dvo = val_off;
+  // the file's buffer: sum(k + 2 + 4 ceil(v / 3)) <= K + 2n + (4V + 8n) / 3,
+  // plus slack; its length comes back with the results
+  p.cap_bytes = kbytes + 2 * n + (4 * vbytes + 8 * n) / 3 + 1 + 16;
+  if (pool_alloc(device, p.cap_bytes, (void**)&t->data, &t->data_cap) != hipSuccess) {
+    t->data = nullptr;
+    return fail(CB_ENOMEM, "device allocation failed for an SSTable buffer");
+  }
+  if (!n) {  // an empty file: nothing to sort, index or bound
+    HIP_TRY(hipMemsetAsync(t->data, 0, 16, s));
+    if (bloom_out) {
+      cb_filter* fp = nullptr;
+      if ((rc = cb_filter_create(m_bits, device, &fp))) return rc;
+      *bloom_out = fp;
+    }
+    t->pend = std::move(pend);  // (no result block: the staged block is released with the table)
+    HIP_TRY(hipStreamSynchronize(s));
+    *table_out = t.release();
+    return CB_OK;
+  }
+  t->nlines = n;
+  if (pool_alloc(device, index_bytes(n), (void**)&t->rec, &t->rec_cap) != hipSuccess) {
+    t->rec = nullptr;
+    return fail(CB_ENOMEM, "device allocation failed for an SSTable index");
+  }
+  carve_index(t.get());
+  ResultSlot slot;
+  if ((rc = result_slot(&slot))) return rc;
+  p.hres = slot.h;
+  p.ev = slot.ev;
+  Workspace& ws = workspace(device, s);
+  std::unique_lock<std::mutex> lk(ws.mu);
+  HIP_TRY(ws.f_flag.reserve(sizeof(cb::CreateResult), s));
+  HIP_TRY(ws.f_tsum.reserve(cb::format_tiles(n) * 8, s));
+  HIP_TRY(ws.f_sk2.reserve(n * sizeof(cb::SortKey), s));
+  HIP_TRY(ws.f_vsp.reserve(n * sizeof(ulonglong2), s));
+  cb::CreateResult* dr = (cb::CreateResult*)ws.f_flag.p;
+  uint64_t* tsum = (uint64_t*)ws.f_tsum.p;
+  HIP_TRY(hipMemsetAsync(dr, 0, cb::kCreateHead, s));
+  HIP_TRY(cb::launch_sorted_check(p.dk, p.dko, p.dvo, n, dr, tsum, kbytes, vbytes, s));
+  // the Bloom build needs neither the order nor the totals (OR is order-free)
+  if (bloom_out) {
+    cb_filter* fp = nullptr;
+    if ((rc = cb_filter_create(m_bits, device, &fp))) return rc;
+    f.reset(fp);
+    if ((rc = insert_locked(ws, fp, p.dk, p.dko, 0, n, s))) return rc;
+  }
+  // the stable sort by key, enqueued before anyone knows whether the batch
+  // needs one: every sort launch returns at once for a sorted batch (memtable
+  // flushes arrive sorted). Bin sort for 4096 < n <= 2^24 (its fallback, at
+  // finalisation, is the merge sort); the merge sort otherwise.
+  const uint32_t T = bin_group_target(n);
+  p.binned = T && T <= cb::bin_sort_max_group() && n > 4096 && n <= (1ull << 24);
+  const uint64_t tmp = p.binned ? cb::bin_sort_tmp_bytes(n, T) : cb::entry_sort_tmp_bytes(n);
+  HIP_TRY(ws.f_sort.reserve(tmp, s));
+  if (p.binned)
+    HIP_TRY(cb::launch_bin_sort(p.dk, p.dko, n, T, (cb::SortKey*)ws.f_sk2.p, ws.f_sort.p, s, p.dvo,
+                                (ulonglong2*)ws.f_vsp.p, tsum, dr));
+  else
+    HIP_TRY(cb::launch_entry_sort(nullptr, (cb::SortKey*)ws.f_sk2.p, (cb::SortKey*)ws.f_sort.p, n, p.dk, p.dko, s,
+                                  p.dvo, (ulonglong2*)ws.f_vsp.p, tsum, &dr->flags[0]));
+  if ((rc = enqueue_format(t.get(), ws, p, dr, s))) return rc;
+  HIP_TRY(hipMemcpyAsync(p.hres, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(p.ev, s));
+  lk.unlock();
+  t->dmap = t->dir ? dmap_slot(t.get()) : nullptr;
+  t->pend = std::move(pend);
+  t->ready.store(false, std::memory_order_release);
+  if (bloom_out) *bloom_out = f.release();
+  *table_out = t.release();
+  return CB_OK;
+}
+
+// Release what a finalised (or destroyed) table no longer needs.
+void drop_pending(cb_table* t) {
+  if (!t->pend) return;
+  TablePending& p = *t->pend;
+  if (p.staged) pool_release(t->device, p.staged, p.staged_cap);
+  result_release(p.hres, p.ev);
+  t->pend.reset();
+}
+
+int finalize_locked(cb_table* t) {
+  TablePending& p = *t->pend;
+  DeviceGuard dg(t->device);
+  if (p.ev) HIP_TRY(hipEventSynchronize(p.ev));
+  if (!p.n) return CB_OK;
+  cb::CreateResult* hr = p.hres;
+  if (hr->flags[4]) {
+    t->ferr = CB_EINVAL;
+    t->ferr_msg = "SsTable::create: the batch's key or value bytes exceed the bounds the table was sized from";
+    return CB_OK;
+  }
+  if (hr->flags[3]) {
+    // the bin sort could not place every record (one bin, or a bin larger
+    // than an LDS tile: keys sharing a long prefix): the merge sort, then the
+    // file again, on the null stream of this device (the create's work is done)
+    hipStream_t s = nullptr;
+    Workspace& ws = workspace(t->device, s);
+    std::lock_guard<std::mutex> lk(ws.mu);
+    HIP_TRY(ws.f_flag.reserve(sizeof(cb::CreateResult), s));
+    HIP_TRY(ws.f_tsum.reserve(cb::format_tiles(p.n) * 8, s));
+    HIP_TRY(ws.f_sk2.reserve(p.n * sizeof(cb::SortKey), s));
+    HIP_TRY(ws.f_vsp.reserve(p.n * sizeof(ulonglong2), s));
+    HIP_TRY(ws.f_sort.reserve(cb::entry_sort_tmp_bytes(p.n), s));
+    cb::CreateResult* dr = (cb::CreateResult*)ws.f_flag.p;
+    uint64_t* tsum = (uint64_t*)ws.f_tsum.p;
+    HIP_TRY(hipMemsetAsync(dr, 0, cb::kCreateHead, s));
+    HIP_TRY(cb::launch_sorted_check(p.dk, p.dko, p.dvo, p.n, dr, tsum, ~0ull, ~0ull, s));
+    HIP_TRY(cb::launch_entry_sort(nullptr, (cb::SortKey*)ws.f_sk2.p, (cb::SortKey*)ws.f_sort.p, p.n, p.dk, p.dko, s,
+                                  p.dvo, (ulonglong2*)ws.f_vsp.p, tsum, nullptr));
+    int rc = enqueue_format(t, ws, p, dr, s);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(hr, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  t->len = hr->len;
+  // zone map: ZoneMap::update over the sorted keys = first / last line
+  t->zidx[0] = hr->idx_min;
+  t->zidx[1] = hr->idx_max;
+  for (int w = 0; w < 2; ++w) {
+    const uint64_t kl = hr->zlen[w];
+    std::string& z = w ? t->zmax : t->zmin;
+    z.assign((const char*)hr->zkey[w], (size_t)std::min<uint64_t>(kl, cb::kZoneInline));
+    if (kl > cb::kZoneInline) {  // a long key: the rest in one more copy
+      const uint64_t i = w ? hr->idx_max : hr->idx_min;
+      uint64_t o = 0;
+      HIP_TRY(hipMemcpy(&o, p.dko + i, 8, hipMemcpyDeviceToHost));
+      z.resize(kl);
+      HIP_TRY(hipMemcpy(&z[cb::kZoneInline], p.dk + o + cb::kZoneInline, kl - cb::kZoneInline,
+                        hipMemcpyDeviceToHost));
+    }
+  }
+  t->has_zone = true;
+  if (hr->flags[1]) {
+    // a key holds '\n' or '\t': the file's lines are not the entries, so
+    // index it the way SsTable::get splits it (src/sstable.rs:142-146)
+    pool_release(t->device, t->rec, t->rec_cap);
+    t->rec = nullptr;
+    t->pfx = t->fence = nullptr;
+    t->dir = nullptr;
+    t->dmap = nullptr;
+    t->nlines = 0;
+    int rc = index_table(t, nullptr);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(nullptr));
+  } else {
+    t->fast = !hr->flags[2] && !g_table_exact;
+  }
+  return CB_OK;
+}
+
+}  // namespace
+
+namespace cbx {
+
+int finalize_table(cb_table* t) {
+  if (!t->ready.load(std::memory_order_acquire)) {
+    std::lock_guard<std::mutex> lk(t->fin_mu);
+    if (!t->ready.load(std::memory_order_acquire)) {
+      const int rc = finalize_locked(t);
+      drop_pending(t);
+      if (rc && !t->ferr) {
+        t->ferr = rc;
+        t->ferr_msg = cbx::g_err;
+      }
+      t->ready.store(true, std::memory_order_release);
+    }
+  }
+  return t->ferr ? fail(t->ferr, t->ferr_msg.c_str()) : CB_OK;
+}
+
+}  // namespace cbx
+
+namespace {
 }  // namespace
 
 extern "C" {
@@ -309,6 +622,11 @@ int cb_table_destroy(cb_table* t) {
   if (!t) return CB_OK;
   {
     DeviceGuard dg(t->device);
+    if (t->pend) {  // enqueued work may still be running: let it finish first
+      std::lock_guard<std::mutex> lk(t->fin_mu);
+      if (t->pend->ev && !t->ready.load()) (void)hipEventSynchronize(t->pend->ev);
+      drop_pending(t);
+    }
     pool_release(t->device, t->data, t->data_cap);
     pool_release(t->device, t->rec, t->rec_cap);  // rec heads the one index allocation
   }
@@ -340,6 +658,7 @@ int cb_table_create(const uint8_t* data, uint64_t len, int device, void* stream,
 
 int cb_table_data(const cb_table* t, const uint8_t** data, uint64_t* len) {
   if (!t) return fail(CB_EINVAL, "null table");
+  if (int rc = finalize_table(const_cast<cb_table*>(t))) return rc;
   if (data) *data = t->data;
   if (len) *len = t->len;
   return CB_OK;
@@ -347,6 +666,7 @@ int cb_table_data(const cb_table* t, const uint8_t** data, uint64_t* len) {
 
 int cb_table_copy(const cb_table* t, uint64_t offset, uint64_t len, uint8_t* out) {
   if (!t || (!out && len)) return fail(CB_EINVAL, "null argument");
+  if (int rc = finalize_table(const_cast<cb_table*>(t))) return rc;
   if (offset > t->len || len > t->len - offset) return fail(CB_EINVAL, "range outside the file");
   if (!len) return CB_OK;
   DeviceGuard dg(t->device);
@@ -359,267 +679,65 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
                       cb_table** table_out, cb_filter** bloom_out, uint64_t* zone_min_idx,
                       uint64_t* zone_max_idx) {
   if (!table_out || !key_off || !val_off) return fail(CB_EINVAL, "null argument");
-  if (n >= 0xFFFFFFFFull) return fail(CB_EINVAL, "too many entries for one table");
-  *table_out = nullptr;
-  if (bloom_out) *bloom_out = nullptr;
   if (zone_min_idx) *zone_min_idx = ~0ull;
   if (zone_max_idx) *zone_max_idx = ~0ull;
-  static const bool trace = getenv("CB_FLUSH_TRACE") != nullptr;  // diagnostic: host timeline to stderr
-  struct Marks {
-    bool on;
-    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-    std::string line;
-    void operator()(const char* what) {
-      if (!on) return;
-      const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-      line += std::string(what) + "=" + std::to_string((int)us) + " ";
-    }
-    ~Marks() {
-      if (on) fprintf(stderr, "[flush] %s\n", line.c_str());
-    }
-  } mark{trace};
-  int rc = cb_init(device);
-  if (rc) return rc;
-  if (bloom_out && n && m_bits == 0)  // BloomFilter::insert's `% 0` (src/bloom.rs:36)
-    return fail(CB_EZEROM, "attempt to calculate the remainder with a divisor of zero");
-  DeviceGuard dg(device);
-  hipStream_t s = (hipStream_t)stream;
-  std::unique_ptr<cb_table, int (*)(cb_table*)> t(new cb_table(), cb_table_destroy);
-  std::unique_ptr<cb_filter, int (*)(cb_filter*)> f(nullptr, cb_filter_destroy);
-  t->device = device;
-  const uint8_t *dk = nullptr, *dv = nullptr;
-  const uint64_t *dko = nullptr, *dvo = nullptr;
-  const cb::SortKey* order = nullptr;
-  ulonglong2* vsp = nullptr;  // sorted value spans (hand-written sort)
-  uint64_t ktot = 0, vtot = 0;
-  Workspace& ws = workspace(device, s);
-  std::unique_lock<std::mutex> lk(ws.mu);
-  if (!ws.hres) {
-    HIP_TRY(hipHostMalloc((void**)&ws.hres, sizeof(cb::CreateResult), hipHostMallocDefault));
-    HIP_TRY(hipEventCreateWithFlags(&ws.ev, hipEventDisableTiming));
-  }
-  cb::CreateResult* hr = ws.hres;
-  // Offsets: host ones are validated and copied (their totals are known
-  // here); device ones are used in place, their totals read back together
-  // with the sortedness flag in ONE round trip below.
-  auto stage_off = [&](DevBuf& doff, const uint64_t* off, const uint64_t** op, uint64_t* tot,
-                       bool* on_dev) -> int {
-    *on_dev = is_device_ptr(off);
-    if (*on_dev) {
-      *op = off;
-      return CB_OK;
-    }
-    for (uint64_t i = 0; i < n; ++i)
-      if (off[i + 1] < off[i]) return fail(CB_EINVAL, "offsets must be non-decreasing");
-    *tot = off[n];
-    HIP_TRY(doff.reserve((n + 1) * 8, s));
-    HIP_TRY(hipMemcpyAsync(doff.p, off, (n + 1) * 8, hipMemcpyHostToDevice, s));
-    *op = (const uint64_t*)doff.p;
-    return CB_OK;
-  };
-  // Bytes: device bytes in place; host bytes copied (device offsets over
-  // host bytes need the total first: one extra round trip, a rare mix).
-  auto stage_bytes = [&](DevBuf& dbytes, const uint8_t* bytes, const uint64_t* off, bool off_dev,
-                         uint64_t* tot, const uint8_t** bp) -> int {
-    if (!bytes || is_device_ptr(bytes)) {
-      *bp = bytes;
-      return CB_OK;
-    }
-    if (off_dev) {
-      HIP_TRY(hipMemcpyAsync(tot, off + n, 8, hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipStreamSynchronize(s));
-    }
-    if (*tot) {
-      HIP_TRY(dbytes.reserve(*tot, s));
-      HIP_TRY(hipMemcpyAsync(dbytes.p, bytes, *tot, hipMemcpyHostToDevice, s));
-    }
-    *bp = (const uint8_t*)dbytes.p;
-    return CB_OK;
-  };
-  bool kdev = false, vdev = false;
-  if ((rc = stage_off(ws.offsets, key_off, &dko, &ktot, &kdev))) return rc;
-  if ((rc = stage_off(ws.f_vo, val_off, &dvo, &vtot, &vdev))) return rc;
-  if ((rc = stage_bytes(ws.keys, keys, key_off, kdev, &ktot, &dk))) return rc;
-  if ((rc = stage_bytes(ws.f_vb, vals, val_off, vdev, &vtot, &dv))) return rc;
-  if (!keys && n) {  // only a batch of empty keys may come without bytes
-    if (kdev) {
-      HIP_TRY(hipMemcpyAsync(&ktot, dko + n, 8, hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipStreamSynchronize(s));
-    }
-    if (ktot) return fail(CB_EINVAL, "null bytes");
-  }
-  HIP_TRY(ws.f_flag.reserve(sizeof(cb::CreateResult), s));
-  cb::CreateResult* dr = (cb::CreateResult*)ws.f_flag.p;
-  // Round trip 1: sortedness and the byte totals. Its wait is covered by the
-  // Bloom build, which needs neither (OR is order-free).
-  hr->flags[0] = 1;
-  hr->flags[1] = 0;
-  hr->flags[2] = 1;
-  hr->flags[3] = 0;
-  HIP_TRY(hipMemcpyAsync(dr->flags, hr->flags, 16, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemsetAsync(dr->dmask, 0, sizeof(dr->dmask), s));
-  HIP_TRY(ws.f_tsum.reserve(cb::format_tiles(n) * 8, s));
-  uint64_t* tsum = (uint64_t*)ws.f_tsum.p;
-  mark("staged");
-  HIP_TRY(cb::launch_sorted_check(dk, dko, dvo, n, dr, tsum, s));
-  HIP_TRY(hipMemcpyAsync(hr, dr, offsetof(cb::CreateResult, len), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipEventRecord(ws.ev, s));
-  // The Bloom build fills the GPU while the host waits for round trip 1: it
-  // needs neither the order nor the totals (OR is order-free). Measured
-  // slower elsewhere: on a side stream beside the sort and the format (the
-  // kernels contend; unsorted 0.236 -> 0.262 ms), and after the format's
-  // enqueue (the same).
-  auto build_bloom = [&]() -> int {  // (keys are non-null or all empty here)
-    if (!bloom_out) return CB_OK;
-    cb_filter* fp = nullptr;
-    int r = cb_filter_create(m_bits, device, &fp);
-    if (r) return r;
-    f.reset(fp);
-    return n ? insert_locked(ws, fp, dk, dko, 0, n, s) : CB_OK;
-  };
-  if ((rc = build_bloom())) return rc;
-  mark("bloom_enq");
-  HIP_TRY(hipEventSynchronize(ws.ev));
-  mark("rt1");
-  if (kdev) ktot = hr->ktot;
-  if (vdev) vtot = hr->vtot;
-  const bool sorted = hr->flags[0] != 0;
-  if ((ktot && !keys) || (vtot && !vals)) return fail(CB_EINVAL, "null bytes");
-  // the file's buffer is sized by the bound sum(k + 2 + 4 ceil(v / 3)) <=
-  // K + 2n + (4V + 8n) / 3, plus slack; its length comes back at the end
-  const uint64_t cap_bytes = ktot + 2 * n + (4 * vtot + 8 * n) / 3 + 1 + 16;
-  if (pool_alloc(device, cap_bytes, (void**)&t->data, &t->data_cap) != hipSuccess) {
-    t->data = nullptr;
-    return fail(CB_ENOMEM, "device allocation failed for an SSTable buffer");
-  }
-  if (!n) {
-    HIP_TRY(hipMemsetAsync(t->data, 0, 16, s));
+  // byte totals: host offsets carry them; device offsets are read back (one
+  // round trip: cb_sstable_create_bounded takes the bounds instead)
+  uint64_t kt = 0, vt = 0;
+  const bool kdev = is_device_ptr(key_off), vdev = is_device_ptr(val_off);
+  if (kdev || vdev) {
+    int rc = cb_init(device);
+    if (rc) return rc;
+    DeviceGuard dg(device);
+    hipStream_t s = (hipStream_t)stream;
+    uint64_t tot[2] = {0, 0};
+    if (kdev) HIP_TRY(hipMemcpyAsync(&tot[0], key_off + n, 8, hipMemcpyDeviceToHost, s));
+    if (vdev) HIP_TRY(hipMemcpyAsync(&tot[1], val_off + n, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (bloom_out) *bloom_out = f.release();
-    *table_out = t.release();
-    return CB_OK;
+    kt = tot[0];
+    vt = tot[1];
   }
-  // stable sort by key (memtable flushes arrive sorted and skip this). Both
-  // sorts leave the value spans and the line tiles in sorted order for
-  // k_format. merge: LDS block sorts, then merge-path rounds; bin: one
-  // binning pass over the directory map's buckets and one LDS sort per
-  // group (sort.hip), falling back to the merge sort when a group outgrows
-  // an LDS tile (flags[3], read at round trip 2).
-  bool binned = false;
-  auto merge_sort = [&]() -> int {
-    HIP_TRY(ws.f_sort.reserve(cb::entry_sort_tmp_bytes(n), s));
-    HIP_TRY(cb::launch_entry_sort(nullptr, (cb::SortKey*)ws.f_sk2.p, (cb::SortKey*)ws.f_sort.p, n, dk, dko, s,
-                                  dvo, vsp, tsum));
-    return CB_OK;
-  };
-  if (!sorted) {
-    HIP_TRY(ws.f_sk2.reserve(n * sizeof(cb::SortKey), s));
-    HIP_TRY(ws.f_vsp.reserve(n * sizeof(ulonglong2), s));
-    vsp = (ulonglong2*)ws.f_vsp.p;
-    order = (cb::SortKey*)ws.f_sk2.p;
-#ifdef CB_EXPERIMENTS
-    static const int bin_T_env = [] {
-      const char* v = getenv("CB_BIN_T");  // group size target (tuning); 0 disables the bin sort
-      return v && *v ? atoi(v) : -1;
-    }();
-#else
-    const int bin_T_env = -1;
-#endif
-    // groups of ~n / 1536 records (six 1024-record group sorts per CU on 256
-    // CUs, one wave), at least 640, at most 1536 (2048-record group sorts)
-    const uint32_t bin_T = bin_T_env >= 0 ? (uint32_t)bin_T_env
-                                          : (uint32_t)std::min<uint64_t>(1536, std::max<uint64_t>(640, (n + 1535) / 1536));
-    if (bin_T && bin_T <= cb::bin_sort_max_group() && n > 4096 && n <= (1ull << 24)) {
-      const cb::DirMap bm = cb::make_dirmap(hr->dmask, n, cb::bin_sort_max_bins());
-      if (bm.nbuckets >= 2) {
-        HIP_TRY(ws.f_sort.reserve(cb::bin_sort_tmp_bytes(n, bm.nbuckets, bin_T), s));
-        HIP_TRY(cb::launch_bin_sort(dk, dko, n, bm, bin_T, (cb::SortKey*)ws.f_sk2.p, ws.f_sort.p, s, dvo, vsp,
-                                    tsum, &dr->flags[3]));
-        binned = true;
-      }
+  if (!kdev) kt = key_off[n];
+  if (!vdev) vt = val_off[n];
+  int rc = sstable_enqueue(keys, key_off, kt, vals, val_off, vt, n, m_bits, device, (hipStream_t)stream, table_out,
+                           bloom_out);
+  if (rc || !(zone_min_idx || zone_max_idx) || !n) return rc;
+  // the zone map's input indices are host values: wait for them
+  cb_table* t = *table_out;
+  if ((rc = finalize_table(t))) {
+    cb_table_destroy(t);
+    *table_out = nullptr;
+    if (bloom_out && *bloom_out) {
+      cb_filter_destroy(*bloom_out);
+      *bloom_out = nullptr;
     }
-    if (!binned && (rc = merge_sort())) return rc;
+    return rc;
   }
-  mark("sort_enq");
-  HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
-  // the line index straight from the entries (entry p is line p), no re-read of the file
-  t->nlines = n;
-  if (pool_alloc(device, index_bytes(n), (void**)&t->rec, &t->rec_cap) != hipSuccess) {
-    t->rec = nullptr;
-    return fail(CB_ENOMEM, "device allocation failed for an SSTable index");
-  }
-  carve_index(t.get());
-  // the directory's map from round trip 1's prefix byte masks (order-free)
-  cb::DirMap dm{};
-  if (t->dir) {
-    dm = cb::make_dirmap(hr->dmask, n);
-    t->dmap = dmap_slot(t.get());
-  }
-  auto format = [&]() -> int {
-    HIP_TRY(cb::launch_format(order, dk, dko, dv, dvo, tsum, n, t->data, t->rec, t->pfx, t->fence, dr,
-                              cap_bytes, s, vsp, t->dir, t->dir ? &dm : nullptr, t->dmap));
-    // Round trip 2: flags, file length, zone bounds
-    HIP_TRY(hipMemcpyAsync(hr, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
-    mark("fmt_enq");
-    HIP_TRY(hipStreamSynchronize(s));
-    mark("rt2");
-    return CB_OK;
-  };
-  if ((rc = format())) return rc;
-  if (binned && hr->flags[3]) {
-    // the bin sort overflowed (a bin of more than an LDS tile: keys sharing a
-    // long prefix): the merge sort, then the file again from clean flags
-    hr->flags[0] = 0;
-    hr->flags[1] = 0;
-    hr->flags[2] = 1;
-    hr->flags[3] = 0;
-    HIP_TRY(hipMemcpyAsync(dr->flags, hr->flags, 16, hipMemcpyHostToDevice, s));
-    if ((rc = merge_sort())) return rc;
-    HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
-    if ((rc = format())) return rc;
-  }
-  t->len = hr->len;
-  // zone map: ZoneMap::update over the sorted keys = first / last line
-  if (zone_min_idx) *zone_min_idx = hr->idx_min;
-  if (zone_max_idx) *zone_max_idx = hr->idx_max;
-  for (int w = 0; w < 2; ++w) {
-    const uint64_t kl = hr->zlen[w];
-    std::string& z = w ? t->zmax : t->zmin;
-    z.assign((const char*)hr->zkey[w], (size_t)std::min<uint64_t>(kl, cb::kZoneInline));
-    if (kl > cb::kZoneInline) {  // a long key: the rest in one more copy
-      const uint64_t i = w ? hr->idx_max : hr->idx_min;
-      uint64_t o = 0;
-      HIP_TRY(hipMemcpy(&o, dko + i, 8, hipMemcpyDeviceToHost));
-      z.resize(kl);
-      HIP_TRY(hipMemcpy(&z[cb::kZoneInline], dk + o + cb::kZoneInline, kl - cb::kZoneInline,
-                        hipMemcpyDeviceToHost));
-    }
-  }
-  t->has_zone = true;
-  if (hr->flags[1]) {
-    // a key holds '\n' or '\t': the file's lines are not the entries, so
-    // index it the way SsTable::get splits it (src/sstable.rs:142-146)
-    pool_release(device, t->rec, t->rec_cap);
-    t->rec = nullptr;
-    t->pfx = t->fence = nullptr;
-    t->dir = nullptr;
-    t->dmap = nullptr;
-    t->nlines = 0;
-    lk.unlock();  // index_table takes the workspace itself
-    if ((rc = index_table(t.get(), s))) return rc;
-  } else {
-    t->fast = hr->flags[2] != 0 && !g_table_exact;
-  }
-  if (bloom_out) *bloom_out = f.release();
-  *table_out = t.release();
-  mark("end");
+  if (zone_min_idx) *zone_min_idx = t->zidx[0];
+  if (zone_max_idx) *zone_max_idx = t->zidx[1];
   return CB_OK;
+}
+
+int cb_sstable_create_bounded(const uint8_t* keys, const uint64_t* key_off, uint64_t key_bytes, const uint8_t* vals,
+                              const uint64_t* val_off, uint64_t val_bytes, uint64_t n, uint64_t m_bits, int device,
+                              void* stream, cb_table** table_out, cb_filter** bloom_out) {
+  if (!table_out || !key_off || !val_off) return fail(CB_EINVAL, "null argument");
+  if (!is_device_ptr(key_off) && key_off[n] > key_bytes) return fail(CB_EINVAL, "key bytes exceed key_bytes");
+  if (!is_device_ptr(val_off) && val_off[n] > val_bytes) return fail(CB_EINVAL, "value bytes exceed val_bytes");
+  return sstable_enqueue(keys, key_off, key_bytes, vals, val_off, val_bytes, n, m_bits, device, (hipStream_t)stream,
+                         table_out, bloom_out);
+}
+
+int cb_table_wait(const cb_table* t) {
+  if (!t) return fail(CB_EINVAL, "null table");
+  return finalize_table(const_cast<cb_table*>(t));
 }
 
 int cb_table_rebuild(const cb_table* t, uint64_t m_bits, void* stream, cb_filter** bloom_out,
                      uint64_t* zone_min_line, uint64_t* zone_max_line) {
   if (!t || !bloom_out) return fail(CB_EINVAL, "null argument");
   *bloom_out = nullptr;
+  if (int rc = finalize_table(const_cast<cb_table*>(t))) return rc;
   if (zone_min_line) *zone_min_line = ~0ull;
   if (zone_max_line) *zone_max_line = ~0ull;
   hipStream_t s = (hipStream_t)stream;
@@ -690,6 +808,7 @@ int cb_table_rebuild(const cb_table* t, uint64_t m_bits, void* stream, cb_filter
 
 int cb_table_zone(const cb_table* t, int which, uint8_t* out, uint64_t cap, uint64_t* len) {
   if (!t || !len || (which != 0 && which != 1)) return fail(CB_EINVAL, "bad argument");
+  if (int rc = finalize_table(const_cast<cb_table*>(t))) return rc;
   if (!t->has_zone) return fail(CB_EINVAL, "table has no zone bounds (not made by cb_sstable_create, or empty)");
   const std::string& z = which ? t->zmax : t->zmin;
   *len = z.size();
@@ -699,6 +818,7 @@ int cb_table_zone(const cb_table* t, int which, uint8_t* out, uint64_t cap, uint
 
 int cb_table_info(const cb_table* t, uint64_t* nlines, uint64_t* bytes) {
   if (!t) return fail(CB_EINVAL, "null table");
+  if (int rc = finalize_table(const_cast<cb_table*>(t))) return rc;
   if (nlines) *nlines = t->nlines;
   if (bytes) *bytes = t->len;
   return CB_OK;
@@ -706,6 +826,7 @@ int cb_table_info(const cb_table* t, uint64_t* nlines, uint64_t* bytes) {
 
 int cb_table_well_formed(const cb_table* t, int* out) {
   if (!t || !out) return fail(CB_EINVAL, "null argument");
+  if (int rc = finalize_table(const_cast<cb_table*>(t))) return rc;
   *out = t->fast ? 1 : 0;
   return CB_OK;
 }
@@ -717,6 +838,7 @@ int cb_table_force_exact(int on) {
 
 int cb_table_lines(const cb_table* t, uint64_t* start, uint32_t* key_len, uint32_t* line_len) {
   if (!t) return fail(CB_EINVAL, "null table");
+  if (int rc = finalize_table(const_cast<cb_table*>(t))) return rc;
   DeviceGuard dg(t->device);
   if (!t->nlines) return CB_OK;
   // strided copies out of the 32-byte records

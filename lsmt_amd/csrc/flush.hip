@@ -98,18 +98,25 @@ __global__ __launch_bounds__(kNT) void k_line_sums(const SortKey* __restrict__ o
   tile_sum(order, ko, vo, n, tsum);
 }
 
-// *ok &= key[i-1] <= key[i] for all i (already in stable-sorted order). Each
-// lane's key comes in as words; the previous one from the neighbour lane.
+static_assert(offsetof(CreateResult, len) == kCreateHead, "the zeroed head of CreateResult");
+
+// r->flags[0] |= key[i-1] > key[i] for some i (not in stable-sorted order).
+// Each lane's key comes in as words; the previous one from the neighbour lane.
 __global__ __launch_bounds__(kNT) void k_sorted_check(const uint8_t* __restrict__ kb,
                                                       const uint64_t* __restrict__ ko,
                                                       const uint64_t* __restrict__ vo, uint64_t n,
-                                                      CreateResult* r, uint64_t* __restrict__ tsum) {
+                                                      CreateResult* r, uint64_t* __restrict__ tsum,
+                                                      uint64_t kmax, uint64_t vmax) {
   const uint64_t p = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   tile_sum(nullptr, ko, vo, n, tsum);  // the line tiles if the input is already sorted
   if (p == 0) {
-    r->ktot = ko[n];
-    r->vtot = vo[n];
+    const uint64_t kt = ko[n], vt = vo[n];
+    r->ktot = kt;
+    r->vtot = vt;
+    // the file buffer was sized from the caller's byte bounds: a batch past
+    // them is refused (k_format writes nothing) and reported by the table
+    if (kt > kmax || vt > vmax) r->flags[4] = 1u;
   }
   uint64_t i = 0, kl = 0, w0 = 0, w1 = 0;
   if (p < n) key_words(nullptr, kb, ko, p, i, kl, w0, w1);
@@ -123,10 +130,10 @@ __global__ __launch_bounds__(kNT) void k_sorted_check(const uint8_t* __restrict_
   uint64_t pi = p - 1;
   if (p < n && lane == 0 && p > 0) key_words(nullptr, kb, ko, p - 1, pi, pkl, pw0, pw1);
   const bool bad = p < n && p > 0 && key_cmp(kb, ko, p - 1, pkl, pw0, pw1, p, kl, w0, w1) > 0;
-  // one plain store of 0 per block holding an inversion (every writer
+  // one plain store of 1 per block holding an inversion (every writer
   // writes the same value): a fully unsorted batch would otherwise queue a
   // returning load and an atomic per block on one word
-  if (__syncthreads_or(bad) && threadIdx.x == 0) r->flags[0] = 0u;
+  if (__syncthreads_or(bad) && threadIdx.x == 0) r->flags[0] = 1u;
 }
 
 
@@ -258,23 +265,29 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
                                                 uint8_t* __restrict__ out, LineRec* __restrict__ rec,
                                                 uint64_t* __restrict__ pfx, uint64_t* __restrict__ fence,
                                                 CreateResult* r, const ulonglong2* __restrict__ vsp,
-                                                uint32_t* __restrict__ dir, DirMap dm, DirMap* dmap_out) {
+                                                uint32_t* __restrict__ dir, DirMap* dmap_out) {
   __shared__ uint32_t stage32[LDSB / 4];
   __shared__ DirMap sdm;  // the directory's map, indexed per lane
   uint8_t* stage = reinterpret_cast<uint8_t*>(stage32);
-  // the bin sort overflowed (a group outgrew its LDS tile and left its slice
-  // of `order` / `vsp` unwritten): nothing here may read those stale records
-  // or write at offsets derived from them; the caller redoes the sort
-  if (r->flags[3]) return;
+  // The bin sort could not place every record (a group outgrew its LDS tile,
+  // or one bin held the batch: its slice of `order` / `vsp` is unwritten), or
+  // the byte totals exceed the bounds the file buffer was sized from: nothing
+  // here may read those records or write at offsets derived from them; the
+  // table redoes the sort (or reports the error) when it is finalised.
+  if (r->flags[3] || r->flags[4]) return;
+  if (!r->flags[0]) {  // the batch was sorted: the sort left nothing, format in input order
+    order = nullptr;
+    vsp = nullptr;
+  }
   const uint64_t p0 = (uint64_t)blockIdx.x * kNT;
   const uint64_t p = p0 + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t pend = p0 + kNT < n ? p0 + kNT : n;
   const bool live = p < n;
   uint64_t i = 0, kl = 0, w0 = 0, w1 = 0;
-  if (dir && threadIdx.x == 0) {
-    sdm = dm;
-    if (blockIdx.x == 0) *dmap_out = dm;  // the table's copy, for the read path
+  if (dir && threadIdx.x == 0) {  // the directory's map from the sampled prefix bytes (order-free)
+    sdm = make_dirmap(r->dmask, n);
+    if (blockIdx.x == 0) *dmap_out = sdm;  // the table's copy, for the read path
   }
   if (live) key_words(order, kb, ko, p, i, kl, w0, w1);
   // the previous entry's key: the neighbour lane's, or loaded by lane 0
@@ -330,7 +343,7 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   }
   // plain stores of one value from every block that has one (no atomics)
   if (__syncthreads_or(special) && threadIdx.x == 0) r->flags[1] = 1u;
-  if (__syncthreads_or(not_inc) && threadIdx.x == 0) r->flags[2] = 0u;
+  if (__syncthreads_or(not_inc) && threadIdx.x == 0) r->flags[2] = 1u;
   if (dir) {
     // the byte-rank directory (sstable.hpp DirMap, dir_fill): line p owns
     // dir[B] for the buckets B in (bucket(line p-1), bucket(line p)]
@@ -408,10 +421,10 @@ hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, S
 
 
 hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, const uint64_t* vo, uint64_t n,
-                               CreateResult* r, uint64_t* tsum, hipStream_t s) {
+                               CreateResult* r, uint64_t* tsum, uint64_t kmax, uint64_t vmax, hipStream_t s) {
   ProfScope ps("k_sorted_check", s);
   hipLaunchKernelGGL(k_sorted_check, dim3(n ? blocks_for(n, kNT) : 1), dim3(kNT), 0, s, kb, ko, vo, n, r,
-                     tsum);
+                     tsum, kmax, vmax);
   return hipGetLastError();
 }
 
@@ -430,18 +443,17 @@ hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
                          uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp, uint32_t* dir,
-                         const DirMap* dm, DirMap* dmap_out) {
+                         DirMap* dmap_out) {
   if (!n) return hipSuccess;
-  if (dir && (!dm || !dmap_out)) return hipErrorInvalidValue;
-  const DirMap d = dir ? *dm : DirMap{};
+  if (dir && !dmap_out) return hipErrorInvalidValue;
   ProfScope ps("k_format", s);
   const dim3 g(blocks_for(n, kNT));
   if (bytes_bound / n * kNT * 5 / 4 <= kFormatLdsSmall)
     hipLaunchKernelGGL(k_format<kFormatLdsSmall>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
-                       rec, pfx, fence, r, order ? vsp : nullptr, dir, d, dmap_out);
+                       rec, pfx, fence, r, order ? vsp : nullptr, dir, dmap_out);
   else
     hipLaunchKernelGGL(k_format<kFormatLdsLarge>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
-                       rec, pfx, fence, r, order ? vsp : nullptr, dir, d, dmap_out);
+                       rec, pfx, fence, r, order ? vsp : nullptr, dir, dmap_out);
   return hipGetLastError();
 }
 

@@ -58,12 +58,16 @@ __device__ __forceinline__ SortKey sort_record(const uint8_t* kb, const uint64_t
 // (src/sstable.rs:66-70).
 __host__ __device__ inline uint64_t line_len(uint64_t kl, uint64_t vl) { return kl + 1 + (vl + 2) / 3 * 4 + 1; }
 
-// What SsTable::create hands back to the host, assembled on the device so that
-// each of its two host round trips is one copy into pinned memory.
+// What SsTable::create leaves on the device for the host, read back in one
+// copy into pinned memory once the table's work has run (cb_sstable_create
+// only enqueues). Every flag starts 0 (the head up to `len` is zeroed by one
+// memset), so no host-written initial values are needed.
 constexpr uint32_t kZoneInline = 256;  // zone bound key bytes carried inline
 struct CreateResult {
-  uint32_t flags[4];          // [0] input sorted, [1] a key holds '\n' / '\t', [2] strictly increasing,
-                              // [3] the bin sort overflowed (redo with the merge sort)
+  uint32_t flags[8];          // [0] unsorted (an inversion was seen), [1] a key holds '\n' / '\t',
+                              // [2] not strictly increasing, [3] the bin sort could not place every
+                              // record (one bin, or a group larger than its tile: redo with the merge
+                              // sort), [4] ko[n] / vo[n] above the caller's byte bounds; [5..7] 0
   uint64_t ktot, vtot;        // ko[n], vo[n]
   uint64_t dmask[kDirPos][4]; // byte values at each position of sampled keys' 8-byte prefixes (DirMap)
   uint64_t len;               // the file's length
@@ -79,13 +83,14 @@ hipError_t launch_sort_keys(const uint8_t* kb, const uint64_t* ko, uint64_t n, S
 // sums of line lengths.
 constexpr uint32_t kFormatTile = 256;
 inline uint64_t format_tiles(uint64_t n) { return n ? (n + kFormatTile - 1) / kFormatTile : 1; }
-// r->flags[0] &= (keys already in non-decreasing order); r->ktot = ko[n],
-// r->vtot = vo[n]; r->dmask |= the prefix bytes of kDirSample evenly spaced
-// keys (zeroed by the caller); tsum = the line tiles in input order (valid
-// if sorted).
+// r->flags[0] |= (keys not in non-decreasing order); r->ktot = ko[n],
+// r->vtot = vo[n], r->flags[4] |= (ko[n] > kmax or vo[n] > vmax); r->dmask
+// |= the prefix bytes of kDirSample evenly spaced keys (r's head zeroed by
+// the caller); tsum = the line tiles in input order (valid if sorted).
 // Launches for any n, n = 0 included.
+constexpr size_t kCreateHead = 32 + 16 + kDirPos * 4 * 8;  // flags, totals, dmask: zeroed per create
 hipError_t launch_sorted_check(const uint8_t* kb, const uint64_t* ko, const uint64_t* vo, uint64_t n,
-                               CreateResult* r, uint64_t* tsum, hipStream_t s);
+                               CreateResult* r, uint64_t* tsum, uint64_t kmax, uint64_t vmax, hipStream_t s);
 // tsum = the line tiles in the order of the sort records.
 hipError_t launch_line_sums(const SortKey* order, const uint64_t* ko, const uint64_t* vo, uint64_t n,
                             uint64_t* tsum, hipStream_t s);
@@ -96,38 +101,45 @@ hipError_t launch_line_sums(const SortKey* order, const uint64_t* ko, const uint
 // vo != nullptr: the last launch also writes, for every output p, vsp[p] =
 // {vo[idx], value length} and tsum = the line tiles in sorted order (what
 // launch_line_sums would), from the records it holds in registers.
+// run_if (nullable, device): every launch returns at once unless *run_if !=
+// 0 (SsTable::create enqueues the sort before it knows the batch's order).
 uint64_t entry_sort_tmp_bytes(uint64_t n);
 hipError_t launch_entry_sort(const SortKey* in, SortKey* out, SortKey* tmp, uint64_t n, const uint8_t* kb,
                              const uint64_t* ko, hipStream_t s, const uint64_t* vo = nullptr,
-                             ulonglong2* vsp = nullptr, uint64_t* tsum = nullptr);
-// The same order by binning (sort.hip "bin sort"): dm's buckets over the
-// keys' prefixes as bins (monotone in the key), groups of ~T records sorted
-// in LDS; out = the sorted records, vsp / tsum as launch_entry_sort's tail.
-// tmp: bin_sort_tmp_bytes. *overflow |= 1 when a group outgrew an LDS tile
-// (out is then incomplete: redo with launch_entry_sort).
-uint64_t bin_sort_tmp_bytes(uint64_t n, uint64_t nbins, uint32_t T);
-uint32_t bin_sort_max_bins();   // dm.nbuckets at most
+                             ulonglong2* vsp = nullptr, uint64_t* tsum = nullptr, const uint32_t* run_if = nullptr);
+// The same order by binning (sort.hip "bin sort"): the buckets of the
+// DirMap every launch derives from r->dmask (at most bin_sort_max_bins()) as
+// bins (monotone in the key), groups of ~T records sorted in LDS; out = the
+// sorted records, vsp / tsum as launch_entry_sort's tail. Every launch
+// returns at once when r->flags[0] is 0 (the batch is sorted). r->flags[3]
+// := 1 when the bins cannot take the batch (a single bin, or a group larger
+// than an LDS tile): out is then incomplete (k_format skips; redo with
+// launch_entry_sort). tmp: bin_sort_tmp_bytes. Enqueued without any host
+// knowledge of the batch beyond n.
+uint64_t bin_sort_tmp_bytes(uint64_t n, uint32_t T);
 uint32_t bin_sort_max_group();  // T at most (one LDS tile)
-hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, const DirMap& dm, uint32_t T,
-                           SortKey* out, void* tmp, hipStream_t s, const uint64_t* vo, ulonglong2* vsp,
-                           uint64_t* tsum, uint32_t* overflow);
+hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, uint32_t T, SortKey* out, void* tmp,
+                           hipStream_t s, const uint64_t* vo, ulonglong2* vsp, uint64_t* tsum, CreateResult* r);
 // The file (lines at the offsets tsum and the line lengths give, then 16
 // zero bytes of slack), its
 // line index without re-reading it (sstable.hpp layout: entry p is line p),
 // and r's flags[1] / flags[2], len and zone bounds, in one pass (n >= 1 for
 // r). bytes_bound (>= the file's length) picks the LDS stage size. The index is valid only when no key holds '\n' or '\t' (a key byte the
 // reference's line split or TAB search would see): flags[1] |= 1 otherwise,
-// and the caller re-indexes the file. flags[2] &= (keys strictly increasing:
-// the well-formed check).
-// vsp (nullable, with order): entry p's {value offset, value length} in
-// sorted order (launch_entry_sort's), read instead of vo[order[p].idx].
-// dir (nullable, with dm): the table's directory (dm->nbuckets + 1 entries),
-// written here from the lines' prefixes (what launch_table_dir would build);
-// dm is also stored at dmap_out.
+// and the caller re-indexes the file. flags[2] |= (keys not strictly
+// increasing: the well-formed check).
+// order / vsp (nullable): the sort's records and value spans, used only when
+// r->flags[0] says the batch was unsorted (a sorted batch is formatted in
+// input order). Nothing is written when r->flags[3] or r->flags[4] is set.
+// vsp: entry p's {value offset, value length} in sorted order
+// (launch_entry_sort's), read instead of vo[order[p].idx].
+// dir (nullable, with dmap_out): the table's directory, its DirMap derived
+// from r->dmask (make_dirmap(dmask, n)) and stored at dmap_out, written here
+// from the lines' prefixes (what launch_table_dir would build).
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
                          uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp = nullptr,
-                         uint32_t* dir = nullptr, const DirMap* dm = nullptr, DirMap* dmap_out = nullptr);
+                         uint32_t* dir = nullptr, DirMap* dmap_out = nullptr);
 
 }  // namespace cb

@@ -219,7 +219,9 @@ __device__ __forceinline__ void cas(SortKey& x, SortKey& y, const RecLess& less)
 }
 
 __global__ __launch_bounds__(kST) void k_sort_block(const SortKey* __restrict__ in, SortKey* __restrict__ out,
-                                                    uint64_t n, RecLess less, SortTail tl) {
+                                                    uint64_t n, RecLess less, SortTail tl,
+                                                    const uint32_t* __restrict__ run_if) {
+  if (run_if && !*run_if) return;  // (uniform) the batch needs no sort
   __shared__ uint64_t lds[3 * kPadded];
   const LdsTile tile{lds};
   const uint64_t base = (uint64_t)blockIdx.x * kTile;
@@ -287,7 +289,9 @@ __device__ __forceinline__ uint64_t wave_merge_split(const SortKey* a, uint64_t 
 }
 
 __global__ __launch_bounds__(kST) void k_sort_merge(const SortKey* __restrict__ in, SortKey* __restrict__ out,
-                                                    uint64_t n, uint64_t w, RecLess less, SortTail tl) {
+                                                    uint64_t n, uint64_t w, RecLess less, SortTail tl,
+                                                    const uint32_t* __restrict__ run_if) {
+  if (run_if && !*run_if) return;  // (uniform) the batch needs no sort
   __shared__ uint64_t lds[3 * kPadded];
   __shared__ uint64_t split[2];
   const LdsTile tile{lds};
@@ -393,10 +397,29 @@ struct LdsTile16 {
   __device__ __forceinline__ uint64_t word(uint32_t g) const { return w[(g % 3) * P + pad(g / 3)]; }
 };
 
+// The bins' map and whether the bin sort runs at all, from r (every bin
+// launch derives them itself: the host enqueues the sort before it knows the
+// batch): it runs when the batch is unsorted and the sampled prefixes give at
+// least two bins; an unsorted batch of one bin is left to the merge sort
+// (flags[3], set by the first block of k_bin_count). Thread 0, into LDS.
+__device__ __forceinline__ bool bin_plan(const CreateResult* r, uint64_t n, DirMap& sdm) {
+  if (!r->flags[0]) return false;  // sorted: no sort at all
+  sdm = make_dirmap(r->dmask, n, kBins);
+  return sdm.nbuckets >= 2;
+}
+
 __global__ __launch_bounds__(kBinNT) void k_bin_count(const uint8_t* __restrict__ kb, const uint64_t* __restrict__ ko,
-                                                      uint64_t n, DirMap dm, uint32_t* __restrict__ cnt) {
+                                                      uint64_t n, CreateResult* r, uint32_t* __restrict__ cnt,
+                                                      uint64_t* __restrict__ tsum, uint64_t ntiles) {
   __shared__ DirMap sdm;
   __shared__ uint32_t hist[kBins];
+  __shared__ uint32_t go;
+  if (threadIdx.x == 0) {
+    go = bin_plan(r, n, sdm);
+    if (!go && r->flags[0] && blockIdx.x == 0) r->flags[3] = 1u;  // unsorted, one bin: the merge sort's
+  }
+  __syncthreads();
+  if (!go) return;
   const uint64_t p0 = (uint64_t)blockIdx.x * kBinChunk + threadIdx.x;
   uint64_t w0[kBinPer];
 #pragma unroll
@@ -406,7 +429,10 @@ __global__ __launch_bounds__(kBinNT) void k_bin_count(const uint8_t* __restrict_
     w0[k] = 0;
     if (p < n) load16(kb + ko[p], ko[p + 1] - ko[p], w0[k], w1);
   }
-  if (threadIdx.x == 0) sdm = dm;
+  // k_bin_sort adds the sorted line tiles into tsum (k_sorted_check left the
+  // input order's there)
+  for (uint64_t i = (uint64_t)blockIdx.x * kBinNT + threadIdx.x; i < ntiles; i += (uint64_t)gridDim.x * kBinNT)
+    tsum[i] = 0;
   for (uint32_t b = threadIdx.x; b < kBins; b += kBinNT) hist[b] = 0;
   __syncthreads();
 #pragma unroll
@@ -429,10 +455,16 @@ __global__ __launch_bounds__(kBinNT) void k_bin_count(const uint8_t* __restrict_
 constexpr uint32_t kOffW = 16;  // waves per k_bin_offsets block
 constexpr uint32_t kOffR = 16;  // rows per wave held in registers
 constexpr uint32_t kBinBlocks = kBins / 64;  // 64-bin blocks at most
-__global__ __launch_bounds__(kOffW * 64) void k_bin_offsets(uint32_t* __restrict__ cnt, uint32_t nblk, uint32_t nb,
-                                                            uint32_t* __restrict__ lstart,
+__global__ __launch_bounds__(kOffW * 64) void k_bin_offsets(uint32_t* __restrict__ cnt, uint32_t nblk, uint64_t n,
+                                                            const CreateResult* r, uint32_t* __restrict__ lstart,
                                                             uint32_t* __restrict__ bsum) {
   __shared__ uint32_t part[kOffW][64];
+  __shared__ DirMap sdm;
+  __shared__ uint32_t go;
+  if (threadIdx.x == 0) go = bin_plan(r, n, sdm) && blockIdx.x * 64 < sdm.nbuckets;
+  __syncthreads();
+  if (!go) return;  // (the grid covers the most bins; blocks past this map's return)
+  const uint32_t nb = (uint32_t)sdm.nbuckets;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, b = blockIdx.x * 64 + lane;
   const uint32_t per = (nblk + kOffW - 1) / kOffW, k0 = min(wv * per, nblk), k1 = min(k0 + per, nblk);
   const bool live = b < nb;
@@ -488,14 +520,20 @@ __device__ __forceinline__ BinPrefix bin_block_prefix(const uint32_t* __restrict
 }
 
 __global__ __launch_bounds__(kBinNT) void k_bin_scatter(const uint8_t* __restrict__ kb,
-                                                        const uint64_t* __restrict__ ko, uint64_t n, DirMap dm,
+                                                        const uint64_t* __restrict__ ko, uint64_t n,
+                                                        const CreateResult* res,
                                                         const uint32_t* __restrict__ cnt,
                                                         const uint32_t* __restrict__ lstart,
-                                                        const uint32_t* __restrict__ bsum, uint32_t nbb,
+                                                        const uint32_t* __restrict__ bsum,
                                                         SortKey* __restrict__ out) {
   __shared__ DirMap sdm;
   __shared__ uint32_t cur[kBins];
   __shared__ uint32_t bpre[kBinBlocks];
+  __shared__ uint32_t go;
+  if (threadIdx.x == 0) go = bin_plan(res, n, sdm);
+  __syncthreads();
+  if (!go) return;
+  const uint32_t nbb = (uint32_t)((sdm.nbuckets + 63) / 64);
   const uint64_t p0 = (uint64_t)blockIdx.x * kBinChunk + threadIdx.x;
   SortKey r[kBinPer];
 #pragma unroll
@@ -503,7 +541,6 @@ __global__ __launch_bounds__(kBinNT) void k_bin_scatter(const uint8_t* __restric
     const uint64_t p = p0 + (uint64_t)k * kBinNT;
     if (p < n) r[k] = sort_record(kb, ko, p);
   }
-  if (threadIdx.x == 0) sdm = dm;
   if (threadIdx.x < 64) {
     const BinPrefix bp = bin_block_prefix(bsum, nbb);
     const uint32_t l = threadIdx.x;
@@ -511,7 +548,7 @@ __global__ __launch_bounds__(kBinNT) void k_bin_scatter(const uint8_t* __restric
     if (2 * l + 1 < nbb) bpre[2 * l + 1] = bp.pre0 + bp.a0;
   }
   __syncthreads();
-  const uint32_t nb = (uint32_t)dm.nbuckets;
+  const uint32_t nb = (uint32_t)sdm.nbuckets;
   for (uint32_t b = threadIdx.x; b < nb; b += kBinNT)
     cur[b] = bpre[b >> 6] + lstart[b] + cnt[(uint64_t)blockIdx.x * nb + b];
   __syncthreads();
@@ -555,16 +592,22 @@ __device__ __forceinline__ uint32_t bin_group_start(uint32_t g, uint32_t G, uint
 template <uint32_t NT>
 __global__ __launch_bounds__(NT) void k_bin_sort(const SortKey* __restrict__ in, SortKey* __restrict__ out,
                                                  const uint32_t* __restrict__ lstart,
-                                                 const uint32_t* __restrict__ bsum, uint32_t nb, uint32_t nbb,
+                                                 const uint32_t* __restrict__ bsum, CreateResult* res,
                                                  uint32_t T, uint32_t G, uint32_t n, RecLess less,
                                                  const uint64_t* __restrict__ vo, ulonglong2* __restrict__ vsp,
-                                                 uint64_t* __restrict__ tsum, uint32_t* __restrict__ overflow) {
+                                                 uint64_t* __restrict__ tsum) {
   static_assert(kFormatTile == 64 * kIPT, "a wave's outputs span at most two format tiles");
   constexpr uint32_t TILE = NT * kIPT;
   using BinTile = LdsTile16<TILE>;
   __shared__ uint64_t lds[3 * BinTile::P];
   const BinTile tile{lds};
   __shared__ uint32_t gb[2];
+  __shared__ DirMap sdm;
+  __shared__ uint32_t go;
+  if (threadIdx.x == 0) go = bin_plan(res, n, sdm);
+  __syncthreads();
+  if (!go) return;
+  const uint32_t nb = (uint32_t)sdm.nbuckets, nbb = (nb + 63) / 64;
   if (threadIdx.x < 128) {  // waves 0 and 1: the group's start and end
     const uint32_t v = bin_group_start(blockIdx.x + (threadIdx.x >> 6), G, T, n, lstart, bsum, nb, nbb);
     if ((threadIdx.x & 63u) == 0) gb[threadIdx.x >> 6] = v;
@@ -572,8 +615,8 @@ __global__ __launch_bounds__(NT) void k_bin_sort(const SortKey* __restrict__ in,
   __syncthreads();
   const uint64_t beg = gb[0], end = gb[1];
   if (end <= beg) return;
-  if (end - beg > TILE) {  // a bin too large for one tile: the caller falls back to the merge sort
-    if (threadIdx.x == 0) atomicOr(overflow, 1u);
+  if (end - beg > TILE) {  // a bin too large for one tile: the table falls back to the merge sort
+    if (threadIdx.x == 0) res->flags[3] = 1u;  // (every writer stores the same value)
     return;
   }
   const uint32_t cnt = (uint32_t)(end - beg);
@@ -636,56 +679,51 @@ __global__ __launch_bounds__(NT) void k_bin_sort(const SortKey* __restrict__ in,
 
 uint64_t entry_sort_tmp_bytes(uint64_t n) { return n * sizeof(SortKey); }
 
-uint64_t bin_sort_tmp_bytes(uint64_t n, uint64_t nbins, uint32_t T) {
-  const uint64_t G = (n + T - 1) / T, nblk = (n + kBinChunk - 1) / kBinChunk;
-  (void)G;
-  return n * sizeof(SortKey) + (nblk * nbins + nbins + kBinBlocks) * 4;
+uint64_t bin_sort_tmp_bytes(uint64_t n, uint32_t T) {
+  const uint64_t nblk = (n + kBinChunk - 1) / kBinChunk;
+  (void)T;
+  // the bins are known only on the device: room for the most of them
+  return n * sizeof(SortKey) + (nblk * kBins + kBins + kBinBlocks) * 4;
 }
 
-uint32_t bin_sort_max_bins() { return kBins; }
 uint32_t bin_sort_max_group() { return kBinTileMax; }
 
-hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, const DirMap& dm, uint32_t T,
-                           SortKey* out, void* tmp, hipStream_t s, const uint64_t* vo, ulonglong2* vsp,
-                           uint64_t* tsum, uint32_t* overflow) {
+hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, uint32_t T, SortKey* out, void* tmp,
+                           hipStream_t s, const uint64_t* vo, ulonglong2* vsp, uint64_t* tsum, CreateResult* r) {
   if (!n) return hipSuccess;
-  const uint32_t nb = (uint32_t)dm.nbuckets;
-  if (nb < 1 || nb > kBins || !T || T > kBinTileMax) return hipErrorInvalidValue;
+  if (!T || T > kBinTileMax || n >= (1ull << 32)) return hipErrorInvalidValue;
   const uint32_t G = (uint32_t)((n + T - 1) / T);
   const uint32_t nblk = (uint32_t)((n + kBinChunk - 1) / kBinChunk);
   SortKey* binned = (SortKey*)tmp;
-  uint32_t* cnt = (uint32_t*)(binned + n);          // nblk x nb
-  uint32_t* lstart = cnt + (uint64_t)nblk * nb;      // nb
-  uint32_t* bsum = lstart + nb;                      // nbb
-  const uint32_t nbb = (nb + 63) / 64;
-  hipError_t e = hipMemsetAsync(tsum, 0, format_tiles(n) * 8, s);
-  if (e != hipSuccess) return e;
+  // cnt is nblk x nb for the device's nb; lstart and bsum sit past the most
+  uint32_t* cnt = (uint32_t*)(binned + n);
+  uint32_t* lstart = cnt + (uint64_t)nblk * kBins;
+  uint32_t* bsum = lstart + kBins;
   {
     ProfScope ps("k_bin_count", s);
-    hipLaunchKernelGGL(k_bin_count, dim3(nblk), dim3(kBinNT), 0, s, kb, ko, n, dm, cnt);
+    hipLaunchKernelGGL(k_bin_count, dim3(nblk), dim3(kBinNT), 0, s, kb, ko, n, r, cnt, tsum, format_tiles(n));
   }
   {
     ProfScope ps("k_bin_offsets", s);
-    hipLaunchKernelGGL(k_bin_offsets, dim3(nbb), dim3(kOffW * 64), 0, s, cnt, nblk, nb, lstart, bsum);
+    hipLaunchKernelGGL(k_bin_offsets, dim3(kBinBlocks), dim3(kOffW * 64), 0, s, cnt, nblk, n, r, lstart, bsum);
   }
   {
     ProfScope ps("k_bin_scatter", s);
-    hipLaunchKernelGGL(k_bin_scatter, dim3(nblk), dim3(kBinNT), 0, s, kb, ko, n, dm, cnt, lstart, bsum, nbb,
-                       binned);
+    hipLaunchKernelGGL(k_bin_scatter, dim3(nblk), dim3(kBinNT), 0, s, kb, ko, n, r, cnt, lstart, bsum, binned);
   }
   ProfScope ps("k_bin_sort", s);
   if (T <= 768)  // 1024-record tiles: room for bins of up to 1024 - T records past the target
-    hipLaunchKernelGGL(k_bin_sort<256>, dim3(G), dim3(256), 0, s, binned, out, lstart, bsum, nb, nbb, T, G,
-                       (uint32_t)n, RecLess{kb, ko}, vo, vsp, tsum, overflow);
+    hipLaunchKernelGGL(k_bin_sort<256>, dim3(G), dim3(256), 0, s, binned, out, lstart, bsum, r, T, G,
+                       (uint32_t)n, RecLess{kb, ko}, vo, vsp, tsum);
   else
-    hipLaunchKernelGGL(k_bin_sort<512>, dim3(G), dim3(512), 0, s, binned, out, lstart, bsum, nb, nbb, T, G,
-                       (uint32_t)n, RecLess{kb, ko}, vo, vsp, tsum, overflow);
+    hipLaunchKernelGGL(k_bin_sort<512>, dim3(G), dim3(512), 0, s, binned, out, lstart, bsum, r, T, G,
+                       (uint32_t)n, RecLess{kb, ko}, vo, vsp, tsum);
   return hipGetLastError();
 }
 
 hipError_t launch_entry_sort(const SortKey* in, SortKey* out, SortKey* tmp, uint64_t n, const uint8_t* kb,
                              const uint64_t* ko, hipStream_t s, const uint64_t* vo, ulonglong2* vsp,
-                             uint64_t* tsum) {
+                             uint64_t* tsum, const uint32_t* run_if) {
   if (!n) return hipSuccess;
   const uint64_t tiles = (n + kTile - 1) / kTile;
   uint32_t rounds = 0;
@@ -696,11 +734,11 @@ hipError_t launch_entry_sort(const SortKey* in, SortKey* out, SortKey* tmp, uint
   ProfScope ps("k_entry_sort", s);
   const SortTail none{nullptr, nullptr, nullptr}, tail{vo, vsp, tsum};
   hipLaunchKernelGGL(k_sort_block, dim3((uint32_t)tiles), dim3(kST), 0, s, in, bufs[rounds & 1], n, less,
-                     rounds ? none : tail);
+                     rounds ? none : tail, run_if);
   for (uint32_t r = 0; r < rounds; ++r) {
     const uint64_t w = (uint64_t)kTile << r;
     hipLaunchKernelGGL(k_sort_merge, dim3((uint32_t)tiles), dim3(kST), 0, s, bufs[(rounds - r) & 1],
-                       bufs[(rounds - r - 1) & 1], n, w, less, r + 1 == rounds ? tail : none);
+                       bufs[(rounds - r - 1) & 1], n, w, less, r + 1 == rounds ? tail : none, run_if);
   }
   return hipGetLastError();
 }

@@ -127,8 +127,8 @@ __host__ __device__ inline uint64_t dir_bucket(const DirMap& d, uint64_t w) {
 }
 
 // The DirMap of a table whose sampled prefixes hold the byte values `mask`,
-// for nl lines: ~target buckets (default dir_target(nl)) (host).
-inline DirMap make_dirmap(const uint64_t (&mask)[kDirPos][4], uint64_t nl, uint64_t target = ~0ull) {
+// for nl lines: ~target buckets (default dir_target(nl)) (host, or one device thread).
+__host__ __device__ inline DirMap make_dirmap(const uint64_t (&mask)[kDirPos][4], uint64_t nl, uint64_t target = ~0ull) {
   DirMap d{};
   if (target == ~0ull) target = dir_target(nl);
   uint64_t D = 1;

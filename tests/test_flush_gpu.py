@@ -279,3 +279,89 @@ def test_create_unsorted_large(gpu, n):
     assert (np.asarray(which) == 0).all()
     got_vals = np.frombuffer(bytes(out), np.uint8).reshape(-1, 16)
     assert np.array_equal(got_vals, vals[idx])
+
+
+def _dev_batches(keys, vals):
+    import torch
+    kd = torch.from_numpy(np.frombuffer(b"".join(keys) or b"\0", np.uint8).copy()).cuda()
+    vd = torch.from_numpy(np.frombuffer(b"".join(vals) or b"\0", np.uint8).copy()).cuda()
+    ko = np.zeros(len(keys) + 1, np.int64)
+    np.cumsum([len(k) for k in keys], out=ko[1:])
+    vo = np.zeros(len(vals) + 1, np.int64)
+    np.cumsum([len(v) for v in vals], out=vo[1:])
+    return (torch.from_numpy(ko).cuda(), kd), (torch.from_numpy(vo).cuda(), vd)
+
+
+@pytest.mark.parametrize("shape", ["sorted", "unsorted", "two_prefixes", "one_prefix", "small"])
+def test_create_enqueue_only_then_finalise(gpu, shape):
+    """cb_sstable_create only enqueues (the device picks: no sort for a sorted
+    batch, the bin sort, or — for keys the bins cannot split — a merge sort
+    when the table is finalised). Five tables in flight on one stream, none
+    waited for until all are queued; every file, zone and filter must equal
+    the oracle's (src/sstable.rs:51-87)."""
+    import torch
+    rng = np.random.default_rng(len(shape))
+    st = torch.cuda.Stream()
+    made, want = [], []
+    for r in range(5):
+        n = 300 if shape == "small" else 60_000
+        base = [bytes(x) for x in workload.key_range(9500 + 10 * r + len(shape), n)]
+        if shape == "two_prefixes":
+            keys = [(b"ns:user:" if i % 2 else b"ns:item:") + k[:6] for i, k in enumerate(base)]
+        elif shape == "one_prefix":
+            keys = [b"default:" + k for k in base]
+        else:
+            keys = base
+        if shape == "sorted":
+            keys = sorted(keys)
+        vals = [bytes(rng.integers(0, 256, int(rng.integers(0, 30)), dtype=np.uint8)) for _ in keys]
+        (ko, kd), (vo, vd) = _dev_batches(keys, vals)
+        kb = gpu.KeyBatch(n=len(keys), data=kd, offsets=ko)
+        vb = gpu.KeyBatch(n=len(vals), data=vd, offsets=vo)
+        made.append(gpu.sstable_create((kb, vb), m=1 << 16, stream=st, wait=False))
+        want.append((keys, vals))
+    for (t, bloom, zone), (keys, vals) in zip(made, want):
+        assert zone is None
+        t.wait()
+        assert t.data() == oracle.sstable_create(list(zip(keys, vals)))
+        assert (t._zone(0), t._zone(1)) == (min(keys), max(keys))
+        o = oracle.OracleFilter(1 << 16)
+        for k in keys:
+            o.insert(k)
+        assert np.array_equal(bloom.bools(), o.bools())
+        assert t.nlines == len(keys)
+
+
+def test_create_bounded_refuses_a_batch_past_its_bounds(gpu):
+    """cb_sstable_create_bounded sizes the file from the caller's byte
+    bounds; a batch whose offsets go past them writes nothing and its table
+    reports CB_EINVAL when finalised (no write past the buffer)."""
+    import ctypes
+    from lsmt_amd import _lib
+    keys = [b"k%05d" % i for i in range(5000)]
+    vals = [b"v" * 20 for _ in keys]
+    (ko, kd), (vo, vd) = _dev_batches(keys, vals)
+    L = _lib.load()
+    th, fh = ctypes.c_void_p(), ctypes.c_void_p()
+    rc = L.cb_sstable_create_bounded(kd.data_ptr(), ko.data_ptr(), 100, vd.data_ptr(), vo.data_ptr(),
+                                     int(vd.numel()), len(keys), 1024, 0, None, ctypes.byref(th), ctypes.byref(fh))
+    assert rc == 0
+    assert L.cb_table_wait(th) == _lib.CB_EINVAL
+    assert L.cb_table_wait(th) == _lib.CB_EINVAL  # sticky
+    L.cb_table_destroy(th)
+    L.cb_filter_destroy(fh)
+
+
+def test_create_pending_table_destroyed_unread(gpu):
+    """A table destroyed before anything finalised it waits for its own work
+    first (no buffer is reused under a running kernel)."""
+    keys = [bytes(x) for x in workload.key_range(9700, 200_000)]
+    vals = [b"x" * 8] * len(keys)
+    (ko, kd), (vo, vd) = _dev_batches(keys, vals)
+    for _ in range(3):
+        t, b, _ = gpu.sstable_create((gpu.KeyBatch(n=len(keys), data=kd, offsets=ko),
+                                      gpu.KeyBatch(n=len(vals), data=vd, offsets=vo)), m=1 << 20, wait=False)
+        t.close()
+        b.close()
+    t, _, zone = gpu.sstable_create(list(zip(keys[:1000], vals[:1000])))
+    assert t.data() == oracle.sstable_create(list(zip(keys[:1000], vals[:1000])))
