@@ -1873,14 +1873,24 @@ int cb_filter_insert_fixed_many(cb_filter* const* filters, uint32_t nf, const ui
       }
     staged = true;
   }
-  const TilePlan p = cb::plan_build(f0->m, nmax, std::min<uint32_t>(nf, cb::kMaxBuildBatch));
+#ifdef CB_EXPERIMENTS
+  static const uint32_t batch_env = [] {  // filters per launch pair (tuning)
+    const char* v = getenv("CB_BUILD_BATCH");
+    const int b = v && *v ? atoi(v) : 0;
+    return b >= 1 && b <= (int)cb::kMaxBuildBatch ? (uint32_t)b : cb::kMaxBuildBatch;
+  }();
+  const uint32_t kBatch = batch_env;
+#else
+  const uint32_t kBatch = cb::kMaxBuildBatch;
+#endif
+  const TilePlan p = cb::plan_build(f0->m, nmax, std::min<uint32_t>(nf, kBatch));
   for (uint32_t i = 0; i < nf; ++i)
     if (!covers(filters[i], p)) return fail(CB_EINVAL, "internal: build tile plan exceeds the filter allocation");
   bool all16 = key_len == 16;
   for (uint32_t i = 0; i < nf; ++i) all16 = all16 && !((uintptr_t)dkeys[i] & 15);
   const int keyk = all16 ? cb::KEY_FIXED16 : cb::KEY_FIXED;
-  for (uint32_t b0 = 0; b0 < nf; b0 += cb::kMaxBuildBatch) {
-    const uint32_t nb = std::min<uint32_t>(cb::kMaxBuildBatch, nf - b0);
+  for (uint32_t b0 = 0; b0 < nf; b0 += kBatch) {
+    const uint32_t nb = std::min<uint32_t>(kBatch, nf - b0);
     cb::BuildBatch bb{};
     for (uint32_t j = 0; j < nb; ++j) {
       cb_filter* f = filters[b0 + j];

@@ -11,3 +11,5 @@ python tools/bench_brief.py gpurun_out/bench_r04a.json || true
 PROF_OUT=gpurun_out/prof_c4 bash tools/profile_round.sh --workload c4 > gpurun_out/profile_c4.log 2>&1 || { tail -20 gpurun_out/profile_c4.log; exit 1; }
 python tools/pmc_summary.py gpurun_out/prof_c4 --json gpurun_out/pmc_c4.json > /dev/null
 tail -12 gpurun_out/profile_c4.log
+timeout -k 10 400 python tools/c4_sweep.py 60 > gpurun_out/c4_sweep.jsonl 2> gpurun_out/c4_sweep.err || { tail -5 gpurun_out/c4_sweep.err; exit 1; }
+cat gpurun_out/c4_sweep.jsonl | cut -c1-220
