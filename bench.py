@@ -776,6 +776,13 @@ def main():
     for _ in range(args.warmup):
         build_step()
     bel = timed(build_step, LK, lanes=b_streams)
+    b_region_us = region["ms"] * 1e3 / region["k"]
+    # the same build on ONE lane (one flush at a time, as a real flush runs):
+    # each step waits for the previous one on the stream
+    BP_saved, BP = BP, 1
+    timed(build_step, LK, lanes=b_streams[:1])
+    b_one_us = region["ms"] * 1e3 / region["k"]
+    BP = BP_saved
     bprof = kernel_ms(["k_build_part", "k_build_tile", "k_insert_direct"], build_step, LK)
     bcold = None
     if not args.no_cold:
@@ -792,13 +799,20 @@ def main():
         assert all(np.array_equal(f.bools(), o.bools()) for f in bfs), "C2 build differs from the oracle"
         del o
     b_alg = 16 * args.build_keys + args.build_m_bits / 8
+    frac = lambda us: round(b_alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
     build = {"metric": "build keys/s (C2: 1M 16-B keys -> one 16 MiB filter, m=2^27)",
              "value": round(args.build_keys * world / (bel / LK), 1), "unit": "keys/s",
              "ms_per_step": round(bel / LK * 1e3, 4), "steps": LK, "path": int(L.cb_last_path()),
              "kernels": {k: round(v["avg_us"], 2) for k, v in bprof.items()},
              "algorithmic_bytes": int(b_alg),
              "step_effective_GBps": round(b_alg / (bel / LK) / 1e9, 1),
-             "pipeline_lanes": BP, "cold": bcold}
+             "pipeline_lanes": BP, "cold": bcold,
+             "region_us_per_step": round(b_region_us, 2), "frac": frac(b_region_us),
+             "one_lane": {"us_per_build": round(b_one_us, 2), "frac": frac(b_one_us),
+                          "note": "one build at a time on one stream (HIP events / K): the latency a flush pays"}}
+    if bcold:
+        bcold["frac"] = frac(bcold["ms_per_step"] * 1e3)
+        bcold["clean_caches"]["frac"] = frac(bcold["clean_caches"]["ms_per_step"] * 1e3)
 
     # ---- PCIe-inclusive end-to-end probe (pinned host keys -> host hits)
     e2e = None

@@ -367,24 +367,32 @@ __global__ __launch_bounds__(kBuildNT) void k_build_tile(BuildBatch bb, uint32_t
         s1 = row[1];
       }
     }
-    uint32_t o[G];
+    // Runs of up to two waves' length (C4's 64 tiles per filter give ~128
+    // entries per run): both rounds of loads for all G runs go out before any
+    // OR, so a wave keeps up to 2G loads in flight instead of waiting on each
+    // run's second half in turn.
+    uint32_t o[G], o2[G];
+    const bool two = __ballot(lane < (uint32_t)G && s1 - s0 > 64u) != 0;  // (uniform)
 #pragma unroll
     for (int u = 0; u < G; ++u) {
       const uint32_t st = __shfl(s0, u, 64), len = __shfl(s1, u, 64) - st;
       const uint32_t b = w + NW * (g0 + u);
-      o[u] = 0xFFFFFFFFu;
+      o[u] = o2[u] = 0xFFFFFFFFu;
       if (lane < len) o[u] = ent[(size_t)b * estride + st + lane];
+      if (two && 64 + lane < len) o2[u] = ent[(size_t)b * estride + st + 64 + lane];
     }
 #pragma unroll
-    for (int u = 0; u < G; ++u)
+    for (int u = 0; u < G; ++u) {
       if (o[u] != 0xFFFFFFFFu) atomicOr(&tile[o[u] >> 5], 1u << (o[u] & 31));
-    // runs longer than one wave (skewed inputs, few partition blocks)
-    if (__ballot(lane < (uint32_t)G && s1 - s0 > 64u)) {
+      if (o2[u] != 0xFFFFFFFFu) atomicOr(&tile[o2[u] >> 5], 1u << (o2[u] & 31));
+    }
+    // runs longer than two waves (skewed inputs, few partition blocks)
+    if (__ballot(lane < (uint32_t)G && s1 - s0 > 128u)) {
 #pragma unroll 1
       for (int u = 0; u < G; ++u) {
         const uint32_t st = __shfl(s0, u, 64), len = __shfl(s1, u, 64) - st;
         const uint32_t* run = ent + (size_t)(w + NW * (g0 + u)) * estride + st;
-        for (uint32_t i = 64 + lane; i < len; i += 64) {
+        for (uint32_t i = 128 + lane; i < len; i += 64) {
           const uint32_t v = run[i];
           atomicOr(&tile[v >> 5], 1u << (v & 31));
         }
