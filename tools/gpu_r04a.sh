@@ -13,3 +13,5 @@ python tools/pmc_summary.py gpurun_out/prof_c4 --json gpurun_out/pmc_c4.json > /
 tail -12 gpurun_out/profile_c4.log
 timeout -k 10 400 python tools/c4_sweep.py 60 > gpurun_out/c4_sweep.jsonl 2> gpurun_out/c4_sweep.err || { tail -5 gpurun_out/c4_sweep.err; exit 1; }
 cat gpurun_out/c4_sweep.jsonl | cut -c1-220
+timeout -k 10 300 python tools/xcd_order.py 200 > gpurun_out/xcd_order.json 2> gpurun_out/xcd_order.err || { tail -5 gpurun_out/xcd_order.err; exit 1; }
+cat gpurun_out/xcd_order.json
