@@ -170,6 +170,7 @@ struct cb_table {
   uint64_t* pfx = nullptr;      // per-line 8-byte key prefix
   uint64_t* fence = nullptr;    // the fence levels above pfx (sstable.hpp)
   uint32_t* dir = nullptr;      // the byte-rank directory (sstable.hpp; nullptr under 16 lines)
+  uint32_t* llen = nullptr;     // per-line length without the '\n' (cb_table_lines; in the index allocation)
   cb::DirMap* dmap = nullptr;   // its map (device, in the index allocation)
   bool fast = false;  // well-formed: TAB on every line, keys strictly increasing
   bool has_zone = false;   // made by cb_sstable_create with n >= 1

@@ -217,11 +217,11 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
   return CB_OK;
 }
 
-// The index of nl lines is one allocation: rec | pfx | fence | dir | dmap.
+// The index of nl lines is one allocation: rec | pfx | fence | dir | dmap | llen.
 size_t dir_bytes(uint64_t nl) { return cb::dir_words(nl) ? ((cb::dir_words(nl) * 4 + 15) & ~15ull) : 0; }
 size_t index_bytes(uint64_t nl) {
   return nl * sizeof(cb::LineRec) + nl * 8 + cb::fence_words(nl) * 8 + 8 + dir_bytes(nl) +
-         (cb::dir_words(nl) ? sizeof(cb::DirMap) : 0);
+         (cb::dir_words(nl) ? sizeof(cb::DirMap) : 0) + nl * 4;
 }
 void carve_index(cb_table* t) {
   const uint64_t nl = t->nlines;
@@ -231,6 +231,7 @@ void carve_index(cb_table* t) {
   uint8_t* d = (uint8_t*)(((uintptr_t)(t->fence + cb::fence_words(nl)) + 15) & ~(uintptr_t)15);
   t->dir = cb::dir_words(nl) ? (uint32_t*)d : nullptr;
   t->dmap = nullptr;  // set once the directory is written (make_dirmap needs every prefix)
+  t->llen = (uint32_t*)(d + (t->dir ? dir_bytes(nl) + sizeof(cb::DirMap) : 0));
 }
 cb::DirMap* dmap_slot(const cb_table* t) {
   return t->dir ? (cb::DirMap*)((uint8_t*)t->dir + dir_bytes(t->nlines)) : nullptr;
@@ -273,9 +274,9 @@ int index_table(cb_table* t, hipStream_t s) {
   const uint32_t one = 1;
   HIP_TRY(hipMemcpyAsync(err + 1, &one, 4, hipMemcpyHostToDevice, s));
   HIP_TRY(cb::launch_line_emit(t->data, len, base, start, end, s));
-  HIP_TRY(cb::launch_line_finish(t->data, len, nl, start, end, t->rec, err, s));
+  HIP_TRY(cb::launch_line_finish(t->data, len, nl, start, end, t->rec, t->llen, err, s));
   // prefix + fence index, value validity and the well-formed check (sstable.hpp)
-  HIP_TRY(cb::launch_line_keys(t->data, nl, t->rec, t->pfx, t->fence, err + 1, s));
+  HIP_TRY(cb::launch_line_keys(t->data, nl, t->rec, t->llen, t->pfx, t->fence, err + 1, s));
   // the byte values of every prefix position (the directory's map)
   uint64_t* dmask = (uint64_t*)(err + 4);
   if (t->dir) {
@@ -364,7 +365,7 @@ int enqueue_format(cb_table* t, Workspace& ws, const TablePending& p, cb::Create
   uint64_t* tsum = (uint64_t*)ws.f_tsum.p;
   HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
   HIP_TRY(cb::launch_format((const cb::SortKey*)ws.f_sk2.p, p.dk, p.dko, p.dv, p.dvo, tsum, n, t->data, t->rec,
-                            t->pfx, t->fence, dr, p.cap_bytes, s, (const ulonglong2*)ws.f_vsp.p, t->dir,
+                            t->pfx, t->fence, t->llen, dr, p.cap_bytes, s, (const ulonglong2*)ws.f_vsp.p, t->dir,
                             t->dir ? dmap_slot(t) : nullptr));
   return CB_OK;
 }
@@ -577,6 +578,7 @@ int finalize_locked(cb_table* t) {
     pool_release(t->device, t->rec, t->rec_cap);
     t->rec = nullptr;
     t->pfx = t->fence = nullptr;
+    t->llen = nullptr;
     t->dir = nullptr;
     t->dmap = nullptr;
     t->nlines = 0;
@@ -848,8 +850,7 @@ int cb_table_lines(const cb_table* t, uint64_t* start, uint32_t* key_len, uint32
     HIP_TRY(hipMemcpy2D(start, 8, r + offsetof(cb::LineRec, start), pitch, 8, t->nlines, hipMemcpyDefault));
   if (key_len)
     HIP_TRY(hipMemcpy2D(key_len, 4, r + offsetof(cb::LineRec, klen), pitch, 4, t->nlines, hipMemcpyDefault));
-  if (line_len)
-    HIP_TRY(hipMemcpy2D(line_len, 4, r + offsetof(cb::LineRec, llen), pitch, 4, t->nlines, hipMemcpyDefault));
+  if (line_len) HIP_TRY(hipMemcpy(line_len, t->llen, t->nlines * 4, hipMemcpyDefault));
   return CB_OK;
 }
 

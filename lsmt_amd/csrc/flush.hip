@@ -264,6 +264,7 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
                                                 const uint64_t* __restrict__ tsum, uint64_t n,
                                                 uint8_t* __restrict__ out, LineRec* __restrict__ rec,
                                                 uint64_t* __restrict__ pfx, uint64_t* __restrict__ fence,
+                                                uint32_t* __restrict__ llen_out,
                                                 CreateResult* r, const ulonglong2* __restrict__ vsp,
                                                 uint32_t* __restrict__ dir, DirMap* dmap_out) {
   __shared__ uint32_t stage32[LDSB / 4];
@@ -325,19 +326,19 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
     lr.start = o;
     lr.pfx2 = w1;  // bytes 8..15 (zero when kl <= 8)
     lr.klen = (uint32_t)kl;
-    lr.llen = (uint32_t)llen;
     lr.vdl = (uint32_t)vl;  // canonical STANDARD encoding: always decodes
-    lr.pad = 0;
+    lr.pfx0 = w0;
     // the index and the file are written once and read by later launches
     // (the read path): non-temporal, no L2 lines to write back at the
     // kernel's end (k_format 52.3 -> 49.2 us after the bin sort)
     typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
     const u32x4_t ra = {(uint32_t)lr.start, (uint32_t)(lr.start >> 32), (uint32_t)lr.pfx2,
                         (uint32_t)(lr.pfx2 >> 32)};
-    const u32x4_t rb = {lr.klen, lr.llen, lr.vdl, 0u};
+    const u32x4_t rb = {lr.klen, lr.vdl, (uint32_t)lr.pfx0, (uint32_t)(lr.pfx0 >> 32)};
     __builtin_nontemporal_store(ra, reinterpret_cast<u32x4_t*>(rec + p));
     __builtin_nontemporal_store(rb, reinterpret_cast<u32x4_t*>(rec + p) + 1);
     __builtin_nontemporal_store(w0, pfx + p);
+    __builtin_nontemporal_store((uint32_t)llen, llen_out + p);
     fence_put(fence, n, p, w0);
     if (p > 0) not_inc = key_cmp(kb, ko, pi, pkl, pw0, pw1, i, kl, w0, w1) >= 0;
   }
@@ -441,19 +442,19 @@ hipError_t launch_line_sums(const SortKey* order, const uint64_t* ko, const uint
 
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
-                         uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
-                         uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp, uint32_t* dir,
-                         DirMap* dmap_out) {
+                         uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, uint32_t* llen,
+                         CreateResult* r, uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp,
+                         uint32_t* dir, DirMap* dmap_out) {
   if (!n) return hipSuccess;
   if (dir && !dmap_out) return hipErrorInvalidValue;
   ProfScope ps("k_format", s);
   const dim3 g(blocks_for(n, kNT));
   if (bytes_bound / n * kNT * 5 / 4 <= kFormatLdsSmall)
     hipLaunchKernelGGL(k_format<kFormatLdsSmall>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
-                       rec, pfx, fence, r, order ? vsp : nullptr, dir, dmap_out);
+                       rec, pfx, fence, llen, r, order ? vsp : nullptr, dir, dmap_out);
   else
     hipLaunchKernelGGL(k_format<kFormatLdsLarge>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
-                       rec, pfx, fence, r, order ? vsp : nullptr, dir, dmap_out);
+                       rec, pfx, fence, llen, r, order ? vsp : nullptr, dir, dmap_out);
   return hipGetLastError();
 }
 

@@ -138,8 +138,8 @@ hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, ui
 // from the lines' prefixes (what launch_table_dir would build).
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
-                         uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, CreateResult* r,
-                         uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp = nullptr,
+                         uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, uint32_t* llen,
+                         CreateResult* r, uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp = nullptr,
                          uint32_t* dir = nullptr, DirMap* dmap_out = nullptr);
 
 }  // namespace cb

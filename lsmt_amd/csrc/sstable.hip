@@ -169,7 +169,8 @@ __global__ __launch_bounds__(kNT) void k_line_finish(const uint8_t* __restrict__
                                                      uint64_t nlines,
                                                      const uint64_t* __restrict__ start,
                                                      const uint64_t* __restrict__ end,
-                                                     LineRec* __restrict__ rec, uint32_t* err) {
+                                                     LineRec* __restrict__ rec, uint32_t* __restrict__ llen,
+                                                     uint32_t* err) {
   const uint64_t l = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   if (l >= nlines) return;
   const uint64_t s = start[l];
@@ -195,14 +196,14 @@ __global__ __launch_bounds__(kNT) void k_line_finish(const uint8_t* __restrict__
   r.start = s;
   r.pfx2 = 0;
   r.klen = k;
-  r.llen = (uint32_t)n;
   r.vdl = kBadValue;
-  r.pad = 0;
+  r.pfx0 = 0;
   rec[l] = r;
+  llen[l] = (uint32_t)n;
 }
 
 __global__ __launch_bounds__(kNT) void k_line_keys(const uint8_t* __restrict__ data, uint64_t nlines,
-                                                   LineRec* __restrict__ rec,
+                                                   LineRec* __restrict__ rec, const uint32_t* __restrict__ llen,
                                                    uint64_t* __restrict__ pfx,
                                                    uint64_t* __restrict__ fence, uint32_t* ok) {
   const uint64_t l = (uint64_t)blockIdx.x * kNT + threadIdx.x;
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(kNT) void k_line_keys(const uint8_t* __restrict__ d
   if (live && good) {
     v = ld8_be(p, r.klen < 8 ? r.klen : 8);
     r.pfx2 = r.klen > 8 ? ld8_be(p + 8, r.klen - 8 < 8 ? r.klen - 8 : 8) : 0;
-    const int64_t d = b64_len(p + r.klen + 1, r.llen - r.klen - 1);
+    const int64_t d = b64_len(p + r.klen + 1, llen[l] - r.klen - 1);
     r.vdl = d < 0 ? kBadValue : (uint32_t)d;
   }
   if (live) {
@@ -224,9 +225,11 @@ __global__ __launch_bounds__(kNT) void k_line_keys(const uint8_t* __restrict__ d
       const LineRec q = rec[l - 1];  // start/klen only: written by k_line_finish
       good = q.klen != kNoSep && bytes_cmp(data + q.start, q.klen, p, r.klen) < 0;
     }
-    // pfx2 and vdl go to separate words so the neighbour read above stays race-free
+    // pfx2, vdl and pfx0 go to their own words so the neighbour read above
+    // (start / klen) stays race-free
     rec[l].pfx2 = r.pfx2;
     rec[l].vdl = r.vdl;
+    rec[l].pfx0 = v;
   }
   // one atomic per block, none once the flag is down
   if (__syncthreads_or(!good) && threadIdx.x == 0 && *(volatile uint32_t*)ok) atomicAnd(ok, 0u);
@@ -371,7 +374,7 @@ typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(1))) u64x2* g64x2;
 static_assert(sizeof(LineRec) == 32 && offsetof(LineRec, pfx2) == 8 && offsetof(LineRec, klen) == 16 &&
-                  offsetof(LineRec, llen) == 20 && offsetof(LineRec, vdl) == 24,
+                  offsetof(LineRec, vdl) == 20 && offsetof(LineRec, pfx0) == 24,
               "grec reads LineRec as two 16-byte words");
 __device__ __forceinline__ LineRec grec(const LineRec* r, uint64_t i) {
   const g64x2 p = (g64x2)(r + i);
@@ -380,9 +383,8 @@ __device__ __forceinline__ LineRec grec(const LineRec* r, uint64_t i) {
   o.start = lo.x;
   o.pfx2 = lo.y;
   o.klen = (uint32_t)hi.x;
-  o.llen = (uint32_t)(hi.x >> 32);
-  o.vdl = (uint32_t)hi.y;
-  o.pad = (uint32_t)(hi.y >> 32);
+  o.vdl = (uint32_t)(hi.x >> 32);
+  o.pfx0 = hi.y;
   return o;
 }
 __device__ __forceinline__ uint64_t g64(const uint64_t* p, uint64_t i) {
@@ -421,12 +423,11 @@ __device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t* a, uint64_t 
   return lo;
 }
 
-// Line l's key against the query, in a well-formed file: prefix first, then
-// the record (r receives it when the prefixes are equal).
+// Line l's key against the query, in a well-formed file: its record (which
+// holds the prefix) in one load, r receives it.
 __device__ __forceinline__ int line_vs_query(const TableView& t, uint64_t l, const Query& q, LineRec& r) {
-  const uint64_t p = g64(t.pfx, l);
-  if (p != q.w0) return p < q.w0 ? -1 : 1;
   r = grec(t.rec, l);
+  if (r.pfx0 != q.w0) return r.pfx0 < q.w0 ? -1 : 1;
   return rec_cmp(t, r, q);
 }
 
@@ -475,11 +476,10 @@ __device__ __forceinline__ int64_t resolve_rec(const TableView& t, const Query& 
 }
 
 __device__ __forceinline__ int64_t resolve_from(const TableView& t, const Query& q, uint64_t b, LineRec& hit) {
-  // line b's prefix and record in one round trip (the record is needed
+  // line b's record holds its prefix: one load (the record is needed
   // whenever the prefix matches, i.e. for every key that is present)
-  const uint64_t p0 = g64(t.pfx, b);
   const LineRec r = grec(t.rec, b);
-  if (p0 != q.w0) return -1;  // p0 > q.w0: b is the prefix's lower bound
+  if (r.pfx0 != q.w0) return -1;  // pfx0 > q.w0: b is the prefix's lower bound
   return resolve_rec(t, q, b, r, hit);
 }
 
@@ -496,7 +496,8 @@ __device__ __forceinline__ void level_down(const TableView& t, uint32_t j, uint6
   hi = (i << kFanBits) < cnt ? (i << kFanBits) : cnt;
 }
 
-constexpr uint32_t kWin = 8;  // buckets of up to this many lines: one round of prefix loads
+constexpr uint32_t kWin = 8;     // buckets of up to this many lines: one round of prefix loads
+constexpr uint32_t kRecWin = 2;  // ... of up to this many: the records alone (32 B each, prefix inside)
 
 // Where x's descent starts: level j and the run [lo, hi) of at most 16
 // entries holding its lower bound (returns false), or true when x is absent
@@ -543,11 +544,30 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
   uint64_t lo, hi;
   // an empty bucket: absent
   if (dir_start(t, dm, q.w0, j, lo, hi)) return -1;
+  if (j == 0 && hi - lo <= kRecWin) {
+    // a bucket of at most kRecWin lines: its records hold the prefixes, so
+    // the records are all that is read (one round of independent loads: one
+    // or two 128-B lines where the prefixes and then the matching record
+    // took two); the matching one is already in registers
+    LineRec rr[kRecWin];
+#pragma unroll
+    for (uint32_t k = 0; k < kRecWin; ++k)
+      if (lo + k < hi) rr[k] = grec(t.rec, lo + k);
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kRecWin; ++k) c += (lo + k < hi && rr[k].pfx0 < q.w0) ? 1u : 0u;
+    if (lo + c == hi) return -1;  // every line below the key: the next one is in a larger bucket
+    LineRec r = rr[0];
+#pragma unroll
+    for (uint32_t k = 1; k < kRecWin; ++k)
+      if (k == c) r = rr[k];
+    if (r.pfx0 != q.w0) return -1;
+    return resolve_rec(t, q, lo + c, r, hit);
+  }
   if (j == 0 && hi - lo <= kWin) {
-    // [lo, hi) is the key's whole bucket (or the whole table): its prefixes
-    // in one round of independent loads, with the record when it is one line
-    // (loading the first two records of every bucket with them measured
-    // within noise: 85-87 vs 88 us per 1M keys)
+    // a larger bucket (or the whole table): its prefixes from the dense
+    // prefix array in one round of independent loads (64 B for 8 lines),
+    // then the matching record
     uint64_t v[kWin];
     // in pairs: two neighbouring prefixes as one 16-byte load where both
     // are in the bucket (one L2 request per pair, not per prefix)
@@ -563,8 +583,6 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
         v[k + 1] = ~0ull;
       }
     }
-    LineRec r1;
-    if (hi - lo == 1) r1 = grec(t.rec, lo);
     uint32_t c = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kWin; ++k) c += (lo + k < hi && v[k] < q.w0) ? 1u : 0u;
@@ -574,7 +592,7 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
 #pragma unroll
     for (uint32_t k = 1; k < kWin; ++k) p0 = k == c ? v[k] : p0;
     if (p0 != q.w0) return -1;
-    return resolve_rec(t, q, lo + c, hi - lo == 1 ? r1 : grec(t.rec, lo + c), hit);
+    return resolve_rec(t, q, lo + c, grec(t.rec, lo + c), hit);
   }
   for (;; --j) {
     const uint64_t i = lower_bound_u64(level_array(t, j), lo, hi, q.w0);
@@ -1045,20 +1063,20 @@ hipError_t launch_line_emit(const uint8_t* data, uint64_t len, const uint64_t* b
 
 hipError_t launch_line_finish(const uint8_t* data, uint64_t len, uint64_t nlines,
                               const uint64_t* start, const uint64_t* end, LineRec* rec,
-                              uint32_t* err, hipStream_t s) {
+                              uint32_t* llen, uint32_t* err, hipStream_t s) {
   if (!nlines) return hipSuccess;
   ProfScope ps("k_line_finish", s);
   hipLaunchKernelGGL(k_line_finish, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, data, len,
-                     nlines, start, end, rec, err);
+                     nlines, start, end, rec, llen, err);
   return hipGetLastError();
 }
 
-hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, LineRec* rec, uint64_t* pfx,
-                            uint64_t* fence, uint32_t* ok, hipStream_t s) {
+hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, LineRec* rec, const uint32_t* llen,
+                            uint64_t* pfx, uint64_t* fence, uint32_t* ok, hipStream_t s) {
   if (!nlines) return hipSuccess;
   ProfScope ps("k_line_keys", s);
   hipLaunchKernelGGL(k_line_keys, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, data, nlines,
-                     rec, pfx, fence, ok);
+                     rec, llen, pfx, fence, ok);
   return hipGetLastError();
 }
 

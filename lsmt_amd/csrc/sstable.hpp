@@ -267,15 +267,18 @@ constexpr uint32_t kBadValue = 0xFFFFFFFFu;  // value that STANDARD.decode rejec
 // Per-line index record (32 B, one load). vdl is computed once at index
 // time: the decoded length of the line's value, or kBadValue when base64
 // 0.21.7 STANDARD.decode would fail (or the line has no TAB) — so the read
-// path never re-validates a value. pfx2 lets keys of <= 16 bytes be
-// compared from the index alone.
+// path never re-validates a value. pfx0 / pfx2 (the key's first 16 bytes)
+// let keys of <= 16 bytes be compared from the record alone, so a search
+// that lands on a directory bucket reads the bucket's records and nothing
+// else (round 4: the prefix array is no longer read next to the record).
+// The line's length, needed only while indexing and by cb_table_lines, is
+// kept apart (llen[], 4 B per line).
 struct alignas(16) LineRec {
   uint64_t start;  // line start offset in the file
   uint64_t pfx2;   // key bytes 8..15, big-endian, zero-padded
   uint32_t klen;   // bytes before the first TAB, or kNoSep
-  uint32_t llen;   // line length (without the '\n')
   uint32_t vdl;    // decoded value length, or kBadValue
-  uint32_t pad;
+  uint64_t pfx0;   // key bytes 0..7, big-endian, zero-padded (= pfx[line])
 };
 
 // One data file and its line index. When the file is well-formed — every
@@ -310,11 +313,11 @@ hipError_t launch_line_emit(const uint8_t* data, uint64_t len, const uint64_t* b
 // rec[l].start/klen/llen; *err |= 1 if a line is 4 GiB or longer
 hipError_t launch_line_finish(const uint8_t* data, uint64_t len, uint64_t nlines,
                               const uint64_t* start, const uint64_t* end, LineRec* rec,
-                              uint32_t* err, hipStream_t s);
-// pfx, rec[l].pfx2 / vdl, fence[j] = pfx[64 j], and the well-formed check:
-// *ok &= (every line has a TAB and key[l-1] < key[l]).
-hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, LineRec* rec, uint64_t* pfx,
-                            uint64_t* fence, uint32_t* ok, hipStream_t s);
+                              uint32_t* llen, uint32_t* err, hipStream_t s);
+// pfx, rec[l].pfx0 / pfx2 / vdl, fence[j] = pfx[64 j], and the well-formed
+// check: *ok &= (every line has a TAB and key[l-1] < key[l]).
+hipError_t launch_line_keys(const uint8_t* data, uint64_t nlines, LineRec* rec, const uint32_t* llen,
+                            uint64_t* pfx, uint64_t* fence, uint32_t* ok, hipStream_t s);
 
 // dir[0 .. dm.nbuckets] of a table whose pfx is sorted, one lane per line
 // (dir_fill; built for every table, used only when the table is
