@@ -322,13 +322,13 @@ __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp,
 // loads back to back (lane i = entry i): two dependent memory round trips per
 // group and no LDS run table or barrier before the ORs.
 // pol: the store policy bits (build_stores(): bit 1 non-temporal write-back).
-template <int G>
-__global__ __launch_bounds__(kBuildNT) void k_build_tile(BuildBatch bb, uint32_t tb, uint32_t T,
+template <int G, int R, uint32_t NT = kBuildNT>
+__global__ __launch_bounds__(NT) void k_build_tile(BuildBatch bb, uint32_t tb, uint32_t T,
                                                          const uint32_t* __restrict__ seg_all,
                                                          uint32_t nblk,
                                                          const uint32_t* __restrict__ ent_all,
                                                          uint32_t estride, uint32_t pol) {
-  constexpr uint32_t NT = kBuildNT, NW = NT / 64;
+  constexpr uint32_t NW = NT / 64;
   static_assert(G <= 64, "one lane per run bound");
   uint32_t* __restrict__ words = bb.words[blockIdx.y];
   const bool fresh = (bb.fresh >> blockIdx.y) & 1u;
@@ -367,32 +367,34 @@ __global__ __launch_bounds__(kBuildNT) void k_build_tile(BuildBatch bb, uint32_t
         s1 = row[1];
       }
     }
-    // Runs of up to two waves' length (C4's 64 tiles per filter give ~128
-    // entries per run): both rounds of loads for all G runs go out before any
-    // OR, so a wave keeps up to 2G loads in flight instead of waiting on each
-    // run's second half in turn.
-    uint32_t o[G], o2[G];
-    const bool two = __ballot(lane < (uint32_t)G && s1 - s0 > 64u) != 0;  // (uniform)
+    // R rounds of run loads (lane i = entry i + 64 r): every load of the G
+    // runs goes out before any OR. R = 2 for long runs (C4's 64 tiles per
+    // filter give ~128 entries per run) with G = 8, so a lane holds G * R =
+    // 16 entries either way (62 VGPRs, 8 waves per SIMD: two 16-wave tiles per
+    // CU; 32 entries per lane took 80 VGPRs and one tile per CU)
+    uint32_t o[R][G];
 #pragma unroll
     for (int u = 0; u < G; ++u) {
       const uint32_t st = __shfl(s0, u, 64), len = __shfl(s1, u, 64) - st;
       const uint32_t b = w + NW * (g0 + u);
-      o[u] = o2[u] = 0xFFFFFFFFu;
-      if (lane < len) o[u] = ent[(size_t)b * estride + st + lane];
-      if (two && 64 + lane < len) o2[u] = ent[(size_t)b * estride + st + 64 + lane];
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        o[q][u] = 0xFFFFFFFFu;
+        if (64 * q + lane < len) o[q][u] = ent[(size_t)b * estride + st + 64 * q + lane];
+      }
     }
 #pragma unroll
-    for (int u = 0; u < G; ++u) {
-      if (o[u] != 0xFFFFFFFFu) atomicOr(&tile[o[u] >> 5], 1u << (o[u] & 31));
-      if (o2[u] != 0xFFFFFFFFu) atomicOr(&tile[o2[u] >> 5], 1u << (o2[u] & 31));
-    }
-    // runs longer than two waves (skewed inputs, few partition blocks)
-    if (__ballot(lane < (uint32_t)G && s1 - s0 > 128u)) {
+    for (int u = 0; u < G; ++u)
+#pragma unroll
+      for (int q = 0; q < R; ++q)
+        if (o[q][u] != 0xFFFFFFFFu) atomicOr(&tile[o[q][u] >> 5], 1u << (o[q][u] & 31));
+    // runs longer than R waves (skewed inputs, few partition blocks)
+    if (__ballot(lane < (uint32_t)G && s1 - s0 > 64u * R)) {
 #pragma unroll 1
       for (int u = 0; u < G; ++u) {
         const uint32_t st = __shfl(s0, u, 64), len = __shfl(s1, u, 64) - st;
         const uint32_t* run = ent + (size_t)(w + NW * (g0 + u)) * estride + st;
-        for (uint32_t i = 128 + lane; i < len; i += 64) {
+        for (uint32_t i = 64 * R + lane; i < len; i += 64) {
           const uint32_t v = run[i];
           atomicOr(&tile[v >> 5], 1u << (v & 31));
         }
@@ -911,10 +913,27 @@ hipError_t launch_build_batch(int keyk, int mode, const BuildBatch& bb, uint32_t
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t lds2 = (size_t)(1u << (p.tb - 5)) * 4;
-  allow_lds(k_build_tile<16>, lds2);
   ProfScope ps("k_build_tile", s);
-  hipLaunchKernelGGL(k_build_tile<16>, dim3(p.T, nb), dim3(kBuildNT), lds2, s, bb, p.tb, p.T, seg,
-                     p.nblk, ent, 2 * p.C, build_stores());
+  // entries per (partition block, tile): 2 C / T on average (tiles of one
+  // filter); two rounds of run loads once that passes ~3/4 of a wave
+#ifdef CB_EXPERIMENTS
+  static const int tile_nt = env_int("CB_BUILD_TILE_NT", 1024);  // 512: half-size tile workgroups
+  if (tile_nt == 512) {
+    allow_lds(k_build_tile<8, 2, 512>, lds2);
+    hipLaunchKernelGGL((k_build_tile<8, 2, 512>), dim3(p.T, nb), dim3(512), lds2, s, bb, p.tb, p.T, seg, p.nblk,
+                       ent, 2 * p.C, build_stores());
+    return hipGetLastError();
+  }
+#endif
+  if (2ull * p.C > 48ull * p.T) {
+    allow_lds(k_build_tile<8, 2>, lds2);
+    hipLaunchKernelGGL((k_build_tile<8, 2>), dim3(p.T, nb), dim3(kBuildNT), lds2, s, bb, p.tb, p.T, seg, p.nblk,
+                       ent, 2 * p.C, build_stores());
+  } else {
+    allow_lds(k_build_tile<16, 1>, lds2);
+    hipLaunchKernelGGL((k_build_tile<16, 1>), dim3(p.T, nb), dim3(kBuildNT), lds2, s, bb, p.tb, p.T, seg,
+                       p.nblk, ent, 2 * p.C, build_stores());
+  }
   return hipGetLastError();
 }
 

@@ -9,9 +9,10 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 steps = sys.argv[1] if len(sys.argv) > 1 else "100"
-SETTINGS = [{}, {"CB_BUILD_BATCH": "16"}, {"CB_BUILD_BATCH": "8"}, {"CB_BUILD_BATCH": "4"},
-            {"CB_BUILD_TB": "18"}, {"CB_BUILD_KPT": "2"}, {"CB_BUILD_STORES": "2"}, {"CB_BUILD_STORES": "0"},
-            {"CB_BUILD_STORES": "3", "CB_BUILD_BATCH": "8"}]
+SETTINGS = [{}, {"CB_BUILD_TB": "18"}, {"CB_BUILD_TILE_NT": "512", "CB_BUILD_TB": "18"},
+            {"CB_BUILD_TILE_NT": "512", "CB_BUILD_TB": "17"}, {"CB_BUILD_TILE_NT": "512"}, {"CB_BUILD_BATCH": "8"}]
+if len(sys.argv) > 2:  # a JSON list of settings instead
+    SETTINGS = json.loads(sys.argv[2])
 for lanes in ("1", "3"):
     for env in SETTINGS:
         e = dict(os.environ, **env)
