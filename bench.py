@@ -701,11 +701,17 @@ def main():
             kbatch = lsmt_amd.KeyBatch(n=nf_e, data=kd, offsets=ko)
             vbatch = lsmt_amd.KeyBatch(n=nf_e, data=vd, offsets=ko)
             made = []
+            fl_no = [0]
 
-            def step_flush():
+            def step_flush(lanes_n=P):
                 # enqueue-only (cb_sstable_create_bounded): the table finalises
-                # on first use; tables are kept, as an LSM keeps its SSTables
-                made.append(lsmt_amd.sstable_create((kbatch, vbatch), m=1 << 26, device=local, stream=sh,
+                # on first use; tables are kept, as an LSM keeps its SSTables.
+                # Consecutive flushes alternate over the pipeline lanes (as
+                # the probe and read legs), each lane with its own stream and
+                # workspace
+                i = fl_no[0] % lanes_n
+                fl_no[0] += 1
+                made.append(lsmt_amd.sstable_create((kbatch, vbatch), m=1 << 26, device=local, stream=lane_sh[i],
                                                     wait=False))
 
             k_fl = max(3, LK // 4)
@@ -719,6 +725,11 @@ def main():
             fel = timed(step_flush, k_fl)
             for t, _, _ in made:
                 t.wait()  # finalised after the region (host reads of the results only)
+            made.clear()
+            # one flush at a time (one stream): the latency one flush pays
+            fel1 = timed(lambda: step_flush(1), k_fl, lanes=lane_streams[:1])
+            for t, _, _ in made:
+                t.wait()
             last = made[-1]
             made.clear()
             made.append(last)
@@ -731,7 +742,10 @@ def main():
             if label == "unsorted" and rank == 0 and world == 1 and not args.no_cpu:
                 flush_file = last[0].data()  # checked against the oracle below
             res[label] = {"entries_per_s": round(nf_e / (fel / k_fl), 1), "ms_per_flush": round(fel / k_fl * 1e3, 3),
-                          "flushes": k_fl, "form": "enqueue-only creates (tables finalised after the region)",
+                          "flushes": k_fl, "pipeline_lanes": P,
+                          "form": "enqueue-only creates (tables finalised after the region)",
+                          "one_lane": {"ms_per_flush": round(fel1 / k_fl * 1e3, 3),
+                                       "entries_per_s": round(nf_e / (fel1 / k_fl), 1)},
                           "file_bytes": out_bytes, "file_GBps": round(out_bytes / (fel / k_fl) / 1e9, 2),
                           "kernels_us": {k: round(v["avg_us"], 2) for k, v in fprof.items()}}
             del made, kd, vd, ko
