@@ -868,48 +868,75 @@ __global__ __launch_bounds__(kNT) void k_wide_get_many(const uint64_t* __restric
                                                        uint64_t* __restrict__ dlen, uint64_t* __restrict__ tsum) {
   const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   const bool live = k < n;
-  const ViewRegs vr = load_views(tv, nt);
   const Query q = make_query<KEYK>(ks, live ? k : 0);
   uint64_t pa = 0, pb = 0;
   if (live) key_positions<KEYK, MODE>(ks, k, mp, pa, pb);
+  const uint64_t* ra = set + pa * R;
+  const uint64_t* rb = set + pb * R;
+  const uint32_t kw[4] = {(uint32_t)(q.w0 >> 32), (uint32_t)q.w0, (uint32_t)(q.w1 >> 32), (uint32_t)q.w1};
+  // The block walks the groups together: each group's 64 views and DirMaps
+  // are staged in LDS once for the block (every search then reads its
+  // table's view and map from LDS, not 56 + 320 B from global memory per
+  // search), and the walk ends when no lane of the block is still looking.
   __shared__ TableView stv[64];
   __shared__ DirMap sdm[64];
-  store_views(vr, nt, stv);
-  stage_maps(stv, nt, sdm);
-  uint64_t d = 0;
-  if (live) {
-    const uint64_t* ra = set + pa * R;
-    const uint64_t* rb = set + pb * R;
-    const uint32_t kw[4] = {(uint32_t)(q.w0 >> 32), (uint32_t)q.w0, (uint32_t)(q.w1 >> 32), (uint32_t)q.w1};
-    int32_t w = -1;
-    uint64_t src = 0;
-    const uint32_t ng = (nt + 63) / 64;
-    for (uint32_t g = 0; g < ng; ++g) {
-      const WideGroup gd = groups[g];
-      const uint32_t t0 = 64 * g;
-      const uint64_t gmask = gd.gn >= 64 ? ~0ull : ((1ull << gd.gn) - 1);
-      uint64_t cand = 0;
-      if (gd.kind == 2) {  // scattered slots: one bit per table
-        for (uint32_t i = 0; i < gd.gn; ++i) {
-          const uint32_t s = slots[t0 + i];
-          if ((ra[s >> 6] >> (s & 63)) & 1ull) cand |= ((rb[s >> 6] >> (s & 63)) & 1ull) << i;
-        }
-      } else {
-        const uint64_t wa = wide_window(ra, R, gd.lo) & gmask;
-        cand = wa ? (wa & wide_window(rb, R, gd.lo)) : 0ull;
-        if (gd.kind == 1 && cand) cand = __builtin_bitreverse64(cand) >> (64 - gd.gn);  // bit gn-1-i -> i
-      }
-      if (z.any && cand) {
-        uint64_t c = cand;
-        while (c) {
-          const uint32_t i = (uint32_t)__builtin_ctzll(c);
-          c &= c - 1;
-          const uint32_t s = gd.kind == 2 ? slots[t0 + i] : gd.kind == 1 ? gd.lo + gd.gn - 1 - i : gd.lo + i;
-          if (!wide_zone_ok<KEYK>(z, s, kw, q.p, q.len)) cand &= ~(1ull << i);
-        }
-      }
-      if (resolve_group<false>(stv, tv, sdm, t0, cand, q, w, src, d)) break;
+  int32_t w = -1;
+  uint64_t src = 0, d = 0;
+  bool active = live;
+  const uint32_t ng = (nt + 63) / 64;
+  for (uint32_t g = 0; g < ng; ++g) {
+    if (!__syncthreads_or(active)) break;  // (also: the previous group's stage is consumed)
+    const uint32_t t0 = 64 * g, gn = nt - t0 < 64 ? nt - t0 : 64;
+    {
+      const uint32_t* vs = reinterpret_cast<const uint32_t*>(tv + t0);
+      uint32_t* vd = reinterpret_cast<uint32_t*>(stv);
+      for (uint32_t i = threadIdx.x; i < gn * kViewDw; i += kNT) vd[i] = vs[i];
     }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < gn * kMapWords; i += kNT) {
+      const uint32_t t = i / kMapWords, j = i - t * kMapWords;
+      const DirMap* gm = stv[t].dmap;
+      if (gm) reinterpret_cast<uint4*>(sdm + t)[j] = reinterpret_cast<const uint4*>(gm)[j];
+    }
+    __syncthreads();
+    if (!active) continue;
+    const WideGroup gd = groups[g];
+    const uint64_t gmask = gd.gn >= 64 ? ~0ull : ((1ull << gd.gn) - 1);
+    uint64_t cand = 0;
+    if (gd.kind == 2) {  // scattered slots: one bit per table
+      for (uint32_t i = 0; i < gd.gn; ++i) {
+        const uint32_t s = slots[t0 + i];
+        if ((ra[s >> 6] >> (s & 63)) & 1ull) cand |= ((rb[s >> 6] >> (s & 63)) & 1ull) << i;
+      }
+    } else {
+      const uint64_t wa = wide_window(ra, R, gd.lo) & gmask;
+      cand = wa ? (wa & wide_window(rb, R, gd.lo)) : 0ull;
+      if (gd.kind == 1 && cand) cand = __builtin_bitreverse64(cand) >> (64 - gd.gn);  // bit gn-1-i -> i
+    }
+    if (z.any && cand) {
+      uint64_t c = cand;
+      while (c) {
+        const uint32_t i = (uint32_t)__builtin_ctzll(c);
+        c &= c - 1;
+        const uint32_t s = gd.kind == 2 ? slots[t0 + i] : gd.kind == 1 ? gd.lo + gd.gn - 1 - i : gd.lo + i;
+        if (!wide_zone_ok<KEYK>(z, s, kw, q.p, q.len)) cand &= ~(1ull << i);
+      }
+    }
+    // the candidates newest first, the group's views and maps from LDS
+    while (cand) {
+      const uint32_t i = (uint32_t)__builtin_ctzll(cand);
+      cand &= cand - 1;
+      LineRec r;
+      if (search(stv[i], q, r, &sdm[i]) < 0) continue;  // Ok(None)
+      if (r.vdl == kBadValue) continue;                  // Err(..) is skipped by `if let Ok(Some(v))`
+      w = (int32_t)(t0 + i);
+      src = (uint64_t)(uintptr_t)(stv[i].data + r.start + r.klen + 1);
+      d = r.vdl;
+      active = false;
+      break;
+    }
+  }
+  if (live) {
     which[k] = w;
     vsrc[k] = src;
     dlen[k] = d;
