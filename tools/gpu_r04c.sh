@@ -11,3 +11,4 @@ python -c "import json;d=json.load(open('gpurun_out/bench_r04c.json'));print('C2
 timeout -k 10 400 python tools/c4_sweep.py 60 > gpurun_out/c4_sweep_c.jsonl 2> gpurun_out/c4_sweep_c.err || { tail -5 gpurun_out/c4_sweep_c.err; exit 1; }
 cut -c1-200 gpurun_out/c4_sweep_c.jsonl
 bash tools/gpu_r04b.sh
+bash tools/gpu_r04d.sh
