@@ -241,7 +241,12 @@ int new_comm(int rank, int world, int device, std::unique_ptr<cb_comm>* out) {
   // (hipStreamWaitEvent before the next collective): a device-scope release
   // is enough, so no system-scope fence (an L2 write-back per record, paid
   // in GPU time every step; round 3 measured the zone-read events' fence)
-  HIP_TRY(hipEventCreateWithFlags(&c->order, hipEventDisableTiming | hipEventDisableSystemFence));
+  unsigned order_flags = hipEventDisableTiming | hipEventDisableSystemFence;
+#ifdef CB_EXPERIMENTS
+  if (const char* e = getenv("CB_ORDER_FENCE"); e && e[0] == '1')  // A/B: the fenced event
+    order_flags = hipEventDisableTiming;
+#endif
+  HIP_TRY(hipEventCreateWithFlags(&c->order, order_flags));
   *out = std::move(c);
   return CB_OK;
 }
