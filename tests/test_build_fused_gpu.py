@@ -1,0 +1,90 @@
+"""The one-launch build (k_build_fused: partition blocks and tiles in one grid,
+handed off through a ticket / done counter pair per stream) against the
+oracle: many builds queued back to back on one stream with no host sync (the
+counter parity flips every launch), the same on four streams at once (each
+stream's own counters), and builds whose tile roles outnumber the partition
+blocks and the reverse. Reference: /root/reference/src/bloom.rs:40-44 via
+src/sstable.rs:62-65."""
+import numpy as np
+import pytest
+
+from lsmt_amd import workload
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+TILED = 2
+
+
+def _bits_equal(g, o):
+    return np.array_equal(g.bools(), o.bools())
+
+
+def _cases(seed, count):
+    rng = np.random.default_rng(seed)
+    ms = [1 << 20, 1 << 22, 100003 * 17, 1 << 27, (1 << 24) + 5]
+    out = []
+    for i in range(count):
+        m = ms[i % len(ms)]
+        n = int(rng.integers(3000, 300_000))
+        out.append((m, workload.key_range(1000 * seed + i, n)))
+    return out
+
+
+def test_fused_back_to_back_one_stream(gpu):
+    import torch
+    gpu.set_path(TILED)
+    try:
+        dev = torch.device("cuda", 0)
+        cases = _cases(1, 24)
+        filters = []
+        for m, keys in cases:
+            f = gpu.BloomFilter(m)
+            f.insert_batch(gpu.DeviceKeys(torch.from_numpy(keys).to(dev)))  # device keys: no host sync
+            filters.append(f)
+        torch.cuda.synchronize(dev)
+        for (m, keys), f in zip(cases, filters):
+            o = oracle.OracleFilter(m)
+            o.insert_fixed(keys)
+            assert _bits_equal(f, o), (m, len(keys))
+    finally:
+        gpu.set_path(0)
+
+
+def test_fused_four_streams(gpu):
+    import torch
+    gpu.set_path(TILED)
+    try:
+        dev = torch.device("cuda", 0)
+        streams = [torch.cuda.Stream(device=dev) for _ in range(4)]
+        cases = _cases(2, 24)
+        dk = [torch.from_numpy(k).to(dev) for _, k in cases]
+        torch.cuda.synchronize(dev)
+        filters = []
+        for i, (m, _) in enumerate(cases):
+            f = gpu.BloomFilter(m)
+            f.insert_batch(gpu.DeviceKeys(dk[i]), stream=streams[i % 4])
+            filters.append(f)
+        torch.cuda.synchronize(dev)
+        for (m, keys), f in zip(cases, filters):
+            o = oracle.OracleFilter(m)
+            o.insert_fixed(keys)
+            assert _bits_equal(f, o), (m, len(keys))
+    finally:
+        gpu.set_path(0)
+
+
+@pytest.mark.parametrize("m,n", [(1 << 27, 5000),       # 256 tiles, 2 partition blocks
+                                 (1 << 16, 1 << 20),    # few tiles, 256 blocks
+                                 (1 << 21, 1)])
+def test_fused_role_balance(gpu, m, n):
+    gpu.set_path(TILED)
+    try:
+        keys = workload.key_range(77, n)
+        g = gpu.BloomFilter(m)
+        g.insert_batch(keys)
+        g.insert_batch(keys[: max(1, n // 3)])  # again into the non-empty filter
+        o = oracle.OracleFilter(m)
+        o.insert_fixed(keys)
+        assert _bits_equal(g, o)
+    finally:
+        gpu.set_path(0)
