@@ -1,8 +1,7 @@
-"""The one-launch build (k_build_fused: partition blocks and tiles in one grid,
-handed off through a ticket / done counter pair per stream) against the
-oracle: many builds queued back to back on one stream with no host sync (the
-counter parity flips every launch), the same on four streams at once (each
-stream's own counters), and builds whose tile roles outnumber the partition
+"""Tiled builds against the oracle when many are in flight: builds queued
+back to back on one stream with no host sync (each reuses the stream's
+partition workspace), the same spread over four streams at once (each
+stream's own workspace), and plans with many more tiles than partition
 blocks and the reverse. Reference: /root/reference/src/bloom.rs:40-44 via
 src/sstable.rs:62-65."""
 import numpy as np
@@ -30,7 +29,7 @@ def _cases(seed, count):
     return out
 
 
-def test_fused_back_to_back_one_stream(gpu):
+def test_builds_back_to_back_one_stream(gpu):
     import torch
     gpu.set_path(TILED)
     try:
@@ -50,7 +49,7 @@ def test_fused_back_to_back_one_stream(gpu):
         gpu.set_path(0)
 
 
-def test_fused_four_streams(gpu):
+def test_builds_four_streams(gpu):
     import torch
     gpu.set_path(TILED)
     try:
@@ -76,7 +75,7 @@ def test_fused_four_streams(gpu):
 @pytest.mark.parametrize("m,n", [(1 << 27, 5000),       # 256 tiles, 2 partition blocks
                                  (1 << 16, 1 << 20),    # few tiles, 256 blocks
                                  (1 << 21, 1)])
-def test_fused_role_balance(gpu, m, n):
+def test_build_tile_block_balance(gpu, m, n):
     gpu.set_path(TILED)
     try:
         keys = workload.key_range(77, n)
