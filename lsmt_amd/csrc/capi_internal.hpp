@@ -185,9 +185,18 @@ struct cb_table {
   std::mutex fin_mu;
   int ferr = 0;
   std::string ferr_msg;
+  // The read path's key buckets (sstable.hpp), built by the table's first
+  // get_many on that call's stream (capi_sstable.cpp table_buckets): usable
+  // at once on that stream, on others once bkt_ev has completed.
+  uint64_t* bkt = nullptr;
+  size_t bkt_cap = 0;
+  uint32_t bkbits = 0;
+  hipEvent_t bkt_ev = nullptr;
+  hipStream_t bkt_stream = nullptr;
+  std::atomic<int> bkt_state{0};  // 0 none yet, 1 enqueued, 2 complete, -1 never (not fast / no memory)
+  std::mutex bkt_mu;
   cb::TableView view() const {
-    return cb::TableView{data, rec, pfx, fence, nlines, cb::fence_levels(nlines), fast ? 1u : 0u,
-                         dmap ? dir : nullptr, dmap};
+    return cb::make_view(data, rec, pfx, fence, nlines, cb::fence_levels(nlines), fast, dmap ? dir : nullptr, dmap);
   }
 };
 

@@ -42,6 +42,50 @@ int table_search_impl(const cb_table* t, const uint8_t* keys, const uint64_t* of
   return CB_OK;
 }
 
+bool buckets_enabled() {
+#ifdef CB_EXPERIMENTS
+  static const bool off = getenv("CB_NO_BUCKETS") && getenv("CB_NO_BUCKETS")[0] == '1';
+  return !off;
+#else
+  return true;
+#endif
+}
+
+// The key buckets (sstable.hpp) for a read on stream s: the first read of a
+// well-formed table enqueues their build on s and uses them at once (stream
+// order); a read on another stream uses them once their event has completed
+// and searches without them until then (never waiting). A table whose bucket
+// memory cannot be had is simply read without them. v receives bkt / bkbits.
+int table_buckets(cb_table* t, hipStream_t s, cb::TableView* v) {
+  int st = t->bkt_state.load(std::memory_order_acquire);
+  if (st < 0 || (st == 0 && (!t->fast || !t->nlines || !buckets_enabled()))) return CB_OK;
+  std::lock_guard<std::mutex> lk(t->bkt_mu);
+  st = t->bkt_state.load(std::memory_order_relaxed);
+  if (st == 0) {
+    const uint32_t bits = cb::bkt_bits(t->nlines);
+    const size_t bytes = ((size_t)1 << bits) * cb::kBktWords * 8;
+    if (pool_alloc(t->device, bytes, (void**)&t->bkt, &t->bkt_cap) != hipSuccess) {
+      t->bkt = nullptr;
+      (void)hipGetLastError();
+      t->bkt_state.store(-1, std::memory_order_release);
+      return CB_OK;
+    }
+    t->bkbits = bits;
+    HIP_TRY(hipMemsetAsync(t->bkt, 0xFF, bytes, s));
+    HIP_TRY(cb::launch_table_buckets(t->rec, t->nlines, t->bkt, bits, s));
+    HIP_TRY(hipEventCreateWithFlags(&t->bkt_ev, hipEventDisableTiming | hipEventDisableSystemFence));
+    HIP_TRY(hipEventRecord(t->bkt_ev, s));
+    t->bkt_stream = s;
+    t->bkt_state.store(st = 1, std::memory_order_release);
+  } else if (st == 1 && s != t->bkt_stream && hipEventQuery(t->bkt_ev) == hipSuccess) {
+    t->bkt_state.store(st = 2, std::memory_order_release);
+  }
+  if (st == 2 || (st == 1 && s == t->bkt_stream)) {
+    cb::view_set_buckets(*v, t->bkt, t->bkbits);
+  }
+  return CB_OK;
+}
+
 // set != NULL: the fused form (cb_set_get_many_*): the gate comes from the
 // FilterSet inside the search kernel, hit_rows are the tables' slots and
 // hits is unused.
@@ -91,6 +135,8 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
     for (uint32_t r : rows) nrows = std::max<uint64_t>(nrows, (uint64_t)r + 1);
   }
   DeviceGuard dg(dev);
+  for (uint32_t i = 0; i < nt; ++i)
+    if (int rc = table_buckets(const_cast<cb_table*>(tables[i]), s, &views[i])) return rc;
   Workspace& ws = workspace(dev, s);
   std::lock_guard<std::mutex> lk(ws.mu);
   StagedKeys sk;
@@ -631,6 +677,8 @@ int cb_table_destroy(cb_table* t) {
     }
     pool_release(t->device, t->data, t->data_cap);
     pool_release(t->device, t->rec, t->rec_cap);  // rec heads the one index allocation
+    if (t->bkt) pool_release(t->device, t->bkt, t->bkt_cap);
+    if (t->bkt_ev) (void)hipEventDestroy(t->bkt_ev);
   }
   delete t;
   return CB_OK;

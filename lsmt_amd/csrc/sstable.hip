@@ -393,7 +393,7 @@ __device__ __forceinline__ uint64_t g64(const uint64_t* p, uint64_t i) {
 
 // SsTable::binary_search (src/sstable.rs:161-179), same mid sequence.
 __device__ __forceinline__ int64_t search_exact(const TableView& t, const Query& q, LineRec& hit) {
-  uint64_t lo = 0, hi = t.nlines;
+  uint64_t lo = 0, hi = t.nlines();
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
     const LineRec r = grec(t.rec, mid);
@@ -445,9 +445,9 @@ __device__ __forceinline__ int64_t resolve_rec(const TableView& t, const Query& 
   }
   if (c > 0) return -1;
   // every line before lo is below the query; gallop to a line above it
-  uint64_t lo = b + 1, hi = t.nlines, step = 1;
-  while (lo < t.nlines) {
-    const uint64_t p = lo + step - 1 < t.nlines ? lo + step - 1 : t.nlines - 1;
+  uint64_t lo = b + 1, hi = t.nlines(), step = 1;
+  while (lo < t.nlines()) {
+    const uint64_t p = lo + step - 1 < t.nlines() ? lo + step - 1 : t.nlines() - 1;
     c = line_vs_query(t, p, q, r);
     if (c == 0) {
       hit = r;
@@ -485,19 +485,57 @@ __device__ __forceinline__ int64_t resolve_from(const TableView& t, const Query&
 
 // Level j's array (0: pfx).
 __device__ __forceinline__ const uint64_t* level_array(const TableView& t, uint32_t j) {
-  return j ? t.fence + level_offset(t.nlines, j) : t.pfx;
+  return j ? t.fence + level_offset(t.nlines(), j) : t.pfx;
 }
 
 // The range of level j-1 that holds the lower bound, from level j's answer i
 // (E_j[i-1] < x <= E_j[i], E_j[i] = E_{j-1}[16 i]): at most 16 entries.
 __device__ __forceinline__ void level_down(const TableView& t, uint32_t j, uint64_t i, uint64_t& lo, uint64_t& hi) {
-  const uint64_t cnt = level_count(t.nlines, j - 1);
+  const uint64_t cnt = level_count(t.nlines(), j - 1);
   lo = i ? ((i - 1) << kFanBits) + 1 : 0;
   hi = (i << kFanBits) < cnt ? (i << kFanBits) : cnt;
 }
 
 constexpr uint32_t kWin = 8;     // buckets of up to this many lines: one round of prefix loads
 constexpr uint32_t kRecWin = 2;  // ... of up to this many: the records alone (32 B each, prefix inside)
+
+// The key buckets' answer (sstable.hpp, TableView::bkt): kBktFound (hit
+// holds the line's record, the line index unknown), -1 (absent, proven by a
+// complete bucket), or kBktGoOn (the directory search decides).
+constexpr int64_t kBktFound = INT64_MAX;
+constexpr int64_t kBktGoOn = -2;
+__device__ __forceinline__ int64_t bucket_probe(const TableView& t, const Query& q, LineRec& hit) {
+  const uint64_t* b = t.bkt + bkt_index(q.w0, t.bkbits()) * kBktWords;
+  // the count and slot 0 first (at one line per bucket on average, most keys
+  // are in slot 0), the next pairs only when needed: fewer registers live
+  const u64x2 a = *(g64x2)(b);
+  const uint64_t cnt = a.x + 1;  // all-ones: empty
+  uint32_t c = 0;
+  if (cnt == 0 || a.y != q.w0) {
+    if (cnt <= 1) return -1;
+    const u64x2 c23 = *(g64x2)(b + 2);
+    c = (c23.x == q.w0) ? 1u : (cnt > 2 && c23.y == q.w0) ? 2u : 4u;
+    if (c == 4u) {
+      if (cnt <= 3) return -1;
+      if (g64(b, 4) != q.w0) return cnt == 4 ? -1 : kBktGoOn;
+      c = 3u;
+    }
+  }
+  const u64x2 tl = *(g64x2)(b + 6 + 2 * c);
+  LineRec r;
+  r.start = tl.y & ((1ull << 40) - 1);
+  r.pfx2 = tl.x;
+  r.klen = (uint32_t)(tl.y >> 40) & 0xFFFu;
+  if (r.klen == 0xFFFu) return kBktGoOn;  // a slot left unwritten (its bucket also holds a line left out)
+  r.vdl = (uint32_t)(tl.y >> 52);
+  r.pfx0 = q.w0;
+  const int cmp = rec_cmp(t, r, q);
+  if (cmp == 0) {
+    hit = r;
+    return kBktFound;
+  }
+  return kBktGoOn;  // another line with this prefix may be the one
+}
 
 // Where x's descent starts: level j and the run [lo, hi) of at most 16
 // entries holding its lower bound (returns false), or true when x is absent
@@ -507,9 +545,9 @@ constexpr uint32_t kRecWin = 2;  // ... of up to this many: the records alone (3
 // [dir[B], dir[B+1]] bracket x's lower bound.
 __device__ __forceinline__ bool dir_start(const TableView& t, const DirMap* dm, uint64_t x, uint32_t& j,
                                           uint64_t& lo, uint64_t& hi) {
-  j = t.nlev;
+  j = t.nlev();
   lo = 0;
-  hi = level_count(t.nlines, j);
+  hi = level_count(t.nlines(), j);
   if (!t.dir) return false;
   const uint64_t bk = dir_bucket(*dm, x);
   // dir[B] and dir[B + 1] as one 8-byte load (one L2 request, not two: the
@@ -517,9 +555,9 @@ __device__ __forceinline__ bool dir_start(const TableView& t, const DirMap* dm, 
   const u32x2 ae = *(const __attribute__((address_space(1))) u32x2*)(t.dir + bk);
   const uint64_t a = ae.x, e = ae.y;
   if (a == e) return true;
-  for (uint32_t l = 0; l < t.nlev; ++l) {
+  for (uint32_t l = 0; l < t.nlev(); ++l) {
     const uint64_t l0 = a >> (kFanBits * l);
-    const uint64_t c = level_count(t.nlines, l);
+    const uint64_t c = level_count(t.nlines(), l);
     uint64_t l1 = (e + (1ull << (kFanBits * l)) - 1) >> (kFanBits * l);
     l1 = l1 < c ? l1 : c;
     if (l1 - l0 <= kFanout) {
@@ -540,6 +578,10 @@ __device__ __forceinline__ bool dir_start(const TableView& t, const DirMap* dm, 
 // record compare when the prefix is unique.
 __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& q, LineRec& hit,
                                                const DirMap* dm) {
+  if (t.bkt) {
+    const int64_t b = bucket_probe(t, q, hit);
+    if (b != kBktGoOn) return b;
+  }
   uint32_t j;
   uint64_t lo, hi;
   // an empty bucket: absent
@@ -597,7 +639,7 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
   for (;; --j) {
     const uint64_t i = lower_bound_u64(level_array(t, j), lo, hi, q.w0);
     if (!j) {
-      if (i >= t.nlines) return -1;
+      if (i >= t.nlines()) return -1;
       return resolve_from(t, q, i, hit);
     }
     level_down(t, j, i, lo, hi);
@@ -606,7 +648,7 @@ __device__ __forceinline__ int64_t search_fast(const TableView& t, const Query& 
 
 // dm: the table's DirMap (LDS or global); used only when t.dir is set.
 __device__ __forceinline__ int64_t search(const TableView& t, const Query& q, LineRec& hit, const DirMap* dm) {
-  return t.fast ? search_fast(t, q, hit, dm) : search_exact(t, q, hit);
+  return t.fast() ? search_fast(t, q, hit, dm) : search_exact(t, q, hit);
 }
 
 // dir from the sorted prefixes, one lane per line (dir_fill). Block 0 also
@@ -631,6 +673,24 @@ __global__ __launch_bounds__(kNT) void k_table_dir(const uint64_t* __restrict__ 
 __global__ __launch_bounds__(kNT) void k_pfx_masks(const uint64_t* __restrict__ pfx, uint64_t nl,
                                                    uint64_t* __restrict__ mask) {
   sample_pfx_masks(nl, [&](uint64_t q) { return pfx[q]; }, mask);
+}
+
+// The key buckets (sstable.hpp) of a fast table, one lane per line: the
+// bucket's count word hands out slots (1 per stored line, 16 per line left
+// out, so a bucket holding one is never taken as complete).
+__global__ __launch_bounds__(kNT) void k_table_buckets(const LineRec* __restrict__ rec, uint64_t nl,
+                                                       uint64_t* __restrict__ bkt, uint32_t bits) {
+  const uint64_t l = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  if (l >= nl) return;
+  const LineRec r = grec(rec, l);
+  const bool keep = r.klen < 4095u && r.vdl <= 4095u && r.start < (1ull << 40);  // klen 0xFFF: unwritten slot
+  uint64_t* b = bkt + bkt_index(r.pfx0, bits) * kBktWords;
+  const uint64_t s = atomicAdd(reinterpret_cast<unsigned long long*>(b), keep ? 1ull : 16ull) + 1;
+  if (keep && s < kBktSlots) {
+    b[1 + s] = r.pfx0;
+    b[6 + 2 * s] = r.pfx2;
+    b[7 + 2 * s] = r.start | ((uint64_t)r.klen << 40) | ((uint64_t)r.vdl << 52);
+  }
 }
 
 // A block's views of the first min(nt, 64) tables into LDS. Barrier inside.
@@ -753,7 +813,7 @@ __device__ __forceinline__ void resolve_key(const TableView* stv, const TableVie
 
 // LDS_VIEWS: nt <= 64 (every view staged in LDS; see resolve_group).
 template <int KEYK, bool LDS_VIEWS>
-__global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ tv, uint32_t nt,
+__global__ __launch_bounds__(kNT, 6) void k_get_many(const TableView* __restrict__ tv, uint32_t nt,
                                                   const uint64_t* __restrict__ hits,
                                                   const uint32_t* __restrict__ rows,
                                                   uint64_t hwords, KeySrc ks, uint64_t n,
@@ -810,7 +870,7 @@ __global__ __launch_bounds__(kNT) void k_get_many(const TableView* __restrict__ 
 // read and the set's random reads overlap the searches' in one kernel. Table
 // t is slot slots[t] (slots NULL: slot t); nt <= W.
 template <int KEYK, int MODE, int W>
-__global__ __launch_bounds__(kNT) void k_set_get_many(const void* __restrict__ set, ModP mp, ZoneView zv,
+__global__ __launch_bounds__(kNT, 6) void k_set_get_many(const void* __restrict__ set, ModP mp, ZoneView zv,
                                                       const TableView* __restrict__ tv, uint32_t nt,
                                                       const uint32_t* __restrict__ slots, KeySrc ks, uint64_t n,
                                                       int32_t* __restrict__ which, uint64_t* __restrict__ vsrc,
@@ -860,7 +920,7 @@ __global__ __launch_bounds__(kNT) void k_set_get_many(const void* __restrict__ s
 // newest first and the first Ok(Some) ends the walk. Views of tables past
 // the first 64 come from global memory.
 template <int KEYK, int MODE>
-__global__ __launch_bounds__(kNT) void k_wide_get_many(const uint64_t* __restrict__ set, uint32_t R, ModP mp,
+__global__ __launch_bounds__(kNT, 5) void k_wide_get_many(const uint64_t* __restrict__ set, uint32_t R, ModP mp,
                                                        WideZone z, const TableView* __restrict__ tv, uint32_t nt,
                                                        const WideGroup* __restrict__ groups,
                                                        const uint32_t* __restrict__ slots, KeySrc ks, uint64_t n,
@@ -1195,6 +1255,14 @@ hipError_t launch_table_search(int keyk, const TableView& t, const KeySrc& ks, u
     case KEY_VAR: hipLaunchKernelGGL(k_table_search<KEY_VAR>, g, dim3(kNT), 0, s, t, ks, n, line); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_table_buckets(const LineRec* rec, uint64_t nlines, uint64_t* bkt, uint32_t bits,
+                                hipStream_t s) {
+  if (!nlines) return hipSuccess;
+  ProfScope ps("k_table_buckets", s);
+  hipLaunchKernelGGL(k_table_buckets, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, rec, nlines, bkt, bits);
   return hipGetLastError();
 }
 

@@ -294,12 +294,60 @@ struct TableView {
   const LineRec* rec;     // nlines
   const uint64_t* pfx;    // nlines
   const uint64_t* fence;  // fence_words(nlines): levels 1..nlev
-  uint64_t nlines;
-  uint32_t nlev;          // fence_levels(nlines)
-  uint32_t fast;
   const uint32_t* dir;    // dmap->nbuckets + 1 entries (nullptr: none)
   const DirMap* dmap;     // the directory's map (device; staged into LDS by the read path)
+  const uint64_t* bkt;    // the key buckets (below; nullptr: none — the read path builds them)
+  uint32_t nl_lo;         // nlines, low 32 bits
+  uint32_t meta;          // nlines >> 32 (8 bits) | nlev << 8 | fast << 16 | bkbits << 24
+  // 64 B: the read kernels stage 64 views per block through registers and LDS
+  __host__ __device__ uint64_t nlines() const { return ((uint64_t)(meta & 255u) << 32) | nl_lo; }
+  __host__ __device__ uint32_t nlev() const { return (meta >> 8) & 255u; }
+  __host__ __device__ bool fast() const { return (meta >> 16) & 1u; }
+  __host__ __device__ uint32_t bkbits() const { return meta >> 24; }
 };
+static_assert(sizeof(TableView) == 64, "TableView is 64 B");
+__host__ __device__ inline TableView make_view(const uint8_t* data, const LineRec* rec, const uint64_t* pfx,
+                                               const uint64_t* fence, uint64_t nlines, uint32_t nlev, bool fast,
+                                               const uint32_t* dir, const DirMap* dmap) {
+  return TableView{data, rec, pfx, fence, dir, dmap, nullptr, (uint32_t)nlines,
+                   (uint32_t)((nlines >> 32) & 255u) | (nlev << 8) | ((fast ? 1u : 0u) << 16)};
+}
+inline void view_set_buckets(TableView& v, const uint64_t* bkt, uint32_t bits) {
+  v.bkt = bkt;
+  v.meta = (v.meta & 0x00FFFFFFu) | (bits << 24);
+}
+
+// Key buckets of a well-formed table (the read path's first probe, built on
+// a table's first get_many): 2^bkbits buckets of 128 B, a line's bucket
+// picked by a multiplicative hash of its 8-byte prefix, 2^bkbits >= nlines
+// (at most one line per bucket on average). Words of bucket b:
+//   [0]      count - 1 (all-ones: empty): 1 per stored line, 16 per line left out
+//   [1..4]   the prefix (pfx0) of slots 0..3
+//   [6+2s]   slot s's pfx2
+//   [7+2s]   slot s's start | klen << 40 | vdl << 52
+// A bucket stores its first four lines, in no particular order; a line with
+// a key of 4095 bytes or more (klen 0xFFF marks an unwritten slot), an undecodable value or one decoding to more
+// than 4095 bytes, or a start at or past 2^40, is left out (and makes its
+// bucket's count say so). A lookup reads words 0..3 (the count and three
+// prefixes, two 16-byte loads of one line), word 4 only when the count passes
+// 3, then the matching slot's pair: one 128-B line where the directory and
+// the record took two or three. A count of at most 4 with no matching prefix
+// is a proof of absence; anything else it cannot settle (a bucket past four
+// lines, a prefix shared by another key) goes on to the directory search.
+constexpr uint32_t kBktWords = 16;
+constexpr uint32_t kBktSlots = 4;
+__host__ __device__ inline uint32_t bkt_bits(uint64_t nlines) {
+  uint32_t b = 1;
+  while (b < 40 && (1ull << b) < nlines) ++b;
+  return b;
+}
+__host__ __device__ inline uint64_t bkt_index(uint64_t pfx0, uint32_t bits) {
+  return (pfx0 * 0x9E3779B97F4A7C15ull) >> (64 - bits);
+}
+// Buckets of a fast table from its records; bkt (2^bits * 128 B) must be
+// all-ones first (the caller's memset).
+hipError_t launch_table_buckets(const LineRec* rec, uint64_t nlines, uint64_t* bkt, uint32_t bits,
+                                hipStream_t s);
 
 // ---- line index build: count -> scan -> emit -> finish ----
 constexpr uint32_t kLineChunk = 4096;  // bytes per block (256 threads x 16 B)

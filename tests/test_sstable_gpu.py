@@ -632,3 +632,46 @@ def test_get_many_async_and_view_cache(gpu):
     with pytest.raises(Exception):
         gpu.get_many(tables, look, out=(np.zeros(n, np.int32), np.zeros(n + 1, np.uint64), np.zeros(16, np.uint8)),
                      wait=False)
+
+
+def test_get_many_key_buckets(gpu):
+    """The read path's key buckets (sstable.hpp, built by a table's first
+    get_many): tables whose lines share 8-byte prefixes (many lines per
+    prefix, so buckets overflow and prefixes collide), lines left out of the
+    buckets (a 5000-byte key, values decoding to more than 4095 bytes, an
+    undecodable value), tables of 1 and 3 lines; the first call (buckets built
+    on its stream), a second one, and one on another stream right after the
+    first (buckets maybe not yet usable there) all equal the oracle."""
+    import base64
+    import torch
+    rng = np.random.default_rng(23)
+    shared = sorted({b"user0000" + bytes(rng.integers(48, 58, 6, dtype=np.uint8)) for _ in range(3000)})
+    plain = [bytes(k) for k in workload.key_range(2400, 20_000)]
+    def lines(keys, t):
+        out = []
+        for i, k in enumerate(keys):
+            if t == 1 and i % 97 == 0:
+                v = base64.b64encode(bytes(5000))  # decodes to 5000 bytes: left out of the buckets
+            elif t == 1 and i % 89 == 0:
+                v = b"!!"  # undecodable
+            else:
+                v = base64.b64encode(bytes([(i + t) % 256] * (i % 20)))
+            out.append(k + b"\t" + v + b"\n")
+        return b"".join(out)
+    big = sorted(plain[:5000] + [b"zz" + b"k" * 4998])  # one 5000-byte key
+    keysets = [shared, sorted(plain), big, [b"aaa-single"], [b"mmm1", b"mmm2", b"mmm3"]]
+    files = [lines(ks, t) for t, ks in enumerate(keysets)]
+    tables = [gpu.Table(f) for f in files]
+    assert all(t.well_formed for t in tables)
+    otables = [oracle.OracleTable(f) for f in files]
+    look = ([k for ks in keysets for k in ks[::3]] + [b"user0000" + bytes(rng.integers(48, 58, 6, dtype=np.uint8))
+                                                      for _ in range(2000)] + [bytes(k) for k in workload.key_range(2401, 3000)])
+    d, o = var(look)
+    kb = gpu.KeyBatch(n=len(look), data=d, offsets=o)
+    ow, ovoff, ovals = oracle.get_many(otables, None, d, o)
+    dev = torch.device("cuda", 0)
+    other = torch.cuda.Stream(device=dev)
+    for i in range(3):
+        which, voff, vals = gpu.get_many(tables, kb, stream=other if i == 1 else None)
+        assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals, i
+    assert (which >= 0).sum() > 0.3 * len(look) and all((which == t).any() for t in range(5))
