@@ -182,6 +182,14 @@ def main():
             os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", "29533"
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
+        # Two communicators share each GPU at N > 1: torch's process group
+        # (barriers and the max-over-ranks timing only) and the library's own
+        # RCCL communicator (cb_comm, the hit exchange). They never have work
+        # in flight together: every torch collective below follows a
+        # torch.cuda.synchronize() of the whole device (timed-region edges,
+        # check flags), and the library issues its collectives in one order on
+        # every rank (comm.cpp's order event). Keep that invariant when adding
+        # a torch collective: sync the device first.
         if rehearse:
             dist.init_process_group("gloo")
         else:
@@ -327,9 +335,10 @@ def main():
 
     def timed(fn, k, lanes=None):
         lanes = lane_streams if lanes is None else lanes
+        torch.cuda.synchronize(dev)  # all streams: every exchange of the K steps is inside
         if use_dist:
             dist.barrier()
-        torch.cuda.synchronize(dev)  # all streams: every exchange of the K steps is inside
+            torch.cuda.synchronize(dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         # every stream is idle here, so the lanes' first steps (issued after
@@ -987,6 +996,7 @@ def main():
             line["valid"] = False
         print(json.dumps(line), file=result, flush=True)
     if use_dist:
+        torch.cuda.synchronize(dev)
         dist.barrier()
         xcomm.close()
         dist.destroy_process_group()
@@ -1008,9 +1018,10 @@ def _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes, fn, k):
     """K steps of fn between a barrier + device sync on both sides; HIP events
     on lanes[0] around them (every other lane joined into the end event).
     Returns (wall seconds, event ms), each the max over ranks."""
+    torch.cuda.synchronize(dev)
     if use_dist:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(lanes[0])
