@@ -243,20 +243,24 @@ __device__ __forceinline__ void wave0_exclusive_scan4(uint32_t* arr, uint32_t le
 }
 
 // pol: the store policy bits (build_stores(): bit 0 write-through entries).
-template <int KEYK, int MODE, int KPT>
+// E: the entry type — uint32_t (offsets in tiles of up to 2^20 bits) or
+// uint16_t (bins of 2^16 bits, tb = 16 here: the sub-tiles of
+// k_build_tile_sub's tiles).
+template <int KEYK, int MODE, int KPT, typename E = uint32_t>
 __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp, uint32_t tb,
                                                          uint32_t T,
                                                          uint32_t* __restrict__ seg_all,
-                                                         uint32_t* __restrict__ ent_all, uint32_t pol) {
+                                                         void* __restrict__ ent_all, uint32_t pol) {
   constexpr uint32_t NT = kBuildNT, C = NT * KPT;
+  static_assert(sizeof(E) == 4 || sizeof(E) == 2, "entry type");
   const KeySrc ks = bb.ks[blockIdx.y];
   const uint64_t n = bb.n[blockIdx.y];
   uint32_t* seg = seg_all + (size_t)blockIdx.y * gridDim.x * (T + 1);
-  uint32_t* ent = ent_all + (size_t)blockIdx.y * gridDim.x * (2 * C);
+  E* ent = reinterpret_cast<E*>(ent_all) + (size_t)blockIdx.y * gridDim.x * (2 * C);
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t Tp = (T + 4) & ~3u;
   uint32_t* hist = smem;  // T + 1 entries: counts, then run starts and the total
-  uint32_t* stage = smem + Tp;
+  E* stage = reinterpret_cast<E*>(smem + Tp);
   const uint32_t tid = threadIdx.x;
   const uint64_t kbase = (uint64_t)blockIdx.x * C;
   CB_STAMP(0);
@@ -296,23 +300,24 @@ __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp,
   for (uint32_t t = tid; t <= T; t += NT) srow[t] = hist[t];
 #pragma unroll
   for (int e = 0; e < 2 * KPT; ++e)
-    if (q[e] != kNone) stage[hist[q[e] >> 20] + er[e]] = q[e] & 0xFFFFFu;
+    if (q[e] != kNone) stage[hist[q[e] >> 20] + er[e]] = (E)(q[e] & 0xFFFFFu);
   __syncthreads();
   CB_STAMP(4);
-  uint32_t* out = ent + (size_t)blockIdx.x * (2 * C);  // 16-B aligned, as is stage
-  const uint32_t n4 = total / 4;
+  E* out = ent + (size_t)blockIdx.x * (2 * C);  // 16-B aligned, as is stage
+  constexpr uint32_t PER = 16 / sizeof(E);      // entries per 16-B store
+  const uint32_t n4 = total / PER;
   // write-through (sc1): the entries go on to the memory side at once, so the
   // kernel's end has no dirty L2 lines to write back, and the tile pass (on
   // other XCDs) still finds them there; C2 on four lanes 101 -> 105-107 G
   // keys/s (non-temporal stores instead made the tile pass's reads slower)
   if (pol & 1u) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, 2 * C * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, 2 * C * sizeof(E), 0x00020000);
     for (uint32_t i = tid; i < n4; i += NT) store16_wt(r, i * 16, reinterpret_cast<const uint4*>(stage)[i]);
   } else {
     for (uint32_t i = tid; i < n4; i += NT)
       reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(stage)[i];
   }
-  for (uint32_t i = 4 * n4 + tid; i < total; i += NT) out[i] = stage[i];
+  for (uint32_t i = PER * n4 + tid; i < total; i += NT) out[i] = stage[i];
   CB_STAMP(5);
 }
 
@@ -413,6 +418,106 @@ __global__ __launch_bounds__(NT) void k_build_tile(BuildBatch bb, uint32_t tb, u
   else
     for (uint32_t i = tid; i < tw / 4; i += NT) gt[i] = lt[i];
   CB_STAMP(4);
+}
+
+// The tile pass over 16-bit entries (batched builds of long runs, C4): the
+// partition binned by sub-tiles of 2^16 bits (S = 2^SUB per tile), so block
+// b's entries for tile t are one contiguous super-run [seg[b][S t],
+// seg[b][S (t+1)]) and sub-tile j's part of it starts at seg[b][S t + j].
+// Lanes 0 .. G (S+1) - 1 load the G blocks' S + 1 bounds; an entry's
+// sub-tile is the number of interior bounds at or below its index (uniform
+// values taken by readlane, S - 1 compares), its bit (j << 16) | entry. Half
+// the entry bytes of k_build_tile for S - 1 compares per entry.
+template <int G, int R, int SUB, uint32_t NT = kBuildNT>
+__global__ __launch_bounds__(NT) void k_build_tile_sub(BuildBatch bb, uint32_t tb, uint32_t T,
+                                                       const uint32_t* __restrict__ seg_all,
+                                                       uint32_t nblk,
+                                                       const uint16_t* __restrict__ ent_all,
+                                                       uint32_t estride, uint32_t pol) {
+  constexpr uint32_t NW = NT / 64, S = 1u << SUB, NB = S + 1;
+  static_assert(G * NB <= 64, "one lane per bound");
+  uint32_t* __restrict__ words = bb.words[blockIdx.y];
+  const bool fresh = (bb.fresh >> blockIdx.y) & 1u;
+  const uint32_t TS = T << SUB;  // bins per filter
+  const uint32_t* __restrict__ seg = seg_all + (size_t)blockIdx.y * nblk * (TS + 1);
+  const uint16_t* __restrict__ ent = ent_all + (size_t)blockIdx.y * nblk * estride;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t tw = 1u << (tb - 5);
+  uint32_t* tile = smem;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const uint32_t t = xcd_tile(blockIdx.x, T);
+  const uint32_t lu = lane / NB, lk = lane - lu * NB;  // this lane's bound: block lu, bound lk
+
+  uint32_t sb = 0;  // first group's bounds in flight while the tile is cleared / loaded
+  {
+    const uint32_t b = w + NW * lu;
+    if (lane < G * NB && b < nblk) sb = seg[(size_t)b * (TS + 1) + (t << SUB) + lk];
+  }
+  uint4* gt = reinterpret_cast<uint4*>(words + (size_t)t * tw);
+  uint4* lt = reinterpret_cast<uint4*>(tile);
+  for (uint32_t i = tid; i < tw / 4; i += NT) lt[i] = fresh ? make_uint4(0, 0, 0, 0) : gt[i];
+  __syncthreads();
+
+  for (uint32_t g0 = 0; w + NW * g0 < nblk; g0 += G) {
+    if (g0) {
+      sb = 0;
+      const uint32_t b = w + NW * (g0 + lu);
+      if (lane < G * NB && b < nblk) sb = seg[(size_t)b * (TS + 1) + (t << SUB) + lk];
+    }
+    uint32_t o[R][G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const uint32_t st = __builtin_amdgcn_readlane(sb, u * NB);
+      const uint32_t len = __builtin_amdgcn_readlane(sb, u * NB + S) - st;
+      const uint32_t b = w + NW * (g0 + u);
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        o[q][u] = 0;
+        if (64 * q + lane < len) o[q][u] = ent[(size_t)b * estride + st + 64 * q + lane];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const uint32_t st = __builtin_amdgcn_readlane(sb, u * NB);
+      const uint32_t len = __builtin_amdgcn_readlane(sb, u * NB + S) - st;
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const uint32_t i = 64 * q + lane;
+        if (i < len) {
+          uint32_t j = 0;
+#pragma unroll
+          for (uint32_t k = 1; k < S; ++k) j += (st + i >= __builtin_amdgcn_readlane(sb, u * NB + k)) ? 1u : 0u;
+          const uint32_t v = (j << 16) | o[q][u];
+          atomicOr(&tile[v >> 5], 1u << (v & 31));
+        }
+      }
+    }
+    // super-runs longer than R waves (skewed inputs)
+    bool longrun = false;
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+      longrun |= __builtin_amdgcn_readlane(sb, u * NB + S) - __builtin_amdgcn_readlane(sb, u * NB) > 64u * R;
+    if (longrun) {
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        const uint32_t st = __builtin_amdgcn_readlane(sb, u * NB);
+        const uint32_t len = __builtin_amdgcn_readlane(sb, u * NB + S) - st;
+        const uint16_t* run = ent + (size_t)(w + NW * (g0 + u)) * estride + st;
+        for (uint32_t i = 64 * R + lane; i < len; i += 64) {
+          uint32_t j = 0;
+#pragma unroll
+          for (uint32_t k = 1; k < S; ++k) j += (st + i >= __builtin_amdgcn_readlane(sb, u * NB + k)) ? 1u : 0u;
+          const uint32_t v = (j << 16) | run[i];
+          atomicOr(&tile[v >> 5], 1u << (v & 31));
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (pol & 2u)
+    for (uint32_t i = tid; i < tw / 4; i += NT) store16_nt(gt + i, lt[i]);
+  else
+    for (uint32_t i = tid; i < tw / 4; i += NT) gt[i] = lt[i];
 }
 
 // Partition for probe: one 8-byte entry per key, bucketed by the tile of bit
@@ -811,6 +916,25 @@ TilePlan plan_build(uint64_t m, uint64_t n, uint32_t nb) {
   if (env_kpt == 1 || env_kpt == 2 || env_kpt == 4) p.kpt = env_kpt;
   p.C = kBuildNT * p.kpt;
   p.nblk = (uint32_t)((n + p.C - 1) / p.C);
+  // Batched builds of long runs (C4: 32 filters of 2^18 keys into 2^25 bits,
+  // ~128 entries per run) move 16-bit entries in 2^16-bit sub-tiles: the
+  // passes are bandwidth-bound there, and the entries are a third of the
+  // bytes. Single builds keep 32-bit entries (their tile pass is bound by its
+  // dependent loads, where the sub-tile arithmetic cost more than the bytes
+  // saved: DESIGN §9.5).
+  // Their tiles are 2^18 bits (4 sub-tiles) worked by 512-thread
+  // workgroups, four per CU instead of two 1024-thread ones on 2^19-bit
+  // tiles: C4 141 -> 128-131 us per step on one lane, 147-151 -> 139-141 on
+  // three (profiles/c4_sub_r04.json).
+  static const int env_sub = env_int("CB_BUILD_SUB", -1);
+  p.sub = 0;
+  if (env_sub != 0 && nb >= 8 && p.tb >= 17 && 2ull * p.C > 48ull * p.T) {
+    if (p.tb == 19 && !env_tb && 2ull * p.C > 48ull * 2 * p.T && ((uint64_t)p.T << 3) <= kMaxTiles) {
+      p.tb = 18;
+      p.T = (uint32_t)((m + (1ull << 18) - 1) >> 18);
+    }
+    if (((uint64_t)p.T << (p.tb - 16)) <= kMaxTiles) p.sub = p.tb - 16;
+  }
   return p;
 }
 
@@ -838,8 +962,8 @@ TilePlan plan_probe(uint64_t m, uint64_t n) {
 
 bool plan_ok(const TilePlan& p) { return p.T <= kMaxTiles; }
 
-size_t build_seg_bytes(const TilePlan& p) { return (size_t)(p.T + 1) * p.nblk * 4; }
-size_t build_ent_bytes(const TilePlan& p) { return (size_t)p.nblk * 2 * p.C * 4; }
+size_t build_seg_bytes(const TilePlan& p) { return ((size_t)(p.T << p.sub) + 1) * p.nblk * 4; }
+size_t build_ent_bytes(const TilePlan& p) { return (size_t)p.nblk * 2 * p.C * (p.sub ? 2 : 4); }
 size_t probe_seg_bytes(const TilePlan& p) { return (size_t)(p.T + 1) * p.nblk * 4; }
 size_t probe_ent_bytes(const TilePlan& p) { return (size_t)p.nblk * p.C * 8; }
 size_t probe_lkey_bytes(const TilePlan& p) { return (size_t)p.nblk * p.C * 2; }
@@ -889,6 +1013,12 @@ static uint32_t build_stores() {
 template <int KK, int MM, int KPT>
 static void build_part(const TilePlan& p, const BuildBatch& bb, uint32_t nb, const ModP& mp,
                        uint32_t* seg, uint32_t* ent, size_t lds, hipStream_t s) {
+  if (p.sub) {  // 16-bit entries binned by 2^16-bit sub-tile
+    allow_lds(k_build_part<KK, MM, KPT, uint16_t>, lds);
+    hipLaunchKernelGGL((k_build_part<KK, MM, KPT, uint16_t>), dim3(p.nblk, nb), dim3(kBuildNT), lds, s, bb, mp,
+                       16u, p.T << p.sub, seg, ent, build_stores());
+    return;
+  }
   allow_lds(k_build_part<KK, MM, KPT>, lds);
   hipLaunchKernelGGL((k_build_part<KK, MM, KPT>), dim3(p.nblk, nb), dim3(kBuildNT), lds, s, bb, mp,
                      p.tb, p.T, seg, ent, build_stores());
@@ -899,7 +1029,9 @@ hipError_t launch_build_batch(int keyk, int mode, const BuildBatch& bb, uint32_t
                               hipStream_t s) {
   if (!nb) return hipSuccess;
   if (!plan_ok(p) || nb > kMaxBuildBatch || p.nblk > kMaxBuildBlocks) return hipErrorInvalidValue;
-  const size_t lds1 = ((size_t)((p.T + 4) & ~3u) + 2 * p.C) * 4;
+  if (p.sub && (p.sub > 3 || p.tb != 16 + p.sub || ((uint64_t)p.T << p.sub) > kMaxTiles)) return hipErrorInvalidValue;
+  const uint32_t TS = p.T << p.sub;  // partition bins
+  const size_t lds1 = (size_t)((TS + 4) & ~3u) * 4 + 2 * p.C * (p.sub ? 2 : 4);
   {
     ProfScope ps("k_build_part", s);
     if (p.kpt == 1) {
@@ -914,6 +1046,26 @@ hipError_t launch_build_batch(int keyk, int mode, const BuildBatch& bb, uint32_t
   if (e != hipSuccess) return e;
   const size_t lds2 = (size_t)(1u << (p.tb - 5)) * 4;
   ProfScope ps("k_build_tile", s);
+  if (p.sub) {
+    const uint16_t* e16 = reinterpret_cast<const uint16_t*>(ent);
+    if (p.sub == 2) {  // 2^18-bit tiles: 512-thread workgroups, four per CU
+      allow_lds(k_build_tile_sub<8, 2, 2, 512>, lds2);
+      hipLaunchKernelGGL((k_build_tile_sub<8, 2, 2, 512>), dim3(p.T, nb), dim3(512), lds2, s, bb, p.tb, p.T, seg,
+                         p.nblk, e16, 2 * p.C, build_stores());
+      return hipGetLastError();
+    }
+#define CB_TILE_SUB(SUBV)                                                                                 \
+  allow_lds(k_build_tile_sub<4, 2, SUBV>, lds2);                                                         \
+  hipLaunchKernelGGL((k_build_tile_sub<4, 2, SUBV>), dim3(p.T, nb), dim3(kBuildNT), lds2, s, bb, p.tb, p.T, seg, \
+                     p.nblk, e16, 2 * p.C, build_stores())
+    if (p.sub == 1) {
+      CB_TILE_SUB(1);
+    } else {
+      CB_TILE_SUB(3);
+    }
+#undef CB_TILE_SUB
+    return hipGetLastError();
+  }
   // entries per (partition block, tile): 2 C / T on average (tiles of one
   // filter); two rounds of run loads once that passes ~3/4 of a wave
 #ifdef CB_EXPERIMENTS

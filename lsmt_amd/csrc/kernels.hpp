@@ -42,6 +42,7 @@ struct TilePlan {
   uint32_t kpt;   // keys per thread in the partition pass
   uint32_t C;     // keys per partition block = threads * kpt
   uint32_t nblk;  // partition blocks = ceil(n / C)
+  uint32_t sub;   // build only: 0, or log2 of the 2^16-bit sub-tiles per tile (16-bit entries)
 };
 
 // nb: filters built together in one launch pair (insert_fixed_many batches).

@@ -87,3 +87,26 @@ def test_build_tile_block_balance(gpu, m, n):
         assert _bits_equal(g, o)
     finally:
         gpu.set_path(0)
+
+
+@pytest.mark.parametrize("m", [1 << 25, (1 << 25) + 12345, 3 << 23])
+def test_batched_long_run_builds(gpu, m):
+    """Batched builds of long runs take 16-bit entries in 2^16-bit sub-tiles
+    (kernels.hip plan_build: C4's shape): 12 filters, ragged counts around
+    2^18 keys, one of them a few keys repeated 60K times (super-runs past the
+    two waves a tile workgroup loads at once), one already holding bits (the
+    tile loaded, not cleared), m a power of two or not. Each against the
+    oracle."""
+    counts = [1 << 18, (1 << 18) - 1, 200_000, 150_000] + [240_000 + 997 * i for i in range(8)]
+    keys = [workload.key_range(5000 + i, c) for i, c in enumerate(counts)]
+    base = workload.key_range(77, 40)
+    keys[2] = np.concatenate([keys[2], np.repeat(base[:3], 60_000, axis=0)])
+    fs = [gpu.BloomFilter(m) for _ in counts]
+    fs[7].insert_batch(workload.key_range(7, 1000))
+    gpu.insert_many(fs, keys)
+    for i, (f, k) in enumerate(zip(fs, keys)):
+        o = oracle.OracleFilter(m)
+        if i == 7:
+            o.insert_fixed(workload.key_range(7, 1000))
+        o.insert_fixed(k)
+        assert _bits_equal(f, o), i

@@ -17,13 +17,15 @@ for lanes in ("1", "3"):
     for env in SETTINGS:
         e = dict(os.environ, **env)
         p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "expbench.py"), "--workload", "c4",
-                            "--steps", steps, "--warmup", "5", "--no-cpu", "--probe-streams", lanes],
+                            "--steps", steps, "--warmup", "5", "--no-cpu", "--probe-streams", lanes]
+                           + (["--check"] if os.environ.get("C4_SWEEP_CHECK") == "1" else []),
                            capture_output=True, text=True, timeout=300, env=e, cwd=ROOT)
         if p.returncode:
             print(json.dumps({"env": env, "lanes": lanes, "error": p.stderr[-800:]}), flush=True)
             break
         d = json.loads(p.stdout.strip().splitlines()[-1])
         leg = d["c4"]
-        print(json.dumps({"env": env, "lanes": lanes, "region_us_per_step": leg["region_us_per_step"],
+        print(json.dumps({"env": env, "lanes": lanes, "golden": d.get("golden_all_filters_bit_exact", leg.get("golden_all_filters_bit_exact")),
+                          "region_us_per_step": leg["region_us_per_step"],
                           "one_lane_us_per_step": leg["one_lane_us_per_step"], "ms_per_step": leg["ms_per_step"],
                           "kernels_us": leg["kernels_us"]}), flush=True)

@@ -1,5 +1,5 @@
-// ubench_build.hip — where the C2 build's time goes (2^20
-// 16-byte keys -> one 2^27-bit filter). Compiles the library's kernels.hip in
+// ubench_build.hip — where a build's time goes (2^20
+// 16-byte keys -> one 2^27-bit filter; or C4's launch pair of 32 filters). Compiles the library's kernels.hip in
 // this translation unit with CB_STAMPS, so the build kernels record
 // s_memrealtime (100 MHz) at their phase boundaries. Reports:
 //   - back-to-back time per launch of an empty 1024-thread kernel of the
@@ -85,52 +85,83 @@ static void phases(const char* name, const std::vector<uint64_t>& st, uint32_t n
   printf("], \"start_spread_us\": %.2f}%s", starts.back(), last ? "" : ", ");
 }
 
-int main() {
+// Usage: ubench_build [c2|c4]. c2: one build of 2^20 keys into m = 2^27;
+// c4: one launch pair of the C4 batch (32 filters of 2^18 keys, m = 2^25).
+int main(int argc, char** argv) {
   using namespace cb;
-  const uint32_t n = 1u << 20;
-  const uint64_t m = 1ull << 27;
+  const bool c4 = argc > 1 && argv[1][0] == 'c' && argv[1][1] == '4';
+  const uint32_t n = c4 ? (1u << 18) : (1u << 20);
+  const uint64_t m = c4 ? (1ull << 25) : (1ull << 27);
+  const uint32_t nb = c4 ? 32 : 1;
   uint4* keys;
   uint32_t *words, *seg, *ent, *dummy;
-  CHECK(hipMalloc(&keys, (size_t)n * 16));
-  hipLaunchKernelGGL(k_keys, dim3(n / 256), dim3(256), 0, 0, keys, n);
+  CHECK(hipMalloc(&keys, (size_t)n * nb * 16));
+  hipLaunchKernelGGL(k_keys, dim3(n * nb / 256), dim3(256), 0, 0, keys, n * nb);
   int mode = 0;
   const ModP mp = make_modp(m, &mode);
-  const TilePlan p = plan_build(m, n);
-  CHECK(hipMalloc(&words, m / 8));
-  CHECK(hipMalloc(&seg, build_seg_bytes(p)));
-  CHECK(hipMalloc(&ent, build_ent_bytes(p)));
+  const TilePlan p = plan_build(m, n, nb);
+  CHECK(hipMalloc(&words, m / 8 * nb));
+  CHECK(hipMalloc(&seg, build_seg_bytes(p) * nb));
+  CHECK(hipMalloc(&ent, build_ent_bytes(p) * nb));
   CHECK(hipMalloc(&dummy, 64));
   BuildBatch bb{};
-  bb.ks[0].bytes = reinterpret_cast<const uint8_t*>(keys);
-  bb.ks[0].key_len = 16;
-  bb.n[0] = n;
-  bb.words[0] = words;
-  bb.fresh = 1;
-  printf("{\"plan\": {\"tb\": %u, \"T\": %u, \"kpt\": %u, \"C\": %u, \"nblk\": %u}, ",
-         p.tb, p.T, p.kpt, p.C, p.nblk);
+  for (uint32_t f = 0; f < nb; ++f) {
+    bb.ks[f].bytes = reinterpret_cast<const uint8_t*>(keys + (size_t)f * n);
+    bb.ks[f].key_len = 16;
+    bb.n[f] = n;
+    bb.words[f] = words + (size_t)f * (m / 32);
+  }
+  bb.fresh = nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1);
+  printf("{\"shape\": \"%s\", \"plan\": {\"tb\": %u, \"T\": %u, \"kpt\": %u, \"C\": %u, \"nblk\": %u, \"nb\": %u, \"sub\": %u}, ",
+         c4 ? "c4" : "c2", p.tb, p.T, p.kpt, p.C, p.nblk, nb, p.sub);
 
   const size_t lds1 = ((size_t)((p.T + 4) & ~3u) + 2 * p.C) * 4;
   const size_t lds2 = (size_t)(1u << (p.tb - 5)) * 4;
-  allow_lds(k_empty, lds2);
-  const float e1 = per_launch_us([&] { hipLaunchKernelGGL(k_empty, dim3(p.nblk), dim3(1024), lds1, 0, dummy); }, 50);
-  const float e2 = per_launch_us([&] { hipLaunchKernelGGL(k_empty, dim3(p.T), dim3(1024), lds2, 0, dummy); }, 50);
-  const float full = per_launch_us([&] { CHECK(launch_build_batch(KEY_FIXED16, mode, bb, 1, mp, p, seg, ent, 0)); }, 50);
-  allow_lds(k_build_tile<16>, lds2);
+  allow_lds(k_empty, lds2 > lds1 ? lds2 : lds1);
+  const float e1 = per_launch_us([&] { hipLaunchKernelGGL(k_empty, dim3(p.nblk, nb), dim3(1024), lds1, 0, dummy); }, 50);
+  const float e2 = per_launch_us([&] { hipLaunchKernelGGL(k_empty, dim3(p.T, nb), dim3(1024), lds2, 0, dummy); }, 50);
+  const float full = per_launch_us([&] { CHECK(launch_build_batch(KEY_FIXED16, mode, bb, nb, mp, p, seg, ent, 0)); }, 50);
+  if (p.kpt != 4) {
+    fprintf(stderr, "plan kpt %u: this tool times the kpt = 4 partition kernel\n", p.kpt);
+    return 1;
+  }
+  if (p.sub && p.sub != 2) {
+    fprintf(stderr, "plan sub %u: this tool times sub = 0 or 2\n", p.sub);
+    return 1;
+  }
+  const size_t lds1s = (size_t)(((p.T << p.sub) + 4) & ~3u) * 4 + 2 * p.C * 2;
   allow_lds(k_build_part<KEY_FIXED16, MOD_POW2_32, 4>, lds1);
-  auto launch_part = [&] {
-    hipLaunchKernelGGL((k_build_part<KEY_FIXED16, MOD_POW2_32, 4>), dim3(p.nblk, 1), dim3(1024), lds1, 0, bb, mp,
-                       p.tb, p.T, seg, ent, build_stores());
+  allow_lds(k_build_part<KEY_FIXED16, MOD_POW2_32, 4, uint16_t>, lds1s);
+  allow_lds((k_build_tile_sub<8, 2, 2, 512>), lds2);
+  auto launch_part = [&] {  // launch_build_batch's partition
+    if (p.sub)
+      hipLaunchKernelGGL((k_build_part<KEY_FIXED16, MOD_POW2_32, 4, uint16_t>), dim3(p.nblk, nb), dim3(1024), lds1s, 0,
+                         bb, mp, 16u, p.T << p.sub, seg, ent, build_stores());
+    else
+      hipLaunchKernelGGL((k_build_part<KEY_FIXED16, MOD_POW2_32, 4>), dim3(p.nblk, nb), dim3(1024), lds1, 0, bb, mp,
+                         p.tb, p.T, seg, ent, build_stores());
   };
+  const bool longruns = 2ull * p.C > 48ull * p.T;  // launch_build_batch's choice
+  auto launch_tile = [&] {
+    if (p.sub)
+      hipLaunchKernelGGL((k_build_tile_sub<8, 2, 2, 512>), dim3(p.T, nb), dim3(512), lds2, 0, bb, p.tb, p.T, seg,
+                         p.nblk, reinterpret_cast<const uint16_t*>(ent), 2 * p.C, build_stores());
+    else if (longruns)
+      hipLaunchKernelGGL((k_build_tile<8, 2>), dim3(p.T, nb), dim3(1024), lds2, 0, bb, p.tb, p.T, seg, p.nblk, ent,
+                         2 * p.C, build_stores());
+    else
+      hipLaunchKernelGGL((k_build_tile<16, 1>), dim3(p.T, nb), dim3(1024), lds2, 0, bb, p.tb, p.T, seg, p.nblk, ent,
+                         2 * p.C, build_stores());
+  };
+  allow_lds(k_build_tile<8, 2>, lds2);
+  allow_lds(k_build_tile<16, 1>, lds2);
   const float part = per_launch_us(launch_part, 50);
-  const float tile = per_launch_us([&] {
-    hipLaunchKernelGGL(k_build_tile<16>, dim3(p.T, 1), dim3(1024), lds2, 0, bb, p.tb, p.T, seg, p.nblk, ent,
-                       2 * p.C, build_stores());
-  }, 50);
+  const float tile = per_launch_us(launch_tile, 50);
   printf("\"empty_part_grid_us\": %.2f, \"empty_tile_grid_us\": %.2f, \"build_step_us\": %.2f, "
          "\"part_alone_us\": %.2f, \"tile_alone_us\": %.2f, ", e1, e2, full, part, tile);
 
   uint64_t* st;
-  const uint32_t nst_blocks = std::max(p.nblk, p.T);
+  const uint32_t nst_blocks = std::max(p.nblk, p.T) * nb;
   CHECK(hipMalloc(&st, (size_t)nst_blocks * 8 * 8));
   CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st)));
   std::vector<uint64_t> h((size_t)nst_blocks * 8);
@@ -138,13 +169,12 @@ int main() {
   launch_part();
   CHECK(hipDeviceSynchronize());
   CHECK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
-  phases("part_stamps", h, p.nblk, 6, false);
+  phases("part_stamps", h, p.nblk * nb, 6, false);
   CHECK(hipMemset(st, 0, (size_t)nst_blocks * 64));
-  hipLaunchKernelGGL(k_build_tile<16>, dim3(p.T, 1), dim3(1024), lds2, 0, bb, p.tb, p.T, seg, p.nblk, ent,
-                     2 * p.C, build_stores());
+  launch_tile();
   CHECK(hipDeviceSynchronize());
   CHECK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
-  phases("tile_stamps", h, p.T, 5, true);
+  phases("tile_stamps", h, p.T * nb, 5, true);
   printf("}\n");
   return 0;
 }
