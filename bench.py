@@ -1147,15 +1147,18 @@ def c4_roofline(leg, world):
     us = leg["region_us_per_step"]
     ach = per_gpu / (us * 1e-6) / 1e9
     r = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-         "frac": round(ach / HBM_PEAK_GBS, 4), "kernel": "k_build_part+k_build_tile",
+         "frac": round(ach / HBM_PEAK_GBS, 4), "kernel": "k_build_part+k_build_tile(_sub)",
          "kernel_avg_us": us, "kernel_avg_source": "HIP events around the timed region / K (lanes overlap)",
          "algorithmic_bytes": int(per_gpu),
          "algorithmic_def": "filters_this_gpu x (16 B x 2^18 keys + 2^25/8 B) (SURVEY.md §8d C4 row)",
          "frac_one_lane": round(per_gpu / (leg["one_lane_us_per_step"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
-    t = 0
-    for k in ("k_build_part", "k_build_tile"):
-        v = _pmc_traffic(k, "pmc_c4_r[0-9]*.json")
-        t = t + v if (v and t is not None) else None
+    # per step: the PMC summary is per launch, and a step is one launch pair
+    # per batch of up to 32 filters (the tile pass is k_build_tile_sub for
+    # C4's batched long runs, k_build_tile otherwise)
+    pairs = -(-leg["filters_this_gpu"] // 32)
+    part = _pmc_traffic("k_build_part", "pmc_c4_r[0-9]*.json")
+    tile = _pmc_traffic("k_build_tile_sub", "pmc_c4_r[0-9]*.json") or _pmc_traffic("k_build_tile", "pmc_c4_r[0-9]*.json")
+    t = pairs * (part + tile) if (part and tile) else None
     r["traffic"] = t if world == 1 else None
     if r["traffic"]:
         r["traffic_over_algorithmic"] = round(t / per_gpu, 3)
