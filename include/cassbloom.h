@@ -337,7 +337,11 @@ int cb_table_search_var(const cb_table* t, const uint8_t* bytes, const uint64_t*
  * waiting (keys, hits, which, val_off and vals must then be device memory;
  * val_off[n] holds the total once the stream has run, and vals is written
  * only if cap >= that total). Calls that repeat the same tables and hit_rows
- * upload nothing, so batches on two streams overlap. */
+ * upload nothing, so batches on two streams overlap. A well-formed table's
+ * first get_many (this or cb_set_get_many) also enqueues the build of its key
+ * buckets on that call's stream (device memory: 128 B per line, rounded up
+ * to a power of two lines; freed with the table); later calls on other
+ * streams use them once that build has run. */
 int cb_get_many_fixed(const cb_table* const* tables, uint32_t nt, const uint64_t* hits,
                       const uint32_t* hit_rows, const uint8_t* keys, uint32_t key_len, uint64_t n,
                       int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap,
