@@ -282,7 +282,19 @@ int insert_locked(Workspace& ws, cb_filter* f, const uint8_t* keys, const uint64
 
   const int path = choose_build_path(f->m, n);
   g_last_path = path;
-  if (path == PATH_DIRECT) {
+  if (path == PATH_DIRECT && f->m <= cb::kInsertLdsMaxBits) {
+    // small filters (the product's m = 1024): the batch ORed in LDS; a fresh
+    // filter built by one block is written whole, without a fill first
+    const bool store_all = f->known_zero && n <= cb::kInsertLdsOneBlock;
+    if (store_all) {
+      std::lock_guard<std::mutex> lk(f->zero_mu);
+      f->needs_zero.store(false);
+      f->needs_pad_zero.store(false);
+    } else {
+      HIP_TRY(ensure_zeroed(f, s));
+    }
+    HIP_TRY(cb::launch_insert_lds(sk.keyk, f->mode, f->words, f->m, f->nwords_alloc, sk.ks, n, f->mp, store_all, s));
+  } else if (path == PATH_DIRECT) {
     HIP_TRY(ensure_zeroed(f, s));
     HIP_TRY(cb::launch_insert_direct(sk.keyk, f->mode, f->words, sk.ks, n, f->mp, s));
   } else {

@@ -409,10 +409,11 @@ uint32_t bin_group_target(uint64_t n) {
 int enqueue_format(cb_table* t, Workspace& ws, const TablePending& p, cb::CreateResult* dr, hipStream_t s) {
   const uint64_t n = p.n;
   uint64_t* tsum = (uint64_t*)ws.f_tsum.p;
-  HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
+  const bool inline_scan = cb::format_tiles(n) <= cb::kFormatInlineTiles;  // small flushes: no scan launch
+  if (!inline_scan) HIP_TRY(cb::launch_tile_scan(tsum, cb::format_tiles(n), &dr->len, s));
   HIP_TRY(cb::launch_format((const cb::SortKey*)ws.f_sk2.p, p.dk, p.dko, p.dv, p.dvo, tsum, n, t->data, t->rec,
                             t->pfx, t->fence, t->llen, dr, p.cap_bytes, s, (const ulonglong2*)ws.f_vsp.p, t->dir,
-                            t->dir ? dmap_slot(t) : nullptr));
+                            t->dir ? dmap_slot(t) : nullptr, inline_scan));
   return CB_OK;
 }
 

@@ -240,6 +240,12 @@ __device__ __forceinline__ uint32_t line16(uint64_t w0, uint64_t w1, uint32_t kl
 // writes its bytes directly.
 constexpr uint32_t kFormatLdsSmall = 16384, kFormatLdsLarge = 32768;
 
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 // SsTable::create's file and everything derived from it, one lane per entry p
 // (= line p; entries in key order):
 // - the line `key \t base64(value) \n` at its offset: the tile sums before
@@ -266,8 +272,9 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
                                                 uint64_t* __restrict__ pfx, uint64_t* __restrict__ fence,
                                                 uint32_t* __restrict__ llen_out,
                                                 CreateResult* r, const ulonglong2* __restrict__ vsp,
-                                                uint32_t* __restrict__ dir, DirMap* dmap_out) {
+                                                uint32_t* __restrict__ dir, DirMap* dmap_out, uint32_t inline_nt) {
   __shared__ uint32_t stage32[LDSB / 4];
+  __shared__ uint64_t s_base;
   __shared__ DirMap sdm;  // the directory's map, indexed per lane
   uint8_t* stage = reinterpret_cast<uint8_t*>(stage32);
   // The bin sort could not place every record (a group outgrew its LDS tile,
@@ -309,7 +316,24 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   // us after a sort.)
   uint64_t total;
   const uint64_t pre = block_scan<kNT>(live ? line_len(kl, vl) : 0, &total);
-  const uint64_t base = tsum[blockIdx.x];  // k_tile_scan: the tiles before
+  uint64_t base;
+  if (inline_nt) {
+    // small batches (<= 64 tiles): the raw tile sums, scanned here by wave 0
+    // instead of by a k_tile_scan launch; block 0 also writes the file length
+    if (threadIdx.x < 64) {
+      const uint64_t v = threadIdx.x < inline_nt ? tsum[threadIdx.x] : 0;
+      const uint64_t before = wave_sum_u64(threadIdx.x < blockIdx.x ? v : 0);
+      const uint64_t all = wave_sum_u64(v);
+      if (threadIdx.x == 0) {
+        s_base = before;
+        if (blockIdx.x == 0) r->len = all;
+      }
+    }
+    __syncthreads();
+    base = s_base;
+  } else {
+    base = tsum[blockIdx.x];  // k_tile_scan: the tiles before
+  }
   const uint64_t o = base + pre;
   bool special = false, not_inc = false;
   if (live) {
@@ -444,17 +468,20 @@ hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, uint32_t* llen,
                          CreateResult* r, uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp,
-                         uint32_t* dir, DirMap* dmap_out) {
+                         uint32_t* dir, DirMap* dmap_out, bool inline_scan) {
   if (!n) return hipSuccess;
   if (dir && !dmap_out) return hipErrorInvalidValue;
+  const uint64_t nb = blocks_for(n, kNT);
+  if (inline_scan && nb > kFormatInlineTiles) return hipErrorInvalidValue;
+  const uint32_t inl = inline_scan ? (uint32_t)nb : 0u;
   ProfScope ps("k_format", s);
-  const dim3 g(blocks_for(n, kNT));
+  const dim3 g((uint32_t)nb);
   if (bytes_bound / n * kNT * 5 / 4 <= kFormatLdsSmall)
     hipLaunchKernelGGL(k_format<kFormatLdsSmall>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
-                       rec, pfx, fence, llen, r, order ? vsp : nullptr, dir, dmap_out);
+                       rec, pfx, fence, llen, r, order ? vsp : nullptr, dir, dmap_out, inl);
   else
     hipLaunchKernelGGL(k_format<kFormatLdsLarge>, g, dim3(kNT), 0, s, order, kb, ko, vb, vo, tsum, n, out,
-                       rec, pfx, fence, llen, r, order ? vsp : nullptr, dir, dmap_out);
+                       rec, pfx, fence, llen, r, order ? vsp : nullptr, dir, dmap_out, inl);
   return hipGetLastError();
 }
 

@@ -136,10 +136,14 @@ hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, ui
 // dir (nullable, with dmap_out): the table's directory, its DirMap derived
 // from r->dmask (make_dirmap(dmask, n)) and stored at dmap_out, written here
 // from the lines' prefixes (what launch_table_dir would build).
+// inline_scan (batches of <= kFormatInlineTiles 256-line tiles): tsum holds
+// the raw tile sums and k_format scans them itself (and writes r->len), so no
+// launch_tile_scan goes first: the product's 1024-entry flushes save a launch.
+constexpr uint64_t kFormatInlineTiles = 64;
 hipError_t launch_format(const SortKey* order, const uint8_t* kb, const uint64_t* ko,
                          const uint8_t* vb, const uint64_t* vo, const uint64_t* tsum, uint64_t n,
                          uint8_t* out, LineRec* rec, uint64_t* pfx, uint64_t* fence, uint32_t* llen,
                          CreateResult* r, uint64_t bytes_bound, hipStream_t s, const ulonglong2* vsp = nullptr,
-                         uint32_t* dir = nullptr, DirMap* dmap_out = nullptr);
+                         uint32_t* dir = nullptr, DirMap* dmap_out = nullptr, bool inline_scan = false);
 
 }  // namespace cb

@@ -21,6 +21,7 @@
 // runs [seg[b][t], seg[b][t+1]) of every block b.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "blockscan.hpp"
@@ -150,6 +151,36 @@ __global__ __launch_bounds__(kBlock) void k_insert_direct(uint32_t* __restrict__
     key_positions<KEYK, MODE>(ks, k, mp, a, b);
     atomicOr(&words[a >> 5], 1u << (a & 31));  // src/bloom.rs:42
     atomicOr(&words[b >> 5], 1u << (b & 31));  // src/bloom.rs:43
+  }
+}
+
+// Filters of at most 2^19 bits (the product's m = 1024 flushes): the filter
+// kept in LDS per block, so 2n ORs land in LDS instead of contending on
+// m/32 words of HBM (1024 keys into m = 1024 by global atomics took 27.5 us,
+// every word taking ~64 serialised memory-side atomics). store_all: one
+// block on a fresh filter writes every allocated word (zeros past nw), so the
+// filter needs no fill first; otherwise each block ORs its non-zero words in.
+template <int KEYK, int MODE>
+__global__ __launch_bounds__(1024) void k_insert_lds(uint32_t* __restrict__ words, uint32_t nw, uint32_t nw_alloc,
+                                                    KeySrc ks, uint64_t n, ModP mp, uint32_t store_all) {
+  extern __shared__ uint32_t lw[];
+  for (uint32_t i = threadIdx.x; i < nw; i += 1024) lw[i] = 0;
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * 1024;
+  for (uint64_t k = (uint64_t)blockIdx.x * 1024 + threadIdx.x; k < n; k += stride) {
+    uint64_t a, b;
+    key_positions<KEYK, MODE>(ks, k, mp, a, b);
+    atomicOr(&lw[a >> 5], 1u << (a & 31));  // src/bloom.rs:42
+    atomicOr(&lw[b >> 5], 1u << (b & 31));  // src/bloom.rs:43
+  }
+  __syncthreads();
+  if (store_all) {
+    for (uint32_t i = threadIdx.x; i < nw_alloc; i += 1024) words[i] = i < nw ? lw[i] : 0u;
+  } else {
+    for (uint32_t i = threadIdx.x; i < nw; i += 1024) {
+      const uint32_t v = lw[i];
+      if (v) atomicOr(&words[i], v);
+    }
   }
 }
 
@@ -978,6 +1009,26 @@ hipError_t launch_insert_direct(int keyk, int mode, uint32_t* words, const KeySr
   CB_DISPATCH(keyk, mode,
               hipLaunchKernelGGL((k_insert_direct<KK, MM>), dim3(grid), dim3(kBlock), 0, s, words,
                                  ks, n, mp));
+  return hipGetLastError();
+}
+
+template <int KK, int MM>
+static void insert_lds(uint32_t* words, uint32_t nw, uint32_t nw_alloc, const KeySrc& ks, uint64_t n, const ModP& mp,
+                       bool store_all, uint32_t grid, size_t lds, hipStream_t s) {
+  allow_lds(k_insert_lds<KK, MM>, lds);
+  hipLaunchKernelGGL((k_insert_lds<KK, MM>), dim3(grid), dim3(1024), lds, s, words, nw, nw_alloc, ks, n, mp,
+                     store_all ? 1u : 0u);
+}
+
+hipError_t launch_insert_lds(int keyk, int mode, uint32_t* words, uint64_t m, uint64_t nw_alloc, const KeySrc& ks,
+                             uint64_t n, const ModP& mp, bool store_all, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t nw = (m + 31) / 32;
+  if (m > kInsertLdsMaxBits || nw_alloc < nw) return hipErrorInvalidValue;
+  const uint32_t grid = store_all ? 1u : (uint32_t)std::min<uint64_t>(128, (n + 8191) / 8192);
+  const size_t lds = nw * 4;
+  ProfScope ps("k_insert_lds", s);
+  CB_DISPATCH(keyk, mode, (insert_lds<KK, MM>(words, (uint32_t)nw, (uint32_t)nw_alloc, ks, n, mp, store_all, grid, lds, s)));
   return hipGetLastError();
 }
 

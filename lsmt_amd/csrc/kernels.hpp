@@ -59,6 +59,14 @@ size_t probe_lkey_bytes(const TilePlan& p);
 
 hipError_t launch_insert_direct(int keyk, int mode, uint32_t* words, const KeySrc& ks, uint64_t n,
                                 const ModP& mp, hipStream_t s);
+// Filters of m <= kInsertLdsMaxBits: the batch ORed into an LDS copy per
+// block. store_all (a fresh filter, n <= kInsertLdsOneBlock): one block writes
+// all nw_alloc words, so no fill is needed first; otherwise the words must be
+// initialised and each block ORs its non-zero words in.
+constexpr uint64_t kInsertLdsMaxBits = 1ull << 19;
+constexpr uint64_t kInsertLdsOneBlock = 8192;
+hipError_t launch_insert_lds(int keyk, int mode, uint32_t* words, uint64_t m, uint64_t nw_alloc, const KeySrc& ks,
+                             uint64_t n, const ModP& mp, bool store_all, hipStream_t s);
 hipError_t launch_probe_direct(int keyk, int mode, const FilterPtrs& fp, uint32_t nf,
                                const KeySrc& ks, uint64_t n, const ModP& mp, uint64_t* hits,
                                uint64_t hwords, hipStream_t s);
