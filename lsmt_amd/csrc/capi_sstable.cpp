@@ -71,6 +71,9 @@ int table_buckets(cb_table* t, hipStream_t s, cb::TableView* v) {
       return CB_OK;
     }
     t->bkbits = bits;
+    // a failure past the allocation leaves the table without buckets for good
+    // (the block is freed with the table) and reports the error once
+    t->bkt_state.store(-1, std::memory_order_relaxed);
     HIP_TRY(hipMemsetAsync(t->bkt, 0xFF, bytes, s));
     HIP_TRY(cb::launch_table_buckets(t->rec, t->nlines, t->bkt, bits, s));
     HIP_TRY(hipEventCreateWithFlags(&t->bkt_ev, hipEventDisableTiming | hipEventDisableSystemFence));
