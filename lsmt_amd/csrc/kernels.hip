@@ -959,8 +959,9 @@ TilePlan plan_build(uint64_t m, uint64_t n, uint32_t nb) {
   // three (profiles/c4_sub_r04.json).
   static const int env_sub = env_int("CB_BUILD_SUB", -1);
   p.sub = 0;
-  if (env_sub != 0 && nb >= 8 && p.tb >= 17 && 2ull * p.C > 48ull * p.T) {
-    if (p.tb == 19 && !env_tb && 2ull * p.C > 48ull * 2 * p.T && ((uint64_t)p.T << 3) <= kMaxTiles) {
+  // (CB_BUILD_SUB=1, experiment builds: every build of tb >= 17 takes them)
+  if (env_sub != 0 && p.tb >= 17 && ((nb >= 8 && 2ull * p.C > 48ull * p.T) || env_sub == 1)) {
+    if (p.tb == 19 && !env_tb && (2ull * p.C > 48ull * 2 * p.T || env_sub == 1) && ((uint64_t)p.T << 3) <= kMaxTiles) {
       p.tb = 18;
       p.T = (uint32_t)((m + (1ull << 18) - 1) >> 18);
     }
