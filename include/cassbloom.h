@@ -121,7 +121,8 @@ int cb_probe_var(const cb_filter* const* filters, uint32_t nf, const uint8_t* by
 int cb_may_contain(const cb_filter* f, const uint8_t* key, uint64_t len, int* out);
 /* Host mirror policy: 1 on, 0 off, -1 auto (the default: on when m <= 2^24,
  * i.e. up to 2 MiB of host words; past that a write records no event, and
- * the first refresh after the mirror is turned on synchronises the device). */
+ * the first refresh after the mirror is turned on synchronises the stream that
+ * write was issued on, not the device). */
 int cb_filter_host_mirror(cb_filter* f, int mode);
 /* *on = whether cb_may_contain uses the mirror; *current = whether the mirror
  * already holds the latest write (either may be NULL). Host only. */
@@ -193,8 +194,9 @@ int cb_set_load_meta(cb_filterset* set, uint32_t slot, const uint8_t* in, uint64
  * real shape — a table per 1024 inserts (src/lib.rs:72,105), hundreds of
  * m = 1024 filters — in one launch: cb_set_get_many_* take up to `width`
  * tables. Its probe reads row b's word only where row a's is non-zero (the
- * reference's `&&`, src/bloom.rs:50). cb_set_probe_pack_fixed and
- * cb_set_probe_allgather_fixed take sets of at most 64 slots. */
+ * reference's `&&`, src/bloom.rs:50). cb_set_probe_pack_fixed takes sets of
+ * at most 64 slots; cb_set_probe_allgather_fixed takes wide sets when every
+ * rank's shard is past 64 rows (below). */
 int cb_set_create(uint64_t m_bits, uint32_t width, int device, cb_filterset** out);
 int cb_set_destroy(cb_filterset* set);
 /* used = 1 + the highest slot assigned so far (the number of hit rows). */
@@ -466,7 +468,10 @@ int cb_hits_allgather(cb_comm* c, const uint64_t* local, uint64_t rows, uint64_t
  * pack (no separate compress pass): positions as cb_hits_compress's, with
  * one directory entry per probe block of 16 hit words of every slot
  * (cb_set_pack_words). ok / sparse_used / overflow as cb_hits_allgather.
- * gated != 0 applies the zone gate (cb_set_probe_gated_fixed). */
+ * gated != 0 applies the zone gate (cb_set_probe_gated_fixed). When the
+ * largest shard passes 64 rows (wide sets), sparse mode probes first and
+ * then runs cb_hits_allgather's sparse exchange (a separate compress pass);
+ * every rank must then hold such a shard, as the shard split guarantees. */
 int cb_set_probe_allgather_fixed(cb_comm* c, const cb_filterset* set, const uint8_t* keys, uint32_t key_len,
                                  uint64_t n, int gated, uint64_t* local_hits, uint64_t total_rows,
                                  uint64_t* full, int mode, uint64_t cap, uint32_t* ok, int* sparse_used,

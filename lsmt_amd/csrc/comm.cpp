@@ -444,7 +444,16 @@ int cb_set_probe_allgather_fixed(cb_comm* c, const cb_filterset* set, const uint
   }
   if (!cap) return fail(CB_EINVAL, "sparse exchange needs cap > 0");
   const uint64_t max_rows = (total_rows + (uint64_t)c->world - 1) / (uint64_t)c->world;
-  if (max_rows > 64) return fail(CB_EINVAL, "more than 64 rows per rank");
+  if (max_rows > 64) {
+    // shards past 64 tables (wide sets: the product's hundreds of m = 1024
+    // tables over a few GPUs): the probe writes the rows, then the separate
+    // compress and the same sparse all-gather (every rank takes this branch:
+    // max_rows is the same everywhere)
+    int rc = set_probe_device(set, keys, key_len, n, gated != 0, local_hits, nullptr, 0, s);
+    if (rc) return rc;
+    return cb_hits_allgather(c, local_hits, rows, hwords, total_rows, full, CB_XCHG_SPARSE, cap, ok, sparse_used,
+                             stream);
+  }
   if (max_rows * hwords * 64 >= (1ull << 32)) return fail(CB_EINVAL, "rows * ceil(n/64) * 64 must be below 2^32");
   const uint64_t nblk = cb::set_probe_blocks(n);
   const size_t pack_words = 2 + cap + 2 * nblk;  // equal on every rank

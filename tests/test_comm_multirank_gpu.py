@@ -331,3 +331,54 @@ def test_host_transport_processes(gpu, world, nf):
     assert not alive and all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     got = dict(q.get(timeout=5) for _ in range(world))
     assert all(got[r] for r in range(world)), got
+
+
+@pytest.mark.parametrize("world,nf", [(2, 150), (3, 200)])
+@pytest.mark.parametrize("mode", ["dense", "sparse", "sparse_async"])
+def test_loopback_probe_allgather_wide(gpu, world, nf, mode):
+    """Shards past 64 tables per rank (wide FilterSets of 128 slots): the
+    probe and the exchange in one call per rank — the sparse form probing
+    first and compressing the rows separately — equal to the oracle's
+    unsharded probe on every rank."""
+    import torch
+
+    import lsmt_amd
+    from lsmt_amd.shard import Comm
+    gf, expect, look = _filters(nf)
+    keys = torch.from_numpy(look).cuda()
+    words = (N + 63) // 64
+    comms = Comm.loopback(world, 0)
+    sets = []
+    for r in range(world):
+        lo, hi = shard_range(nf, world, r)
+        assert hi - lo > 64
+        s = lsmt_amd.FilterSet(M, 128)
+        s.assign_all(gf[lo:hi])
+        sets.append(s)
+    torch.cuda.synchronize()
+    cap = sparse_cap(N, nf, world)
+    streams = [torch.cuda.Stream() for _ in range(world)]
+    fulls = [torch.full((nf, words), -1, dtype=torch.int64, device="cuda") for _ in range(world)]
+    locs = [torch.full((shard_range(nf, world, r)[1] - shard_range(nf, world, r)[0], words), -1,
+                       dtype=torch.int64, device="cuda") for r in range(world)]
+    oks = [torch.ones(1, dtype=torch.int32, device="cuda") for _ in range(world)]
+
+    def rank(r):
+        ok = oks[r] if mode.endswith("async") else None
+        used = comms[r].probe_allgather(sets[r], keys, nf, locs[r], fulls[r], sparse=mode != "dense", cap=cap,
+                                        ok=ok, stream=streams[r])
+        streams[r].synchronize()
+        return used
+
+    try:
+        used = _run_ranks(world, rank)
+        assert all(u == (mode != "dense") for u in used), used
+        for r in range(world):
+            lo, hi = shard_range(nf, world, r)
+            assert np.array_equal(locs[r].cpu().numpy().view(np.uint64), expect[lo:hi]), f"rank {r} rows"
+            assert np.array_equal(fulls[r].cpu().numpy().view(np.uint64), expect), f"rank {r} map"
+            if mode == "sparse_async":
+                assert int(oks[r].item()) == 1
+    finally:
+        for c in comms:
+            c.close()
