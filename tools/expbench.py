@@ -14,7 +14,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-EXP = os.path.join(ROOT, "build", "exp", "libcassbloom.so")
+EXP = os.environ.get("EXPBENCH_LIB") or os.path.join(ROOT, "build", "exp", "libcassbloom.so")  # another build to A/B
 
 spec = importlib.util.spec_from_file_location("lsmt_amd._lib", os.path.join(ROOT, "lsmt_amd", "_lib.py"))
 _lib = importlib.util.module_from_spec(spec)
