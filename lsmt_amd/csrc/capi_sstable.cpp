@@ -63,7 +63,7 @@ int table_buckets(cb_table* t, hipStream_t s, cb::TableView* v) {
   st = t->bkt_state.load(std::memory_order_relaxed);
   if (st == 0) {
     const uint32_t bits = cb::bkt_bits(t->nlines);
-    const size_t bytes = ((size_t)1 << bits) * cb::kBktWords * 8;
+    const size_t bytes = (size_t)cb::bkt_bytes(bits);  // the buckets and their summary words
     if (pool_alloc(t->device, bytes, (void**)&t->bkt, &t->bkt_cap) != hipSuccess) {
       t->bkt = nullptr;
       (void)hipGetLastError();

@@ -504,11 +504,17 @@ constexpr uint32_t kRecWin = 2;  // ... of up to this many: the records alone (3
 // complete bucket), or kBktGoOn (the directory search decides).
 constexpr int64_t kBktFound = INT64_MAX;
 constexpr int64_t kBktGoOn = -2;
-__device__ __forceinline__ int64_t bucket_probe(const TableView& t, const Query& q, LineRec& hit) {
+// The bucket's first 16 bytes (its count and slot 0's prefix) for key word
+// w0: what bucket_probe reads first.
+__device__ __forceinline__ u64x2 bucket_head(const TableView& t, uint64_t w0) {
+  return *(g64x2)(t.bkt + bkt_index(w0, t.bkbits()) * kBktWords);
+}
+
+// bucket_probe with its first load (bucket_head) already made.
+__device__ __forceinline__ int64_t bucket_probe_from(const TableView& t, const Query& q, LineRec& hit, u64x2 a) {
   const uint64_t* b = t.bkt + bkt_index(q.w0, t.bkbits()) * kBktWords;
   // the count and slot 0 first (at one line per bucket on average, most keys
   // are in slot 0), the next pairs only when needed: fewer registers live
-  const u64x2 a = *(g64x2)(b);
   const uint64_t cnt = a.x + 1;  // all-ones: empty
   uint32_t c = 0;
   if (cnt == 0 || a.y != q.w0) {
@@ -535,6 +541,10 @@ __device__ __forceinline__ int64_t bucket_probe(const TableView& t, const Query&
     return kBktFound;
   }
   return kBktGoOn;  // another line with this prefix may be the one
+}
+
+__device__ __forceinline__ int64_t bucket_probe(const TableView& t, const Query& q, LineRec& hit) {
+  return bucket_probe_from(t, q, hit, bucket_head(t, q.w0));
 }
 
 // Where x's descent starts: level j and the run [lo, hi) of at most 16
@@ -691,6 +701,20 @@ __global__ __launch_bounds__(kNT) void k_table_buckets(const LineRec* __restrict
     b[6 + 2 * s] = r.pfx2;
     b[7 + 2 * s] = r.start | ((uint64_t)r.klen << 40) | ((uint64_t)r.vdl << 52);
   }
+}
+
+// The buckets' summary words (sstable.hpp bkt_fp), one lane per bucket,
+// after k_table_buckets.
+__global__ __launch_bounds__(kNT) void k_table_bucket_fp(uint64_t* __restrict__ bkt, uint32_t bits) {
+  const uint64_t nbk = 1ull << bits;
+  const uint64_t i = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  if (i >= nbk) return;
+  const uint64_t* b = bkt + i * kBktWords;
+  const uint64_t cnt = b[0] + 1;  // all-ones: empty
+  uint64_t f = cnt <= kBktSlots ? cnt : 15u;
+  if (f != 15u)
+    for (uint32_t s = 0; s < (uint32_t)cnt; ++s) f |= (uint64_t)bkt_fp(b[1 + s]) << (4 + 15 * s);
+  bkt[nbk * kBktWords + i] = f;
 }
 
 // A block's views of the first min(nt, 64) tables into LDS. Barrier inside.
@@ -982,15 +1006,35 @@ __global__ __launch_bounds__(kNT, 5) void k_wide_get_many(const uint64_t* __rest
         if (!wide_zone_ok<KEYK>(z, s, kw, q.p, q.len)) cand &= ~(1ull << i);
       }
     }
-    // the candidates newest first, the group's views and maps from LDS
+    // the candidates newest first, the group's views and maps from LDS. At
+    // the product's m = 1024 most candidates are false positives (~3/4 of
+    // the tables pass the Bloom gate); each is settled by its key bucket's
+    // 8-byte summary word (sstable.hpp bkt_fp), which stays in the L2s,
+    // before any bucket line is read (a complete bucket without the key's
+    // fingerprint: Ok(None)). Loading the words of 2 or 4 candidates at once
+    // measured the same (profiles/wide_summary_r04.json).
+    const uint32_t kfp = bkt_fp(q.w0);
     while (cand) {
       const uint32_t i = (uint32_t)__builtin_ctzll(cand);
       cand &= cand - 1;
+      const TableView& v = stv[i];
+      if (v.bkt && v.fast()) {
+        const uint32_t bits = v.bkbits();
+        const uint64_t sw = g64(v.bkt, (1ull << bits) * kBktWords + bkt_index(q.w0, bits));
+        const uint32_t nst = (uint32_t)(sw & 15u);
+        if (nst <= kBktSlots) {
+          bool fpm = false;
+#pragma unroll
+          for (uint32_t s = 0; s < kBktSlots; ++s)
+            fpm |= s < nst && (uint32_t)((sw >> (4 + 15 * s)) & 0x7FFFu) == kfp;
+          if (!fpm) continue;  // Ok(None)
+        }
+      }
       LineRec r;
-      if (search(stv[i], q, r, &sdm[i]) < 0) continue;  // Ok(None)
-      if (r.vdl == kBadValue) continue;                  // Err(..) is skipped by `if let Ok(Some(v))`
+      if (search(v, q, r, &sdm[i]) < 0) continue;  // Ok(None)
+      if (r.vdl == kBadValue) continue;             // Err(..) is skipped by `if let Ok(Some(v))`
       w = (int32_t)(t0 + i);
-      src = (uint64_t)(uintptr_t)(stv[i].data + r.start + r.klen + 1);
+      src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
       d = r.vdl;
       active = false;
       break;
@@ -1263,6 +1307,7 @@ hipError_t launch_table_buckets(const LineRec* rec, uint64_t nlines, uint64_t* b
   if (!nlines) return hipSuccess;
   ProfScope ps("k_table_buckets", s);
   hipLaunchKernelGGL(k_table_buckets, dim3(blocks_for(nlines, kNT)), dim3(kNT), 0, s, rec, nlines, bkt, bits);
+  hipLaunchKernelGGL(k_table_bucket_fp, dim3(blocks_for(1ull << bits, kNT)), dim3(kNT), 0, s, bkt, bits);
   return hipGetLastError();
 }
 

@@ -344,8 +344,21 @@ __host__ __device__ inline uint32_t bkt_bits(uint64_t nlines) {
 __host__ __device__ inline uint64_t bkt_index(uint64_t pfx0, uint32_t bits) {
   return (pfx0 * 0x9E3779B97F4A7C15ull) >> (64 - bits);
 }
-// Buckets of a fast table from its records; bkt (2^bits * 128 B) must be
-// all-ones first (the caller's memset).
+// After the buckets, one 8-byte summary word per bucket (the wide read path
+// settles its many false-positive candidates from these alone: 8 B per
+// bucket stay in the L2s where the 128-B buckets would be fetched from the
+// Infinity Cache): bits 0-3 the stored count, 0-4, or 15 when the bucket is
+// not complete (more than four lines, or a line left out); bits 4 + 15 s ..
+// 18 + 15 s slot s's 15-bit fingerprint of its prefix (bkt_fp). A complete
+// bucket none of whose fingerprints matches the key's proves absence.
+__host__ __device__ inline uint32_t bkt_fp(uint64_t pfx0) {
+  return (uint32_t)((pfx0 * 0xC2B2AE3D27D4EB4Full) >> 49);
+}
+__host__ __device__ inline uint64_t bkt_bytes(uint32_t bits) {
+  return ((uint64_t)1 << bits) * (kBktWords * 8 + 8);
+}
+// Buckets of a fast table from its records, then their summary words; bkt
+// (bkt_bytes(bits)) must be all-ones first (the caller's memset).
 hipError_t launch_table_buckets(const LineRec* rec, uint64_t nlines, uint64_t* bkt, uint32_t bits,
                                 hipStream_t s);
 
