@@ -89,14 +89,16 @@ def test_build_tile_block_balance(gpu, m, n):
         gpu.set_path(0)
 
 
-@pytest.mark.parametrize("m", [1 << 25, (1 << 25) + 12345, 3 << 23])
+@pytest.mark.parametrize("m", [1 << 25, (1 << 25) + 12345, 3 << 23, 1 << 22, 1 << 26])
 def test_batched_long_run_builds(gpu, m):
     """Batched builds of long runs take 16-bit entries in 2^16-bit sub-tiles
     (kernels.hip plan_build: C4's shape): 12 filters, ragged counts around
     2^18 keys, one of them a few keys repeated 60K times (super-runs past the
     two waves a tile workgroup loads at once), one already holding bits (the
-    tile loaded, not cleared), m a power of two or not. Each against the
-    oracle."""
+    tile loaded, not cleared), m a power of two or not. The m's take every
+    tile-kernel instantiation: 2^18-bit tiles of 4 sub-tiles (2^25, 3 2^23),
+    2^17-bit tiles of 2 (2^22) and 2^19-bit tiles of 8 (2^26). Each against
+    the oracle."""
     counts = [1 << 18, (1 << 18) - 1, 200_000, 150_000] + [240_000 + 997 * i for i in range(8)]
     keys = [workload.key_range(5000 + i, c) for i, c in enumerate(counts)]
     base = workload.key_range(77, 40)
