@@ -82,18 +82,20 @@ constexpr uint32_t K(uint32_t mul, int w, int p) {
   for (int j = 0; j < 4; ++j) k |= ((powm(mul, 15 - (4 * w + j)) >> (8 * p)) & 0xFFu) << (8 * j);
   return k;
 }
+// The seed term rides in plane 0's accumulator (the dot4 wraps mod 2^32,
+// clamp off) and the planes combine by shift-adds: three v_lshl_add_u32.
 template <uint32_t MUL, uint32_t SEED>
 __device__ __forceinline__ uint32_t fold(const uint4& v) {
+  constexpr uint32_t H0 = SEED * powm(MUL, 16);
   uint32_t acc[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    uint32_t a = __builtin_amdgcn_udot4(v.x, K(MUL, 0, p), 0u, false);
+    uint32_t a = __builtin_amdgcn_udot4(v.x, K(MUL, 0, p), p == 0 ? H0 : 0u, false);
     a = __builtin_amdgcn_udot4(v.y, K(MUL, 1, p), a, false);
     a = __builtin_amdgcn_udot4(v.z, K(MUL, 2, p), a, false);
     acc[p] = __builtin_amdgcn_udot4(v.w, K(MUL, 3, p), a, false);
   }
-  constexpr uint32_t H0 = SEED * powm(MUL, 16);
-  return H0 + acc[0] + (acc[1] << 8) + (acc[2] << 16) + (acc[3] << 24);
+  return acc[0] + (acc[1] << 8) + (acc[2] << 16) + (acc[3] << 24);
 }
 }  // namespace dot16
 

@@ -273,7 +273,89 @@ __device__ __forceinline__ void wave0_exclusive_scan4(uint32_t* arr, uint32_t le
   }
 }
 
+// A 16-byte key's two positions packed as partition entries ((bin << 20) |
+// offset in the bin, bins of 2^tb bits), 0xFFFFFFFF for both when !live.
+// 32-bit arithmetic where the positions are (MOD_POW2_32).
+template <int MODE>
+__device__ __forceinline__ void pack_positions(const uint4& kv, bool live, const ModP& mp, uint32_t tb, uint32_t& qa,
+                                               uint32_t& qb) {
+  const uint32_t tmask = (1u << tb) - 1u;
+  uint32_t a32, b32, ah, bh;
+  if constexpr (MODE == MOD_POW2_32) {
+    uint32_t h1, h2;
+    hash16_u32(kv, h1, h2);
+    const uint32_t mask = static_cast<uint32_t>(mp.mask);
+    a32 = h1 & mask;
+    b32 = h2 & mask;
+    ah = a32 >> tb;
+    bh = b32 >> tb;
+  } else {
+    uint64_t a, b;
+    key_positions_u4<MODE>(kv, mp, a, b);
+    a32 = (uint32_t)a;
+    b32 = (uint32_t)b;
+    ah = (uint32_t)(a >> tb);
+    bh = (uint32_t)(b >> tb);
+  }
+  qa = live ? (ah << 20) | (a32 & tmask) : 0xFFFFFFFFu;
+  qb = live ? (bh << 20) | (b32 & tmask) : 0xFFFFFFFFu;
+}
+
+// A partition block's LDS phases once its entries are in registers (q: packed
+// (bin << 20) | offset, 0xFFFFFFFF for none): ranks from LDS atomics, the bin
+// scan, the seg row (run starts and the total), the tile-sorted entries into
+// LDS and out to `out` as one contiguous region. Barriers inside; the block's
+// LDS is free again when it returns except for the final store's reads of
+// `stage` (the caller's next LDS write must follow a barrier).
 // pol: the store policy bits (build_stores(): bit 0 write-through entries).
+template <int KPT, typename E>
+__device__ __forceinline__ void part_phases(const uint32_t (&q)[2 * KPT], uint32_t T, uint32_t* smem,
+                                            uint32_t* __restrict__ srow, E* __restrict__ out, uint32_t pol) {
+  constexpr uint32_t NT = kBuildNT, C = NT * KPT;
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  const uint32_t Tp = (T + 4) & ~3u;
+  // hist: T + 1 entries (counts, then run starts and the total), zero to Tp,
+  // then a discard word at Tp for the lanes without an entry
+  uint32_t* hist = smem;
+  E* stage = reinterpret_cast<E*>(smem + Tp + 4);
+  const uint32_t tid = threadIdx.x;
+  uint32_t er[2 * KPT];
+  for (uint32_t i = tid; i < Tp; i += NT) hist[i] = 0;
+  __syncthreads();
+  CB_STAMP(1);
+  // every lane adds (no branch per entry, whose merges cost more VALU than
+  // the rare discards on the last block's padding)
+#pragma unroll
+  for (int e = 0; e < 2 * KPT; ++e) er[e] = atomicAdd(&hist[q[e] != kNone ? q[e] >> 20 : Tp], 1u);
+  __syncthreads();
+  CB_STAMP(2);
+  wave0_exclusive_scan4(hist, Tp);  // Tp >= T + 1: hist[T] = the total
+  __syncthreads();
+  CB_STAMP(3);
+  const uint32_t total = hist[T];
+  for (uint32_t t = tid; t <= T; t += NT) srow[t] = hist[t];
+#pragma unroll
+  for (int e = 0; e < 2 * KPT; ++e)
+    if (q[e] != kNone) stage[hist[q[e] >> 20] + er[e]] = (E)(q[e] & 0xFFFFFu);
+  __syncthreads();
+  CB_STAMP(4);
+  constexpr uint32_t PER = 16 / sizeof(E);  // entries per 16-B store (out and stage 16-B aligned)
+  const uint32_t n4 = total / PER;
+  // write-through (sc1): the entries go on to the memory side at once, so the
+  // kernel's end has no dirty L2 lines to write back, and the tile pass (on
+  // other XCDs) still finds them there; C2 on four lanes 101 -> 105-107 G
+  // keys/s (non-temporal stores instead made the tile pass's reads slower)
+  if (pol & 1u) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, 2 * C * sizeof(E), 0x00020000);
+    for (uint32_t i = tid; i < n4; i += NT) store16_wt(r, i * 16, reinterpret_cast<const uint4*>(stage)[i]);
+  } else {
+    for (uint32_t i = tid; i < n4; i += NT)
+      reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(stage)[i];
+  }
+  if (tid < total - PER * n4) out[PER * n4 + tid] = stage[PER * n4 + tid];  // the < PER left over
+  CB_STAMP(5);
+}
+
 // E: the entry type — uint32_t (offsets in tiles of up to 2^20 bits) or
 // uint16_t (bins of 2^16 bits, tb = 16 here: the sub-tiles of
 // k_build_tile_sub's tiles).
@@ -289,9 +371,6 @@ __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp,
   uint32_t* seg = seg_all + (size_t)blockIdx.y * gridDim.x * (T + 1);
   E* ent = reinterpret_cast<E*>(ent_all) + (size_t)blockIdx.y * gridDim.x * (2 * C);
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t Tp = (T + 4) & ~3u;
-  uint32_t* hist = smem;  // T + 1 entries: counts, then run starts and the total
-  E* stage = reinterpret_cast<E*>(smem + Tp);
   const uint32_t tid = threadIdx.x;
   const uint64_t kbase = (uint64_t)blockIdx.x * C;
   CB_STAMP(0);
@@ -302,54 +381,39 @@ __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp,
   // one register per entry instead of a 64-bit position and a tile.
   static_assert(kMaxTiles <= 4096 && kMaxTileBits <= 20, "packed entry");
   constexpr uint32_t kNone = 0xFFFFFFFFu;
-  const uint32_t tmask = (1u << tb) - 1u;
-  uint32_t q[2 * KPT], er[2 * KPT];
+  uint32_t q[2 * KPT];
+  if constexpr (KEYK == KEY_FIXED16) {
+    // every lane loads all its keys first (indices clamped to the last key,
+    // so no per-key branch serialises the loads behind each other's waits)
+    uint4 kv[KPT];
+    if (kbase < n) {  // uniform
+      const uint4* keys = reinterpret_cast<const uint4*>(ks.bytes);
 #pragma unroll
-  for (int j = 0; j < KPT; ++j) {
-    const uint64_t k = kbase + (uint64_t)j * NT + tid;
-    q[2 * j] = q[2 * j + 1] = kNone;
-    if (k < n) {
-      uint64_t a, b;
-      key_positions<KEYK, MODE>(ks, k, mp, a, b);
-      q[2 * j] = ((uint32_t)(a >> tb) << 20) | ((uint32_t)a & tmask);
-      q[2 * j + 1] = ((uint32_t)(b >> tb) << 20) | ((uint32_t)b & tmask);
+      for (int j = 0; j < KPT; ++j) {
+        const uint64_t k = kbase + (uint64_t)j * NT + tid;
+        kv[j] = keys[k < n ? k : n - 1];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const uint64_t k = kbase + (uint64_t)j * NT + tid;
+      pack_positions<MODE>(kv[j], k < n, mp, tb, q[2 * j], q[2 * j + 1]);
+    }
+  } else {
+    const uint32_t tmask = (1u << tb) - 1u;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const uint64_t k = kbase + (uint64_t)j * NT + tid;
+      q[2 * j] = q[2 * j + 1] = kNone;
+      if (k < n) {
+        uint64_t a, b;
+        key_positions<KEYK, MODE>(ks, k, mp, a, b);
+        q[2 * j] = ((uint32_t)(a >> tb) << 20) | ((uint32_t)a & tmask);
+        q[2 * j + 1] = ((uint32_t)(b >> tb) << 20) | ((uint32_t)b & tmask);
+      }
     }
   }
-  for (uint32_t i = tid; i < Tp; i += NT) hist[i] = 0;
-  __syncthreads();
-  CB_STAMP(1);
-#pragma unroll
-  for (int e = 0; e < 2 * KPT; ++e)
-    if (q[e] != kNone) er[e] = atomicAdd(&hist[q[e] >> 20], 1u);
-  __syncthreads();
-  CB_STAMP(2);
-  wave0_exclusive_scan4(hist, Tp);  // Tp >= T + 1: hist[T] = the total
-  __syncthreads();
-  CB_STAMP(3);
-  const uint32_t total = hist[T];
-  uint32_t* srow = seg + (size_t)blockIdx.x * (T + 1);
-  for (uint32_t t = tid; t <= T; t += NT) srow[t] = hist[t];
-#pragma unroll
-  for (int e = 0; e < 2 * KPT; ++e)
-    if (q[e] != kNone) stage[hist[q[e] >> 20] + er[e]] = (E)(q[e] & 0xFFFFFu);
-  __syncthreads();
-  CB_STAMP(4);
-  E* out = ent + (size_t)blockIdx.x * (2 * C);  // 16-B aligned, as is stage
-  constexpr uint32_t PER = 16 / sizeof(E);      // entries per 16-B store
-  const uint32_t n4 = total / PER;
-  // write-through (sc1): the entries go on to the memory side at once, so the
-  // kernel's end has no dirty L2 lines to write back, and the tile pass (on
-  // other XCDs) still finds them there; C2 on four lanes 101 -> 105-107 G
-  // keys/s (non-temporal stores instead made the tile pass's reads slower)
-  if (pol & 1u) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, 2 * C * sizeof(E), 0x00020000);
-    for (uint32_t i = tid; i < n4; i += NT) store16_wt(r, i * 16, reinterpret_cast<const uint4*>(stage)[i]);
-  } else {
-    for (uint32_t i = tid; i < n4; i += NT)
-      reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(stage)[i];
-  }
-  for (uint32_t i = PER * n4 + tid; i < total; i += NT) out[i] = stage[i];
-  CB_STAMP(5);
+  part_phases<KPT, E>(q, T, smem, seg + (size_t)blockIdx.x * (T + 1), ent + (size_t)blockIdx.x * (2 * C), pol);
 }
 
 // Wave w owns partition blocks b = w + NW*u. Per group of 16: lanes 0..15
@@ -1083,7 +1147,7 @@ hipError_t launch_build_batch(int keyk, int mode, const BuildBatch& bb, uint32_t
   if (!plan_ok(p) || nb > kMaxBuildBatch || p.nblk > kMaxBuildBlocks) return hipErrorInvalidValue;
   if (p.sub && (p.sub > 3 || p.tb != 16 + p.sub || ((uint64_t)p.T << p.sub) > kMaxTiles)) return hipErrorInvalidValue;
   const uint32_t TS = p.T << p.sub;  // partition bins
-  const size_t lds1 = (size_t)((TS + 4) & ~3u) * 4 + 2 * p.C * (p.sub ? 2 : 4);
+  const size_t lds1 = (size_t)(((TS + 4) & ~3u) + 4) * 4 + 2 * p.C * (p.sub ? 2 : 4);  // part_phases: hist, discard, stage
   {
     ProfScope ps("k_build_part", s);
     if (p.kpt == 1) {

@@ -115,7 +115,7 @@ int main(int argc, char** argv) {
   printf("{\"shape\": \"%s\", \"plan\": {\"tb\": %u, \"T\": %u, \"kpt\": %u, \"C\": %u, \"nblk\": %u, \"nb\": %u, \"sub\": %u}, ",
          c4 ? "c4" : "c2", p.tb, p.T, p.kpt, p.C, p.nblk, nb, p.sub);
 
-  const size_t lds1 = ((size_t)((p.T + 4) & ~3u) + 2 * p.C) * 4;
+  const size_t lds1 = ((size_t)((p.T + 4) & ~3u) + 4 + 2 * p.C) * 4;  // hist, discard word, stage
   const size_t lds2 = (size_t)(1u << (p.tb - 5)) * 4;
   allow_lds(k_empty, lds2 > lds1 ? lds2 : lds1);
   const float e1 = per_launch_us([&] { hipLaunchKernelGGL(k_empty, dim3(p.nblk, nb), dim3(1024), lds1, 0, dummy); }, 50);
@@ -129,7 +129,7 @@ int main(int argc, char** argv) {
     fprintf(stderr, "plan sub %u: this tool times sub = 0 or 2\n", p.sub);
     return 1;
   }
-  const size_t lds1s = (size_t)(((p.T << p.sub) + 4) & ~3u) * 4 + 2 * p.C * 2;
+  const size_t lds1s = (size_t)((((p.T << p.sub) + 4) & ~3u) + 4) * 4 + 2 * p.C * 2;
   allow_lds(k_build_part<KEY_FIXED16, MOD_POW2_32, 4>, lds1);
   allow_lds(k_build_part<KEY_FIXED16, MOD_POW2_32, 4, uint16_t>, lds1s);
   allow_lds((k_build_tile_sub<8, 2, 2, 512>), lds2);
