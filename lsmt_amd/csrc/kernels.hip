@@ -385,7 +385,7 @@ __global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp,
   if constexpr (KEYK == KEY_FIXED16) {
     // every lane loads all its keys first (indices clamped to the last key,
     // so no per-key branch serialises the loads behind each other's waits)
-    uint4 kv[KPT];
+    uint4 kv[KPT] = {};  // (a block past this filter's keys hashes zeros, all discarded)
     if (kbase < n) {  // uniform
       const uint4* keys = reinterpret_cast<const uint4*>(ks.bytes);
 #pragma unroll

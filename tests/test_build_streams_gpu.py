@@ -97,9 +97,11 @@ def test_batched_long_run_builds(gpu, m):
     two waves a tile workgroup loads at once), one already holding bits (the
     tile loaded, not cleared), m a power of two or not. The m's take every
     tile-kernel instantiation: 2^18-bit tiles of 4 sub-tiles (2^25, 3 2^23),
-    2^17-bit tiles of 2 (2^22) and 2^19-bit tiles of 8 (2^26). Each against
-    the oracle."""
-    counts = [1 << 18, (1 << 18) - 1, 200_000, 150_000] + [240_000 + 997 * i for i in range(8)]
+    2^17-bit tiles of 2 (2^22) and 2^19-bit tiles of 8 (2^26). Filters of 0,
+    1 and 5000 keys leave partition blocks with no keys of theirs (the
+    partition pass's clamped loads and discard word). Each against the
+    oracle."""
+    counts = [1 << 18, (1 << 18) - 1, 200_000, 150_000, 0, 1, 5000] + [240_000 + 997 * i for i in range(5)]
     keys = [workload.key_range(5000 + i, c) for i, c in enumerate(counts)]
     base = workload.key_range(77, 40)
     keys[2] = np.concatenate([keys[2], np.repeat(base[:3], 60_000, axis=0)])
