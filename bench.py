@@ -1158,13 +1158,14 @@ def c4_roofline(leg, world):
          "algorithmic_bytes": int(per_gpu),
          "algorithmic_def": "filters_this_gpu x (16 B x 2^18 keys + 2^25/8 B) (SURVEY.md §8d C4 row)",
          "frac_one_lane": round(per_gpu / (leg["one_lane_us_per_step"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
-    # per step: the PMC summary is per launch, and a step is one launch pair
-    # per batch of up to 32 filters (the tile pass is k_build_tile_sub for
-    # C4's batched long runs, k_build_tile otherwise)
-    pairs = -(-leg["filters_this_gpu"] // 32)
+    # per step: the PMC summary is per launch of the run it was recorded on
+    # (its filters_per_launch: 32 before the batch limit went to 64), so the
+    # bytes scale per filter (the tile pass is k_build_tile_sub for C4's
+    # batched long runs, k_build_tile otherwise)
+    fpl = _pmc_field("pmc_c4_r[0-9]*.json", "filters_per_launch", 32)
     part = _pmc_traffic("k_build_part", "pmc_c4_r[0-9]*.json")
     tile = _pmc_traffic("k_build_tile_sub", "pmc_c4_r[0-9]*.json") or _pmc_traffic("k_build_tile", "pmc_c4_r[0-9]*.json")
-    t = pairs * (part + tile) if (part and tile) else None
+    t = int(leg["filters_this_gpu"] * (part + tile) / fpl) if (part and tile) else None
     r["traffic"] = t if world == 1 else None
     if r["traffic"]:
         r["traffic_over_algorithmic"] = round(t / per_gpu, 3)
@@ -1513,6 +1514,19 @@ def _random_read_roofline():
     except Exception:
         return None
     return None
+
+
+def _pmc_field(pattern, key, default):
+    """A top-level field of the newest committed PMC summary matching pattern."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    if not files:
+        return default
+    try:
+        with open(files[-1]) as fh:
+            return json.load(fh).get(key, default)
+    except Exception:
+        return default
 
 
 def _pmc_traffic(kernel, pattern="pmc_r[0-9]*.json"):

@@ -99,7 +99,7 @@ int cb_filter_insert_var(cb_filter* f, const uint8_t* bytes, const uint64_t* off
 
 /* Concurrent flush builds: filters[i] += keys[i][0 .. n[i]) (key_len bytes
  * each), all filters of one m on one device, built together (one partition
- * and one tile launch per 32 filters). Each keys[i] may be host or device. */
+ * and one tile launch per 64 filters). Each keys[i] may be host or device. */
 int cb_filter_insert_fixed_many(cb_filter* const* filters, uint32_t nf, const uint8_t* const* keys,
                                 uint32_t key_len, const uint64_t* n, void* stream);
 

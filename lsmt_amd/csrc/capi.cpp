@@ -1917,7 +1917,7 @@ int cb_filter_insert_fixed_many(cb_filter* const* filters, uint32_t nf, const ui
       bb.ks[j].key_len = key_len;
       bb.n[j] = n[b0 + j];
       bb.words[j] = f->words;
-      bb.fresh |= (f->known_zero ? 1u : 0u) << j;
+      bb.fresh |= (f->known_zero ? 1ull : 0ull) << j;
     }
     HIP_TRY(ws.seg.reserve(cb::build_seg_bytes(p) * nb, s));
     HIP_TRY(ws.ent.reserve(cb::build_ent_bytes(p) * nb, s));

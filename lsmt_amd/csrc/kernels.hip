@@ -431,7 +431,7 @@ __global__ __launch_bounds__(NT) void k_build_tile(BuildBatch bb, uint32_t tb, u
   constexpr uint32_t NW = NT / 64;
   static_assert(G <= 64, "one lane per run bound");
   uint32_t* __restrict__ words = bb.words[blockIdx.y];
-  const bool fresh = (bb.fresh >> blockIdx.y) & 1u;
+  const bool fresh = (bb.fresh >> blockIdx.y) & 1ull;
   const uint32_t* __restrict__ seg = seg_all + (size_t)blockIdx.y * nblk * (T + 1);
   const uint32_t* __restrict__ ent = ent_all + (size_t)blockIdx.y * nblk * estride;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -532,7 +532,7 @@ __global__ __launch_bounds__(NT) void k_build_tile_sub(BuildBatch bb, uint32_t t
   constexpr uint32_t NW = NT / 64, S = 1u << SUB, NB = S + 1;
   static_assert(G * NB <= 64, "one lane per bound");
   uint32_t* __restrict__ words = bb.words[blockIdx.y];
-  const bool fresh = (bb.fresh >> blockIdx.y) & 1u;
+  const bool fresh = (bb.fresh >> blockIdx.y) & 1ull;
   const uint32_t TS = T << SUB;  // bins per filter
   const uint32_t* __restrict__ seg = seg_all + (size_t)blockIdx.y * nblk * (TS + 1);
   const uint16_t* __restrict__ ent = ent_all + (size_t)blockIdx.y * nblk * estride;

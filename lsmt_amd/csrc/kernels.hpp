@@ -27,13 +27,14 @@ struct FilterPtrs {
 
 // A batch of filters (same m) built together: one partition launch and one
 // tile launch for all of them (blockIdx.y = filter). C4's concurrent flushes.
-constexpr uint32_t kMaxBuildBatch = 32;
+constexpr uint32_t kMaxBuildBatch = 64;
 struct BuildBatch {
   KeySrc ks[kMaxBuildBatch];
   uint64_t n[kMaxBuildBatch];
   uint32_t* words[kMaxBuildBatch];
-  uint32_t fresh;  // bit i: filter i is known all-zero
+  uint64_t fresh;  // bit i: filter i is known all-zero
 };
+static_assert(sizeof(BuildBatch) <= 3072, "a launch's arguments stay within the 4 KiB kernarg limit");
 
 // Geometry of one tiled pass (build or probe) over filters of m bits.
 struct TilePlan {

@@ -111,7 +111,7 @@ int main(int argc, char** argv) {
     bb.n[f] = n;
     bb.words[f] = words + (size_t)f * (m / 32);
   }
-  bb.fresh = nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1);
+  bb.fresh = nb == 64 ? ~0ull : ((1ull << nb) - 1);
   printf("{\"shape\": \"%s\", \"plan\": {\"tb\": %u, \"T\": %u, \"kpt\": %u, \"C\": %u, \"nblk\": %u, \"nb\": %u, \"sub\": %u}, ",
          c4 ? "c4" : "c2", p.tb, p.T, p.kpt, p.C, p.nblk, nb, p.sub);
 
