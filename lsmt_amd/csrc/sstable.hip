@@ -939,10 +939,10 @@ __global__ __launch_bounds__(kNT, 6) void k_set_get_many(const void* __restrict_
 // (tables.iter().rev(), src/lib.rs:130): the group's candidate bits are a
 // 64-bit window of row a AND the same window of row b, the latter read only
 // when the former is non-zero (src/bloom.rs:50), reordered to table order
-// (groups[g].kind); the zone gate drops gated candidates outside their
-// bounds (src/sstable.rs:138); then resolve_group searches the candidates
-// newest first and the first Ok(Some) ends the walk. Views of tables past
-// the first 64 come from global memory.
+// (groups[g].kind); then the candidates newest first: each one's bucket
+// summary word, the zone gate for gated tables (src/sstable.rs:138), the
+// search, and the first Ok(Some) ends the walk. The group's views and maps
+// are staged in LDS.
 template <int KEYK, int MODE>
 __global__ __launch_bounds__(kNT, 5) void k_wide_get_many(const uint64_t* __restrict__ set, uint32_t R, ModP mp,
                                                        WideZone z, const TableView* __restrict__ tv, uint32_t nt,
@@ -997,15 +997,6 @@ __global__ __launch_bounds__(kNT, 5) void k_wide_get_many(const uint64_t* __rest
       cand = wa ? (wa & wide_window(rb, R, gd.lo)) : 0ull;
       if (gd.kind == 1 && cand) cand = __builtin_bitreverse64(cand) >> (64 - gd.gn);  // bit gn-1-i -> i
     }
-    if (z.any && cand) {
-      uint64_t c = cand;
-      while (c) {
-        const uint32_t i = (uint32_t)__builtin_ctzll(c);
-        c &= c - 1;
-        const uint32_t s = gd.kind == 2 ? slots[t0 + i] : gd.kind == 1 ? gd.lo + gd.gn - 1 - i : gd.lo + i;
-        if (!wide_zone_ok<KEYK>(z, s, kw, q.p, q.len)) cand &= ~(1ull << i);
-      }
-    }
     // the candidates newest first, the group's views and maps from LDS. At
     // the product's m = 1024 most candidates are false positives (~3/4 of
     // the tables pass the Bloom gate); each is settled by its key bucket's
@@ -1013,6 +1004,9 @@ __global__ __launch_bounds__(kNT, 5) void k_wide_get_many(const uint64_t* __rest
     // before any bucket line is read (a complete bucket without the key's
     // fingerprint: Ok(None)). Loading the words of 2 or 4 candidates at once
     // measured the same (profiles/wide_summary_r04.json).
+    // The zone gate (src/sstable.rs:138) is checked after the summary word:
+    // both only answer Ok(None), so their order leaves the walk's result as
+    // it is, and the summary word settles nearly every candidate first.
     const uint32_t kfp = bkt_fp(q.w0);
     while (cand) {
       const uint32_t i = (uint32_t)__builtin_ctzll(cand);
@@ -1029,6 +1023,10 @@ __global__ __launch_bounds__(kNT, 5) void k_wide_get_many(const uint64_t* __rest
             fpm |= s < nst && (uint32_t)((sw >> (4 + 15 * s)) & 0x7FFFu) == kfp;
           if (!fpm) continue;  // Ok(None)
         }
+      }
+      if (z.any) {
+        const uint32_t s = gd.kind == 2 ? slots[t0 + i] : gd.kind == 1 ? gd.lo + gd.gn - 1 - i : gd.lo + i;
+        if (!wide_zone_ok<KEYK>(z, s, kw, q.p, q.len)) continue;  // Ok(None)
       }
       LineRec r;
       if (search(v, q, r, &sdm[i]) < 0) continue;  // Ok(None)
