@@ -947,6 +947,8 @@ __global__ __launch_bounds__(kNT, 6) void k_set_get_many(const void* __restrict_
 // 671-679 / 792-809 / 816-820 M gets/s against 517-519 one at a time (300
 // tables of m = 1024); 16 doubles the scratch spill (36 -> 72 B per lane).
 constexpr uint32_t kScreen = 8;
+// (Five waves per SIMD at its natural 96 VGPRs: forcing six, 80 VGPRs with
+// 112 B of scratch per lane, measured 606-617 against 782-804 M gets/s.)
 template <int KEYK, int MODE>
 __global__ __launch_bounds__(kNT, 5) void k_wide_get_many(const uint64_t* __restrict__ set, uint32_t R, ModP mp,
                                                        WideZone z, const TableView* __restrict__ tv, uint32_t nt,
