@@ -286,7 +286,13 @@ int cb_sstable_create(const uint8_t* keys, const uint64_t* key_off, const uint8_
                       uint64_t* zone_max_idx);
 /* The same, enqueue-only for device offsets too: key_bytes / val_bytes bound
  * key_off[n] / val_off[n] (the file buffer is sized from them). A batch past
- * its bounds writes no file; its table reports CB_EINVAL when finalised. */
+ * its bounds writes no file; its table reports CB_EINVAL when finalised, and
+ * the Bloom filter returned with it must be discarded (device offsets past a
+ * device buffer's end are the caller's error, as for any device pointer).
+ * Host key or value bytes with device offsets are checked before the call
+ * returns (one read-back of the offsets' totals): the bytes are staged into a
+ * block of exactly key_bytes / val_bytes, so a batch past them is refused
+ * with CB_EINVAL and nothing is enqueued. */
 int cb_sstable_create_bounded(const uint8_t* keys, const uint64_t* key_off, uint64_t key_bytes, const uint8_t* vals,
                               const uint64_t* val_off, uint64_t val_bytes, uint64_t n, uint64_t m_bits, int device,
                               void* stream, cb_table** table_out, cb_filter** bloom_out);
@@ -317,6 +323,13 @@ int cb_table_rebuild(const cb_table* t, uint64_t m_bits, void* stream, cb_filter
 int cb_table_well_formed(const cb_table* t, int* out);
 /* Tests/bench: tables created while on != 0 always use the exact trajectory. */
 int cb_table_force_exact(int on);
+/* The read path's key buckets (136 B per line, rounded up to a power of two
+ * lines: 64 MiB for 512K lines, 2.3 GiB for 2^24) are built for a table only
+ * when they take at most max_bytes AND at most a quarter of the device memory
+ * free when they are built; otherwise that table is searched without them
+ * (same answers, ~20 % slower reads). max_bytes = 0 turns them off for tables
+ * read from now on; the default is 1 GiB. Process-wide. */
+int cb_table_bucket_limit(uint64_t max_bytes);
 /* The line index: start offset, key length (bytes before the first TAB, or
  * UINT32_MAX when the line has none) and line length; host or device out. */
 int cb_table_lines(const cb_table* t, uint64_t* start, uint32_t* key_len, uint32_t* line_len);
@@ -341,9 +354,10 @@ int cb_table_search_var(const cb_table* t, const uint8_t* bytes, const uint64_t*
  * only if cap >= that total). Calls that repeat the same tables and hit_rows
  * upload nothing, so batches on two streams overlap. A well-formed table's
  * first get_many (this or cb_set_get_many) also enqueues the build of its key
- * buckets on that call's stream (device memory: 128 B per line, rounded up
- * to a power of two lines; freed with the table); later calls on other
- * streams use them once that build has run. */
+ * buckets on that call's stream (device memory: 136 B per line, rounded up
+ * to a power of two lines; freed with the table) when they fit the budget
+ * set by cb_table_bucket_limit; later calls on any stream enqueue a wait for
+ * that build (never a host wait) until it is seen complete. */
 int cb_get_many_fixed(const cb_table* const* tables, uint32_t nt, const uint64_t* hits,
                       const uint32_t* hit_rows, const uint8_t* keys, uint32_t key_len, uint64_t n,
                       int32_t* which, uint64_t* val_off, uint8_t* vals, uint64_t cap,

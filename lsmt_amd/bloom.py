@@ -715,6 +715,14 @@ class Table:
         (lo+hi)/2 search trajectory (tests / bench)."""
         check(_L().cb_table_force_exact(int(bool(on))))
 
+    @staticmethod
+    def bucket_limit(max_bytes: int) -> None:
+        """The most device bytes one table's read-path key buckets may take
+        (0: none for tables read from now on; default 1 GiB, and never over a
+        quarter of the free device memory). Tables past it are searched
+        without buckets: same answers, slower reads."""
+        check(_L().cb_table_bucket_limit(int(max_bytes)))
+
     def lines(self):
         """(start uint64[n], key_len uint32[n] (0xFFFFFFFF = no TAB), line_len uint32[n])."""
         n = self.nlines

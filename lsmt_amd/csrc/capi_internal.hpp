@@ -148,7 +148,13 @@ inline cb::WideZone wide_zone_view(const cb_filterset* set) {
 // enqueued work has run (capi_sstable.cpp finalize_table): the event after
 // the result copy, the pinned result block, and what a fallback sort needs
 // (the batch: the caller's device buffers, or the table's own staged copy).
+// Owns the staged block and the result slot of an enqueued SsTable::create;
+// the destructor returns both (capi_sstable.cpp), so an error return from the
+// enqueue leaks neither. Destroy it only once its work can no longer run
+// (finalised, or the stream synchronised).
 struct TablePending {
+  ~TablePending();
+  int device = 0;
   hipEvent_t ev = nullptr;
   cb::CreateResult* hres = nullptr;  // pinned, from the result pool
   hipStream_t stream = nullptr;      // the creation stream (the fallback runs on it)
@@ -186,13 +192,12 @@ struct cb_table {
   int ferr = 0;
   std::string ferr_msg;
   // The read path's key buckets (sstable.hpp), built by the table's first
-  // get_many on that call's stream (capi_sstable.cpp table_buckets): usable
-  // at once on that stream, on others once bkt_ev has completed.
+  // get_many on that call's stream (capi_sstable.cpp table_buckets); every
+  // later read enqueues a wait on bkt_ev until it has been seen complete.
   uint64_t* bkt = nullptr;
   size_t bkt_cap = 0;
   uint32_t bkbits = 0;
   hipEvent_t bkt_ev = nullptr;
-  hipStream_t bkt_stream = nullptr;
   std::atomic<int> bkt_state{0};  // 0 none yet, 1 enqueued, 2 complete, -1 never (not fast / no memory)
   std::mutex bkt_mu;
   cb::TableView view() const {

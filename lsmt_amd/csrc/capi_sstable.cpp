@@ -17,6 +17,22 @@ using namespace cbx;
 namespace {
 
 bool g_table_exact = false;  // cb_table_force_exact: index files for the exact-trajectory search only
+std::atomic<uint64_t> g_bucket_limit{1ull << 30};  // cb_table_bucket_limit
+
+// The most bytes a table's key buckets may take on this device now: the
+// process-wide limit, and a quarter of the free device memory (the buckets
+// are kept for the table's lifetime and must not starve later flushes).
+uint64_t bucket_budget(int device) {
+  const uint64_t lim = g_bucket_limit.load(std::memory_order_relaxed);
+  if (!lim) return 0;
+  size_t free_b = 0, total_b = 0;
+  DeviceGuard dg(device);
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return std::min<uint64_t>(lim, free_b / 4);
+}
 
 int table_search_impl(const cb_table* t, const uint8_t* keys, const uint64_t* offsets,
                       uint32_t key_len, uint64_t n, int64_t* line_out, hipStream_t s) {
@@ -52,40 +68,48 @@ bool buckets_enabled() {
 }
 
 // The key buckets (sstable.hpp) for a read on stream s: the first read of a
-// well-formed table enqueues their build on s and uses them at once (stream
-// order); a read on another stream uses them once their event has completed
-// and searches without them until then (never waiting). A table whose bucket
-// memory cannot be had is simply read without them. v receives bkt / bkbits.
+// well-formed table enqueues their build on s and records bkt_ev after it.
+// Until that event is seen complete, every read (on any stream, the building
+// one included) enqueues a wait on it before using the buckets: the host never
+// blocks, and no reader relies on stream-handle identity (the same handle can
+// name another stream: hipStreamPerThread from two threads, or a destroyed
+// stream's handle reused). A table whose bucket memory cannot be had is simply
+// read without them. v receives bkt / bkbits.
 int table_buckets(cb_table* t, hipStream_t s, cb::TableView* v) {
   int st = t->bkt_state.load(std::memory_order_acquire);
   if (st < 0 || (st == 0 && (!t->fast || !t->nlines || !buckets_enabled()))) return CB_OK;
-  std::lock_guard<std::mutex> lk(t->bkt_mu);
-  st = t->bkt_state.load(std::memory_order_relaxed);
-  if (st == 0) {
-    const uint32_t bits = cb::bkt_bits(t->nlines);
-    const size_t bytes = (size_t)cb::bkt_bytes(bits);  // the buckets and their summary words
-    if (pool_alloc(t->device, bytes, (void**)&t->bkt, &t->bkt_cap) != hipSuccess) {
-      t->bkt = nullptr;
-      (void)hipGetLastError();
-      t->bkt_state.store(-1, std::memory_order_release);
-      return CB_OK;
+  if (st == 1 || st == 0) {
+    std::lock_guard<std::mutex> lk(t->bkt_mu);
+    st = t->bkt_state.load(std::memory_order_relaxed);
+    if (st == 0) {
+      const uint32_t bits = cb::bkt_bits(t->nlines);
+      const size_t bytes = (size_t)cb::bkt_bytes(bits);  // the buckets and their summary words
+      if (bytes > bucket_budget(t->device) ||
+          pool_alloc(t->device, bytes, (void**)&t->bkt, &t->bkt_cap) != hipSuccess) {
+        t->bkt = nullptr;
+        (void)hipGetLastError();
+        t->bkt_state.store(-1, std::memory_order_release);
+        return CB_OK;
+      }
+      t->bkbits = bits;
+      // a failure past the allocation leaves the table without buckets for good
+      // (the block is freed with the table) and reports the error once
+      t->bkt_state.store(-1, std::memory_order_relaxed);
+      HIP_TRY(hipMemsetAsync(t->bkt, 0xFF, bytes, s));
+      HIP_TRY(cb::launch_table_buckets(t->rec, t->nlines, t->bkt, bits, s));
+      HIP_TRY(hipEventCreateWithFlags(&t->bkt_ev, hipEventDisableTiming | hipEventDisableSystemFence));
+      HIP_TRY(hipEventRecord(t->bkt_ev, s));
+      t->bkt_state.store(st = 1, std::memory_order_release);
+      // (s itself is ordered after the build: no wait needed on this call)
+    } else if (st == 1) {
+      if (hipEventQuery(t->bkt_ev) == hipSuccess) {
+        t->bkt_state.store(st = 2, std::memory_order_release);
+      } else {
+        HIP_TRY(hipStreamWaitEvent(s, t->bkt_ev, 0));
+      }
     }
-    t->bkbits = bits;
-    // a failure past the allocation leaves the table without buckets for good
-    // (the block is freed with the table) and reports the error once
-    t->bkt_state.store(-1, std::memory_order_relaxed);
-    HIP_TRY(hipMemsetAsync(t->bkt, 0xFF, bytes, s));
-    HIP_TRY(cb::launch_table_buckets(t->rec, t->nlines, t->bkt, bits, s));
-    HIP_TRY(hipEventCreateWithFlags(&t->bkt_ev, hipEventDisableTiming | hipEventDisableSystemFence));
-    HIP_TRY(hipEventRecord(t->bkt_ev, s));
-    t->bkt_stream = s;
-    t->bkt_state.store(st = 1, std::memory_order_release);
-  } else if (st == 1 && s != t->bkt_stream && hipEventQuery(t->bkt_ev) == hipSuccess) {
-    t->bkt_state.store(st = 2, std::memory_order_release);
   }
-  if (st == 2 || (st == 1 && s == t->bkt_stream)) {
-    cb::view_set_buckets(*v, t->bkt, t->bkbits);
-  }
+  if (st >= 1) cb::view_set_buckets(*v, t->bkt, t->bkbits);
   return CB_OK;
 }
 
@@ -395,6 +419,15 @@ void result_release(cb::CreateResult* h, hipEvent_t ev) {
   g_res_free.push_back(ResultSlot{h, ev});
 }
 
+}  // namespace
+
+TablePending::~TablePending() {
+  if (staged) pool_release(device, staged, staged_cap);
+  result_release(hres, ev);
+}
+
+namespace {
+
 // Bin-sort group target: ~n / 1536 records (six 1024-record group sorts per
 // CU on 256 CUs, one wave), at least 640, at most 1536 (2048-record sorts).
 uint32_t bin_group_target(uint64_t n) {
@@ -437,8 +470,19 @@ int sstable_enqueue(const uint8_t* keys, const uint64_t* key_off, uint64_t kbyte
   t->device = device;
   std::unique_ptr<TablePending> pend(new TablePending());
   TablePending& p = *pend;
+  p.device = device;
   p.n = n;
   p.stream = s;
+  // an error return past this point may leave work enqueued that reads the
+  // staged block or writes the result slot: finish the stream before `pend`
+  // hands them back (declared after pend, so it runs first)
+  struct SyncOnError {
+    hipStream_t s;
+    bool ok = false;
+    ~SyncOnError() {
+      if (!ok) (void)hipStreamSynchronize(s);
+    }
+  } on_error{s};
   // Host inputs go into one block the table owns (the work reads them after
   // this call returns, and a fallback sort at finalisation reads them again);
   // device inputs are used in place.
@@ -450,6 +494,17 @@ int sstable_enqueue(const uint8_t* keys, const uint64_t* key_off, uint64_t kbyte
   if (vo_h)
     for (uint64_t i = 0; i < n; ++i)
       if (val_off[i + 1] < val_off[i]) return fail(CB_EINVAL, "offsets must be non-decreasing");
+  if ((kb_h && !ko_h) || (vb_h && !vo_h)) {
+    // host bytes with device offsets: they are staged into exactly kbytes /
+    // vbytes, so offsets past those would send every kernel past the staged
+    // block. Check the totals before anything is enqueued (one read-back).
+    uint64_t tot[2] = {0, 0};
+    if (kb_h && !ko_h) HIP_TRY(hipMemcpyAsync(&tot[0], key_off + n, 8, hipMemcpyDeviceToHost, s));
+    if (vb_h && !vo_h) HIP_TRY(hipMemcpyAsync(&tot[1], val_off + n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (tot[0] > kbytes) return fail(CB_EINVAL, "key bytes exceed key_bytes");
+    if (tot[1] > vbytes) return fail(CB_EINVAL, "value bytes exceed val_bytes");
+  }
   auto up16 = [](uint64_t x) { return (x + 15) & ~15ull; };
   const uint64_t offb = up16((n + 1) * 8);
   const uint64_t stage = (ko_h ? offb : 0) + (vo_h ? offb : 0) + (kb_h ? up16(kbytes) : 0) + (vb_h ? up16(vbytes) : 0);
@@ -505,6 +560,7 @@ int sstable_enqueue(const uint8_t* keys, const uint64_t* key_off, uint64_t kbyte
     }
     t->pend = std::move(pend);  // (no result block: the staged block is released with the table)
     HIP_TRY(hipStreamSynchronize(s));
+    on_error.ok = true;
     *table_out = t.release();
     return CB_OK;
   }
@@ -556,6 +612,7 @@ int sstable_enqueue(const uint8_t* keys, const uint64_t* key_off, uint64_t kbyte
   t->dmap = t->dir ? dmap_slot(t.get()) : nullptr;
   t->pend = std::move(pend);
   t->ready.store(false, std::memory_order_release);
+  on_error.ok = true;
   if (bloom_out) *bloom_out = f.release();
   *table_out = t.release();
   return CB_OK;
@@ -563,11 +620,7 @@ int sstable_enqueue(const uint8_t* keys, const uint64_t* key_off, uint64_t kbyte
 
 // Release what a finalised (or destroyed) table no longer needs.
 void drop_pending(cb_table* t) {
-  if (!t->pend) return;
-  TablePending& p = *t->pend;
-  if (p.staged) pool_release(t->device, p.staged, p.staged_cap);
-  result_release(p.hres, p.ev);
-  t->pend.reset();
+  t->pend.reset();  // (~TablePending returns the staged block and the result slot)
 }
 
 int finalize_locked(cb_table* t) {
@@ -887,6 +940,11 @@ int cb_table_well_formed(const cb_table* t, int* out) {
 
 int cb_table_force_exact(int on) {
   g_table_exact = on != 0;
+  return CB_OK;
+}
+
+int cb_table_bucket_limit(uint64_t max_bytes) {
+  g_bucket_limit.store(max_bytes, std::memory_order_relaxed);
   return CB_OK;
 }
 
