@@ -82,6 +82,10 @@ def parse():
                         "its own hit buffers; for N > 1 they share the rank's one RCCL communicator)")
     p.add_argument("--force-dist", action="store_true",
                    help="initialise the process group and run the exchange path even at N=1")
+    p.add_argument("--leg", choices=["c5", "wide"], default=None,
+                   help="run only that secondary leg (the C5 rank slice, or the wide fan-out) and print one "
+                        "line holding it: the rocprofv3 passes of tools/profile_round.sh, so the trace and the "
+                        "counters hold that leg's kernels alone")
     p.add_argument("--dry-run", action="store_true",
                    help="launch / join the ranks over gloo and report them; no GPU work")
     p.add_argument("--rehearse-one-gpu", action="store_true",
@@ -182,21 +186,16 @@ def main():
             os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", "29533"
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        # Two communicators share each GPU at N > 1: torch's process group
-        # (barriers and the max-over-ranks timing only) and the library's own
-        # RCCL communicator (cb_comm, the hit exchange). They never have work
-        # in flight together: every torch collective below follows a
-        # torch.cuda.synchronize() of the whole device (timed-region edges,
-        # check flags), and the library issues its collectives in one order on
-        # every rank (comm.cpp's order event). Keep that invariant when adding
-        # a torch collective: sync the device first.
-        if rehearse:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)
-    # host-side reductions (timing max, check flags): on the device for RCCL,
-    # on the CPU for the gloo rehearsal
-    red_dev = torch.device("cpu") if rehearse else dev
+        # ONE RCCL communicator per GPU: the library's own (cb_comm, the hit
+        # exchange, created below from a 128-byte id). torch.distributed is
+        # only the launcher's rendezvous, the barriers at the timed regions'
+        # edges and the max-over-ranks timing, all host-side, so its process
+        # group is gloo on every path (no second NCCL/RCCL communicator on the
+        # device, no torch collective that could interleave with the library's
+        # on a GPU stream). Every barrier follows a device synchronize.
+        dist.init_process_group("gloo")
+    # host-side reductions (timing max, check flags) run on the CPU (gloo)
+    red_dev = torch.device("cpu")
     log(f"[rank {rank}] local rank {local_rank} on cuda:{local} of world {world}")
 
     import lsmt_amd
@@ -210,6 +209,8 @@ def main():
 
     if args.workload == "c4":
         return run_c4(args, torch, dist, world, rank, local, dev, use_dist, result, red_dev)
+    if args.leg:
+        return run_leg(args, torch, dist, world, rank, local, dev, use_dist, result, red_dev)
     seed_base, absent_seed = 100, 999
     if args.workload == "c5":  # key(1000+f, i), absent key(9999, i)
         seed_base, absent_seed = 1000, 9999
@@ -527,6 +528,9 @@ def main():
         if one_lane_us:
             roof["kernel_avg_us_one_lane"] = round(one_lane_us, 2)
             roof["frac_one_lane"] = round(alg_bytes / (one_lane_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+        if c3_default:
+            roof["traffic_source"] = _pmc_source("c3")
+            roof["profile_check"] = _profile_check("c3", [dominant], alg_bytes, roof.get("frac_one_lane"))
         if roof["traffic"]:  # the memory-side bytes the kernel moves (PMC), at the same time per launch
             roof["traffic_GBps"] = round(roof["traffic"] / dur_s / 1e9, 1)
             roof["traffic_frac"] = round(roof["traffic"] / dur_s / 1e9 / HBM_PEAK_GBS, 4)
@@ -1106,8 +1110,12 @@ def c4_leg(args, torch, dist, world, rank, local, dev, use_dist, red_dev, steps,
     nstep[0] = 0
     P_saved, P = P, 1
     el1, ev1_ms = _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes[:1], step, steps)
-    P = P_saved
+    # per-launch durations on ONE lane (each launch alone on the chip, so a
+    # figure is that kernel's own time plus its dispatch gap, comparable with
+    # rocprofv3's one-lane trace in profiles/; with three lanes a launch's
+    # duration would include its overlap with the other lanes' launches)
     kus = _kernel_us(L, torch, dev, ["k_build_part", "k_build_tile"], step, min(steps, 50))
+    P = P_saved
     torch.cuda.synchronize(dev)
     # the line's value is the faster schedule: at C4's size one batched build
     # fills the chip, and concurrent lanes can lose more to sharing the L2s
@@ -1121,7 +1129,7 @@ def c4_leg(args, torch, dist, world, rank, local, dev, use_dist, red_dev, steps,
            "lanes_region_us_per_step": round(ev_ms * 1e3 / steps, 2),
            "one_lane_us_per_step": round(ev1_ms * 1e3 / steps, 2),
            "value": round(nf_total * kpf / (el_b / steps), 1), "unit": "keys/s (all GPUs)",
-           "kernels_us": kus}
+           "kernels_us": kus, "kernels_us_source": "library HIP events around each launch, one lane"}
     if check:
         g = _golden()["c4"]
         good = True
@@ -1162,13 +1170,16 @@ def c4_roofline(leg, world):
     # (its filters_per_launch: 32 before the batch limit went to 64), so the
     # bytes scale per filter (the tile pass is k_build_tile_sub for C4's
     # batched long runs, k_build_tile otherwise)
-    fpl = _pmc_field("pmc_c4_r[0-9]*.json", "filters_per_launch", 32)
-    part = _pmc_traffic("k_build_part", "pmc_c4_r[0-9]*.json")
-    tile = _pmc_traffic("k_build_tile_sub", "pmc_c4_r[0-9]*.json") or _pmc_traffic("k_build_tile", "pmc_c4_r[0-9]*.json")
+    fpl = _pmc_field("c4", "filters_per_launch", 32)
+    part = _pmc_traffic("k_build_part", "c4")
+    tile = _pmc_traffic("k_build_tile_sub", "c4") or _pmc_traffic("k_build_tile", "c4")
     t = int(leg["filters_this_gpu"] * (part + tile) / fpl) if (part and tile) else None
     r["traffic"] = t if world == 1 else None
     if r["traffic"]:
         r["traffic_over_algorithmic"] = round(t / per_gpu, 3)
+        r["traffic_source"] = _pmc_source("c4")
+    if world == 1 and leg["filters_this_gpu"] == _pmc_field("c4", "filters_per_launch", 0):
+        r["profile_check"] = _profile_check("c4", ["k_build_part", "k_build_tile_sub"], per_gpu, r["frac_one_lane"])
     return r
 
 
@@ -1230,10 +1241,14 @@ def c5_leg(args, torch, dev, local, world, rank, steps, warmup, lanes_n, check, 
                         "algorithmic_bytes": int(alg),
                         "algorithmic_def": f"64 B x {sectors} distinct sectors + 16n + F*n/8 "
                                            "(SURVEY.md §8d alternative layout)",
-                        "traffic": _pmc_traffic("k_set_probe", "pmc_c5_r[0-9]*.json")}}
+                        "traffic": _pmc_traffic("k_set_probe", "c5"), "traffic_source": _pmc_source("c5")}}
     rr = _random_read_roofline()
     if rr:
         out["roofline"]["random_read_frac"] = round(rand_reads / (us * 1e-6) / rr, 4)
+    out["roofline"]["profile_check"] = _profile_check("c5", [out["roofline"]["kernel"]], alg,
+                                                      out["roofline"]["frac_one_lane"])
+    if out["roofline"]["traffic"]:
+        out["roofline"]["traffic_over_algorithmic"] = round(out["roofline"]["traffic"] / alg, 3)
     if check:
         torch.cuda.synchronize(dev)
         got = hits[0].cpu().numpy().view(np.uint64)
@@ -1293,6 +1308,35 @@ def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result, red_dev
             line["rehearsal"] = f"{world} ranks on ONE GPU (gloo): checks the N-rank flow, not a scaling measurement"
             line["valid"] = False
         print(json.dumps(line), file=result, flush=True)
+    if use_dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_leg(args, torch, dist, world, rank, local, dev, use_dist, result, red_dev):
+    """`--leg c5|wide`: one secondary leg alone, its dict as the line's
+    "c5" / "wide_fanout" field (the profiling passes' workload; the default
+    line runs the same functions)."""
+    import lsmt_amd
+    from lsmt_amd import _lib, workload
+    L = _lib.load()
+    lanes = [torch.cuda.current_stream(dev)]
+    if args.leg == "c5":
+        out = c5_leg(args, torch, dev, local, world, rank, args.steps, args.warmup, args.probe_streams,
+                     not args.no_cpu, red_dev, dist, use_dist)
+        key = "c5"
+    else:
+        def timed(fn, k, lanes=lanes):
+            return _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes, fn, k)[0]
+
+        def kernel_ms(names, fn, k):
+            return _kernel_us(L, torch, dev, names, fn, k)
+        out = wide_fanout_leg(args, torch, dev, local, lanes[0].cuda_stream, args.steps * 20, timed, kernel_ms,
+                              lsmt_amd, workload)
+        key = "wide_fanout"
+    if rank == 0:
+        print(json.dumps({"leg": args.leg, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          key: out}), file=result, flush=True)
     if use_dist:
         dist.barrier()
         dist.destroy_process_group()
@@ -1516,35 +1560,66 @@ def _random_read_roofline():
     return None
 
 
-def _pmc_field(pattern, key, default):
-    """A top-level field of the newest committed PMC summary matching pattern."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
-    if not files:
-        return default
-    try:
-        with open(files[-1]) as fh:
-            return json.load(fh).get(key, default)
-    except Exception:
-        return default
+PMC_INDEX = os.path.join(ROOT, "profiles", "pmc_index.json")
 
 
-def _pmc_traffic(kernel, pattern="pmc_r[0-9]*.json"):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
-    summary matching `pattern` under profiles/ (FETCH_SIZE/WRITE_SIZE with the
-    gfx950 corrections; C3 by default, pmc_c4_r*/pmc_c5_r* for those shapes),
-    or None when no PMC run has been recorded for it."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))  # the round summaries
-    if not files:
-        return None
+def _pmc_summary(shape):
+    """(file name, summary dict) of the PMC summary profiles/pmc_index.json
+    names for `shape` ("c3", "c4", "c5", "wide"): an explicit choice per
+    round, not the newest-looking file name (a lexicographic sort
+    picked pmc_r04a over pmc_r04). (None, None) when the shape has none."""
     try:
-        with open(files[-1]) as fh:
-            d = json.load(fh)
-        v = d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
-        return int(v) if v else None
+        with open(PMC_INDEX) as fh:
+            name = json.load(fh).get(shape)
+        if not name:
+            return None, None
+        with open(os.path.join(ROOT, "profiles", name)) as fh:
+            return name, json.load(fh)
     except Exception:
+        return None, None
+
+
+def _pmc_field(shape, key, default):
+    """A top-level field of the shape's indexed PMC summary."""
+    _, d = _pmc_summary(shape)
+    return d.get(key, default) if d else default
+
+
+def _pmc_traffic(kernel, shape="c3"):
+    """HBM bytes per launch of `kernel` from the shape's indexed rocprofv3 PMC
+    summary (FETCH_SIZE/WRITE_SIZE priced per request size, the gfx950
+    corrections of tools/pmc_summary.py), or None when none was recorded."""
+    _, d = _pmc_summary(shape)
+    if not d:
         return None
+    v = d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+    return int(v) if v else None
+
+
+def _pmc_source(shape):
+    name, _ = _pmc_summary(shape)
+    return f"profiles/{name}" if name else None
+
+
+def _profile_check(shape, kernels, alg_bytes, line_frac_one_lane):
+    """The roofline fraction recomputed from the shape's committed rocprofv3
+    one-lane trace (the sum of `kernels`' average one-lane dispatch durations
+    = one step) beside the line's own one-lane (HIP-event) fraction: the two
+    clocks, and their ratio (within 3 %)."""
+    name, d = _pmc_summary(shape)
+    if not d:
+        return None
+    ks = d.get("kernels", {})
+    us = [ks.get(k, {}).get("avg_us_one_lane") for k in kernels]
+    if not all(us):
+        return None
+    step = sum(us)
+    frac = alg_bytes / (step * 1e-6) / 1e9 / HBM_PEAK_GBS
+    out = {"source": f"profiles/{name} (rocprofv3 --kernel-trace, one lane)", "kernels": list(kernels),
+           "step_us": round(step, 2), "frac": round(frac, 4)}
+    if line_frac_one_lane:
+        out["ratio_to_line_frac_one_lane"] = round(frac / line_frac_one_lane, 4)
+    return out
 
 
 def c4_cpu_baseline(nf, kpf, m):

@@ -4,7 +4,8 @@
 Read bytes are priced per request size (32/64/128 B request counters) because
 gfx950's FETCH_SIZE counts a 128-B request as 64 B (MI355X_MICROARCH.md §HBM);
 FETCH_SIZE is reported beside it. WRITE_SIZE is exact for 16-B/lane stores.
-Usage: python tools/pmc_summary.py gpurun_out/prof [--json out.json]
+Usage: python tools/pmc_summary.py gpurun_out/prof [--json out.json] [key=value ...]
+(key=value pairs are copied into the JSON, e.g. shape=c4 filters_per_launch=64)
 """
 import collections
 import csv
@@ -23,11 +24,32 @@ def short(name):
 def main():
     root = sys.argv[1]
     out_json = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
+    meta = {}
+    for a in sys.argv[2:]:
+        if "=" in a:
+            k, v = a.split("=", 1)
+            meta[k] = int(v) if v.isdigit() else v
     dur = {}
     stats = glob.glob(os.path.join(root, "kt", "*kernel_stats.csv"))
     if stats:
         for r in csv.DictReader(open(stats[0])):
-            dur[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3}
+            k = short(r["Name"])
+            c, t = int(r["Calls"]), float(r["TotalDurationNs"])
+            if k in dur:  # template instances of one kernel: merged
+                c, t = c + dur[k]["calls"], t + dur[k]["avg_us"] * 1e3 * dur[k]["calls"]
+            dur[k] = {"calls": c, "avg_us": t / c / 1e3}
+    # the one-lane trace (kt1: launches do not overlap, so a dispatch's
+    # duration is the kernel's own time): the figure bench.py's profile check
+    # compares with its event-timed one-lane step
+    dur1 = {}
+    stats1 = glob.glob(os.path.join(root, "kt1", "*kernel_stats.csv"))
+    if stats1:
+        for r in csv.DictReader(open(stats1[0])):
+            k = short(r["Name"])
+            c, t = int(r["Calls"]), float(r["TotalDurationNs"])
+            if k in dur1:  # template instances of one kernel: merged
+                c, t = c + dur1[k]["calls"], t + dur1[k]["avg_us"] * 1e3 * dur1[k]["calls"]
+            dur1[k] = {"calls": c, "avg_us": t / c / 1e3}
     # busy time per launch: the union of each kernel's [start, end) intervals
     # over its dispatches, / dispatches (= the average duration when launches
     # do not overlap; the per-step share when pipeline lanes overlap them)
@@ -58,11 +80,14 @@ def main():
         for (d, k, c), v in per.items():
             ctr[k][c].append(v)
     res = {}
-    for k in sorted(set(dur) | set(ctr)):
+    for k in sorted(set(dur) | set(dur1) | set(ctr)):
         c = {n: sum(v) / len(v) for n, v in ctr[k].items()}
         e = {"avg_us": round(dur.get(k, {}).get("avg_us", 0.0), 3), "calls": dur.get(k, {}).get("calls", 0)}
         if k in busy:
             e["busy_us_per_launch"] = round(busy[k], 3)
+        if k in dur1:
+            e["avg_us_one_lane"] = round(dur1[k]["avg_us"], 3)
+            e["calls_one_lane"] = dur1[k]["calls"]
         e.update({n: round(v, 1) for n, v in c.items()})
         if all(n in c for n in ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")):
             rd = 32 * c["TCC_EA0_RDREQ_32B_sum"] + 64 * c["TCC_EA0_RDREQ_64B_sum"] + 128 * c["TCC_EA0_RDREQ_128B_sum"]
@@ -79,7 +104,8 @@ def main():
         print(k, json.dumps(e))
     if out_json:
         with open(out_json, "w") as fh:
-            json.dump({"source": "tools/profile_round.sh + tools/pmc_summary.py", "kernels": res}, fh, indent=1)
+            json.dump(dict({"source": "tools/profile_round.sh + tools/pmc_summary.py", "kernels": res}, **meta), fh,
+                      indent=1)
 
 
 if __name__ == "__main__":
