@@ -82,6 +82,9 @@ def parse():
                         "its own hit buffers; for N > 1 they share the rank's one RCCL communicator)")
     p.add_argument("--force-dist", action="store_true",
                    help="initialise the process group and run the exchange path even at N=1")
+    p.add_argument("--set-dense", choices=["auto", "on", "off"], default="auto",
+                   help="FilterSet probes of dense batches (cb_set_dense): auto = the region-partitioned "
+                        "probe when a batch holds >= 2 keys per 128-B set line (C5), on / off = always / never")
     p.add_argument("--leg", choices=["c5", "wide"], default=None,
                    help="run only that secondary leg (the C5 rank slice, or the wide fan-out) and print one "
                         "line holding it: the rocprofv3 passes of tools/profile_round.sh, so the trace and the "
@@ -204,6 +207,7 @@ def main():
 
     L = _lib.load()
     lsmt_amd.set_path(args.path)
+    lsmt_amd.set_dense({"auto": 0, "on": 1, "off": -1}[args.set_dense])
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
 
@@ -1224,6 +1228,10 @@ def c5_leg(args, torch, dev, local, world, rank, steps, warmup, lanes_n, check, 
     nstep[0] = 0
     Psaved, P = P, 1
     _, ev1_ms = _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes[:1], step, steps)
+    from lsmt_amd import _lib
+    path = int(_lib.load().cb_last_path())  # 6: the dense (region-partitioned) probe, 3: k_set_probe
+    kern = ["k_dense_part", "k_dense_probe"] if path == 6 else ["k_set_probe"]
+    kus = _kernel_us(_lib.load(), torch, dev, kern, step, min(steps, 20))  # one lane (P = 1 still)
     P = Psaved
     sectors, rand_reads = _set_sectors(filters, look_np, m, F)
     alg = 64 * sectors + 16 * n + F * n / 8
@@ -1234,19 +1242,24 @@ def c5_leg(args, torch, dev, local, world, rank, steps, warmup, lanes_n, check, 
            "ms_per_step": round(el / steps * 1e3, 4), "region_us_per_step": round(us, 2),
            "one_lane_us_per_step": round(ev1_ms * 1e3 / steps, 2),
            "value": round(n * F * world / (el / steps), 1), "unit": "probes/s (all GPUs)",
+           "path": "dense (k_dense_part + k_dense_probe: keys partitioned by set region, regions staged in LDS)"
+                   if path == 6 else "k_set_probe (one random set line per read)",
+           "kernels_us": {k: v["avg_us"] for k, v in kus.items()},
+           "kernels_us_source": "library HIP events around each launch, one lane",
            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(ach / HBM_PEAK_GBS, 4),
                         "frac_one_lane": round(alg / (ev1_ms * 1e-3 / steps) / 1e9 / HBM_PEAK_GBS, 4),
-                        "kernel": "k_set_probe", "kernel_avg_us": round(us, 2),
+                        "kernel": "+".join(kern), "kernel_avg_us": round(us, 2),
                         "algorithmic_bytes": int(alg),
                         "algorithmic_def": f"64 B x {sectors} distinct sectors + 16n + F*n/8 "
-                                           "(SURVEY.md §8d alternative layout)",
-                        "traffic": _pmc_traffic("k_set_probe", "c5"), "traffic_source": _pmc_source("c5")}}
+                                           "(SURVEY.md §8d alternative layout)"}}
+    traffic = [_pmc_traffic(k, "c5") for k in kern]
+    out["roofline"]["traffic"] = sum(traffic) if all(traffic) else None
+    out["roofline"]["traffic_source"] = _pmc_source("c5")
     rr = _random_read_roofline()
-    if rr:
+    if rr and path != 6:
         out["roofline"]["random_read_frac"] = round(rand_reads / (us * 1e-6) / rr, 4)
-    out["roofline"]["profile_check"] = _profile_check("c5", [out["roofline"]["kernel"]], alg,
-                                                      out["roofline"]["frac_one_lane"])
+    out["roofline"]["profile_check"] = _profile_check("c5", kern, alg, out["roofline"]["frac_one_lane"])
     if out["roofline"]["traffic"]:
         out["roofline"]["traffic_over_algorithmic"] = round(out["roofline"]["traffic"] / alg, 3)
     if check:
@@ -1323,7 +1336,7 @@ def run_leg(args, torch, dist, world, rank, local, dev, use_dist, result, red_de
     lanes = [torch.cuda.current_stream(dev)]
     if args.leg == "c5":
         out = c5_leg(args, torch, dev, local, world, rank, args.steps, args.warmup, args.probe_streams,
-                     not args.no_cpu, red_dev, dist, use_dist)
+                     True, red_dev, dist, use_dist)  # golden + oracle row always; the CPU baseline unless --no-cpu
         key = "c5"
     else:
         def timed(fn, k, lanes=lanes):

@@ -507,9 +507,16 @@ int cb_hits_expand_set(const uint32_t* packs, uint32_t nranks, uint64_t cap, con
 /* Path selection: 0 = auto, 1 = force direct (per-key atomics / gathers),
  * 2 = force tiled (LDS-staged filter tiles). Process-wide. */
 int cb_set_path(int path);
+/* FilterSet probes of dense batches (at least 2 keys per 128-B line of the
+ * set: the C5 shape) take the region-partitioned probe, which streams the set
+ * through LDS once instead of reading a random line per key; same hits.
+ * mode 0 = by density (default), 1 = whenever the set allows it (32- or
+ * 64-slot sets, m <= 2^32 in at most 4096 regions of 64 KiB; tests), -1 =
+ * never. Never for gated probes or the fused exchange pack. Process-wide. */
+int cb_set_dense(int mode);
 /* Path the last insert/probe on this thread used (1 direct, 2 tiled, 3 FilterSet,
  * 4 FilterSet zero-copy: pinned host keys and hits read/written by the kernel,
- * 5 cb_may_contain answered from the host mirror). */
+ * 5 cb_may_contain answered from the host mirror, 6 FilterSet dense probe). */
 int cb_last_path(void);
 /* Per-kernel timing with HIP events recorded on each launch's own stream
  * (off by default). Kernel names: "k_insert_direct", "k_probe_direct",

@@ -65,6 +65,13 @@ def last_path() -> int:
     return int(_L().cb_last_path())
 
 
+def set_dense(mode: int) -> None:
+    """FilterSet probes of dense batches: 0 by density (default), 1 the
+    region-partitioned probe whenever the set allows it, -1 never
+    (cb_set_dense; last_path() is 6 after a dense probe)."""
+    check(_L().cb_set_dense(int(mode)))
+
+
 # ---- key batches ---------------------------------------------------------------
 
 def _ptr_of(x):

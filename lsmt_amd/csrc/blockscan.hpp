@@ -20,6 +20,37 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
   return x;
 }
 
+// Exclusive scan of arr[0..len4) in LDS by wave 0 alone (the other waves wait
+// at the caller's next barrier): one barrier fewer than block_exclusive_scan
+// and no cross-wave partials. len4 is a multiple of 4 and arr 16-B aligned and
+// zero past the counts, so each lane takes whole quads: one ds_read_b128
+// round, the wave scan, one ds_write_b128 round (a word at a time the scan
+// took ~1 us of k_build_part's 7.7 at 257 tiles). Over the zero padding the
+// exclusive prefix is the total, so arr[len] receives it for any len < len4.
+__device__ __forceinline__ void wave0_exclusive_scan4(uint32_t* arr, uint32_t len4) {
+  if (threadIdx.x >= 64) return;
+  const uint32_t lane = threadIdx.x, q = len4 / 4;
+  const uint32_t per = (q + 63) / 64;
+  const uint32_t beg = min(lane * per, q), end = min(beg + per, q);
+  uint4* a4 = reinterpret_cast<uint4*>(arr);
+  uint32_t sum = 0;
+  for (uint32_t i = beg; i < end; ++i) {
+    const uint4 v = a4[i];
+    sum += v.x + v.y + v.z + v.w;
+  }
+  uint32_t run = wave_inclusive_scan(sum) - sum;
+  for (uint32_t i = beg; i < end; ++i) {
+    const uint4 v = a4[i];
+    uint4 o;
+    o.x = run;
+    o.y = o.x + v.x;
+    o.z = o.y + v.y;
+    o.w = o.z + v.z;
+    run = o.w + v.w;
+    a4[i] = o;
+  }
+}
+
 // Block-wide exclusive scan of one uint64 per thread (NT threads). Returns the
 // thread's prefix; *total = block sum. Contains barriers: call uniformly.
 template <int NT>

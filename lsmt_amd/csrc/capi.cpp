@@ -525,6 +525,28 @@ int set_probe_zero_copy(const cb_filterset* set, const uint8_t* keys, uint32_t k
   return CB_OK;
 }
 
+// The dense set probe (densefs.hip) for this batch? cb_set_dense: 0 auto (by
+// density), 1 whenever the shape allows it, -1 never. Never with the zone gate
+// or a fused exchange pack.
+std::atomic<int> g_set_dense{0};
+
+bool use_dense(const cb_filterset* set, uint64_t n, bool gated, bool pack) {
+  const int mode = g_set_dense.load(std::memory_order_relaxed);
+  if (mode < 0 || gated || pack || set_is_wide(set)) return false;
+  if (mode > 0) return set->width <= 64 && set->m <= (1ull << 32) &&
+                       cb::dense_regions(set->width, set->m) <= 4096 && set->m;
+  return cb::set_probe_dense_ok(set->width, set->m, n);
+}
+
+int dense_probe(Workspace& ws, const cb_filterset* set, int keyk, const cb::KeySrc& ks, uint64_t n,
+                uint64_t* hits, uint64_t hwords, hipStream_t s) {
+  HIP_TRY(ws.dense.reserve(cb::dense_scratch_bytes(set->width, set->m, n), s));
+  HIP_TRY(cb::launch_set_probe_dense(keyk, set->mode, set->width, set->words, set->used, ks, n, set->mp, hits, hwords,
+                                     ws.dense.p, s));
+  g_last_path = 6;
+  return CB_OK;
+}
+
 int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t* offsets,
                    uint32_t key_len, uint64_t n, uint64_t* hits, hipStream_t s, bool gated) {
   if (!set) return fail(CB_EINVAL, "null set");
@@ -550,10 +572,13 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
     HIP_TRY(ws.hits.reserve((size_t)set->used * hwords * 8, s));
     dhits = (uint64_t*)ws.hits.p;
   }
+  const bool dense = use_dense(set, n, gated && set->zany, false);
   if (set_is_wide(set)) {
     const cb::WideZone wz = wide_zone_view(set);
     HIP_TRY(cb::launch_wide_probe(sk.keyk, set->mode, set->R, (const uint64_t*)set->words, set->used, sk.ks, n,
                                   set->mp, (gated && set->zany) ? &wz : nullptr, dhits, hwords, s));
+  } else if (dense) {
+    if ((rc = dense_probe(ws, set, sk.keyk, sk.ks, n, dhits, hwords, s))) return rc;
   } else {
     HIP_TRY(cb::launch_set_probe(sk.keyk, set->mode, set->width, set->words, set->any, set->used,
                                  sk.ks, n, set->mp, (gated && set->zany) ? &zv : nullptr, dhits,
@@ -563,7 +588,7 @@ int set_probe_impl(const cb_filterset* set, const uint8_t* keys, const uint64_t*
     int zr = note_zone_read(set, s);
     if (zr) return zr;
   }
-  g_last_path = 3;
+  if (!dense) g_last_path = 3;
   if (host_hits) {
     HIP_TRY(hipMemcpyAsync(hits, dhits, (size_t)set->used * hwords * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -610,7 +635,9 @@ int set_probe_device(const cb_filterset* set, const uint8_t* keys, uint32_t key_
     sink = cb::PackSink{sink_pack, cap, reinterpret_cast<unsigned long long*>(st->ctl), st->parity};
   }
   hipError_t e;
-  if (set_is_wide(set)) {
+  if (use_dense(set, n, gated && set->zany, sink_pack != nullptr)) {
+    return dense_probe(ws, set, keyk, ks, n, hits, hwords, s);
+  } else if (set_is_wide(set)) {
     const cb::WideZone wz = wide_zone_view(set);
     e = cb::launch_wide_probe(keyk, set->mode, set->R, (const uint64_t*)set->words, set->used, ks, n, set->mp,
                               (gated && set->zany) ? &wz : nullptr, hits, hwords, s);
@@ -998,6 +1025,11 @@ int cb_set_path(int path) {
   return CB_OK;
 }
 int cb_last_path(void) { return g_last_path; }
+int cb_set_dense(int mode) {
+  if (mode < -1 || mode > 1) return fail(CB_EINVAL, "mode must be -1, 0 or 1");
+  g_set_dense.store(mode, std::memory_order_relaxed);
+  return CB_OK;
+}
 
 int cb_device_count(int* out) {
   if (!out) return fail(CB_EINVAL, "null out");

@@ -167,7 +167,15 @@ struct TablePending {
 };
 
 // An SSTable data file resident in HBM with its line index (sstable.hpp).
+// A process-unique table id (never reused, unlike a freed table's addresses):
+// caches keyed by the tables they were built from compare these.
+inline uint64_t next_table_uid() {
+  static std::atomic<uint64_t> next{1};
+  return next.fetch_add(1, std::memory_order_relaxed);
+}
+
 struct cb_table {
+  uint64_t uid = next_table_uid();
   int device = 0;
   uint64_t len = 0, nlines = 0;
   uint8_t* data = nullptr;      // the file + 16 bytes of slack
@@ -259,10 +267,14 @@ struct Workspace {
   std::vector<uint8_t> t_views_host;
   std::vector<uint32_t> t_rows_host;
   DevBuf t_groups;                          // a wide set's table groups (cb::WideGroup)
+  DevBuf w_scr;                             // the wide walk's screen (sstable.hpp WideScreen)
+  std::vector<uint64_t> w_scr_sig;          // what it was built from (table uids, slots, buckets)
+  uint32_t w_scr_bits = 0, w_scr_hbits = 0;
   std::vector<uint8_t> t_groups_host;
   DevBuf i_cnt, i_base, i_tmp, i_end, i_err, i_start;                 // line indexing
   DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_tsum, f_flag, f_vsp;  // SsTable::create
   DevBuf x_ctl;                   // cb_hits_compress: slot / finish counters (zeroed once)
+  DevBuf dense;                   // the dense set probe's entries and run table (densefs.hip)
   std::vector<std::shared_ptr<WriteMark>> marks;  // write marks, reused once no filter holds them
   cb::CompressState xst;
   cb::CreateResult* hres = nullptr;  // pinned host mirror of f_flag (SsTable::create)

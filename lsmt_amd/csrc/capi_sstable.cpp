@@ -113,6 +113,50 @@ int table_buckets(cb_table* t, hipStream_t s, cb::TableView* v) {
   return CB_OK;
 }
 
+// The wide walk's screen for these tables in these slots (sstable.hpp
+// WideScreen): built on s after their buckets, and kept in the stream's
+// workspace until the tables, their slots or their buckets change (compared
+// by the tables' process-unique ids). Only when the tables share one bucket
+// count and the screen stays small; otherwise the walk runs without it.
+constexpr uint32_t kScreenHbits = 5;                  // 32 fingerprint bins
+constexpr uint64_t kScreenMaxBytes = 16ull << 20;
+int wide_screen(Workspace& ws, const cb_table* const* tables, const std::vector<cb::TableView>& views,
+                const std::vector<uint32_t>& rows, uint32_t R, const cb::TableView* dviews, const uint32_t* drows,
+                hipStream_t s, cb::WideScreen* out) {
+  const uint32_t nt = (uint32_t)views.size();
+#ifdef CB_EXPERIMENTS
+  static const bool off = getenv("CB_NO_SCREEN") && getenv("CB_NO_SCREEN")[0] == '1';  // the A/B
+  if (off) return CB_OK;
+#endif
+  uint32_t bits = 0;
+  for (const auto& v : views)
+    if (v.bkt && v.fast()) {
+      bits = v.bkbits();
+      break;
+    }
+  if (!bits || cb::wide_screen_bytes(R, bits, kScreenHbits) > kScreenMaxBytes) return CB_OK;
+  std::vector<uint64_t> sig;
+  sig.reserve(4 + 4 * (size_t)nt);
+  sig.push_back(nt);
+  sig.push_back(R);
+  sig.push_back(bits);
+  sig.push_back(kScreenHbits);
+  for (uint32_t i = 0; i < nt; ++i) {
+    sig.push_back(tables[i]->uid);
+    sig.push_back(rows.empty() ? i : rows[i]);
+    sig.push_back((uint64_t)(uintptr_t)views[i].bkt);
+    sig.push_back(views[i].meta);
+  }
+  if (sig != ws.w_scr_sig) {
+    HIP_TRY(ws.w_scr.reserve(cb::wide_screen_bytes(R, bits, kScreenHbits), s));
+    HIP_TRY(cb::launch_wide_screen(dviews, rows.empty() ? nullptr : drows, nt, R, bits, kScreenHbits,
+                                   (uint64_t*)ws.w_scr.p, s));
+    ws.w_scr_sig.swap(sig);
+  }
+  *out = cb::WideScreen{(const uint64_t*)ws.w_scr.p, bits, kScreenHbits, 0};
+  return CB_OK;
+}
+
 // set != NULL: the fused form (cb_set_get_many_*): the gate comes from the
 // FilterSet inside the search kernel, hit_rows are the tables' slots and
 // hits is unused.
@@ -245,10 +289,12 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
       ws.t_groups_host.assign(gb, gb + gbytes);
     }
     const cb::WideZone wz = wide_zone_view(set);
+    cb::WideScreen scr{nullptr, 0, 0, 0};
+    if ((rc = wide_screen(ws, tables, views, rows, set->R, dviews, drows, s, &scr))) return rc;
     HIP_TRY(cb::launch_wide_get_many(sk.keyk, set->mode, set->R, (const uint64_t*)set->words, set->mp,
                                      set->zany ? &wz : nullptr, dviews, nt, (const cb::WideGroup*)ws.t_groups.p,
                                      need_slots ? drows : nullptr, sk.ks, n, dwhich, (uint64_t*)ws.t_line.p,
-                                     (uint64_t*)ws.t_dlen.p, tsum, s));
+                                     (uint64_t*)ws.t_dlen.p, tsum, s, scr.scr ? &scr : nullptr));
     if (set->zany && (rc = note_zone_read(set, s))) return rc;
   } else if (set) {
     const cb::ZoneView zv = set_zone_view(set);

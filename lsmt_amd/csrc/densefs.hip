@@ -1,0 +1,328 @@
+// densefs.hip — the FilterSet probe for dense batches: keys partitioned by
+// set region, each region of the set streamed through LDS once.
+//
+// Same answer as k_set_probe (filterset.hip): per key, (a, b) = (h1 % m,
+// h2 % m) (/root/reference/src/bloom.rs:26-37) and mask = set[a] & set[b]
+// for every slot at once, set[b] read only where set[a] != 0 (the `&&` of
+// may_contain, src/bloom.rs:48-51), over Database::get's table fan-out
+// (src/lib.rs:129-134). What changes is the order of the reads. At C5's
+// density (10M keys against a 256 MiB set of 2M 128-B lines) k_set_probe
+// reads every line ~7 times, each a random 128-B fill: 14.3M fills, 1.8 GB
+// of fabric traffic for 0.26 GB of distinct sectors. Here:
+//
+//   k_dense_part  (1024 threads x 7 keys per block): hash, bin every key by
+//                 the 64 KiB region of the set holding set[a] (LDS rank
+//                 atomics, one wave scan), write the block's entries
+//                 region-sorted {b, a's offset in the region << 16 | key index
+//                 in the block} as one contiguous run list, the run starts
+//                 into column `block` of a region-major table (u16), and zero
+//                 the block's hit words (no separate memset);
+//   k_dense_probe (one workgroup per region, two per CU): stage the region
+//                 (64 KiB, coalesced) in LDS, gather the region's runs from
+//                 every partition block (a block scan of their lengths, each
+//                 lane finding its entry's run by binary search), set[a] from
+//                 LDS, set[b] by one global read only where set[a] != 0, and
+//                 the few non-zero masks ORed into the hit rows (atomicOr).
+//
+// The set is read once as a stream (256 MiB) instead of ~10M random fills;
+// the entries cost one 8-B round trip per key, and set[b] stays a random read
+// for the ~45 % of keys whose set[a] is non-zero. Regions are dealt to XCDs
+// in contiguous ranges, so the run lines adjacent regions share are fetched
+// once per XCD. Selected by density (capi.cpp set_probe_*); results are the
+// same bits, checked against the oracle (tests/test_dense_probe_gpu.py).
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "blockscan.hpp"
+#include "filterset.hpp"
+#include "profile.hpp"
+#include "setmask.hpp"
+
+namespace cb {
+namespace {
+
+constexpr uint32_t kDenseNT = 1024;
+constexpr uint32_t kDenseKPT = 7;
+constexpr uint32_t kDenseC = kDenseNT * kDenseKPT;  // keys per partition block (a multiple of 64)
+static_assert(kDenseC % 64 == 0 && kDenseC < 65536, "block keys: whole hit words, u16 run starts");
+constexpr uint32_t kRegionBytes = 65536;  // one region of the set, staged in LDS
+constexpr uint32_t kDenseMaxRegions = 4096;  // the partition histogram (16 KiB of LDS)
+constexpr uint32_t kDenseMaxBlocks = 2048;   // partition blocks per launch pair (the probe's run table)
+constexpr uint32_t kProbeU = 4;              // entries per lane per round of the probe
+// The partition pass at its natural 84 VGPRs runs five waves per SIMD (one
+// 16-wave block per CU, though LDS would take two); the experiment build can
+// force eight (two blocks per CU, 80 B of spill per lane) for the A/B.
+#if defined(CB_EXPERIMENTS) && defined(CB_DENSE_PART_LB8)
+#define CB_DENSE_PART_WAVES 8
+#else
+#define CB_DENSE_PART_WAVES 1
+#endif
+
+// XCD-aware region order (workgroups are dealt round-robin over the 8 XCDs):
+// XCD x takes regions [x R/8, (x+1) R/8) in order.
+__device__ __forceinline__ uint32_t xcd_region(uint32_t bid, uint32_t R) {
+  if (R & 7u) return bid;
+  return (bid & 7u) * (R >> 3) + (bid >> 3);
+}
+
+// Keys [k0 + blockIdx.x C, ...) of the chunk: positions, region bins, the
+// block's region-sorted entries and its column of the run-start table.
+template <int KEYK, int MODE, int W>
+__global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(KeySrc ks, uint64_t k0, uint64_t n, ModP mp,
+                                                         uint32_t rshift, uint32_t R,
+                                                         uint16_t* __restrict__ seg, uint32_t segstride,
+                                                         uint2* __restrict__ ent, uint64_t* __restrict__ hits,
+                                                         uint64_t hwords, uint32_t used) {
+  constexpr uint32_t NT = kDenseNT, KPT = kDenseKPT, C = kDenseC;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t Rp = (R + 4) & ~3u;  // hist: R + 1 counts (zero-padded to Rp), a discard word at Rp
+  uint32_t* hist = smem;
+  uint2* stage = reinterpret_cast<uint2*>(smem + Rp + 4);
+  const uint32_t tid = threadIdx.x;
+  const uint64_t kb = k0 + (uint64_t)blockIdx.x * C;  // the block's first key
+  const uint32_t pmask = (1u << rshift) - 1u;
+  for (uint32_t i = tid; i < Rp + 4; i += NT) hist[i] = 0;
+  // positions first: every key load of the thread in flight together
+  uint32_t pa[KPT], pb[KPT];
+  bool live[KPT];
+  if constexpr (KEYK == KEY_FIXED16 && MODE == MOD_POW2_32) {
+    const uint4* keys = reinterpret_cast<const uint4*>(ks.bytes);
+    uint4 kv[KPT];
+#pragma unroll
+    for (int j = 0; j < (int)KPT; ++j) {
+      const uint64_t k = kb + (uint64_t)j * NT + tid;
+      live[j] = k < n;
+      kv[j] = keys[live[j] ? k : n - 1];
+    }
+#pragma unroll
+    for (int j = 0; j < (int)KPT; ++j) {
+      uint32_t h1, h2;
+      hash16_u32(kv[j], h1, h2);
+      pa[j] = h1 & (uint32_t)mp.mask;
+      pb[j] = h2 & (uint32_t)mp.mask;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < (int)KPT; ++j) {
+      const uint64_t k = kb + (uint64_t)j * NT + tid;
+      live[j] = k < n;
+      uint64_t a = 0, b = 0;
+      if (live[j]) key_positions<KEYK, MODE>(ks, k, mp, a, b);
+      pa[j] = (uint32_t)a;  // m <= 2^32: positions fit (dense_ok)
+      pb[j] = (uint32_t)b;
+    }
+  }
+  __syncthreads();
+  uint32_t er[KPT];
+#pragma unroll
+  for (int j = 0; j < (int)KPT; ++j) er[j] = atomicAdd(&hist[live[j] ? pa[j] >> rshift : Rp], 1u);
+  __syncthreads();
+  wave0_exclusive_scan4(hist, Rp);  // hist[R] = the block's entry count
+  __syncthreads();
+  // column blockIdx.x of the region-major run-start table (row R: the count)
+  for (uint32_t t = tid; t <= R; t += NT) seg[(uint64_t)t * segstride + blockIdx.x] = (uint16_t)hist[t];
+#pragma unroll
+  for (int j = 0; j < (int)KPT; ++j)
+    if (live[j])
+      stage[hist[pa[j] >> rshift] + er[j]] = make_uint2(pb[j], ((pa[j] & pmask) << 16) | (j * NT + tid));
+  // the block's hit words (keys kb .. kb + C, whole words) start at zero:
+  // the probe only ORs the set bits in
+  {
+    const uint64_t nw = (n + 63) / 64, w0 = kb / 64;
+    constexpr uint32_t WPB = C / 64;
+    for (uint32_t i = tid; i < used * WPB; i += NT) {
+      const uint32_t f = i / WPB, w = i % WPB;
+      if (w0 + w < nw) hits[(uint64_t)f * hwords + w0 + w] = 0ull;
+    }
+  }
+  __syncthreads();
+  const uint32_t total = hist[R];
+  uint2* out = ent + (uint64_t)blockIdx.x * C;
+  const uint32_t n2 = total / 2;
+  for (uint32_t i = tid; i < n2; i += NT) reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(stage)[i];
+  if (tid == 0 && (total & 1u)) out[total - 1] = stage[total - 1];
+}
+
+// Last b with P[b] <= j (P: exclusive prefix of the runs' lengths, P[0] = 0).
+__device__ __forceinline__ uint32_t run_of(const uint32_t* P, uint32_t nblk, uint32_t j) {
+  uint32_t lo = 0, hi = nblk;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (P[mid] <= j)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo - 1;
+}
+
+template <int W>
+__global__ __launch_bounds__(kDenseNT, 8) void k_dense_probe(const void* __restrict__ setp, uint64_t m,
+                                                             uint32_t rshift, uint32_t R,
+                                                             const uint16_t* __restrict__ seg, uint32_t segstride,
+                                                             uint32_t nblk, const uint2* __restrict__ ent,
+                                                             uint64_t k0, uint64_t* __restrict__ hits,
+                                                             uint64_t hwords) {
+  typedef typename std::conditional<W == 32, uint32_t, uint64_t>::type word_t;
+  constexpr uint32_t NT = kDenseNT, C = kDenseC, P = kRegionBytes / sizeof(word_t);
+  __shared__ __attribute__((aligned(16))) word_t stage[P];
+  __shared__ uint32_t scan[kDenseMaxBlocks + 1];
+  __shared__ uint16_t starts[kDenseMaxBlocks];
+  const word_t* __restrict__ set = reinterpret_cast<const word_t*>(setp);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t r = xcd_region(blockIdx.x, R);
+  const uint64_t p0 = (uint64_t)r << rshift;
+  // the region's words in flight (64 KiB: four 16-B loads per lane) with the
+  // run table's two rows
+  constexpr uint32_t PER4 = 16 / sizeof(word_t), N4 = P / PER4;
+  uint4 v[N4 / NT];
+#pragma unroll
+  for (uint32_t j = 0; j < N4 / NT; ++j) {
+    const uint64_t p = p0 + (uint64_t)(j * NT + tid) * PER4;
+    if (p + PER4 <= m) {
+      v[j] = reinterpret_cast<const uint4*>(set + p)[0];
+    } else {  // the last region's tail (m not a multiple of the region)
+      word_t t[PER4];
+#pragma unroll
+      for (uint32_t q = 0; q < PER4; ++q) t[q] = p + q < m ? set[p + q] : (word_t)0;
+      v[j] = *reinterpret_cast<const uint4*>(t);
+    }
+  }
+  uint32_t s0[2] = {0, 0}, len[2] = {0, 0};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const uint32_t b = 2 * tid + u;
+    if (b < nblk) {
+      s0[u] = seg[(uint64_t)r * segstride + b];
+      len[u] = (uint32_t)seg[(uint64_t)(r + 1) * segstride + b] - s0[u];
+    }
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < N4 / NT; ++j) reinterpret_cast<uint4*>(stage)[j * NT + tid] = v[j];
+  uint64_t total64;
+  const uint32_t pre = (uint32_t)block_scan<NT>((uint64_t)(len[0] + len[1]), &total64);
+  const uint32_t E = (uint32_t)total64;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const uint32_t b = 2 * tid + u;
+    if (b < nblk) {
+      scan[b] = pre + (u ? len[0] : 0u);
+      starts[b] = (uint16_t)s0[u];
+    }
+  }
+  if (tid == 0) scan[nblk] = E;
+  __syncthreads();
+  for (uint32_t base = 0; base < E; base += kProbeU * NT) {
+    // a round of kProbeU entries per lane: every load of the round in
+    // flight together (entries, then the set[b] reads)
+    uint2 e[kProbeU];
+    uint32_t blk[kProbeU];
+#pragma unroll
+    for (uint32_t u = 0; u < kProbeU; ++u) {
+      const uint32_t i = base + u * NT + tid;
+      blk[u] = 0;
+      e[u] = make_uint2(0, 0xFFFFFFFFu);
+      if (i < E) {
+        blk[u] = run_of(scan, nblk, i);
+        e[u] = ent[(uint64_t)blk[u] * C + starts[blk[u]] + (i - scan[blk[u]])];
+      }
+    }
+    word_t va[kProbeU], vb[kProbeU];
+#pragma unroll
+    for (uint32_t u = 0; u < kProbeU; ++u) va[u] = e[u].y != 0xFFFFFFFFu ? stage[e[u].y >> 16] : (word_t)0;
+#pragma unroll
+    for (uint32_t u = 0; u < kProbeU; ++u) vb[u] = va[u] ? set[e[u].x] : (word_t)0;  // src/bloom.rs:50's &&
+#pragma unroll
+    for (uint32_t u = 0; u < kProbeU; ++u) {
+      word_t mask = va[u] & vb[u];
+      if (mask) {
+        const uint64_t key = k0 + (uint64_t)blk[u] * C + (e[u].y & 0xFFFFu);
+        const unsigned long long bit = 1ull << (key & 63u);
+        unsigned long long* row = reinterpret_cast<unsigned long long*>(hits) + key / 64;
+        while (mask) {
+          const uint32_t f = (uint32_t)__builtin_ctzll((uint64_t)mask);
+          mask &= mask - 1;
+          atomicOr(row + (uint64_t)f * hwords, bit);
+        }
+      }
+    }
+  }
+}
+
+template <int KK, int MM, int WW>
+void dense_part(uint32_t nblk, size_t lds, hipStream_t s, const KeySrc& ks, uint64_t k0, uint64_t kend,
+                const ModP& mp, uint32_t rshift, uint32_t R, uint16_t* seg, uint32_t stride, uint2* ent,
+                uint64_t* hits, uint64_t hwords, uint32_t used) {
+  hipLaunchKernelGGL((k_dense_part<KK, MM, WW>), dim3(nblk), dim3(kDenseNT), lds, s, ks, k0, kend, mp, rshift, R,
+                     seg, stride, ent, hits, hwords, used);
+}
+
+}  // namespace
+
+uint32_t dense_regions(uint32_t width, uint64_t m) {
+  const uint64_t P = kRegionBytes / (width / 8);
+  return (uint32_t)((m + P - 1) / P);
+}
+
+bool set_probe_dense_ok(uint32_t width, uint64_t m, uint64_t n) {
+  if ((width != 32 && width != 64) || !m || m > (1ull << 32)) return false;
+  const uint32_t R = dense_regions(width, m);
+  if (R > kDenseMaxRegions) return false;
+  // keys per 128-B line of the set: the streamed region pays for itself once
+  // each line would take ~2 random fills (C3: 0.5 per line, C5: 4.8)
+  const uint64_t lines = (m * (width / 8) + 127) / 128;
+  return n >= 2 * lines;
+}
+
+uint64_t dense_scratch_bytes(uint32_t width, uint64_t m, uint64_t n) {
+  const uint64_t chunk = (uint64_t)kDenseMaxBlocks * kDenseC;
+  const uint64_t nk = n < chunk ? n : chunk;
+  const uint64_t nblk = (nk + kDenseC - 1) / kDenseC;
+  const uint64_t stride = (nblk + 7) & ~7ull;
+  const uint64_t segb = ((uint64_t)dense_regions(width, m) + 1) * stride * 2;
+  return nblk * kDenseC * 8 + ((segb + 255) & ~255ull);
+}
+
+hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void* set, uint32_t used,
+                                  const KeySrc& ks, uint64_t n, const ModP& mp, uint64_t* hits, uint64_t hwords,
+                                  void* scratch, hipStream_t s) {
+  if (!n || !used) return hipSuccess;
+  if (!set_probe_dense_ok(width, mp.m, n)) return hipErrorInvalidValue;
+  const uint32_t R = dense_regions(width, mp.m);
+  const uint32_t rshift = width == 32 ? 14 : 13;  // 64 KiB of 4-B or 8-B words
+  const uint64_t chunk = (uint64_t)kDenseMaxBlocks * kDenseC;
+  const uint64_t nk0 = n < chunk ? n : chunk;
+  const uint32_t nblk0 = (uint32_t)((nk0 + kDenseC - 1) / kDenseC);
+  const uint32_t stride = (nblk0 + 7) & ~7u;
+  uint2* ent = reinterpret_cast<uint2*>(scratch);
+  uint16_t* seg = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(scratch) + (uint64_t)nblk0 * kDenseC * 8);
+  const size_t lds1 = (size_t)(((R + 4) & ~3u) + 4) * 4 + (size_t)kDenseC * 8;
+  for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
+    const uint64_t nk = n - k0 < chunk ? n - k0 : chunk;
+    const uint32_t nblk = (uint32_t)((nk + kDenseC - 1) / kDenseC);
+    {
+      ProfScope ps("k_dense_part", s);
+      // the keys of this chunk: k in [k0, k0 + nk), indices global
+      CB_SET_DISPATCH(keyk, mode, width,
+                      (dense_part<KK, MM, WW>(nblk, lds1, s, ks, k0, k0 + nk, mp, rshift, R, seg, stride, ent, hits,
+                                              hwords, used)));
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    {
+      ProfScope ps("k_dense_probe", s);
+      if (width == 32)
+        hipLaunchKernelGGL((k_dense_probe<32>), dim3(R), dim3(kDenseNT), 0, s, set, mp.m, rshift, R, seg, stride,
+                           nblk, ent, k0, hits, hwords);
+      else
+        hipLaunchKernelGGL((k_dense_probe<64>), dim3(R), dim3(kDenseNT), 0, s, set, mp.m, rshift, R, seg, stride,
+                           nblk, ent, k0, hits, hwords);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
+}
+
+}  // namespace cb

@@ -44,4 +44,18 @@ hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
                             const ModP& mp, const ZoneView* zones, uint64_t* hits,
                             uint64_t hwords, hipStream_t s, const PackSink* sink = nullptr);
 
+// Dense batches (densefs.hip): the same hits from a region-partitioned probe
+// that streams the set through LDS once. set_probe_dense_ok: the shapes it
+// takes (32- or 64-slot sets, m <= 2^32 with at most 4096 regions of 64 KiB)
+// and whether the batch is dense enough to pay (n >= 2 keys per 128-B line
+// of the set). scratch: dense_scratch_bytes of device memory (the entries
+// and the run table; reusable once the launch pair has run). No zone gate
+// and no exchange pack: callers keep k_set_probe for those.
+bool set_probe_dense_ok(uint32_t width, uint64_t m, uint64_t n);
+uint32_t dense_regions(uint32_t width, uint64_t m);
+uint64_t dense_scratch_bytes(uint32_t width, uint64_t m, uint64_t n);
+hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void* set, uint32_t used,
+                                  const KeySrc& ks, uint64_t n, const ModP& mp, uint64_t* hits, uint64_t hwords,
+                                  void* scratch, hipStream_t s);
+
 }  // namespace cb

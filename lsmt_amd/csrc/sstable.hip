@@ -933,6 +933,41 @@ __global__ __launch_bounds__(kNT, 6) void k_set_get_many(const void* __restrict_
   if (threadIdx.x == 0) tsum[blockIdx.x] = total;
 }
 
+// The wide walk's screen (wideset.hpp WideScreen): bit (B, h, slot) is clear
+// only when the table in that slot has a complete key bucket B none of whose
+// stored fingerprints falls in bin h (fp & (H - 1)). One thread per (table,
+// bucket); bits are ORed in (tables share screen words). Tables whose
+// buckets the screen cannot speak for (none yet, not well-formed, another
+// bucket count) set every bin: they always pass.
+__global__ __launch_bounds__(kNT) void k_wide_screen(const TableView* __restrict__ tv, const uint32_t* __restrict__ slots,
+                                                     uint32_t nt, uint32_t R, uint32_t bits, uint32_t hbits,
+                                                     uint64_t* __restrict__ scr) {
+  const uint64_t nb = 1ull << bits, H = 1ull << hbits;
+  const uint64_t idx = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  if (idx >= nb * nt) return;
+  const uint32_t i = (uint32_t)(idx >> bits);
+  const uint64_t B = idx & (nb - 1);
+  const uint32_t slot = slots ? slots[i] : i;
+  const TableView v = tv[i];
+  uint64_t bins = ~0ull;  // bit h: some stored fingerprint falls in bin h (all: no proof)
+  if (v.bkt && v.fast() && v.bkbits() == bits) {
+    const uint64_t sw = v.bkt[nb * kBktWords + B];
+    const uint32_t nst = (uint32_t)(sw & 15u);
+    if (nst <= kBktSlots) {
+      bins = 0;
+      for (uint32_t s = 0; s < nst; ++s) bins |= 1ull << ((sw >> (4 + 15 * s)) & (H - 1));
+    }
+  }
+  if (hbits < 6) bins &= (1ull << H) - 1;
+  unsigned long long* row = reinterpret_cast<unsigned long long*>(scr) + B * H * R + (slot >> 6);
+  const unsigned long long bit = 1ull << (slot & 63u);
+  while (bins) {
+    const uint32_t h = (uint32_t)__builtin_ctzll(bins);
+    bins &= bins - 1;
+    atomicOr(row + (uint64_t)h * R, bit);
+  }
+}
+
 // Database::get in one launch over a wide set (wideset.hpp): k_set_get_many
 // for more than 64 tables. Per key: rows a and b of the set (h1 % m, h2 % m,
 // src/bloom.rs:26-37); then the tables in groups of 64, newest first
@@ -955,7 +990,8 @@ __global__ __launch_bounds__(kNT, 5) void k_wide_get_many(const uint64_t* __rest
                                                        const WideGroup* __restrict__ groups,
                                                        const uint32_t* __restrict__ slots, KeySrc ks, uint64_t n,
                                                        int32_t* __restrict__ which, uint64_t* __restrict__ vsrc,
-                                                       uint64_t* __restrict__ dlen, uint64_t* __restrict__ tsum) {
+                                                       uint64_t* __restrict__ dlen, uint64_t* __restrict__ tsum,
+                                                       WideScreen ws) {
   const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   const bool live = k < n;
   const Query q = make_query<KEYK>(ks, live ? k : 0);
@@ -963,6 +999,11 @@ __global__ __launch_bounds__(kNT, 5) void k_wide_get_many(const uint64_t* __rest
   if (live) key_positions<KEYK, MODE>(ks, k, mp, pa, pb);
   const uint64_t* ra = set + pa * R;
   const uint64_t* rb = set + pb * R;
+  // the screen row of this key's bucket and fingerprint bin: one R-word row
+  // says, for every slot at once, whether the summary word could pass
+  const uint64_t* rs = ws.scr ? ws.scr + ((bkt_index(q.w0, ws.bits) << ws.hbits) +
+                                          (bkt_fp(q.w0) & ((1u << ws.hbits) - 1u))) * R
+                              : nullptr;
   const uint32_t kw[4] = {(uint32_t)(q.w0 >> 32), (uint32_t)q.w0, (uint32_t)(q.w1 >> 32), (uint32_t)q.w1};
   // The block walks the groups together: each group's 64 views and DirMaps
   // are staged in LDS once for the block (every search then reads its
@@ -1001,7 +1042,16 @@ __global__ __launch_bounds__(kNT, 5) void k_wide_get_many(const uint64_t* __rest
     } else {
       const uint64_t wa = wide_window(ra, R, gd.lo) & gmask;
       cand = wa ? (wa & wide_window(rb, R, gd.lo)) : 0ull;
+      if (cand && rs) cand &= wide_window(rs, R, gd.lo);  // the screen (slot order, like the rows)
       if (gd.kind == 1 && cand) cand = __builtin_bitreverse64(cand) >> (64 - gd.gn);  // bit gn-1-i -> i
+    }
+    if (gd.kind == 2 && cand && rs) {
+      uint64_t sc = 0;
+      for (uint32_t i = 0; i < gd.gn; ++i) {
+        const uint32_t s = slots[t0 + i];
+        sc |= ((rs[s >> 6] >> (s & 63)) & 1ull) << i;
+      }
+      cand &= sc;
     }
     // the candidates newest first, the group's views and maps from LDS. At
     // the product's m = 1024 most candidates are false positives (~3/4 of
@@ -1417,18 +1467,31 @@ hipError_t launch_set_get_many(int keyk, int mode, uint32_t width, const void* s
   return hipGetLastError();
 }
 
+hipError_t launch_wide_screen(const TableView* tv, const uint32_t* slots, uint32_t nt, uint32_t R, uint32_t bits,
+                              uint32_t hbits, uint64_t* scr, hipStream_t s) {
+  if (!nt || bits > 24 || hbits > 6) return hipErrorInvalidValue;
+  ProfScope ps("k_wide_screen", s);
+  const hipError_t e = hipMemsetAsync(scr, 0, wide_screen_bytes(R, bits, hbits), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_wide_screen, dim3(blocks_for(((uint64_t)nt) << bits, kNT)), dim3(kNT), 0, s, tv, slots, nt, R,
+                     bits, hbits, scr);
+  return hipGetLastError();
+}
+
 hipError_t launch_wide_get_many(int keyk, int mode, uint32_t R, const uint64_t* set, const ModP& mp,
                                 const WideZone* zones, const TableView* tv, uint32_t nt, const WideGroup* groups,
                                 const uint32_t* slots, const KeySrc& ks, uint64_t n, int32_t* which,
-                                uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum, hipStream_t s) {
+                                uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum, hipStream_t s,
+                                const WideScreen* screen) {
   if (!n) return hipSuccess;
   if (!nt || nt > 64 * R || R > kWideMax / 64) return hipErrorInvalidValue;
   const WideZone z = zones ? *zones : WideZone{nullptr, nullptr, nullptr, nullptr, 0};
+  const WideScreen sc = screen ? *screen : WideScreen{nullptr, 0, 0, 0};
   const dim3 g(blocks_for(n, kNT));
   ProfScope ps("k_wide_get_many", s);
 #define WG(KK, MM)                                                                                                 \
   hipLaunchKernelGGL((k_wide_get_many<KK, MM>), g, dim3(kNT), 0, s, set, R, mp, z, tv, nt, groups, slots, ks, n, \
-                     which, vsrc, dlen, tsum)
+                     which, vsrc, dlen, tsum, sc)
   switch (keyk * 3 + mode) {
     case 0: WG(KEY_FIXED16, MOD_POW2_32); break;
     case 1: WG(KEY_FIXED16, MOD_POW2_64); break;

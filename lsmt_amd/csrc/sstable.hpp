@@ -433,10 +433,28 @@ hipError_t launch_set_get_many(int keyk, int mode, uint32_t width, const void* s
 // zones (nullable), then the same walk and outputs as launch_get_many.
 struct WideZone;
 struct WideGroup;
+// The wide walk's screen: for a set whose tables share one bucket count
+// (2^bits), row (B << hbits) + h (R words, slot-major like the set's rows)
+// has slot s's bit clear only when that table's key bucket B is complete and
+// holds no fingerprint (bkt_fp) in bin h = fp & (2^hbits - 1): a key whose
+// bucket is B and whose fingerprint falls in bin h is then absent from that
+// table (Ok(None)) without its summary word being read. scr == nullptr: none.
+struct WideScreen {
+  const uint64_t* scr;
+  uint32_t bits, hbits, pad;
+};
+__host__ __device__ inline uint64_t wide_screen_bytes(uint32_t R, uint32_t bits, uint32_t hbits) {
+  return ((uint64_t)1 << (bits + hbits)) * R * 8;
+}
+// Builds the screen of tables tv[0..nt) in slots slots[i] (nullptr: slot i)
+// into scr (wide_screen_bytes), on stream s after their buckets.
+hipError_t launch_wide_screen(const TableView* tv, const uint32_t* slots, uint32_t nt, uint32_t R, uint32_t bits,
+                              uint32_t hbits, uint64_t* scr, hipStream_t s);
 hipError_t launch_wide_get_many(int keyk, int mode, uint32_t R, const uint64_t* set, const ModP& mp,
                                 const WideZone* zones, const TableView* tv, uint32_t nt, const WideGroup* groups,
                                 const uint32_t* slots, const KeySrc& ks, uint64_t n, int32_t* which,
-                                uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum, hipStream_t s);
+                                uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum, hipStream_t s,
+                                const WideScreen* screen = nullptr);
 hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uint64_t* hits,
                            const uint32_t* rows, uint64_t hwords, const KeySrc& ks, uint64_t n,
                            int32_t* which, uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum,

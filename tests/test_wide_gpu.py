@@ -140,3 +140,70 @@ def test_wide_ragged_keys_and_updates(gpu, m, width, nf):
     expect[7] = oracle.OracleFilter(m)
     got = s.probe(gpu.KeyBatch(n=len(keys), data=data, offsets=offs))
     assert np.array_equal(got, oracle.probe_var(expect, data, offs))
+
+
+def test_wide_screen_mixed_buckets_and_rebuilt_tables(gpu):
+    """The wide walk's screen (sstable.hpp WideScreen: per bucket and
+    fingerprint bin, one bit per slot that could still hold the key) against
+    the oracle's walk: tables of two bucket counts (the screen speaks for the
+    common one, the others always pass), tables whose keys share their first
+    8 bytes (crowded buckets past four lines: no proof of absence), the same
+    call repeated (the cached screen), and tables replaced by new ones (the
+    screen is rebuilt from the new tables' ids, not their addresses)."""
+    rng = np.random.default_rng(77)
+    pool = workload.key_range(5151, 40_000)
+
+    def make(t):
+        if t % 17 == 5:  # crowded: 600 keys sharing the 8-byte prefix "crowded:"
+            ks = [b"crowded:" + bytes(pool[i][:8]) for i in rng.choice(len(pool), 600, replace=False)]
+        else:
+            nk = 3000 if t % 11 == 3 else 1024  # 2^12 buckets for some tables, 2^10 for most
+            ks = [bytes(pool[i]) for i in rng.choice(len(pool), nk, replace=False)]
+        ks = sorted(set(ks))
+        ents = [(k, b"v%03d:%s" % (t, k[-4:])) for k in ks]
+        tb, bloom, zone = gpu.sstable_create(ents, m=1024)
+        return tb, bloom, zone, ents
+
+    nt = 130
+    made = [make(t) for t in range(nt)]
+    crowd = [b"crowded:" + bytes(pool[i][:8]) for i in rng.integers(0, len(pool), 1000)]
+    look = np.concatenate([pool[rng.integers(0, len(pool), 5000)], workload.key_range(5252, 1000),
+                           np.frombuffer(b"".join(crowd), np.uint8).reshape(-1, 16)])[rng.permutation(7000)]
+
+    def expect():
+        data, offs = np.ascontiguousarray(look.reshape(-1)), np.arange(0, 16 * (len(look) + 1), 16, dtype=np.uint64)
+        ofs, ozs, ots = [], [], []
+        for t in range(nt - 1, -1, -1):
+            tb, _, zone, ents = made[t]
+            o = oracle.OracleFilter(1024)
+            for k, _ in ents:
+                o.insert(k)
+            ofs.append(o)
+            ozs.append(oracle.OracleZone(zone.min, zone.max))
+            ots.append(oracle.OracleTable(tb.data()))
+        return oracle.get_many(ots, oracle.probe_gated(ofs, ozs, data, offs), data, offs)
+
+    def run():
+        s = gpu.FilterSet(1024, width=192)
+        for t in range(nt):
+            s.assign(t, made[t][1])
+            s.set_zone(t, made[t][2])
+        tabs = [made[t][0] for t in range(nt - 1, -1, -1)]
+        slots = np.arange(nt, dtype=np.uint32)[::-1].copy()
+        return gpu.get_many(tabs, look, filterset=s, hit_rows=slots)
+
+    for _ in range(2):  # the second call reuses the stream's screen
+        which, voff, vals = run()
+        ow, ovoff, ovals = expect()
+        assert np.array_equal(np.asarray(which), ow)
+        assert np.array_equal(np.asarray(voff, dtype=np.uint64), ovoff) and vals == ovals
+    for t in (0, 40, 77, 129):  # replaced tables: new content, possibly at the old addresses
+        made[t] = None
+    import gc
+    gc.collect()
+    for t in (0, 40, 77, 129):
+        made[t] = make(t + 1000)
+    which, voff, vals = run()
+    ow, ovoff, ovals = expect()
+    assert np.array_equal(np.asarray(which), ow)
+    assert np.array_equal(np.asarray(voff, dtype=np.uint64), ovoff) and vals == ovals
