@@ -533,8 +533,7 @@ std::atomic<int> g_set_dense{0};
 bool use_dense(const cb_filterset* set, uint64_t n, bool gated, bool pack) {
   const int mode = g_set_dense.load(std::memory_order_relaxed);
   if (mode < 0 || gated || pack || set_is_wide(set)) return false;
-  if (mode > 0) return set->width <= 64 && set->m <= (1ull << 32) &&
-                       cb::dense_regions(set->width, set->m) <= 4096 && set->m;
+  if (mode > 0) return cb::set_dense_shape_ok(set->width, set->m);
   return cb::set_probe_dense_ok(set->width, set->m, n);
 }
 

@@ -265,10 +265,12 @@ uint32_t dense_regions(uint32_t width, uint64_t m) {
   return (uint32_t)((m + P - 1) / P);
 }
 
+bool set_dense_shape_ok(uint32_t width, uint64_t m) {
+  return (width == 32 || width == 64) && m && m <= (1ull << 32) && dense_regions(width, m) <= kDenseMaxRegions;
+}
+
 bool set_probe_dense_ok(uint32_t width, uint64_t m, uint64_t n) {
-  if ((width != 32 && width != 64) || !m || m > (1ull << 32)) return false;
-  const uint32_t R = dense_regions(width, m);
-  if (R > kDenseMaxRegions) return false;
+  if (!set_dense_shape_ok(width, m)) return false;
   // keys per 128-B line of the set: the streamed region pays for itself once
   // each line would take ~2 random fills (C3: 0.5 per line, C5: 4.8)
   const uint64_t lines = (m * (width / 8) + 127) / 128;
@@ -288,7 +290,7 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
                                   const KeySrc& ks, uint64_t n, const ModP& mp, uint64_t* hits, uint64_t hwords,
                                   void* scratch, hipStream_t s) {
   if (!n || !used) return hipSuccess;
-  if (!set_probe_dense_ok(width, mp.m, n)) return hipErrorInvalidValue;
+  if (!set_dense_shape_ok(width, mp.m)) return hipErrorInvalidValue;
   const uint32_t R = dense_regions(width, mp.m);
   const uint32_t rshift = width == 32 ? 14 : 13;  // 64 KiB of 4-B or 8-B words
   const uint64_t chunk = (uint64_t)kDenseMaxBlocks * kDenseC;

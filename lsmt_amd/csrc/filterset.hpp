@@ -52,6 +52,7 @@ hipError_t launch_set_probe(int keyk, int mode, uint32_t width, const void* set,
 // and the run table; reusable once the launch pair has run). No zone gate
 // and no exchange pack: callers keep k_set_probe for those.
 bool set_probe_dense_ok(uint32_t width, uint64_t m, uint64_t n);
+bool set_dense_shape_ok(uint32_t width, uint64_t m);  // the shape alone (forced mode)
 uint32_t dense_regions(uint32_t width, uint64_t m);
 uint64_t dense_scratch_bytes(uint32_t width, uint64_t m, uint64_t n);
 hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void* set, uint32_t used,
