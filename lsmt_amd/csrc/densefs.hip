@@ -14,9 +14,9 @@
 //                 the 64 KiB region of the set holding set[a] (LDS rank
 //                 atomics, one wave scan), write the block's entries
 //                 region-sorted {b, a's offset in the region << 16 | key index
-//                 in the block} as one contiguous run list, the run starts
-//                 into column `block` of a region-major table (u16), and zero
-//                 the block's hit words (no separate memset);
+//                 in the block} as one contiguous run list, its run starts
+//                 as one row of a block-major table (u16), and zero the
+//                 block's hit words (no separate memset);
 //   k_dense_probe (one workgroup per region, two per CU): stage the region
 //                 (64 KiB, coalesced) in LDS, gather the region's runs from
 //                 every partition block (a block scan of their lengths, each
@@ -32,6 +32,7 @@
 // same bits, checked against the oracle (tests/test_dense_probe_gpu.py).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "blockscan.hpp"
@@ -118,10 +119,34 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
 #pragma unroll
   for (int j = 0; j < (int)KPT; ++j) er[j] = atomicAdd(&hist[live[j] ? pa[j] >> rshift : Rp], 1u);
   __syncthreads();
-  wave0_exclusive_scan4(hist, Rp);  // hist[R] = the block's entry count
-  __syncthreads();
-  // column blockIdx.x of the region-major run-start table (row R: the count)
-  for (uint32_t t = tid; t <= R; t += NT) seg[(uint64_t)t * segstride + blockIdx.x] = (uint16_t)hist[t];
+  {
+    // exclusive scan of the R + 1 counts by every wave (a wave-0 scan of
+    // 4096 bins is a ~2 us chain per block): thread t owns RPT consecutive
+    // bins, one block scan of the thread sums, then the prefixes in place
+    constexpr uint32_t RPT = (kDenseMaxRegions + 4 + NT - 1) / NT;
+    uint32_t c[RPT], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < RPT; ++j) {
+      const uint32_t i = tid * RPT + j;
+      c[j] = i < Rp ? hist[i] : 0u;
+      sum += c[j];
+    }
+    uint64_t tot;
+    uint32_t run = (uint32_t)block_scan<NT>(sum, &tot);
+#pragma unroll
+    for (uint32_t j = 0; j < RPT; ++j) {
+      const uint32_t i = tid * RPT + j;
+      if (i < Rp) hist[i] = run;
+      run += c[j];
+    }
+  }
+  __syncthreads();  // hist[r] = region r's run start in the block, hist[R] = the block's entry count
+  // row blockIdx.x of the block-major run-start table (R + 1 u16, coalesced;
+  // the probe reads its two columns, L2-resident per XCD)
+  {
+    uint16_t* row = seg + (uint64_t)blockIdx.x * segstride;
+    for (uint32_t t = tid; t <= R; t += NT) row[t] = (uint16_t)hist[t];
+  }
 #pragma unroll
   for (int j = 0; j < (int)KPT; ++j)
     if (live[j])
@@ -163,7 +188,7 @@ __global__ __launch_bounds__(kDenseNT, 8) void k_dense_probe(const void* __restr
                                                              const uint16_t* __restrict__ seg, uint32_t segstride,
                                                              uint32_t nblk, const uint2* __restrict__ ent,
                                                              uint64_t k0, uint64_t* __restrict__ hits,
-                                                             uint64_t hwords) {
+                                                             uint64_t hwords, uint32_t xflags) {
   typedef typename std::conditional<W == 32, uint32_t, uint64_t>::type word_t;
   constexpr uint32_t NT = kDenseNT, C = kDenseC, P = kRegionBytes / sizeof(word_t);
   __shared__ __attribute__((aligned(16))) word_t stage[P];
@@ -194,8 +219,9 @@ __global__ __launch_bounds__(kDenseNT, 8) void k_dense_probe(const void* __restr
   for (int u = 0; u < 2; ++u) {
     const uint32_t b = 2 * tid + u;
     if (b < nblk) {
-      s0[u] = seg[(uint64_t)r * segstride + b];
-      len[u] = (uint32_t)seg[(uint64_t)(r + 1) * segstride + b] - s0[u];
+      const uint16_t* row = seg + (uint64_t)b * segstride;
+      s0[u] = row[r];
+      len[u] = (uint32_t)row[r + 1] - s0[u];
     }
   }
 #pragma unroll
@@ -232,11 +258,12 @@ __global__ __launch_bounds__(kDenseNT, 8) void k_dense_probe(const void* __restr
 #pragma unroll
     for (uint32_t u = 0; u < kProbeU; ++u) va[u] = e[u].y != 0xFFFFFFFFu ? stage[e[u].y >> 16] : (word_t)0;
 #pragma unroll
-    for (uint32_t u = 0; u < kProbeU; ++u) vb[u] = va[u] ? set[e[u].x] : (word_t)0;  // src/bloom.rs:50's &&
+    for (uint32_t u = 0; u < kProbeU; ++u)
+      vb[u] = va[u] ? ((xflags & 1u) ? va[u] : set[e[u].x]) : (word_t)0;  // src/bloom.rs:50's &&
 #pragma unroll
     for (uint32_t u = 0; u < kProbeU; ++u) {
       word_t mask = va[u] & vb[u];
-      if (mask) {
+      if (mask && !(xflags & 2u)) {
         const uint64_t key = k0 + (uint64_t)blk[u] * C + (e[u].y & 0xFFFFu);
         const unsigned long long bit = 1ull << (key & 63u);
         unsigned long long* row = reinterpret_cast<unsigned long long*>(hits) + key / 64;
@@ -281,8 +308,8 @@ uint64_t dense_scratch_bytes(uint32_t width, uint64_t m, uint64_t n) {
   const uint64_t chunk = (uint64_t)kDenseMaxBlocks * kDenseC;
   const uint64_t nk = n < chunk ? n : chunk;
   const uint64_t nblk = (nk + kDenseC - 1) / kDenseC;
-  const uint64_t stride = (nblk + 7) & ~7ull;
-  const uint64_t segb = ((uint64_t)dense_regions(width, m) + 1) * stride * 2;
+  const uint64_t stride = ((uint64_t)dense_regions(width, m) + 1 + 63) & ~63ull;  // u16 per region, 128-B rows
+  const uint64_t segb = nblk * stride * 2;
   return nblk * kDenseC * 8 + ((segb + 255) & ~255ull);
 }
 
@@ -296,10 +323,17 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
   const uint64_t chunk = (uint64_t)kDenseMaxBlocks * kDenseC;
   const uint64_t nk0 = n < chunk ? n : chunk;
   const uint32_t nblk0 = (uint32_t)((nk0 + kDenseC - 1) / kDenseC);
-  const uint32_t stride = (nblk0 + 7) & ~7u;
+  const uint32_t stride = (R + 1 + 63) & ~63u;
   uint2* ent = reinterpret_cast<uint2*>(scratch);
   uint16_t* seg = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(scratch) + (uint64_t)nblk0 * kDenseC * 8);
   const size_t lds1 = (size_t)(((R + 4) & ~3u) + 4) * 4 + (size_t)kDenseC * 8;
+  uint32_t xflags = 0;
+#ifdef CB_EXPERIMENTS
+  // timing-only A/B (the hits are wrong): CB_DENSE_X bit 0 skips the set[b]
+  // gathers, bit 1 the hit atomics
+  static const uint32_t env_x = getenv("CB_DENSE_X") ? (uint32_t)atoi(getenv("CB_DENSE_X")) : 0u;
+  xflags = env_x;
+#endif
   for (uint64_t k0 = 0; k0 < n; k0 += chunk) {
     const uint64_t nk = n - k0 < chunk ? n - k0 : chunk;
     const uint32_t nblk = (uint32_t)((nk + kDenseC - 1) / kDenseC);
@@ -316,10 +350,10 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
       ProfScope ps("k_dense_probe", s);
       if (width == 32)
         hipLaunchKernelGGL((k_dense_probe<32>), dim3(R), dim3(kDenseNT), 0, s, set, mp.m, rshift, R, seg, stride,
-                           nblk, ent, k0, hits, hwords);
+                           nblk, ent, k0, hits, hwords, xflags);
       else
         hipLaunchKernelGGL((k_dense_probe<64>), dim3(R), dim3(kDenseNT), 0, s, set, mp.m, rshift, R, seg, stride,
-                           nblk, ent, k0, hits, hwords);
+                           nblk, ent, k0, hits, hwords, xflags);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
