@@ -1230,7 +1230,7 @@ def c5_leg(args, torch, dev, local, world, rank, steps, warmup, lanes_n, check, 
     _, ev1_ms = _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes[:1], step, steps)
     from lsmt_amd import _lib
     path = int(_lib.load().cb_last_path())  # 6: the dense (region-partitioned) probe, 3: k_set_probe
-    kern = ["k_dense_part", "k_dense_probe"] if path == 6 else ["k_set_probe"]
+    kern = ["k_dense_part", "k_dense_seg_t", "k_dense_probe"] if path == 6 else ["k_set_probe"]
     kus = _kernel_us(_lib.load(), torch, dev, kern, step, min(steps, 20))  # one lane (P = 1 still)
     P = Psaved
     sectors, rand_reads = _set_sectors(filters, look_np, m, F)
@@ -1242,7 +1242,8 @@ def c5_leg(args, torch, dev, local, world, rank, steps, warmup, lanes_n, check, 
            "ms_per_step": round(el / steps * 1e3, 4), "region_us_per_step": round(us, 2),
            "one_lane_us_per_step": round(ev1_ms * 1e3 / steps, 2),
            "value": round(n * F * world / (el / steps), 1), "unit": "probes/s (all GPUs)",
-           "path": "dense (k_dense_part + k_dense_probe: keys partitioned by set region, regions staged in LDS)"
+           "path": "dense (k_dense_part + k_dense_seg_t + k_dense_probe: keys partitioned by set region, regions "
+                   "staged in LDS)"
                    if path == 6 else "k_set_probe (one random set line per read)",
            "kernels_us": {k: v["avg_us"] for k, v in kus.items()},
            "kernels_us_source": "library HIP events around each launch, one lane",

@@ -17,6 +17,7 @@
 //                 in the block} as one contiguous run list, its run starts
 //                 as one row of a block-major table (u16), and zero the
 //                 block's hit words (no separate memset);
+//   k_dense_seg_t transposes the run-start table to region-major (LDS tiles);
 //   k_dense_probe (one workgroup per region, two per CU): stage the region
 //                 (64 KiB, coalesced) in LDS, gather the region's runs from
 //                 every partition block (a block scan of their lengths, each
@@ -169,6 +170,29 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
   if (tid == 0 && (total & 1u)) out[total - 1] = stage[total - 1];
 }
 
+// The run-start table, block-major [nblk][R + 1] (the partition pass's
+// coalesced rows) -> region-major [R + 1][tstride] (the probe's contiguous
+// columns), through 64 x 64 LDS tiles: every load and store is a 128-B row
+// piece. (Storing each block's column scattered from the partition pass
+// cost it ~13 us; reading the block-major rows scattered from the probe,
+// ~33 us.)
+__global__ __launch_bounds__(256) void k_dense_seg_t(const uint16_t* __restrict__ in, uint32_t istride,
+                                                      uint32_t nblk, uint32_t nrow, uint16_t* __restrict__ out,
+                                                      uint32_t ostride) {
+  __shared__ uint16_t tile[64][66];
+  const uint32_t tx = threadIdx.x & 63u, ty = threadIdx.x >> 6;
+  const uint32_t b0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+  for (uint32_t i = ty; i < 64; i += 4) {
+    const uint32_t b = b0 + i, r = r0 + tx;
+    tile[i][tx] = (b < nblk && r < nrow) ? in[(uint64_t)b * istride + r] : (uint16_t)0;
+  }
+  __syncthreads();
+  for (uint32_t i = ty; i < 64; i += 4) {
+    const uint32_t r = r0 + i, b = b0 + tx;
+    if (r < nrow && b < nblk) out[(uint64_t)r * ostride + b] = tile[tx][i];
+  }
+}
+
 // Last b with P[b] <= j (P: exclusive prefix of the runs' lengths, P[0] = 0).
 __device__ __forceinline__ uint32_t run_of(const uint32_t* P, uint32_t nblk, uint32_t j) {
   uint32_t lo = 0, hi = nblk;
@@ -218,10 +242,9 @@ __global__ __launch_bounds__(kDenseNT, 8) void k_dense_probe(const void* __restr
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const uint32_t b = 2 * tid + u;
-    if (b < nblk) {
-      const uint16_t* row = seg + (uint64_t)b * segstride;
-      s0[u] = row[r];
-      len[u] = (uint32_t)row[r + 1] - s0[u];
+    if (b < nblk) {  // rows r and r + 1 of the region-major table: contiguous over the blocks
+      s0[u] = seg[(uint64_t)r * segstride + b];
+      len[u] = (uint32_t)seg[(uint64_t)(r + 1) * segstride + b] - s0[u];
     }
   }
 #pragma unroll
@@ -308,8 +331,9 @@ uint64_t dense_scratch_bytes(uint32_t width, uint64_t m, uint64_t n) {
   const uint64_t chunk = (uint64_t)kDenseMaxBlocks * kDenseC;
   const uint64_t nk = n < chunk ? n : chunk;
   const uint64_t nblk = (nk + kDenseC - 1) / kDenseC;
-  const uint64_t stride = ((uint64_t)dense_regions(width, m) + 1 + 63) & ~63ull;  // u16 per region, 128-B rows
-  const uint64_t segb = nblk * stride * 2;
+  const uint64_t R1 = (uint64_t)dense_regions(width, m) + 1;
+  const uint64_t stride = (R1 + 63) & ~63ull, tstride = (nblk + 63) & ~63ull;  // u16, 128-B rows
+  const uint64_t segb = nblk * stride * 2 + R1 * tstride * 2;
   return nblk * kDenseC * 8 + ((segb + 255) & ~255ull);
 }
 
@@ -323,9 +347,10 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
   const uint64_t chunk = (uint64_t)kDenseMaxBlocks * kDenseC;
   const uint64_t nk0 = n < chunk ? n : chunk;
   const uint32_t nblk0 = (uint32_t)((nk0 + kDenseC - 1) / kDenseC);
-  const uint32_t stride = (R + 1 + 63) & ~63u;
+  const uint32_t stride = (R + 1 + 63) & ~63u, tstride = (nblk0 + 63) & ~63u;
   uint2* ent = reinterpret_cast<uint2*>(scratch);
   uint16_t* seg = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(scratch) + (uint64_t)nblk0 * kDenseC * 8);
+  uint16_t* segT = seg + (uint64_t)nblk0 * stride;
   const size_t lds1 = (size_t)(((R + 4) & ~3u) + 4) * 4 + (size_t)kDenseC * 8;
   uint32_t xflags = 0;
 #ifdef CB_EXPERIMENTS
@@ -347,12 +372,19 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
       if (e != hipSuccess) return e;
     }
     {
+      ProfScope ps("k_dense_seg_t", s);
+      hipLaunchKernelGGL(k_dense_seg_t, dim3((nblk + 63) / 64, (R + 1 + 63) / 64), dim3(256), 0, s, seg, stride, nblk,
+                         R + 1, segT, tstride);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    {
       ProfScope ps("k_dense_probe", s);
       if (width == 32)
-        hipLaunchKernelGGL((k_dense_probe<32>), dim3(R), dim3(kDenseNT), 0, s, set, mp.m, rshift, R, seg, stride,
+        hipLaunchKernelGGL((k_dense_probe<32>), dim3(R), dim3(kDenseNT), 0, s, set, mp.m, rshift, R, segT, tstride,
                            nblk, ent, k0, hits, hwords, xflags);
       else
-        hipLaunchKernelGGL((k_dense_probe<64>), dim3(R), dim3(kDenseNT), 0, s, set, mp.m, rshift, R, seg, stride,
+        hipLaunchKernelGGL((k_dense_probe<64>), dim3(R), dim3(kDenseNT), 0, s, set, mp.m, rshift, R, segT, tstride,
                            nblk, ent, k0, hits, hwords, xflags);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
