@@ -656,6 +656,10 @@ int set_probe_device(const cb_filterset* set, const uint8_t* keys, uint32_t key_
   return CB_OK;
 }
 
+bool set_probe_dense(const cb_filterset* set, uint64_t n, bool gated) {
+  return use_dense(set, n, gated && set->zany, false);
+}
+
 int note_zone_read(const cb_filterset* set, hipStream_t s) {
   std::lock_guard<std::mutex> lk(set->zmu);
   hipEvent_t& ev = set->zread[s];

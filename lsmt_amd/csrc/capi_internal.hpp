@@ -296,6 +296,10 @@ int compress_state(Workspace& ws, hipStream_t s, cb::CompressState** out);
 // claim words). Used by cb_set_probe_pack_fixed and the comm layer.
 int set_probe_device(const cb_filterset* set, const uint8_t* keys, uint32_t key_len, uint64_t n, bool gated,
                      uint64_t* hits, uint32_t* sink_pack, uint64_t cap, hipStream_t s);
+// Whether a probe of n keys with these settings takes the dense (region-
+// partitioned) FilterSet probe, which writes no exchange pack: the fused
+// probe + sparse exchange then compresses the rows in a separate pass.
+bool set_probe_dense(const cb_filterset* set, uint64_t n, bool gated);
 
 // A launch that reads set's device zone table was enqueued on s (capi.cpp).
 int note_zone_read(const cb_filterset* set, hipStream_t s);

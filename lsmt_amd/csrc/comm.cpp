@@ -444,11 +444,12 @@ int cb_set_probe_allgather_fixed(cb_comm* c, const cb_filterset* set, const uint
   }
   if (!cap) return fail(CB_EINVAL, "sparse exchange needs cap > 0");
   const uint64_t max_rows = (total_rows + (uint64_t)c->world - 1) / (uint64_t)c->world;
-  if (max_rows > 64) {
+  if (max_rows > 64 || set_probe_dense(set, n, gated != 0)) {
     // shards past 64 tables (wide sets: the product's hundreds of m = 1024
-    // tables over a few GPUs): the probe writes the rows, then the separate
+    // tables over a few GPUs), and dense batches (C5: the region-partitioned
+    // probe writes no pack): the probe writes the rows, then the separate
     // compress and the same sparse all-gather (every rank takes this branch:
-    // max_rows is the same everywhere)
+    // max_rows, n and the sets' shape are the same everywhere)
     int rc = set_probe_device(set, keys, key_len, n, gated != 0, local_hits, nullptr, 0, s);
     if (rc) return rc;
     return cb_hits_allgather(c, local_hits, rows, hwords, total_rows, full, CB_XCHG_SPARSE, cap, ok, sparse_used,

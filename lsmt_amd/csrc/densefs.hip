@@ -75,15 +75,10 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
                                                          uint32_t rshift, uint32_t R,
                                                          uint16_t* __restrict__ seg, uint32_t segstride,
                                                          uint2* __restrict__ ent, uint64_t* __restrict__ hits,
-                                                         uint64_t hwords, uint32_t used, uint32_t nblk,
-                                                         uint16_t* __restrict__ segT, uint32_t tstride) {
+                                                         uint64_t hwords, uint32_t used) {
   constexpr uint32_t NT = kDenseNT, KPT = kDenseKPT, C = kDenseC;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  // segT != nullptr: the run starts go straight into column b of the
-  // region-major table, the blocks dealt to XCDs in contiguous ranges so the
-  // 64 blocks sharing a 128-B line of a column write it in one L2
-  const uint32_t b = segT ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
-  if (b >= nblk) return;
+  const uint32_t b = blockIdx.x;
   const uint32_t Rp = (R + 4) & ~3u;  // hist: R + 1 counts (zero-padded to Rp), a discard word at Rp
   uint32_t* hist = smem;
   uint2* stage = reinterpret_cast<uint2*>(smem + Rp + 4);
@@ -150,9 +145,7 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
   __syncthreads();  // hist[r] = region r's run start in the block, hist[R] = the block's entry count
   // row blockIdx.x of the block-major run-start table (R + 1 u16, coalesced;
   // the probe reads its two columns, L2-resident per XCD)
-  if (segT) {
-    for (uint32_t t = tid; t <= R; t += NT) segT[(uint64_t)t * tstride + b] = (uint16_t)hist[t];
-  } else {
+  {
     uint16_t* row = seg + (uint64_t)b * segstride;
     for (uint32_t t = tid; t <= R; t += NT) row[t] = (uint16_t)hist[t];
   }
@@ -181,9 +174,10 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
 // The run-start table, block-major [nblk][R + 1] (the partition pass's
 // coalesced rows) -> region-major [R + 1][tstride] (the probe's contiguous
 // columns), through 64 x 64 LDS tiles: every load and store is a 128-B row
-// piece. (Storing each block's column scattered from the partition pass
-// cost it ~13 us; reading the block-major rows scattered from the probe,
-// ~33 us.)
+// piece. (Measured against: each block's column stored scattered from the
+// partition pass, 86 against 73 us for that pass; the same with the blocks
+// dealt to XCDs in contiguous ranges, 88 us; the probe reading the
+// block-major rows scattered, +33 us for the probe. This launch: 12 us.)
 __global__ __launch_bounds__(256) void k_dense_seg_t(const uint16_t* __restrict__ in, uint32_t istride,
                                                       uint32_t nblk, uint32_t nrow, uint16_t* __restrict__ out,
                                                       uint32_t ostride) {
@@ -311,10 +305,9 @@ __global__ __launch_bounds__(kDenseNT, 8) void k_dense_probe(const void* __restr
 template <int KK, int MM, int WW>
 void dense_part(uint32_t nblk, size_t lds, hipStream_t s, const KeySrc& ks, uint64_t k0, uint64_t kend,
                 const ModP& mp, uint32_t rshift, uint32_t R, uint16_t* seg, uint32_t stride, uint2* ent,
-                uint64_t* hits, uint64_t hwords, uint32_t used, uint16_t* segT, uint32_t tstride) {
-  const uint32_t grid = segT ? (nblk + 7) & ~7u : nblk;
-  hipLaunchKernelGGL((k_dense_part<KK, MM, WW>), dim3(grid), dim3(kDenseNT), lds, s, ks, k0, kend, mp, rshift, R,
-                     seg, stride, ent, hits, hwords, used, nblk, segT, tstride);
+                uint64_t* hits, uint64_t hwords, uint32_t used) {
+  hipLaunchKernelGGL((k_dense_part<KK, MM, WW>), dim3(nblk), dim3(kDenseNT), lds, s, ks, k0, kend, mp, rshift, R,
+                     seg, stride, ent, hits, hwords, used);
 }
 
 }  // namespace
@@ -362,10 +355,7 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
   uint16_t* segT = seg + (uint64_t)nblk0 * stride;
   const size_t lds1 = (size_t)(((R + 4) & ~3u) + 4) * 4 + (size_t)kDenseC * 8;
   uint32_t xflags = 0;
-  bool direct = false;  // the partition pass writes the region-major table itself (no k_dense_seg_t)
 #ifdef CB_EXPERIMENTS
-  static const bool env_direct = getenv("CB_DENSE_DIRECT") && getenv("CB_DENSE_DIRECT")[0] == '1';
-  direct = env_direct;
   // timing-only A/B (the hits are wrong): CB_DENSE_X bit 0 skips the set[b]
   // gathers, bit 1 the hit atomics
   static const uint32_t env_x = getenv("CB_DENSE_X") ? (uint32_t)atoi(getenv("CB_DENSE_X")) : 0u;
@@ -379,11 +369,11 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
       // the keys of this chunk: k in [k0, k0 + nk), indices global
       CB_SET_DISPATCH(keyk, mode, width,
                       (dense_part<KK, MM, WW>(nblk, lds1, s, ks, k0, k0 + nk, mp, rshift, R, seg, stride, ent, hits,
-                                              hwords, used, direct ? segT : nullptr, tstride)));
+                                              hwords, used)));
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
-    if (!direct) {
+    {
       ProfScope ps("k_dense_seg_t", s);
       hipLaunchKernelGGL(k_dense_seg_t, dim3((nblk + 63) / 64, (R + 1 + 63) / 64), dim3(256), 0, s, seg, stride, nblk,
                          R + 1, segT, tstride);
