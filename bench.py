@@ -1482,6 +1482,35 @@ def wide_fanout_leg(args, torch, dev, local, sh, LK, timed, kernel_ms, lsmt_amd,
            "kernels_us": {kk: round(v["avg_us"], 2) for kk, v in kus.items()},
            "launches_per_batch": {"search": 1, "tile_scan": 1, "b64_decode": 1},
            "table_build_s": round(flush_s, 2)}
+    # roofline of the search launch: its compulsory HBM bytes are the keys
+    # (16 B) and its three per-lookup outputs (which 4 B, value source 8 B,
+    # decoded length 8 B), plus one 128-B key-bucket line per found key; the
+    # set's rows (40 KB), the screen (1.3 MB) and the summary words (2.4 MB)
+    # stay in every XCD's L2. It is bound by dependent L2 round trips (rows ->
+    # screen -> summary words of the survivors -> bucket line), not by bytes.
+    wk = kus.get("k_wide_get_many", {}).get("avg_us")
+    if wk:
+        alg = n * (16 + 4 + 8 + 8) + found * 128
+        wr = {"bound": "latency (dependent L2 round trips per lookup)", "kernel": "k_wide_get_many",
+              "kernel_avg_us": wk, "algorithmic_bytes": int(alg),
+              "algorithmic_def": "n x (16 B key + 20 B outputs) + 128 B bucket line per found key",
+              "achieved": round(alg / (wk * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "frac": round(alg / (wk * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+        name, d = _pmc_summary("wide")
+        e = (d or {}).get("kernels", {}).get("k_wide_get_many", {})
+        if e.get("hbm_bytes_per_launch"):
+            wr["traffic"] = int(e["hbm_bytes_per_launch"])
+            wr["traffic_source"] = f"profiles/{name}"
+            if e.get("TCC_HIT_sum") is not None and e.get("TCC_MISS_sum") is not None:
+                req = e["TCC_HIT_sum"] + e["TCC_MISS_sum"]
+                wr["l2_requests_per_launch"] = int(req)
+                wr["l2_hit_rate"] = round(e["TCC_HIT_sum"] / req, 4) if req else None
+                wr["l2_requests_per_lookup"] = round(req / n, 1)
+            if e.get("avg_us_one_lane"):
+                wr["profile_check"] = {"source": f"profiles/{name} (rocprofv3 --kernel-trace)",
+                                       "kernel_us": e["avg_us_one_lane"],
+                                       "ratio_to_line_kernel_us": round(wk / e["avg_us_one_lane"], 4)}
+        out["roofline"] = wr
     if not args.no_cpu:
         from oracle import oracle
         smp = 4096
