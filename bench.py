@@ -1660,6 +1660,12 @@ def _profile_check(shape, kernels, alg_bytes, line_frac_one_lane):
     frac = alg_bytes / (step * 1e-6) / 1e9 / HBM_PEAK_GBS
     out = {"source": f"profiles/{name} (rocprofv3 --kernel-trace, one lane)", "kernels": list(kernels),
            "step_us": round(step, 2), "frac": round(frac, 4)}
+    ev = d.get("events_one_lane_us", {})
+    if ev.get("traced"):  # the same traced run's own HIP-event step: the two clocks on one run
+        out["traced_run_events_us"] = ev["traced"]
+        out["ratio_to_traced_run_events"] = round(ev["traced"] / step, 4)
+    if ev.get("plain"):  # the profiled box's untraced run of the same command
+        out["plain_run_events_us"] = ev["plain"]
     if line_frac_one_lane:
         out["ratio_to_line_frac_one_lane"] = round(frac / line_frac_one_lane, 4)
     return out

@@ -100,6 +100,28 @@ def main():
             if t:
                 e["hbm_GBps"] = round(e["hbm_bytes_per_launch"] / (t * 1e3), 1)
         res[k] = e
+    # the bench's own one-lane step (HIP events) in the traced run (kt1) and
+    # in the plain run before it, for the shape the summary is for
+    lines = {}
+    for tag, fn in (("traced", "kt1_bench.json"), ("plain", "plain1_bench.json")):
+        try:
+            d = json.loads(open(os.path.join(root, fn)).read().strip().splitlines()[-1])
+        except Exception:
+            continue
+        shape = meta.get("shape")
+        us = None
+        if shape == "c4" and d.get("c4"):
+            us = d["c4"].get("one_lane_us_per_step")
+        elif shape == "c5" and d.get("c5"):
+            us = d["c5"].get("one_lane_us_per_step")
+        elif shape == "wide" and d.get("wide_fanout"):
+            us = d["wide_fanout"].get("kernels_us", {}).get("k_wide_get_many")
+        elif shape == "c3" and d.get("roofline"):
+            us = d["roofline"].get("kernel_avg_us_one_lane")
+        if us:
+            lines[tag] = us
+    if lines:
+        meta["events_one_lane_us"] = lines
     for k, e in res.items():
         print(k, json.dumps(e))
     if out_json:

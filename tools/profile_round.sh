@@ -22,6 +22,10 @@ case $SHAPE in
   *) echo "unknown shape $SHAPE"; exit 2 ;;
 esac
 BENCH="$BENCH $*"
+# the same one-lane command without the profiler first: the bench's own
+# (HIP-event) step on this box, beside the traced one (tracing can lengthen
+# short back-to-back launches)
+timeout -k 10 300 $BENCH --probe-streams 1 > $OUT/plain1_bench.json 2> $OUT/plain1.err || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $BENCH > $OUT/kt_bench.json 2> $OUT/kt.err || exit 1
 BENCH="$BENCH --probe-streams 1"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt1 -o kt1 --output-format csv -- $BENCH > $OUT/kt1_bench.json 2> $OUT/kt1.err || exit 1
