@@ -35,6 +35,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Bloom probes/sec device-resident (1M keys × 32 filters); build keys/sec"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+SPIN_CYCLES_PER_US = 2100  # torch.cuda._sleep cycles per microsecond (~2.1 GHz shader clock)
 
 
 def log(*a):
@@ -423,6 +424,11 @@ def main():
             step_no[0] = 0  # the rep's step runs on lane 0 (= `stream`, where the events are)
             if r < reps:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                # device-resident: a ~200 us spin holds the
+                # stream while the host issues the step, so the interval is
+                # the step's device time, not the host's issue latency (the
+                # spin touches no memory: the caches stay as the flush left them)
+                torch.cuda._sleep(SPIN_CYCLES_PER_US * 200)
                 e0.record(stream)
                 fn()
                 e1.record(stream)
@@ -435,6 +441,31 @@ def main():
         torch.cuda.synchronize(dev)
         return (float(np.median(step_ms)),
                 {nm: round(float(np.median(v)), 2) for nm, v in kus.items() if v})
+
+    def gated_steps(fn, k, st):
+        """K steps of fn queued behind a spin kernel on st (so the GPU starts
+        them only after the host has issued all of them): (device us per
+        step from HIP events around them, host issue us per step, whether the
+        spin outlasted the issue)."""
+        torch.cuda.synchronize(dev)
+        # (while the GPU spins, a deep single-stream queue slows the host's
+        # issue to ~75 us per C2 build on this stack: keep k modest and the
+        # spin long enough for all of it)
+        spin_us = 4000 + 120 * k
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        es = torch.cuda.Event(enable_timing=True)
+        es.record(st)
+        torch.cuda._sleep(SPIN_CYCLES_PER_US * spin_us)
+        e0.record(st)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        issue = time.perf_counter() - t0
+        e1.record(st)
+        torch.cuda.synchronize(dev)
+        # the spin must still have been running when the last step was issued
+        ok = issue * 1e3 < es.elapsed_time(e0)
+        return e0.elapsed_time(e1) * 1e3 / k, issue * 1e6 / k, bool(ok)
 
     probe_kernels = ["k_part_probe", "k_tile_probe", "k_masks_to_hits", "k_probe_direct",
                      "k_set_probe"]
@@ -812,7 +843,10 @@ def main():
     # each step waits for the previous one on the stream
     BP_saved, BP = BP, 1
     timed(build_step, LK, lanes=b_streams[:1])
-    b_one_us = region["ms"] * 1e3 / region["k"]
+    b_one_issued_us = region["ms"] * 1e3 / region["k"]
+    # ... and its device time: the LK steps queued behind a spin kernel first,
+    # so the host's per-step issue (Python + the C call) is not in the interval
+    b_one_us, b_issue_us, b_gated_ok = gated_steps(build_step, 64, stream)
     BP = BP_saved
     bprof = kernel_ms(["k_build_part", "k_build_tile", "k_insert_direct"], build_step, LK)
     bcold = None
@@ -840,7 +874,12 @@ def main():
              "pipeline_lanes": BP, "cold": bcold,
              "region_us_per_step": round(b_region_us, 2), "frac": frac(b_region_us),
              "one_lane": {"us_per_build": round(b_one_us, 2), "frac": frac(b_one_us),
-                          "note": "one build at a time on one stream (HIP events / K): the latency a flush pays"}}
+                          "note": "one build at a time on one stream, device time: HIP events around K builds "
+                                  "queued behind a spin kernel (the latency a flush's kernels take)",
+                          "queued_fully": b_gated_ok, "host_issue_us_per_build": round(b_issue_us, 2),
+                          "host_issued_us_per_build": round(b_one_issued_us, 2),
+                          "host_issued_note": "the same K builds issued live from Python: a build's device "
+                                              "time or the host's issue time, whichever is longer"}}
     if bcold:
         bcold["frac"] = frac(bcold["ms_per_step"] * 1e3)
         bcold["clean_caches"]["frac"] = frac(bcold["clean_caches"]["ms_per_step"] * 1e3)
