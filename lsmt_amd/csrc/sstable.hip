@@ -981,11 +981,20 @@ __global__ __launch_bounds__(kNT) void k_wide_screen(const TableView* __restrict
 // The wide walk's summary words loaded together: 4 / 8 / 16 at once measured
 // 671-679 / 792-809 / 816-820 M gets/s against 517-519 one at a time (300
 // tables of m = 1024); 16 doubles the scratch spill (36 -> 72 B per lane).
+#if defined(CB_EXPERIMENTS) && defined(CB_WIDE_SCREEN_BATCH)
+constexpr uint32_t kScreen = CB_WIDE_SCREEN_BATCH;
+#else
 constexpr uint32_t kScreen = 8;
+#endif
 // (Five waves per SIMD at its natural 96 VGPRs: forcing six, 80 VGPRs with
 // 112 B of scratch per lane, measured 606-617 against 782-804 M gets/s.)
+#if defined(CB_EXPERIMENTS) && defined(CB_WIDE_LB4)
+#define CB_WIDE_WAVES 4
+#else
+#define CB_WIDE_WAVES 5
+#endif
 template <int KEYK, int MODE>
-__global__ __launch_bounds__(kNT, 5) void k_wide_get_many(const uint64_t* __restrict__ set, uint32_t R, ModP mp,
+__global__ __launch_bounds__(kNT, CB_WIDE_WAVES) void k_wide_get_many(const uint64_t* __restrict__ set, uint32_t R, ModP mp,
                                                        WideZone z, const TableView* __restrict__ tv, uint32_t nt,
                                                        const WideGroup* __restrict__ groups,
                                                        const uint32_t* __restrict__ slots, KeySrc ks, uint64_t n,
