@@ -986,15 +986,14 @@ constexpr uint32_t kScreen = CB_WIDE_SCREEN_BATCH;
 #else
 constexpr uint32_t kScreen = 8;
 #endif
-// (Five waves per SIMD at its natural 96 VGPRs: forcing six, 80 VGPRs with
-// 112 B of scratch per lane, measured 606-617 against 782-804 M gets/s.)
-#if defined(CB_EXPERIMENTS) && defined(CB_WIDE_LB4)
-#define CB_WIDE_WAVES 4
-#else
-#define CB_WIDE_WAVES 5
-#endif
+// (Round 4, before the screen: five waves per SIMD at its natural 96 VGPRs;
+// forcing six, 80 VGPRs with 112 B of scratch per lane, measured 606-617
+// against 782-804 M gets/s.)
+// Four waves per SIMD, 109 VGPRs and no spill (round 5, with the screen):
+// 1.81-1.84 against 1.63 G gets/s for five waves at 96 VGPRs and 56 B of
+// spill per lane (tools/gpu/r05_wide4.sh, alternating on one box).
 template <int KEYK, int MODE>
-__global__ __launch_bounds__(kNT, CB_WIDE_WAVES) void k_wide_get_many(const uint64_t* __restrict__ set, uint32_t R, ModP mp,
+__global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __restrict__ set, uint32_t R, ModP mp,
                                                        WideZone z, const TableView* __restrict__ tv, uint32_t nt,
                                                        const WideGroup* __restrict__ groups,
                                                        const uint32_t* __restrict__ slots, KeySrc ks, uint64_t n,
