@@ -124,9 +124,12 @@ int wide_screen(Workspace& ws, const cb_table* const* tables, const std::vector<
                 const std::vector<uint32_t>& rows, uint32_t R, const cb::TableView* dviews, const uint32_t* drows,
                 hipStream_t s, cb::WideScreen* out) {
   const uint32_t nt = (uint32_t)views.size();
+  uint32_t hbits = kScreenHbits;
 #ifdef CB_EXPERIMENTS
   static const bool off = getenv("CB_NO_SCREEN") && getenv("CB_NO_SCREEN")[0] == '1';  // the A/B
   if (off) return CB_OK;
+  static const int env_h = getenv("CB_SCREEN_HBITS") ? atoi(getenv("CB_SCREEN_HBITS")) : -1;
+  if (env_h >= 0 && env_h <= 6) hbits = (uint32_t)env_h;
 #endif
   uint32_t bits = 0;
   for (const auto& v : views)
@@ -134,13 +137,13 @@ int wide_screen(Workspace& ws, const cb_table* const* tables, const std::vector<
       bits = v.bkbits();
       break;
     }
-  if (!bits || cb::wide_screen_bytes(R, bits, kScreenHbits) > kScreenMaxBytes) return CB_OK;
+  if (!bits || cb::wide_screen_bytes(R, bits, hbits) > kScreenMaxBytes) return CB_OK;
   std::vector<uint64_t> sig;
   sig.reserve(4 + 4 * (size_t)nt);
   sig.push_back(nt);
   sig.push_back(R);
   sig.push_back(bits);
-  sig.push_back(kScreenHbits);
+  sig.push_back(hbits);
   for (uint32_t i = 0; i < nt; ++i) {
     sig.push_back(tables[i]->uid);
     sig.push_back(rows.empty() ? i : rows[i]);
@@ -148,12 +151,12 @@ int wide_screen(Workspace& ws, const cb_table* const* tables, const std::vector<
     sig.push_back(views[i].meta);
   }
   if (sig != ws.w_scr_sig) {
-    HIP_TRY(ws.w_scr.reserve(cb::wide_screen_bytes(R, bits, kScreenHbits), s));
-    HIP_TRY(cb::launch_wide_screen(dviews, rows.empty() ? nullptr : drows, nt, R, bits, kScreenHbits,
+    HIP_TRY(ws.w_scr.reserve(cb::wide_screen_bytes(R, bits, hbits), s));
+    HIP_TRY(cb::launch_wide_screen(dviews, rows.empty() ? nullptr : drows, nt, R, bits, hbits,
                                    (uint64_t*)ws.w_scr.p, s));
     ws.w_scr_sig.swap(sig);
   }
-  *out = cb::WideScreen{(const uint64_t*)ws.w_scr.p, bits, kScreenHbits, 0};
+  *out = cb::WideScreen{(const uint64_t*)ws.w_scr.p, bits, hbits, 0};
   return CB_OK;
 }
 

@@ -1032,12 +1032,14 @@ __global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __rest
       for (uint32_t i = threadIdx.x; i < gn * kViewDw; i += kNT) vd[i] = vs[i];
     }
     __syncthreads();
+#if !(defined(CB_EXPERIMENTS) && defined(CB_WIDE_NO_SDM))
     for (uint32_t i = threadIdx.x; i < gn * kMapWords; i += kNT) {
       const uint32_t t = i / kMapWords, j = i - t * kMapWords;
       const DirMap* gm = stv[t].dmap;
       if (gm) reinterpret_cast<uint4*>(sdm + t)[j] = reinterpret_cast<const uint4*>(gm)[j];
     }
     __syncthreads();
+#endif
     if (!active) continue;
     const WideGroup gd = groups[g];
     const uint64_t gmask = gd.gn >= 64 ? ~0ull : ((1ull << gd.gn) - 1);
@@ -1120,7 +1122,11 @@ __global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __rest
         }
         const TableView& v = stv[i];
         LineRec r;
+#if defined(CB_EXPERIMENTS) && defined(CB_WIDE_NO_SDM)
+        if (search(v, q, r, v.dmap) < 0) continue;  // Ok(None)
+#else
         if (search(v, q, r, &sdm[i]) < 0) continue;  // Ok(None)
+#endif
         if (r.vdl == kBadValue) continue;             // Err(..) is skipped by `if let Ok(Some(v))`
         w = (int32_t)(t0 + i);
         src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
