@@ -352,6 +352,48 @@ def test_create_bounded_refuses_a_batch_past_its_bounds(gpu):
     L.cb_filter_destroy(fh)
 
 
+def test_create_bounded_host_bytes_device_offsets(gpu):
+    """Host key (or value) bytes with device offsets: the bytes are staged into
+    a block of exactly the declared bounds, so offsets past them are refused
+    by the call itself (CB_EINVAL, nothing enqueued, no table or filter
+    returned), and a batch within them builds the reference's file and filter
+    (the kernels used to read past the staged block)."""
+    import ctypes
+    from lsmt_amd import _lib
+    keys = [b"h%05d" % i for i in range(3000)]
+    vals = [b"w" * 12 for _ in keys]
+    (ko, kd), (vo, vd) = _dev_batches(keys, vals)
+    kh = kd.cpu().numpy()  # the same bytes in (pageable) host memory
+    vh = vd.cpu().numpy()
+    L = _lib.load()
+    for kb, vb in ((kh, vd), (kd, vh)):  # host keys / host values, device offsets for both
+        th, fh = ctypes.c_void_p(), ctypes.c_void_p()
+        kp = kb.ctypes.data if isinstance(kb, np.ndarray) else kb.data_ptr()
+        vp = vb.ctypes.data if isinstance(vb, np.ndarray) else vb.data_ptr()
+        short_k = 100 if isinstance(kb, np.ndarray) else int(kd.numel())
+        short_v = 100 if isinstance(vb, np.ndarray) else int(vd.numel())
+        rc = L.cb_sstable_create_bounded(kp, ko.data_ptr(), short_k, vp, vo.data_ptr(), short_v, len(keys), 1024, 0,
+                                         None, ctypes.byref(th), ctypes.byref(fh))
+        assert rc == _lib.CB_EINVAL and not th.value and not fh.value
+        rc = L.cb_sstable_create_bounded(kp, ko.data_ptr(), int(kd.numel()), vp, vo.data_ptr(), int(vd.numel()),
+                                         len(keys), 1024, 0, None, ctypes.byref(th), ctypes.byref(fh))
+        assert rc == 0 and L.cb_table_wait(th) == 0
+        n = ctypes.c_uint64()
+        dp = ctypes.c_void_p()
+        assert L.cb_table_data(th, ctypes.byref(dp), ctypes.byref(n)) == 0
+        buf = np.zeros(n.value, np.uint8)
+        assert L.cb_table_copy(th, 0, n.value, buf.ctypes.data) == 0
+        assert buf.tobytes() == oracle.sstable_create(list(zip(keys, vals)))
+        o = oracle.OracleFilter(1024)
+        for k in keys:
+            o.insert(k)
+        got = np.zeros(1024, np.uint8)
+        assert L.cb_filter_export_bools(fh, got.ctypes.data, None) == 0
+        assert np.array_equal(got, o.bools())
+        L.cb_table_destroy(th)
+        L.cb_filter_destroy(fh)
+
+
 def test_create_pending_table_destroyed_unread(gpu):
     """A table destroyed before anything finalised it waits for its own work
     first (no buffer is reused under a running kernel)."""

@@ -675,3 +675,54 @@ def test_get_many_key_buckets(gpu):
         which, voff, vals = gpu.get_many(tables, kb, stream=other if i == 1 else None)
         assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals, i
     assert (which >= 0).sum() > 0.3 * len(look) and all((which == t).any() for t in range(5))
+
+
+def test_get_many_bucket_budget_and_cross_stream_waits(gpu):
+    """cb_table_bucket_limit: tables read while the limit is 0 (or below their
+    buckets' size) are searched without key buckets, with the reference's
+    answers; later tables get them again at the default. Reads on several
+    streams right after a table's first read enqueue a wait for its bucket
+    build (no stream-handle identity), and every answer equals the
+    oracle's."""
+    import torch
+    keys = [bytes(k) for k in workload.key_range(2500, 30_000)]
+    data = b"".join(k + b"\t" + base64_of(i) + b"\n" for i, k in enumerate(sorted(keys)))
+    look = keys[::5] + [bytes(k) for k in workload.key_range(2501, 4000)]
+    d, o = var(look)
+    kb = gpu.KeyBatch(n=len(look), data=d, offsets=o)
+    ow, ovoff, ovals = oracle.get_many([oracle.OracleTable(data)], None, d, o)
+    try:
+        gpu.Table.bucket_limit(0)
+        t0 = gpu.Table(data)
+        which, voff, vals = gpu.get_many([t0], kb)
+        assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals
+        gpu.Table.bucket_limit(1024)  # smaller than this table's 2^15 x 136 B
+        t1 = gpu.Table(data)
+        which, voff, vals = gpu.get_many([t1], kb)
+        assert np.array_equal(which, ow) and vals == ovals
+    finally:
+        gpu.Table.bucket_limit(1 << 30)
+    t2 = gpu.Table(data)
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(4)]
+    n = len(look)
+    kd = gpu.KeyBatch(n=n, data=torch.from_numpy(d).to(dev), offsets=torch.from_numpy(o.view(np.int64)).to(dev))
+    bufs = [(torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n + 1, dtype=torch.int64, device=dev),
+             torch.empty(len(ovals) + 16, dtype=torch.uint8, device=dev)) for _ in streams]
+    # enqueue-only reads on four streams, back to back: the first builds the
+    # buckets on its stream, the other three enqueue waits for that build
+    with torch.cuda.stream(streams[0]):
+        torch.cuda._sleep(20_000_000)  # hold the building stream so the others queue behind its event
+    for st, out in zip(streams, bufs):
+        gpu.get_many([t2], kd, stream=st, out=out, wait=False)
+    torch.cuda.synchronize()
+    for which, voff, vals in bufs:
+        tot = int(voff[n].item())
+        assert np.array_equal(which.cpu().numpy(), ow)
+        assert np.array_equal(voff.cpu().numpy().view(np.uint64), ovoff)
+        assert bytes(vals[:tot].cpu().numpy()) == ovals
+
+
+def base64_of(i):
+    import base64
+    return base64.b64encode(b"val%d" % i)
