@@ -79,6 +79,15 @@ int main(int argc, char** argv) {
       return 1;
     }
     if (init(0)) return 1;
+    // C2_FUSED=-1 / 0: the two-launch or the one-launch single build
+    // (cb_set_build_fused, libraries from round 5 on)
+    if (const char* fz = getenv("C2_FUSED")) {
+      auto set_fused = (int (*)(int))dlsym(L, "cb_set_build_fused");
+      if (!set_fused || set_fused(atoi(fz))) {
+        fprintf(stderr, "%s: cb_set_build_fused(%s) unavailable\n", argv[li], fz);
+        return 1;
+      }
+    }
     void* f = nullptr;
     if (create(m, 0, &f)) return 1;
     auto step = [&]() {
@@ -111,7 +120,8 @@ int main(int argc, char** argv) {
       cold.push_back(ms * 1e3f);
     }
     std::sort(cold.begin(), cold.end());
-    printf("{\"lib\": \"%s\", \"one_lane_us\": [", argv[li]);
+    printf("{\"lib\": \"%s\", \"fused\": \"%s\", \"one_lane_us\": [", argv[li],
+           getenv("C2_FUSED") ? getenv("C2_FUSED") : "default");
     for (size_t i = 0; i < warm.size(); ++i) printf("%s%.2f", i ? ", " : "", warm[i]);
     printf("], \"cold_us_median\": %.2f}\n", (cold[3] + cold[4]) / 2);
     fflush(stdout);
