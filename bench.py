@@ -742,7 +742,21 @@ def main():
         fk = workload.key_range(7000, nf_e)
         fv = workload.table_value(fk, 1)
         res = {}
-        for label, keys_np in (("sorted", workload.sort_keys16(fk)), ("unsorted", fk)):
+
+        def shared_prefix_keys(n, seed):
+            # every key under one 8-byte prefix ("default:" + 8 hex digits of a
+            # permutation): one bin for the bin sort, so the merge sort it
+            # enqueues after itself runs (capi_sstable.cpp sstable_enqueue)
+            perm = np.random.default_rng(seed).permutation(n).astype(np.uint32)
+            hexd = np.frombuffer(b"0123456789abcdef", np.uint8)
+            out = np.empty((n, 16), np.uint8)
+            out[:, :8] = np.frombuffer(b"default:", np.uint8)
+            for c in range(8):
+                out[:, 8 + c] = hexd[(perm >> (28 - 4 * c)) & 15]
+            return out
+
+        for label, keys_np in (("sorted", workload.sort_keys16(fk)), ("unsorted", fk),
+                               ("unsorted_shared_prefix", shared_prefix_keys(nf_e, 7001))):
             kd = torch.from_numpy(np.ascontiguousarray(keys_np.reshape(-1))).to(dev)
             vd = torch.from_numpy(np.ascontiguousarray(fv.reshape(-1))).to(dev)
             ko = torch.from_numpy(np.arange(0, 16 * (nf_e + 1), 16, dtype=np.int64)).to(dev)
@@ -801,7 +815,8 @@ def main():
                            "data file + index + Bloom filter + zone, inputs in HBM",
                  "kernels_us_source": "library HIP events around each launch (cb_profile): a launch's figure also "
                                       "holds its dispatch gap; rocprofv3 durations are in profiles/ (DESIGN.md §6)",
-                 "sorted_input": res["sorted"], "unsorted_input": res["unsorted"]}
+                 "sorted_input": res["sorted"], "unsorted_input": res["unsorted"],
+                 "unsorted_shared_prefix_input": res["unsorted_shared_prefix"]}
         if rank == 0 and world == 1 and not args.no_cpu:
             from oracle import oracle
             sample = 1 << 17

@@ -514,19 +514,13 @@ int cb_set_path(int path);
  * 64-slot sets, m <= 2^32 in at most 4096 regions of 64 KiB; tests), -1 =
  * never. Never for gated probes or the fused exchange pack. Process-wide. */
 int cb_set_dense(int mode);
-/* Single tiled builds (one filter of m >= 2^20 bits, the C2 shape) as one
- * launch whose tile workgroups wait on the partition workgroups' arrival
- * counters, instead of a partition launch and a tile launch; same bits.
- * mode 0 or 1 = wherever the tile plan allows it (default), -1 = never.
- * Process-wide. */
-int cb_set_build_fused(int mode);
 /* Path the last insert/probe on this thread used (1 direct, 2 tiled, 3 FilterSet,
  * 4 FilterSet zero-copy: pinned host keys and hits read/written by the kernel,
  * 5 cb_may_contain answered from the host mirror, 6 FilterSet dense probe). */
 int cb_last_path(void);
 /* Per-kernel timing with HIP events recorded on each launch's own stream
  * (off by default). Kernel names: "k_insert_direct", "k_probe_direct",
- * "k_build_part", "k_build_tile", "k_build_fused", "k_part_probe", "k_tile_probe",
+ * "k_build_part", "k_build_tile", "k_part_probe", "k_tile_probe",
  * "k_masks_to_hits", "k_set_build", "k_set_or_slot", "k_set_put_slot",
  * "k_set_probe". cb_profile_read waits for pending events and returns the
  * accumulated milliseconds and launch count for one kernel. */

@@ -18,7 +18,6 @@ from .bloom import (  # noqa: E402
     insert_many,
     last_path,
     probe,
-    set_build_fused,
     set_dense,
     set_path,
     unpack_hits,
@@ -34,6 +33,6 @@ from .bloom import (  # noqa: E402
 )
 
 __all__ = ["BloomFilter", "BloomProto", "DeviceKeys", "FilterSet", "insert_many", "KeyBatch", "device_count", "last_path",
-           "probe", "set_build_fused", "set_dense", "set_path", "unpack_hits", "zone_bounds", "ZoneMap", "TableMeta", "Table", "get_many", "sstable_create",
+           "probe", "set_dense", "set_path", "unpack_hits", "zone_bounds", "ZoneMap", "TableMeta", "Table", "get_many", "sstable_create",
            "hits_compress", "hits_expand", "hits_expand_set"]
 __version__ = "0.1.0"

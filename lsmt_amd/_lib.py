@@ -155,7 +155,6 @@ def load():
         "cb_table_force_exact": ([i32], i32),
         "cb_table_bucket_limit": ([u64], i32),
         "cb_set_dense": ([i32], i32),
-        "cb_set_build_fused": ([i32], i32),
         "cb_table_search_fixed": ([P, u8p, u32, u64, P, P], i32),
         "cb_table_search_var": ([P, u8p, P, u64, P, P], i32),
         "cb_get_many_fixed": ([P, u32, P, P, u8p, u32, u64, P, P, P, u64, pu64, P], i32),

@@ -72,13 +72,6 @@ def set_dense(mode: int) -> None:
     check(_L().cb_set_dense(int(mode)))
 
 
-def set_build_fused(mode: int) -> None:
-    """Single tiled builds (the C2 shape) as one launch: 0 / 1 wherever the
-    tile plan allows it (default), -1 never: a partition launch and a tile
-    launch (cb_set_build_fused; the same bits either way)."""
-    check(_L().cb_set_build_fused(int(mode)))
-
-
 # ---- key batches ---------------------------------------------------------------
 
 def _ptr_of(x):

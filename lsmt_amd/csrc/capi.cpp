@@ -141,11 +141,6 @@ int g_path_override = 0;  // 0 auto, 1 direct, 2 tiled
 
 constexpr int PATH_DIRECT = 1, PATH_TILED = 2;
 
-// Single tiled builds as one launch (kernels.hip k_build_fused)?
-// cb_set_build_fused: 0 / 1 wherever the plan allows it (default), -1 never
-// (k_build_part + k_build_tile).
-std::atomic<int> g_build_fused{0};
-
 uint64_t alloc_words_for(uint64_t m) {
   // Pad to whole 2^18-bit tiles (the largest LDS tile) so tiled passes never
   // read or write past the allocation; small filters pad to one 2^16-bit
@@ -326,19 +321,8 @@ int insert_locked(Workspace& ws, cb_filter* f, const uint8_t* keys, const uint64
       if (!covers(f, p)) return fail(CB_EINVAL, "internal: build tile plan exceeds the filter allocation");
       HIP_TRY(ws.seg.reserve(cb::build_seg_bytes(p), s));
       HIP_TRY(ws.ent.reserve(cb::build_ent_bytes(p), s));
-      if (g_build_fused.load(std::memory_order_relaxed) >= 0 && cb::build_fused_ok(p)) {
-        if (!ws.b_sync.p) {  // the arrival counters, zeroed once (k_build_fused keeps them so)
-          HIP_TRY(ws.b_sync.reserve(cb::kBuildSyncBytes, s));
-          HIP_TRY(hipMemsetAsync(ws.b_sync.p, 0, cb::kBuildSyncBytes, s));
-          ws.b_par = 0;
-        }
-        HIP_TRY(cb::launch_build_fused(keyk, f->mode, f->words, f->known_zero, ks, nk, f->mp, p, (uint32_t*)ws.seg.p,
-                                       (uint32_t*)ws.ent.p, (uint32_t*)ws.b_sync.p, ws.b_par, s));
-        ws.b_par ^= 1u;
-      } else {
-        HIP_TRY(cb::launch_build_tiled(keyk, f->mode, f->words, f->known_zero, ks, nk, f->mp, p,
-                                       (uint32_t*)ws.seg.p, (uint32_t*)ws.ent.p, s));
-      }
+      HIP_TRY(cb::launch_build_tiled(keyk, f->mode, f->words, f->known_zero, ks, nk, f->mp, p,
+                                     (uint32_t*)ws.seg.p, (uint32_t*)ws.ent.p, s));
       f->known_zero = false;
     }
   }
@@ -1047,11 +1031,6 @@ int cb_last_path(void) { return g_last_path; }
 int cb_set_dense(int mode) {
   if (mode < -1 || mode > 1) return fail(CB_EINVAL, "mode must be -1, 0 or 1");
   g_set_dense.store(mode, std::memory_order_relaxed);
-  return CB_OK;
-}
-int cb_set_build_fused(int mode) {
-  if (mode < -1 || mode > 1) return fail(CB_EINVAL, "mode must be -1, 0 or 1");
-  g_build_fused.store(mode, std::memory_order_relaxed);
   return CB_OK;
 }
 

@@ -161,7 +161,7 @@ struct TablePending {
   const uint8_t *dk = nullptr, *dv = nullptr;
   const uint64_t *dko = nullptr, *dvo = nullptr;
   uint64_t n = 0, cap_bytes = 0;
-  bool binned = false;                // the bin sort was enqueued (a fallback may be needed)
+  bool binned = false;                // the bin sort was enqueued (its merge-sort fallback after it)
   void* staged = nullptr;             // host inputs staged into this pool block
   size_t staged_cap = 0;
 };
@@ -275,8 +275,6 @@ struct Workspace {
   DevBuf f_vb, f_vo, f_sk, f_sk2, f_sort, f_tsum, f_flag, f_vsp;  // SsTable::create
   DevBuf x_ctl;                   // cb_hits_compress: slot / finish counters (zeroed once)
   DevBuf dense;                   // the dense set probe's entries and run table (densefs.hip)
-  DevBuf b_sync;                  // k_build_fused's arrival counters (zeroed once)
-  uint32_t b_par = 0;             // the counter set the next fused build on this stream uses
   std::vector<std::shared_ptr<WriteMark>> marks;  // write marks, reused once no filter holds them
   cb::CompressState xst;
   cb::CreateResult* hres = nullptr;  // pinned host mirror of f_flag (SsTable::create)

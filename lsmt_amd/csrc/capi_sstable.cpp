@@ -432,11 +432,11 @@ int index_table(cb_table* t, hipStream_t s) {
 // build, the sort the device picks, tile scan, format) and one copy of the
 // CreateResult into a pinned block, followed by an event; nothing waits. The
 // host-side results (file length, zone bounds, the well-formed flag) are read
-// when the table is first used (finalize_table). Two cases need the host
-// there: a batch the bin sort could not place (one bin, or a bin larger than
-// an LDS tile: the merge sort and the format run again, synchronously) and a
-// key holding '\n' or '\t' (the file is re-indexed the way SsTable::get
-// splits it). Until a table is finalised its inputs must stay valid (host
+// when the table is first used (finalize_table). One case needs the host
+// there: a key holding '\n' or '\t' (the file is re-indexed the way
+// SsTable::get splits it). A batch the bin sort cannot place (one bin, or a
+// bin larger than an LDS tile) is sorted again on the device, by the merge
+// sort enqueued after it that runs only then. Until a table is finalised its inputs must stay valid (host
 // inputs are staged into a block the table owns).
 
 // Pinned result blocks and their events, reused across tables.
@@ -650,10 +650,16 @@ int sstable_enqueue(const uint8_t* keys, const uint64_t* key_off, uint64_t kbyte
   p.binned = T && T <= cb::bin_sort_max_group() && n > 4096 && n <= (1ull << 24);
   const uint64_t tmp = p.binned ? cb::bin_sort_tmp_bytes(n, T) : cb::entry_sort_tmp_bytes(n);
   HIP_TRY(ws.f_sort.reserve(tmp, s));
-  if (p.binned)
+  if (p.binned) {
     HIP_TRY(cb::launch_bin_sort(p.dk, p.dko, n, T, (cb::SortKey*)ws.f_sk2.p, ws.f_sort.p, s, p.dvo,
                                 (ulonglong2*)ws.f_vsp.p, tsum, dr));
-  else
+    // its fallback, on the device and on this stream: the merge sort, whose
+    // launches return at once unless the bin sort set flags[3] (one bin, or a
+    // bin larger than an LDS tile: keys sharing a long prefix); it rewrites
+    // the records, value spans and tile sums whole
+    HIP_TRY(cb::launch_entry_sort(nullptr, (cb::SortKey*)ws.f_sk2.p, (cb::SortKey*)ws.f_sort.p, n, p.dk, p.dko, s,
+                                  p.dvo, (ulonglong2*)ws.f_vsp.p, tsum, &dr->flags[3]));
+  } else
     HIP_TRY(cb::launch_entry_sort(nullptr, (cb::SortKey*)ws.f_sk2.p, (cb::SortKey*)ws.f_sort.p, n, p.dk, p.dko, s,
                                   p.dvo, (ulonglong2*)ws.f_vsp.p, tsum, &dr->flags[0]));
   if ((rc = enqueue_format(t.get(), ws, p, dr, s))) return rc;
@@ -685,29 +691,8 @@ int finalize_locked(cb_table* t) {
     t->ferr_msg = "SsTable::create: the batch's key or value bytes exceed the bounds the table was sized from";
     return CB_OK;
   }
-  if (hr->flags[3]) {
-    // the bin sort could not place every record (one bin, or a bin larger
-    // than an LDS tile: keys sharing a long prefix): the merge sort, then the
-    // file again, on the null stream of this device (the create's work is done)
-    hipStream_t s = nullptr;
-    Workspace& ws = workspace(t->device, s);
-    std::lock_guard<std::mutex> lk(ws.mu);
-    HIP_TRY(ws.f_flag.reserve(sizeof(cb::CreateResult), s));
-    HIP_TRY(ws.f_tsum.reserve(cb::format_tiles(p.n) * 8, s));
-    HIP_TRY(ws.f_sk2.reserve(p.n * sizeof(cb::SortKey), s));
-    HIP_TRY(ws.f_vsp.reserve(p.n * sizeof(ulonglong2), s));
-    HIP_TRY(ws.f_sort.reserve(cb::entry_sort_tmp_bytes(p.n), s));
-    cb::CreateResult* dr = (cb::CreateResult*)ws.f_flag.p;
-    uint64_t* tsum = (uint64_t*)ws.f_tsum.p;
-    HIP_TRY(hipMemsetAsync(dr, 0, cb::kCreateHead, s));
-    HIP_TRY(cb::launch_sorted_check(p.dk, p.dko, p.dvo, p.n, dr, tsum, ~0ull, ~0ull, s));
-    HIP_TRY(cb::launch_entry_sort(nullptr, (cb::SortKey*)ws.f_sk2.p, (cb::SortKey*)ws.f_sort.p, p.n, p.dk, p.dko, s,
-                                  p.dvo, (ulonglong2*)ws.f_vsp.p, tsum, nullptr));
-    int rc = enqueue_format(t, ws, p, dr, s);
-    if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(hr, dr, sizeof(cb::CreateResult), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-  }
+  // (hr->flags[3]: the bin sort could not place the batch and the merge sort
+  // ran after it on the create's stream; the file is already written)
   t->len = hr->len;
   // zone map: ZoneMap::update over the sorted keys = first / last line
   t->zidx[0] = hr->idx_min;

@@ -277,12 +277,11 @@ __global__ __launch_bounds__(kNT) void k_format(const SortKey* __restrict__ orde
   __shared__ uint64_t s_base;
   __shared__ DirMap sdm;  // the directory's map, indexed per lane
   uint8_t* stage = reinterpret_cast<uint8_t*>(stage32);
-  // The bin sort could not place every record (a group outgrew its LDS tile,
-  // or one bin held the batch: its slice of `order` / `vsp` is unwritten), or
-  // the byte totals exceed the bounds the file buffer was sized from: nothing
-  // here may read those records or write at offsets derived from them; the
-  // table redoes the sort (or reports the error) when it is finalised.
-  if (r->flags[3] || r->flags[4]) return;
+  // The byte totals exceed the bounds the file buffer was sized from: nothing
+  // here may write at offsets derived from them; the table reports the error
+  // when it is finalised. (A batch the bin sort could not place, flags[3],
+  // was sorted again by the merge sort enqueued after it.)
+  if (r->flags[4]) return;
   if (!r->flags[0]) {  // the batch was sorted: the sort left nothing, format in input order
     order = nullptr;
     vsp = nullptr;

@@ -66,8 +66,8 @@ constexpr uint32_t kZoneInline = 256;  // zone bound key bytes carried inline
 struct CreateResult {
   uint32_t flags[8];          // [0] unsorted (an inversion was seen), [1] a key holds '\n' / '\t',
                               // [2] not strictly increasing, [3] the bin sort could not place every
-                              // record (one bin, or a group larger than its tile: redo with the merge
-                              // sort), [4] ko[n] / vo[n] above the caller's byte bounds; [5..7] 0
+                              // record (one bin, or a group larger than its tile: the merge sort enqueued
+                              // after it runs), [4] ko[n] / vo[n] above the caller's byte bounds; [5..7] 0
   uint64_t ktot, vtot;        // ko[n], vo[n]
   uint64_t dmask[kDirPos][4]; // byte values at each position of sampled keys' 8-byte prefixes (DirMap)
   uint64_t len;               // the file's length
@@ -113,9 +113,10 @@ hipError_t launch_entry_sort(const SortKey* in, SortKey* out, SortKey* tmp, uint
 // sorted records, vsp / tsum as launch_entry_sort's tail. Every launch
 // returns at once when r->flags[0] is 0 (the batch is sorted). r->flags[3]
 // := 1 when the bins cannot take the batch (a single bin, or a group larger
-// than an LDS tile): out is then incomplete (k_format skips; redo with
-// launch_entry_sort). tmp: bin_sort_tmp_bytes. Enqueued without any host
-// knowledge of the batch beyond n.
+// than an LDS tile): out is then incomplete, and the caller enqueues
+// launch_entry_sort after it with run_if = &r->flags[3], which redoes the
+// order, vsp and tsum whole. tmp: bin_sort_tmp_bytes. Enqueued without any
+// host knowledge of the batch beyond n.
 uint64_t bin_sort_tmp_bytes(uint64_t n, uint32_t T);
 uint32_t bin_sort_max_group();  // T at most (one LDS tile)
 hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, uint32_t T, SortKey* out, void* tmp,
@@ -130,7 +131,7 @@ hipError_t launch_bin_sort(const uint8_t* kb, const uint64_t* ko, uint64_t n, ui
 // increasing: the well-formed check).
 // order / vsp (nullable): the sort's records and value spans, used only when
 // r->flags[0] says the batch was unsorted (a sorted batch is formatted in
-// input order). Nothing is written when r->flags[3] or r->flags[4] is set.
+// input order). Nothing is written when r->flags[4] is set.
 // vsp: entry p's {value offset, value length} in sorted order
 // (launch_entry_sort's), read instead of vo[order[p].idx].
 // dir (nullable, with dmap_out): the table's directory, its DirMap derived

@@ -56,7 +56,6 @@ __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) u32x4* gptr_u4;
 typedef const __attribute__((address_space(1))) uint32_t* gptr_u32;
-typedef __attribute__((address_space(1))) uint32_t gu32;  // words other workgroups of a launch read
 
 // Non-temporal 16-B store, for data written once and read only by later
 // launches: no L2 allocation to write back at the kernel's end.
@@ -242,11 +241,6 @@ constexpr uint32_t kPartThreads = 256;
 // Fewer, larger tiles (~256 for C2) and larger blocks make the average run
 // ~32 entries = one 128-B line.
 constexpr uint32_t kBuildNT = 1024;
-// k_build_fused's register budget: <= 64 VGPRs (8 waves per SIMD), no spill;
-// its LDS request keeps it at one workgroup per CU (launch_build_fused)
-#ifndef CB_BUILD_FUSED_WAVES
-#define CB_BUILD_FUSED_WAVES 8
-#endif
 
 // A 16-byte key's two positions packed as partition entries ((bin << 20) |
 // offset in the bin, bins of 2^tb bits), 0xFFFFFFFF for both when !live.
@@ -283,10 +277,7 @@ __device__ __forceinline__ void pack_positions(const uint4& kv, bool live, const
 // LDS is free again when it returns except for the final store's reads of
 // `stage` (the caller's next LDS write must follow a barrier).
 // pol: the store policy bits (build_stores(): bit 0 write-through entries).
-// PUB (k_build_fused's partition blocks): the run row and the < PER left-over
-// entries also leave write-through (sc1), so every byte the tile blocks read
-// in the same launch was stored sc1 (the hand-off there).
-template <int KPT, typename E, bool PUB = false>
+template <int KPT, typename E>
 __device__ __forceinline__ void part_phases(const uint32_t (&q)[2 * KPT], uint32_t T, uint32_t* smem,
                                             uint32_t* __restrict__ srow, E* __restrict__ out, uint32_t pol) {
   constexpr uint32_t NT = kBuildNT, C = NT * KPT;
@@ -311,12 +302,7 @@ __device__ __forceinline__ void part_phases(const uint32_t (&q)[2 * KPT], uint32
   __syncthreads();
   CB_STAMP(3);
   const uint32_t total = hist[T];
-  for (uint32_t t = tid; t <= T; t += NT) {
-    if constexpr (PUB)
-      __hip_atomic_store((gu32*)(srow + t), hist[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-      srow[t] = hist[t];
-  }
+  for (uint32_t t = tid; t <= T; t += NT) srow[t] = hist[t];
 #pragma unroll
   for (int e = 0; e < 2 * KPT; ++e)
     if (q[e] != kNone) stage[hist[q[e] >> 20] + er[e]] = (E)(q[e] & 0xFFFFFu);
@@ -328,34 +314,35 @@ __device__ __forceinline__ void part_phases(const uint32_t (&q)[2 * KPT], uint32
   // kernel's end has no dirty L2 lines to write back, and the tile pass (on
   // other XCDs) still finds them there; C2 on four lanes 101 -> 105-107 G
   // keys/s (non-temporal stores instead made the tile pass's reads slower)
-  if ((pol & 1u) || PUB) {
+  if (pol & 1u) {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, 2 * C * sizeof(E), 0x00020000);
     for (uint32_t i = tid; i < n4; i += NT) store16_wt(r, i * 16, reinterpret_cast<const uint4*>(stage)[i]);
   } else {
     for (uint32_t i = tid; i < n4; i += NT)
       reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(stage)[i];
   }
-  if (tid < total - PER * n4) {  // the < PER left over
-    if constexpr (PUB) {
-      static_assert(sizeof(E) == 4, "sc1 stores of 32-bit entries");
-      __hip_atomic_store((gu32*)(out + PER * n4 + tid), stage[PER * n4 + tid], __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      out[PER * n4 + tid] = stage[PER * n4 + tid];
-    }
-  }
+  if (tid < total - PER * n4) out[PER * n4 + tid] = stage[PER * n4 + tid];  // the < PER left over
   CB_STAMP(5);
 }
 
-// One partition block: keys [b C, (b + 1) C) of ks -> its run row srow and its
-// tile-sorted entries out.
-template <int KEYK, int MODE, int KPT, typename E, bool PUB>
-__device__ __forceinline__ void part_block(const KeySrc& ks, uint64_t n, const ModP& mp, uint32_t tb, uint32_t T,
-                                           uint32_t b, uint32_t* __restrict__ srow, E* __restrict__ out,
-                                           uint32_t* smem, uint32_t pol) {
+// E: the entry type — uint32_t (offsets in tiles of up to 2^20 bits) or
+// uint16_t (bins of 2^16 bits, tb = 16 here: the sub-tiles of
+// k_build_tile_sub's tiles).
+template <int KEYK, int MODE, int KPT, typename E = uint32_t>
+__global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp, uint32_t tb,
+                                                         uint32_t T,
+                                                         uint32_t* __restrict__ seg_all,
+                                                         void* __restrict__ ent_all, uint32_t pol) {
   constexpr uint32_t NT = kBuildNT, C = NT * KPT;
+  static_assert(sizeof(E) == 4 || sizeof(E) == 2, "entry type");
+  const KeySrc ks = bb.ks[blockIdx.y];
+  const uint64_t n = bb.n[blockIdx.y];
+  uint32_t* seg = seg_all + (size_t)blockIdx.y * gridDim.x * (T + 1);
+  E* ent = reinterpret_cast<E*>(ent_all) + (size_t)blockIdx.y * gridDim.x * (2 * C);
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t tid = threadIdx.x;
-  const uint64_t kbase = (uint64_t)b * C;
+  const uint64_t kbase = (uint64_t)blockIdx.x * C;
+  CB_STAMP(0);
 
   // positions first: every key load of the thread is in flight together.
   // Each entry is kept packed as (tile << 20) | offset in the tile (tiles <
@@ -395,107 +382,60 @@ __device__ __forceinline__ void part_block(const KeySrc& ks, uint64_t n, const M
       }
     }
   }
-  part_phases<KPT, E, PUB>(q, T, smem, srow, out, pol);
+  part_phases<KPT, E>(q, T, smem, seg + (size_t)blockIdx.x * (T + 1), ent + (size_t)blockIdx.x * (2 * C), pol);
 }
 
-// E: the entry type — uint32_t (offsets in tiles of up to 2^20 bits) or
-// uint16_t (bins of 2^16 bits, tb = 16 here: the sub-tiles of
-// k_build_tile_sub's tiles).
-template <int KEYK, int MODE, int KPT, typename E = uint32_t>
-__global__ __launch_bounds__(kBuildNT) void k_build_part(BuildBatch bb, ModP mp, uint32_t tb,
-                                                         uint32_t T,
-                                                         uint32_t* __restrict__ seg_all,
-                                                         void* __restrict__ ent_all, uint32_t pol) {
-  constexpr uint32_t C = kBuildNT * KPT;
-  static_assert(sizeof(E) == 4 || sizeof(E) == 2, "entry type");
-  uint32_t* seg = seg_all + (size_t)blockIdx.y * gridDim.x * (T + 1);
-  E* ent = reinterpret_cast<E*>(ent_all) + (size_t)blockIdx.y * gridDim.x * (2 * C);
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  CB_STAMP(0);
-  part_block<KEYK, MODE, KPT, E, false>(bb.ks[blockIdx.y], bb.n[blockIdx.y], mp, tb, T, blockIdx.x,
-                                        seg + (size_t)blockIdx.x * (T + 1), ent + (size_t)blockIdx.x * (2 * C), smem,
-                                        pol);
-}
-
-// A word of the partition's output: a plain load, or (FUSED: written by
-// other workgroups of the same launch) an sc1 load, which bypasses this CU's
-// L1 (k_build_fused's hand-off).
-template <bool FUSED>
-__device__ __forceinline__ uint32_t part_word(const uint32_t* p) {
-  if constexpr (FUSED)
-    return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    return *(gptr_u32)p;
-}
-
-// k_build_fused's tile blocks: wave 0 polls the partition's arrival counters
-// (sync: kBuildSyncShards shards of set par, one 128-B line each; partition
-// block b adds 1 to shard b % 8) until every partition block has published.
-// Bounded: a give-up sets sync[kBuildSyncErr] (the tile is then wrong).
-constexpr uint32_t kBuildSyncShards = 8, kBuildSyncStride = 32;
-constexpr uint32_t kBuildSyncErr = 2 * kBuildSyncShards * kBuildSyncStride;
-constexpr uint32_t kBuildSpinMax = 1u << 22;  // ~seconds of polling
-
-__device__ __forceinline__ void wait_partition(uint32_t* sync, uint32_t par, uint32_t nblk, uint32_t lane) {
-  gu32* const gs = (gu32*)sync;
-  const uint32_t sh = lane & (kBuildSyncShards - 1);
-  const uint32_t want = lane < kBuildSyncShards ? nblk / kBuildSyncShards + (sh < nblk % kBuildSyncShards) : 0u;
-  gu32* const word = gs + (par * kBuildSyncShards + sh) * kBuildSyncStride;
-  for (uint32_t spins = 0;; ++spins) {
-    const uint32_t got =
-        lane < kBuildSyncShards ? __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    if (__all(got >= want)) return;
-    if (spins == kBuildSpinMax) {
-      if (lane == 0) __hip_atomic_store(gs + kBuildSyncErr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
-
-// Wave w owns partition blocks b = w + NW*u. Per group of G: lanes 0..G-1
-// load the G blocks' run bounds (seg[b][t], seg[b][t+1]), shuffles hand each
-// run's start and length to the whole wave, and the wave issues the G run
+// Wave w owns partition blocks b = w + NW*u. Per group of 16: lanes 0..15
+// load the 16 blocks' run bounds (seg[b][t], seg[b][t+1]), shuffles hand each
+// run's start and length to the whole wave, and the wave issues the 16 run
 // loads back to back (lane i = entry i): two dependent memory round trips per
 // group and no LDS run table or barrier before the ORs.
 // pol: the store policy bits (build_stores(): bit 1 non-temporal write-back).
-// FUSED (k_build_fused): the tile is cleared while the partition still runs,
-// then wave 0 waits for it, and every load of its output is an sc1 load.
-template <int G, int R, uint32_t NT, bool FUSED>
-__device__ __forceinline__ void tile_block(uint32_t* __restrict__ words, bool fresh, uint32_t tb, uint32_t T, uint32_t t,
-                                           const uint32_t* __restrict__ seg, uint32_t nblk,
-                                           const uint32_t* __restrict__ ent, uint32_t estride, uint32_t pol,
-                                           uint32_t* smem, uint32_t* sync, uint32_t par) {
+template <int G, int R, uint32_t NT = kBuildNT>
+__global__ __launch_bounds__(NT) void k_build_tile(BuildBatch bb, uint32_t tb, uint32_t T,
+                                                         const uint32_t* __restrict__ seg_all,
+                                                         uint32_t nblk,
+                                                         const uint32_t* __restrict__ ent_all,
+                                                         uint32_t estride, uint32_t pol) {
   constexpr uint32_t NW = NT / 64;
   static_assert(G <= 64, "one lane per run bound");
+  uint32_t* __restrict__ words = bb.words[blockIdx.y];
+  const bool fresh = (bb.fresh >> blockIdx.y) & 1ull;
+  const uint32_t* __restrict__ seg = seg_all + (size_t)blockIdx.y * nblk * (T + 1);
+  const uint32_t* __restrict__ ent = ent_all + (size_t)blockIdx.y * nblk * estride;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t tw = 1u << (tb - 5);
   uint32_t* tile = smem;
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const uint32_t t = xcd_tile(blockIdx.x, T);
+  CB_STAMP(0);
 
+  // first group's run bounds in flight while the tile is cleared / loaded
   uint32_t s0 = 0, s1 = 0;
-  auto bounds = [&](uint32_t g0) {
-    s0 = s1 = 0;
-    const uint32_t b = w + NW * (g0 + lane);
+  {
+    const uint32_t b = w + NW * lane;
     if (lane < (uint32_t)G && b < nblk) {
       const uint32_t* row = seg + (size_t)b * (T + 1) + t;
-      s0 = part_word<FUSED>(row);
-      s1 = part_word<FUSED>(row + 1);
+      s0 = row[0];
+      s1 = row[1];
     }
-  };
-  // first group's run bounds in flight while the tile is cleared / loaded
-  if constexpr (!FUSED) bounds(0);
+  }
   uint4* gt = reinterpret_cast<uint4*>(words + (size_t)t * tw);
   uint4* lt = reinterpret_cast<uint4*>(tile);
   for (uint32_t i = tid; i < tw / 4; i += NT) lt[i] = fresh ? make_uint4(0, 0, 0, 0) : gt[i];
-  if constexpr (FUSED) {
-    if (w == 0) wait_partition(sync, par, nblk, lane);
-  }
   __syncthreads();
   CB_STAMP(1);
-  if constexpr (FUSED) bounds(0);
 
   for (uint32_t g0 = 0; w + NW * g0 < nblk; g0 += G) {
-    if (g0) bounds(g0);
+    if (g0) {
+      s0 = s1 = 0;
+      const uint32_t b = w + NW * (g0 + lane);
+      if (lane < (uint32_t)G && b < nblk) {
+        const uint32_t* row = seg + (size_t)b * (T + 1) + t;
+        s0 = row[0];
+        s1 = row[1];
+      }
+    }
     // R rounds of run loads (lane i = entry i + 64 r): every load of the G
     // runs goes out before any OR. R = 2 for long runs (C4's 64 tiles per
     // filter give ~128 entries per run) with G = 8, so a lane holds G * R =
@@ -509,7 +449,7 @@ __device__ __forceinline__ void tile_block(uint32_t* __restrict__ words, bool fr
 #pragma unroll
       for (int q = 0; q < R; ++q) {
         o[q][u] = 0xFFFFFFFFu;
-        if (64 * q + lane < len) o[q][u] = part_word<FUSED>(ent + (size_t)b * estride + st + 64 * q + lane);
+        if (64 * q + lane < len) o[q][u] = ent[(size_t)b * estride + st + 64 * q + lane];
       }
     }
 #pragma unroll
@@ -524,7 +464,7 @@ __device__ __forceinline__ void tile_block(uint32_t* __restrict__ words, bool fr
         const uint32_t st = __shfl(s0, u, 64), len = __shfl(s1, u, 64) - st;
         const uint32_t* run = ent + (size_t)(w + NW * (g0 + u)) * estride + st;
         for (uint32_t i = 64 * R + lane; i < len; i += 64) {
-          const uint32_t v = part_word<FUSED>(run + i);
+          const uint32_t v = run[i];
           atomicOr(&tile[v >> 5], 1u << (v & 31));
         }
       }
@@ -542,64 +482,6 @@ __device__ __forceinline__ void tile_block(uint32_t* __restrict__ words, bool fr
   else
     for (uint32_t i = tid; i < tw / 4; i += NT) gt[i] = lt[i];
   CB_STAMP(4);
-}
-
-template <int G, int R, uint32_t NT = kBuildNT>
-__global__ __launch_bounds__(NT) void k_build_tile(BuildBatch bb, uint32_t tb, uint32_t T,
-                                                   const uint32_t* __restrict__ seg_all, uint32_t nblk,
-                                                   const uint32_t* __restrict__ ent_all, uint32_t estride,
-                                                   uint32_t pol) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  CB_STAMP(0);
-  tile_block<G, R, NT, false>(bb.words[blockIdx.y], (bb.fresh >> blockIdx.y) & 1ull, tb, T, xcd_tile(blockIdx.x, T),
-                              seg_all + (size_t)blockIdx.y * nblk * (T + 1), nblk,
-                              ent_all + (size_t)blockIdx.y * nblk * estride, estride, pol, smem, nullptr, 0);
-}
-
-// A single tiled build (C2: 1M keys into one 2^27-bit filter) as ONE launch
-// instead of k_build_part + k_build_tile: workgroups [0, nblk) partition as
-// k_build_part does and publish; workgroups [nblk, nblk + T) clear their LDS
-// tile as soon as they are resident (on CUs whose partition workgroup has
-// finished), wait for every partition block (wait_partition), then OR their
-// runs in and write the tile as k_build_tile does. One launch boundary fewer
-// per build: C2 cold (after a 1 GiB write) 21.1-21.2 -> 20.0 us; warm one
-// lane unchanged at 15.4-15.7 us (tools/gpu/r05_fused4.sh, same box,
-// alternating).
-// Forward progress: a tile workgroup waits only for partition workgroups,
-// which precede it in the grid and never wait themselves; the wait is
-// bounded all the same.
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the
-// sc1 table): every byte the tile workgroups read (entries, run rows) is
-// stored sc1 (part_phases<PUB>), every storing wave drains (s_waitcnt
-// vmcnt(0)), a workgroup barrier, then one lane's agent-scope atomic add;
-// the consumer polls with sc1 loads and reads everything with sc1 loads.
-// Counters: two sets of shards; this launch counts on set par, and its
-// workgroup 0 clears set par ^ 1 for the next launch on the stream (the host
-// flips par per launch; both sets are zeroed when allocated).
-template <int KEYK, int MODE, int KPT, int G, int R>
-__global__ __launch_bounds__(kBuildNT, CB_BUILD_FUSED_WAVES) void k_build_fused(
-    KeySrc ks, uint64_t n, ModP mp, uint32_t tb, uint32_t T, uint32_t nblk, uint32_t* __restrict__ words,
-    uint32_t fresh, uint32_t* __restrict__ seg, uint32_t* __restrict__ ent, uint32_t* __restrict__ sync, uint32_t par) {
-  constexpr uint32_t C = kBuildNT * KPT;
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  CB_STAMP(0);
-  const uint32_t b = blockIdx.x, tid = threadIdx.x;
-  if (b < nblk) {
-    part_block<KEYK, MODE, KPT, uint32_t, true>(ks, n, mp, tb, T, b, seg + (size_t)b * (T + 1), ent + (size_t)b * (2 * C),
-                                                smem, 1u);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    gu32* const gs = (gu32*)sync;
-    if (tid == 0)
-      __hip_atomic_fetch_add(gs + (par * kBuildSyncShards + (b & (kBuildSyncShards - 1))) * kBuildSyncStride, 1u,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (b == 0 && tid < kBuildSyncShards)
-      __hip_atomic_store(gs + ((par ^ 1u) * kBuildSyncShards + tid) * kBuildSyncStride, 0u, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  tile_block<G, R, kBuildNT, true>(words, fresh != 0, tb, T, xcd_tile(b - nblk, T), seg, nblk, ent, 2 * C, 2u, smem,
-                                   sync, par);
 }
 
 // The tile pass over 16-bit entries (batched builds of long runs, C4): the
@@ -1302,56 +1184,6 @@ hipError_t launch_build_tiled(int keyk, int mode, uint32_t* words, bool fresh, c
   bb.words[0] = words;
   bb.fresh = fresh ? 1u : 0u;
   return launch_build_batch(keyk, mode, bb, 1, mp, p, seg, ent, s);
-}
-
-bool build_fused_ok(const TilePlan& p) {
-  // one filter, 32-bit entries, tiles of at most 64 KiB of LDS
-  return plan_ok(p) && !p.sub && (p.kpt == 1 || p.kpt == 2 || p.kpt == 4) && p.tb <= 19 &&
-         p.nblk <= kMaxBuildBlocks;
-}
-
-template <int KK, int MM, int G, int R>
-static void build_fused(const TilePlan& p, const KeySrc& ks, uint64_t n, const ModP& mp, uint32_t* words, bool fresh,
-                        uint32_t* seg, uint32_t* ent, uint32_t* sync, uint32_t par, size_t lds, hipStream_t s) {
-#define CB_FUSED_KPT(KPTV)                                                                                     \
-  allow_lds(k_build_fused<KK, MM, KPTV, G, R>, lds);                                                           \
-  hipLaunchKernelGGL((k_build_fused<KK, MM, KPTV, G, R>), dim3(p.nblk + p.T), dim3(kBuildNT), lds, s, ks, n, mp, \
-                     p.tb, p.T, p.nblk, words, fresh ? 1u : 0u, seg, ent, sync, par)
-  if (p.kpt == 4) {
-    CB_FUSED_KPT(4);
-  } else if (p.kpt == 2) {
-    CB_FUSED_KPT(2);
-  } else {
-    CB_FUSED_KPT(1);
-  }
-#undef CB_FUSED_KPT
-}
-
-hipError_t launch_build_fused(int keyk, int mode, uint32_t* words, bool fresh, const KeySrc& ks, uint64_t n,
-                              const ModP& mp, const TilePlan& p, uint32_t* seg, uint32_t* ent, uint32_t* sync,
-                              uint32_t par, hipStream_t s) {
-  if (!n) return hipSuccess;
-  if (!build_fused_ok(p) || par > 1) return hipErrorInvalidValue;
-  static_assert(kBuildSyncBytes >= (kBuildSyncErr + 1) * 4, "sync words");
-  const size_t lds1 = (size_t)(((p.T + 4) & ~3u) + 4) * 4 + 2 * p.C * 4;  // part_phases: hist, discard, stage
-  const size_t lds2 = (size_t)(1u << (p.tb - 5)) * 4;                       // the tile
-  // At least 96 KiB: one workgroup per CU. With the natural 64 KiB two fit,
-  // the dispatcher packs two partition workgroups into one CU while its
-  // neighbour idles, and the build took 20.3-21.5 us instead of 15.4-15.8
-  // (tools/gpu/r05_fused2.sh, r05_fused3.sh; half-size partition blocks
-  // filling both slots of every CU measured the same 20.3-21.2).
-#ifndef CB_BUILD_FUSED_LDS
-#define CB_BUILD_FUSED_LDS 98304
-#endif
-  const size_t lds = std::max<size_t>(std::max(lds1, lds2), CB_BUILD_FUSED_LDS);
-  ProfScope ps("k_build_fused", s);
-  // the run-load shape k_build_tile takes for these runs (launch_build_batch)
-  if (2ull * p.C > 48ull * p.T) {
-    CB_DISPATCH(keyk, mode, (build_fused<KK, MM, 8, 2>(p, ks, n, mp, words, fresh, seg, ent, sync, par, lds, s)));
-  } else {
-    CB_DISPATCH(keyk, mode, (build_fused<KK, MM, 16, 1>(p, ks, n, mp, words, fresh, seg, ent, sync, par, lds, s)));
-  }
-  return hipGetLastError();
 }
 
 hipError_t launch_probe_partition(int keyk, int mode, const KeySrc& ks, uint64_t n,

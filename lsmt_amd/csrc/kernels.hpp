@@ -80,16 +80,6 @@ hipError_t launch_build_batch(int keyk, int mode, const BuildBatch& bb, uint32_t
 hipError_t launch_build_tiled(int keyk, int mode, uint32_t* words, bool fresh, const KeySrc& ks,
                               uint64_t n, const ModP& mp, const TilePlan& p, uint32_t* seg,
                               uint32_t* ent, hipStream_t s);
-// The same single build as one launch (k_build_fused: partition and tile
-// workgroups in one grid, the tiles waiting on the partition's arrival
-// counters). sync: kBuildSyncBytes of device memory, zeroed once when
-// allocated and then used only by this stream's fused builds; par: flipped by
-// the caller after every launch (build_fused_ok plans only).
-constexpr size_t kBuildSyncBytes = 17 * 128;
-bool build_fused_ok(const TilePlan& p);
-hipError_t launch_build_fused(int keyk, int mode, uint32_t* words, bool fresh, const KeySrc& ks, uint64_t n,
-                              const ModP& mp, const TilePlan& p, uint32_t* seg, uint32_t* ent, uint32_t* sync,
-                              uint32_t par, hipStream_t s);
 // Probe = partition the key batch once per filter size (K1), then per launch
 // of <= 64 filters: tile pass (K2) into masks (ceil(nf/32) * n uint32) and the
 // ballot transpose into hits (K3).

@@ -16,7 +16,7 @@ if rp:
     print(f"read path {rp['value'] / 1e9:.2f} G gets/s")
 f = d.get("flush")
 if f:
-    for k in ("sorted_input", "unsorted_input"):
+    for k in ("sorted_input", "unsorted_input", "unsorted_shared_prefix_input"):
         if k in f:
             print(f"flush {k}: {f[k]['ms_per_flush']} ms  {f[k]['kernels_us']}")
 for k in ("c4", "c5"):

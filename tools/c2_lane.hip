@@ -80,7 +80,8 @@ int main(int argc, char** argv) {
     }
     if (init(0)) return 1;
     // C2_FUSED=-1 / 0: the two-launch or the one-launch single build
-    // (cb_set_build_fused, libraries from round 5 on)
+    // (cb_set_build_fused: round 5's one-launch experiment, since removed;
+    // DESIGN.md §5 "Why the build stays two launches")
     if (const char* fz = getenv("C2_FUSED")) {
       auto set_fused = (int (*)(int))dlsym(L, "cb_set_build_fused");
       if (!set_fused || set_fused(atoi(fz))) {
