@@ -10,9 +10,10 @@
 // reads every line ~7 times, each a random 128-B fill: 14.3M fills, 1.8 GB
 // of fabric traffic for 0.26 GB of distinct sectors. Here:
 //
-//   k_dense_part  (1024 threads x 7 keys per block): hash, bin every key by
-//                 the 64 KiB region of the set holding set[a] (LDS rank
-//                 atomics, one wave scan), write the block's entries
+//   k_dense_part  (1024 threads x 3 batches of 4 keys per block): hash, bin
+//                 every key by the 64 KiB region of the set holding set[a]
+//                 (LDS count atomics, a block scan, LDS cursor atomics),
+//                 write the block's entries
 //                 region-sorted {b, a's offset in the region << 16 | key index
 //                 in the block} as one contiguous run list, its run starts
 //                 as one row of a block-major table (u16), and zero the
@@ -45,18 +46,41 @@ namespace cb {
 namespace {
 
 constexpr uint32_t kDenseNT = 1024;
-constexpr uint32_t kDenseKPT = 7;
-constexpr uint32_t kDenseC = kDenseNT * kDenseKPT;  // keys per partition block (a multiple of 64)
+// A partition block ranks NB batches of KPT keys per thread (C = 12288 keys):
+// batch g + 1's key loads are in flight while batch g's ranks are taken, and
+// fewer, larger blocks shorten the probe's per-region run table. One batch
+// of 7 keys per thread (C = 7168, 1396 blocks at C5) measured 209-211 us per
+// C5 step on three lanes; two of 5 (977 blocks) 194-196; three of 4 (814
+// blocks) 190-191 (tools/gpu/r05_c5nb.sh, same box, alternating).
+#if defined(CB_EXPERIMENTS) && defined(CB_DENSE_KPT)
+constexpr uint32_t kDenseKPT = CB_DENSE_KPT;  // (experiment builds: keys per partition thread and batch)
+#else
+constexpr uint32_t kDenseKPT = 4;
+#endif
+#if defined(CB_EXPERIMENTS) && defined(CB_DENSE_NB)
+constexpr uint32_t kDenseNB = CB_DENSE_NB;  // (experiment builds: key batches per partition block)
+#else
+constexpr uint32_t kDenseNB = 3;
+#endif
+constexpr uint32_t kDenseC = kDenseNT * kDenseKPT * kDenseNB;  // keys per partition block (a multiple of 64)
 static_assert(kDenseC % 64 == 0 && kDenseC < 65536, "block keys: whole hit words, u16 run starts");
 constexpr uint32_t kRegionBytes = 65536;  // one region of the set, staged in LDS
 constexpr uint32_t kDenseMaxRegions = 4096;  // the partition histogram (16 KiB of LDS)
 constexpr uint32_t kDenseMaxBlocks = 2048;   // partition blocks per launch pair (the probe's run table)
 constexpr uint32_t kProbeU = 4;              // entries per lane per round of the probe
-// The partition pass at its natural 84 VGPRs runs five waves per SIMD (one
+// The partition pass at its natural 84-89 VGPRs runs five waves per SIMD (one
 // 16-wave block per CU, though LDS would take two); the experiment build can
-// force eight (two blocks per CU, 80 B of spill per lane) for the A/B.
+// force eight (two blocks per CU: 80-116 B of spill per lane at 7 keys per
+// thread) and fewer keys per thread (CB_DENSE_KPT) for the A/B. Two blocks
+// per CU at 5 keys per thread (12 B of spill): this pass 72.5 -> 55.5 us, but
+// 1954 partition blocks instead of 1396 cost the probe 9 us, and the C5 step
+// on three lanes went 209-211 -> 221-225 us (one lane 249 -> 242); at 4 keys
+// per thread (no spill) the batch needs two chunks and the set is streamed
+// twice: 265-268 us (tools/gpu/r05_c5part.sh).
 #if defined(CB_EXPERIMENTS) && defined(CB_DENSE_PART_LB8)
 #define CB_DENSE_PART_WAVES 8
+#elif defined(CB_EXPERIMENTS) && defined(CB_DENSE_PART_W)
+#define CB_DENSE_PART_WAVES CB_DENSE_PART_W
 #else
 #define CB_DENSE_PART_WAVES 1
 #endif
@@ -86,40 +110,49 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
   const uint64_t kb = k0 + (uint64_t)b * C;  // the block's first key
   const uint32_t pmask = (1u << rshift) - 1u;
   for (uint32_t i = tid; i < Rp + 4; i += NT) hist[i] = 0;
-  // positions first: every key load of the thread in flight together
-  uint32_t pa[KPT], pb[KPT];
-  bool live[KPT];
-  if constexpr (KEYK == KEY_FIXED16 && MODE == MOD_POW2_32) {
-    const uint4* keys = reinterpret_cast<const uint4*>(ks.bytes);
-    uint4 kv[KPT];
+  // positions first: every key load of a batch in flight together; with
+  // NB > 1 batches, batch g + 1's loads go out while batch g's ranks are taken
+  constexpr uint32_t NB = kDenseNB, CB = NT * KPT;  // keys per batch
+  // no rank is kept per key: the count pass's atomics only count, and the
+  // scatter takes each entry's slot from a second atomic on its bin's cursor
+  // (two registers per key instead of three; an entry's place inside its run
+  // is immaterial to the probe)
+  uint32_t pa[NB][KPT], pb[NB][KPT];
+  bool live[NB][KPT];
 #pragma unroll
-    for (int j = 0; j < (int)KPT; ++j) {
-      const uint64_t k = kb + (uint64_t)j * NT + tid;
-      live[j] = k < n;
-      kv[j] = keys[live[j] ? k : n - 1];
-    }
+  for (uint32_t g = 0; g < NB; ++g) {
+    const uint64_t kg = kb + (uint64_t)g * CB;
+    if constexpr (KEYK == KEY_FIXED16 && MODE == MOD_POW2_32) {
+      uint4 kv[KPT];
+      const uint4* keys = reinterpret_cast<const uint4*>(ks.bytes);
 #pragma unroll
-    for (int j = 0; j < (int)KPT; ++j) {
-      uint32_t h1, h2;
-      hash16_u32(kv[j], h1, h2);
-      pa[j] = h1 & (uint32_t)mp.mask;
-      pb[j] = h2 & (uint32_t)mp.mask;
-    }
-  } else {
+      for (int j = 0; j < (int)KPT; ++j) {
+        const uint64_t k = kg + (uint64_t)j * NT + tid;
+        live[g][j] = k < n;
+        kv[j] = keys[live[g][j] ? k : n - 1];
+      }
 #pragma unroll
-    for (int j = 0; j < (int)KPT; ++j) {
-      const uint64_t k = kb + (uint64_t)j * NT + tid;
-      live[j] = k < n;
-      uint64_t a = 0, b = 0;
-      if (live[j]) key_positions<KEYK, MODE>(ks, k, mp, a, b);
-      pa[j] = (uint32_t)a;  // m <= 2^32: positions fit (dense_ok)
-      pb[j] = (uint32_t)b;
+      for (int j = 0; j < (int)KPT; ++j) {
+        uint32_t h1, h2;
+        hash16_u32(kv[j], h1, h2);
+        pa[g][j] = h1 & (uint32_t)mp.mask;
+        pb[g][j] = h2 & (uint32_t)mp.mask;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < (int)KPT; ++j) {
+        const uint64_t k = kg + (uint64_t)j * NT + tid;
+        live[g][j] = k < n;
+        uint64_t a = 0, b = 0;
+        if (live[g][j]) key_positions<KEYK, MODE>(ks, k, mp, a, b);
+        pa[g][j] = (uint32_t)a;  // m <= 2^32: positions fit (dense_ok)
+        pb[g][j] = (uint32_t)b;
+      }
     }
+    if (g == 0) __syncthreads();  // hist zeroed
+#pragma unroll
+    for (int j = 0; j < (int)KPT; ++j) atomicAdd(&hist[live[g][j] ? pa[g][j] >> rshift : Rp], 1u);
   }
-  __syncthreads();
-  uint32_t er[KPT];
-#pragma unroll
-  for (int j = 0; j < (int)KPT; ++j) er[j] = atomicAdd(&hist[live[j] ? pa[j] >> rshift : Rp], 1u);
   __syncthreads();
   {
     // exclusive scan of the R + 1 counts by every wave (a wave-0 scan of
@@ -149,10 +182,15 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
     uint16_t* row = seg + (uint64_t)b * segstride;
     for (uint32_t t = tid; t <= R; t += NT) row[t] = (uint16_t)hist[t];
   }
+  __syncthreads();  // the run row is out: hist becomes the bins' cursors
 #pragma unroll
-  for (int j = 0; j < (int)KPT; ++j)
-    if (live[j])
-      stage[hist[pa[j] >> rshift] + er[j]] = make_uint2(pb[j], ((pa[j] & pmask) << 16) | (j * NT + tid));
+  for (uint32_t g = 0; g < NB; ++g)
+#pragma unroll
+    for (int j = 0; j < (int)KPT; ++j)
+      if (live[g][j]) {
+        const uint32_t at = atomicAdd(&hist[pa[g][j] >> rshift], 1u);
+        stage[at] = make_uint2(pb[g][j], ((pa[g][j] & pmask) << 16) | (g * CB + j * NT + tid));
+      }
   // the block's hit words (keys kb .. kb + C, whole words) start at zero:
   // the probe only ORs the set bits in
   {

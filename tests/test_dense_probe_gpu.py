@@ -21,6 +21,7 @@ from oracle import oracle
 pytestmark = pytest.mark.gpu
 
 DENSE_PATH = 6
+C = 12288  # keys per partition block (densefs.hip kDenseC)
 
 
 @pytest.fixture
@@ -44,7 +45,7 @@ def build(gpu, m, nf, kpf, seed):
 
 
 @pytest.mark.parametrize("width,nf", [(32, 1), (32, 5), (32, 32), (64, 37), (64, 64)])
-@pytest.mark.parametrize("n", [1, 63, 64, 7167, 7168, 7169, 50_001])
+@pytest.mark.parametrize("n", [1, 63, 64, 4095, 4097, C - 1, C, C + 1, 50_001])
 def test_dense_matches_oracle(dense, width, nf, n):
     m = 1 << 20
     filters, refs = build(dense, m, nf, 6000, 700)
@@ -107,7 +108,7 @@ def test_dense_device_buffers_and_padding_words(dense):
     m = 1 << 21
     filters, refs = build(dense, m, 11, 7000, 740)
     s = dense.FilterSet.from_filters(filters, width=32)
-    n = 3 * 7168 + 100
+    n = 3 * C + 100
     look = workload.probe_lookups(n, 11, 7000, seed_base=740, absent_seed=993)
     nw = (n + 63) // 64
     out = torch.full((13, nw), -1, dtype=torch.int64, device="cuda")
@@ -119,13 +120,13 @@ def test_dense_device_buffers_and_padding_words(dense):
 
 
 def test_dense_chunks(dense):
-    # more keys than one launch pair takes (2048 partition blocks of 7168
-    # keys = 14,680,064): two chunks, the second's key indices offset
+    # more keys than one launch pair takes (2048 partition blocks of C keys
+    # = 25,165,824): two chunks, the second's key indices offset
     import torch
     m = 1 << 20
     filters, refs = build(dense, m, 3, 4000, 750)
     s = dense.FilterSet.from_filters(filters, width=32)
-    n = 2048 * 7168 + 70_001
+    n = 2048 * C + 70_001
     look = workload.probe_lookups(n, 3, 4000, seed_base=750, absent_seed=992)
     out = torch.zeros((3, (n + 63) // 64), dtype=torch.int64, device="cuda")
     s.probe(dense.DeviceKeys(torch.from_numpy(look).cuda()), out=out)

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 5: dense partition blocks of two key batches (CB_DENSE_NB=2, build/xb2k*)
+# and the cursor-scatter form (CB_DENSE_CURSOR, build/xc*) against one batch of
+# 7 keys per thread: fewer, larger partition blocks,
+# experiment builds build/xk*w*, alternating, two reps.
+set -o pipefail
+mkdir -p gpurun_out/r05
+O=gpurun_out/r05
+show() {
+python -c "
+import json;d=json.load(open('$1'))['c5'];r=d['roofline']
+print('$2', 'region', d['region_us_per_step'], 'one-lane', d['one_lane_us_per_step'], 'frac', r['frac'], d.get('kernels_us'), 'golden', d.get('golden_slice_bit_exact'), 'oracle', d.get('oracle_row_bit_exact'))"
+}
+for rep in 1 2; do
+  for v in ${VARIANTS:-b2k5 c2k5 c2k6 c3k4}; do
+    EXPBENCH_LIB=build/x$v/libcassbloom.so timeout -k 10 300 python tools/expbench.py --leg c5 --no-cpu --steps 20 --warmup 3 > $O/c5nb_${v}_$rep.json 2> $O/c5nb_${v}_$rep.err || { tail -20 $O/c5nb_${v}_$rep.err; exit 1; }
+    show $O/c5nb_${v}_$rep.json "$v"
+  done
+done
