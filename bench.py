@@ -278,6 +278,8 @@ def main():
     # never share a buffer, so no cross-stream event is needed per step.
     P = args.probe_streams
     lane_streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(P - 1)]
+    global _LANES
+    _LANES = lane_streams
     lane_sh = [st.cuda_stream for st in lane_streams]
     # The exchange runs through the C ABI (cb_hits_allgather over the
     # library's own RCCL communicator, lsmt_amd/csrc/comm.cpp): the same call
@@ -955,6 +957,14 @@ def main():
     # golden + oracle checks): C4's 64 builds split over the ranks (strong
     # scaling); C5's per-GPU slice (rank r: filters 32(r mod 8) .. +31 of 256)
     c4 = c5 = None
+
+    def run_c5():
+        c5 = c5_leg(args, torch, dev, local, world, rank, max(args.steps, LK // 4), args.warmup,
+                    args.probe_streams, True, red_dev, dist, use_dist)
+        log(f"[c5] {c5['value'] / 1e12:.3f} T probes/s, {c5['region_us_per_step']} us/step, "
+            f"frac {c5['roofline']['frac']}, golden {c5.get('golden_slice_bit_exact')}")
+        return c5
+
     if args.workload == "c3" and not args.no_c4:
         c4 = c4_leg(args, torch, dist, world, rank, local, dev, use_dist, red_dev, LK, args.warmup,
                     args.probe_streams, check=True, oracle_sample=0 if args.no_cpu else 4)
@@ -964,10 +974,7 @@ def main():
         log(f"[c4] {c4['value'] / 1e9:.1f} G keys/s, {c4['region_us_per_step']} us/step, "
             f"frac {c4['roofline']['frac']}, golden {c4.get('golden_all_filters_bit_exact')}")
     if args.workload == "c3" and not args.no_c5:
-        c5 = c5_leg(args, torch, dev, local, world, rank, max(args.steps, LK // 4), args.warmup,
-                    args.probe_streams, True, red_dev, dist, use_dist)
-        log(f"[c5] {c5['value'] / 1e12:.3f} T probes/s, {c5['region_us_per_step']} us/step, "
-            f"frac {c5['roofline']['frac']}, golden {c5.get('golden_slice_bit_exact')}")
+        c5 = run_c5()
 
     if args.check:
         # Every rank checks its own rows and, in the exchanged map, the rows
@@ -1147,7 +1154,7 @@ def c4_leg(args, torch, dist, world, rank, local, dev, use_dist, red_dev, steps,
     nf_total, kpf, m = 64, 1 << 18, 1 << 25
     lo, hi = shard_range(nf_total, world, rank)
     P = lanes_n
-    lanes = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(P - 1)]
+    lanes = leg_lanes(torch, dev, P)
     keys = [torch.from_numpy(workload.c4_filter_keys(f, kpf)).to(dev) for f in range(lo, hi)]
     fsets = [[lsmt_amd.BloomFilter(m, device=local) for _ in range(lo, hi)] for _ in range(P)]
     batches = [lsmt_amd.DeviceKeys(k) for k in keys]
@@ -1241,6 +1248,23 @@ def c4_roofline(leg, world):
     return r
 
 
+_LANES = None  # the default line's lane streams, made once at its start
+
+
+def leg_lanes(torch, dev, P):
+    """A leg's P pipeline lanes: the line's own lane streams when it has made
+    them (every leg of one line on the same streams), else the current stream
+    and P - 1 from torch's pool. HIP multiplexes streams onto a few hardware
+    queues (GPU_MAX_HW_QUEUES, 4 here) in creation order, and lanes sharing a
+    queue run one after the other: the C5 leg on the current stream plus two
+    more pool streams drawn after the C4 leg's took 206-208 us per step on
+    three lanes, against 188-189 on the line's lanes, on fresh pool streams
+    or on hipStreamCreate streams (tools/gpu/r05_c5ctx3.sh)."""
+    if _LANES and len(_LANES) >= P:
+        return list(_LANES[:P])
+    return [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(P - 1)]
+
+
 def c5_leg(args, torch, dev, local, world, rank, steps, warmup, lanes_n, check, red_dev, dist, use_dist):
     """BASELINE C5, one rank's slice of the read fan-out (src/lib.rs:129-134
     over 256 tables, 32 per GPU at 8 GPUs): 10M lookups (SURVEY.md §8d C5
@@ -1267,7 +1291,7 @@ def c5_leg(args, torch, dev, local, world, rank, steps, warmup, lanes_n, check, 
     fset.assign_all(filters)
     words = (n + 63) // 64
     P = lanes_n
-    lanes = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(P - 1)]
+    lanes = leg_lanes(torch, dev, P)
     hits = [torch.zeros((F, words), dtype=torch.int64, device=dev) for _ in range(P)]
     nstep = [0]
 
