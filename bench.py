@@ -1168,8 +1168,7 @@ def c4_leg(args, torch, dist, world, rank, local, dev, use_dist, red_dev, steps,
             f.clear(stream=sh)
         lsmt_amd.insert_many(fsets[i], batches, stream=sh)
 
-    for _ in range(warmup):
-        step()
+    warm_up(torch, dev, step, warmup)
     el, ev_ms = _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes, step, steps)
     # one lane: each batched build alone on the chip (its own duration)
     nstep[0] = 0
@@ -1249,6 +1248,25 @@ def c4_roofline(leg, world):
 
 
 _LANES = None  # the default line's lane streams, made once at its start
+WARM_S = 0.3   # a secondary leg's time-based warm-up (warm_up)
+
+
+def warm_up(torch, dev, step, steps, seconds=WARM_S):
+    """A secondary leg's untimed warm-up: at least `steps` steps, and steps
+    until `seconds` of wall time have passed, so the chip's clocks have ramped
+    whether the leg runs inside the default line (after seconds of other
+    legs) or alone in a fresh process (tools/profile_round.sh). C4 alone after
+    5 steps ran at 121.5-123.4 us per step against 112.5-113.3 after 3000
+    (tools/gpu/r05_warm.sh); the profiles' one-lane durations were taken that
+    way, which round 4 and early round 5 read as box-to-box variation."""
+    t0 = time.perf_counter()
+    i = 0
+    while i < steps or time.perf_counter() - t0 < seconds:
+        step()
+        i += 1
+        if i % 64 == 0:
+            torch.cuda.synchronize(dev)  # bounded queue depth, and the elapsed time is the device's
+    torch.cuda.synchronize(dev)
 
 
 def leg_lanes(torch, dev, P):
@@ -1300,8 +1318,7 @@ def c5_leg(args, torch, dev, local, world, rank, steps, warmup, lanes_n, check, 
         nstep[0] += 1
         fset.probe(keys, out=hits[i], stream=lanes[i].cuda_stream)
 
-    for _ in range(warmup):
-        step()
+    warm_up(torch, dev, step, warmup)
     el, ev_ms = _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes, step, steps)
     nstep[0] = 0
     Psaved, P = P, 1
@@ -1547,8 +1564,7 @@ def wide_fanout_leg(args, torch, dev, local, sh, LK, timed, kernel_ms, lsmt_amd,
         lsmt_amd.get_many(newest_first, keys, filterset=fset, hit_rows=slots, out=(which, voff, vals), stream=sh,
                           wait=False)
 
-    for _ in range(2):
-        step()
+    warm_up(torch, dev, step, 2)
     k = max(3, LK // 20)
     el = timed(step, k, lanes=[torch.cuda.current_stream(dev)])
     kus = kernel_ms(["k_wide_get_many", "k_tile_scan", "k_b64_decode"], step, k)
