@@ -35,7 +35,6 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Bloom probes/sec device-resident (1M keys × 32 filters); build keys/sec"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
-SPIN_CYCLES_PER_US = 2100  # torch.cuda._sleep cycles per microsecond (~2.1 GHz shader clock)
 
 
 def log(*a):
@@ -417,20 +416,24 @@ def main():
         rd = torch.ones(1 << 27, dtype=torch.int32, device=dev) if clean else None
         step_ms, kus = [], {nm: [] for nm in names}
         for r in range(2 * reps):
-            flush.fill_(r)
-            if clean:
-                rd.sum()
             torch.cuda.synchronize(dev)
             if use_dist:
                 dist.barrier()
+            flush.fill_(r)
+            if clean:
+                rd.sum()
             step_no[0] = 0  # the rep's step runs on lane 0 (= `stream`, where the events are)
+            if r >= reps:
+                torch.cuda.synchronize(dev)
             if r < reps:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                # device-resident: a ~200 us spin holds the
-                # stream while the host issues the step, so the interval is
-                # the step's device time, not the host's issue latency (the
-                # spin touches no memory: the caches stay as the flush left them)
-                torch.cuda._sleep(SPIN_CYCLES_PER_US * 200)
+                # device-resident: the cache-evicting write
+                # (~0.2 ms, on the same stream) is still running while the
+                # host issues the step, so the interval is the step's device
+                # time, not the host's issue latency. (Round 5 first gated
+                # with a 200 us spin kernel after a synchronize; the chip
+                # idles through a spin, and C2 one lane measured 0.5 us slower
+                # behind an 11.7 ms one: tools/c2_gate.py.)
                 e0.record(stream)
                 fn()
                 e1.record(stream)
@@ -444,30 +447,33 @@ def main():
         return (float(np.median(step_ms)),
                 {nm: round(float(np.median(v)), 2) for nm, v in kus.items() if v})
 
-    def gated_steps(fn, k, st):
-        """K steps of fn queued behind a spin kernel on st (so the GPU starts
-        them only after the host has issued all of them): (device us per
-        step from HIP events around them, host issue us per step, whether the
-        spin outlasted the issue)."""
+    def gated_steps(fn, k, st, w=600):
+        """K steps of fn queued behind W more steps of fn on st (the host
+        issues faster than the device runs them, so the device starts the K
+        timed steps only after the host has issued all of them): (device us
+        per step from HIP events around the K, host issue us per step, whether
+        the W steps outlasted the issue). The gate is real work rather than a
+        spin kernel: behind an ~11.7 ms one-wave spin the same C2 builds
+        measured 15.9-16.0 us, behind 600 builds 15.45-15.5 (the chip idles
+        through a spin; tools/c2_gate.py)."""
         torch.cuda.synchronize(dev)
-        # (while the GPU spins, a deep single-stream queue slows the host's
-        # issue to ~75 us per C2 build on this stack: keep k modest and the
-        # spin long enough for all of it)
-        spin_us = 4000 + 120 * k
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         es = torch.cuda.Event(enable_timing=True)
-        es.record(st)
-        torch.cuda._sleep(SPIN_CYCLES_PER_US * spin_us)
-        e0.record(st)
         t0 = time.perf_counter()
+        es.record(st)
+        for _ in range(w):
+            fn()
+        e0.record(st)
+        t1 = time.perf_counter()
         for _ in range(k):
             fn()
-        issue = time.perf_counter() - t0
+        t2 = time.perf_counter()
         e1.record(st)
         torch.cuda.synchronize(dev)
-        # the spin must still have been running when the last step was issued
-        ok = issue * 1e3 < es.elapsed_time(e0)
-        return e0.elapsed_time(e1) * 1e3 / k, issue * 1e6 / k, bool(ok)
+        # the gate's steps must still have been running when the last timed
+        # step was issued
+        ok = (t2 - t0) * 1e3 < es.elapsed_time(e0)
+        return e0.elapsed_time(e1) * 1e3 / k, (t2 - t1) * 1e6 / k, bool(ok)
 
     probe_kernels = ["k_part_probe", "k_tile_probe", "k_masks_to_hits", "k_probe_direct",
                      "k_set_probe"]
@@ -861,8 +867,8 @@ def main():
     BP_saved, BP = BP, 1
     timed(build_step, LK, lanes=b_streams[:1])
     b_one_issued_us = region["ms"] * 1e3 / region["k"]
-    # ... and its device time: the LK steps queued behind a spin kernel first,
-    # so the host's per-step issue (Python + the C call) is not in the interval
+    # ... and its device time: 64 steps queued behind 600 more, so the host's
+    # per-step issue (Python + the C call) is not in the interval
     b_one_us, b_issue_us, b_gated_ok = gated_steps(build_step, 64, stream)
     BP = BP_saved
     bprof = kernel_ms(["k_build_part", "k_build_tile", "k_insert_direct"], build_step, LK)
@@ -891,8 +897,8 @@ def main():
              "pipeline_lanes": BP, "cold": bcold,
              "region_us_per_step": round(b_region_us, 2), "frac": frac(b_region_us),
              "one_lane": {"us_per_build": round(b_one_us, 2), "frac": frac(b_one_us),
-                          "note": "one build at a time on one stream, device time: HIP events around K builds "
-                                  "queued behind a spin kernel (the latency a flush's kernels take)",
+                          "note": "one build at a time on one stream, device time: HIP events around 64 builds "
+                                  "queued behind 600 more (the latency a flush's kernels take)",
                           "queued_fully": b_gated_ok, "host_issue_us_per_build": round(b_issue_us, 2),
                           "host_issued_us_per_build": round(b_one_issued_us, 2),
                           "host_issued_note": "the same K builds issued live from Python: a build's device "
