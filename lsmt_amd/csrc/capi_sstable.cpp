@@ -118,9 +118,12 @@ int table_buckets(cb_table* t, hipStream_t s, cb::TableView* v) {
 // workspace until the tables, their slots or their buckets change (compared
 // by the tables' process-unique ids). Only when the tables share one bucket
 // count and the screen stays small; otherwise the walk runs without it.
-// 64 fingerprint bins: 1.91-1.92 G gets/s against 1.84-1.87 for 32 bins and
-// 1.76-1.77 for 16 (300 tables of 1024 lines; a 2.6 MB screen)
-constexpr uint32_t kScreenHbits = 6;
+// The most fingerprint bins (up to 256) whose screen fits kScreenMaxBytes.
+// 300 tables of 1024 lines: 64 bins (a 2.6 MB screen) 1.91-1.92 G gets/s
+// against 1.84-1.87 for 32 and 1.76-1.77 for 16; then 256 bins (10.5 MB)
+// 1.92-1.99 against 1.89-1.92 for 64 and 1.90-1.96 for 128
+// (tools/gpu/r05_wide5.sh, r05_wide6.sh, alternating on one box).
+constexpr uint32_t kScreenHbits = 8;
 constexpr uint64_t kScreenMaxBytes = 16ull << 20;
 int wide_screen(Workspace& ws, const cb_table* const* tables, const std::vector<cb::TableView>& views,
                 const std::vector<uint32_t>& rows, uint32_t R, const cb::TableView* dviews, const uint32_t* drows,
@@ -131,7 +134,7 @@ int wide_screen(Workspace& ws, const cb_table* const* tables, const std::vector<
   static const bool off = getenv("CB_NO_SCREEN") && getenv("CB_NO_SCREEN")[0] == '1';  // the A/B
   if (off) return CB_OK;
   static const int env_h = getenv("CB_SCREEN_HBITS") ? atoi(getenv("CB_SCREEN_HBITS")) : -1;
-  if (env_h >= 0 && env_h <= 6) hbits = (uint32_t)env_h;
+  if (env_h >= 0 && env_h <= 8) hbits = (uint32_t)env_h;
 #endif
   uint32_t bits = 0;
   for (const auto& v : views)
@@ -139,6 +142,7 @@ int wide_screen(Workspace& ws, const cb_table* const* tables, const std::vector<
       bits = v.bkbits();
       break;
     }
+  while (hbits > 4 && bits && cb::wide_screen_bytes(R, bits, hbits) > kScreenMaxBytes) --hbits;
   if (!bits || cb::wide_screen_bytes(R, bits, hbits) > kScreenMaxBytes) return CB_OK;
   std::vector<uint64_t> sig;
   sig.reserve(4 + 4 * (size_t)nt);

@@ -949,23 +949,17 @@ __global__ __launch_bounds__(kNT) void k_wide_screen(const TableView* __restrict
   const uint64_t B = idx & (nb - 1);
   const uint32_t slot = slots ? slots[i] : i;
   const TableView v = tv[i];
-  uint64_t bins = ~0ull;  // bit h: some stored fingerprint falls in bin h (all: no proof)
+  unsigned long long* row = reinterpret_cast<unsigned long long*>(scr) + B * H * R + (slot >> 6);
+  const unsigned long long bit = 1ull << (slot & 63u);
   if (v.bkt && v.fast() && v.bkbits() == bits) {
     const uint64_t sw = v.bkt[nb * kBktWords + B];
     const uint32_t nst = (uint32_t)(sw & 15u);
-    if (nst <= kBktSlots) {
-      bins = 0;
-      for (uint32_t s = 0; s < nst; ++s) bins |= 1ull << ((sw >> (4 + 15 * s)) & (H - 1));
+    if (nst <= kBktSlots) {  // the bins of the stored fingerprints
+      for (uint32_t s = 0; s < nst; ++s) atomicOr(row + ((sw >> (4 + 15 * s)) & (H - 1)) * R, bit);
+      return;
     }
   }
-  if (hbits < 6) bins &= (1ull << H) - 1;
-  unsigned long long* row = reinterpret_cast<unsigned long long*>(scr) + B * H * R + (slot >> 6);
-  const unsigned long long bit = 1ull << (slot & 63u);
-  while (bins) {
-    const uint32_t h = (uint32_t)__builtin_ctzll(bins);
-    bins &= bins - 1;
-    atomicOr(row + (uint64_t)h * R, bit);
-  }
+  for (uint64_t h = 0; h < H; ++h) atomicOr(row + h * R, bit);  // no proof: every bin
 }
 
 // Database::get in one launch over a wide set (wideset.hpp): k_set_get_many
@@ -1483,7 +1477,7 @@ hipError_t launch_set_get_many(int keyk, int mode, uint32_t width, const void* s
 
 hipError_t launch_wide_screen(const TableView* tv, const uint32_t* slots, uint32_t nt, uint32_t R, uint32_t bits,
                               uint32_t hbits, uint64_t* scr, hipStream_t s) {
-  if (!nt || bits > 24 || hbits > 6) return hipErrorInvalidValue;
+  if (!nt || bits > 24 || hbits > 8) return hipErrorInvalidValue;
   ProfScope ps("k_wide_screen", s);
   const hipError_t e = hipMemsetAsync(scr, 0, wide_screen_bytes(R, bits, hbits), s);
   if (e != hipSuccess) return e;
