@@ -1185,11 +1185,28 @@ constexpr uint64_t kSmallB64Bytes = 18;
 __device__ __forceinline__ void b64_small_load(const uint8_t* src, uint64_t dl, SmallB64& v) {
   const uint64_t len = (dl + 2) / 3 * 4;
   const uintptr_t a = (uintptr_t)src;
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
   v.sh = (uint32_t)(a & 3);
+#ifndef CB_B64_DWORD_LOADS
+  // three 16-B loads of the aligned 48 B holding the chars (each clamped to
+  // the last 16 B the chars reach, so no load leaves their span), then the 7
+  // dwords from dword (a & 15) / 4 on: 3 load instructions per value instead
+  // of 7 (the loads' random lines are the kernel's cost)
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) u32x4* gq;
+  const gq q = (gq)(a & ~(uintptr_t)15);
+  const uint32_t lastq = ((uint32_t)(a & 15) + (uint32_t)len - 1) >> 4;
+  const u32x4 q0 = q[0], q1 = q[lastq < 1 ? lastq : 1], q2 = q[lastq < 2 ? lastq : 2];
+  const uint32_t d[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+  const uint32_t o = (uint32_t)(a & 12) >> 2;
+#pragma unroll
+  for (uint32_t i = 0; i < 7; ++i)
+    v.x[i] = o == 0 ? d[i] : o == 1 ? d[i + 1] : o == 2 ? d[i + 2] : d[i + 3];
+#else
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
   const uint32_t last = (v.sh + (uint32_t)len + 3) / 4 - 1;
 #pragma unroll
   for (uint32_t i = 0; i < 7; ++i) v.x[i] = w[i < last ? i : last];
+#endif
 }
 
 // dl <= 18 bytes decoded from the loaded dwords (realigned: y = one quad).
@@ -1216,6 +1233,9 @@ constexpr uint32_t kDecodeLds = 16384;  // staged output bytes per block
 // are one contiguous output range; when it fits in LDS, lanes decode into LDS
 // and the block writes the range with aligned dword stores, else lanes write
 // their bytes directly.
+#ifdef CB_EXPERIMENTS
+__constant__ int g_b64_x;
+#endif
 __global__ __launch_bounds__(kNT) void k_b64_decode(const uint64_t* __restrict__ vsrc,
                                                     const uint64_t* __restrict__ dlen,
                                                     const uint64_t* __restrict__ tsum, uint64_t n,
@@ -1234,7 +1254,13 @@ __global__ __launch_bounds__(kNT) void k_b64_decode(const uint64_t* __restrict__
   const bool write = out && vn <= cap;     // uniform
   SmallB64 sv;
   const bool small = dl && dl <= kSmallB64Bytes;
+#ifdef CB_EXPERIMENTS
+  // (timing-only A/B, wrong bytes: CB_B64_X bit 0 skips the value loads)
+  if (write && small && !(g_b64_x & 1)) b64_small_load(src, dl, sv);
+  if (g_b64_x & 1) sv = SmallB64{{0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u}, 0};
+#else
   if (write && small) b64_small_load(src, dl, sv);
+#endif
   uint64_t total;
   const uint64_t pre = block_scan<kNT>(dl, &total);
   const uint64_t o = base + pre;
@@ -1524,6 +1550,14 @@ hipError_t launch_tile_scan(uint64_t* tsum, uint64_t nt, uint64_t* total_out, hi
 
 hipError_t launch_b64_decode(const uint64_t* vsrc, const uint64_t* dlen, const uint64_t* tsum,
                              uint64_t n, uint64_t* voff, uint8_t* out, uint64_t cap, hipStream_t s) {
+#ifdef CB_EXPERIMENTS
+  static const int env_x = [] {
+    const int x = getenv("CB_B64_X") ? atoi(getenv("CB_B64_X")) : 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_b64_x), &x, sizeof(x));
+    return x;
+  }();
+  (void)env_x;
+#endif
   if (!n) return hipSuccess;
   ProfScope ps("k_b64_decode", s);
   hipLaunchKernelGGL(k_b64_decode, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, vsrc, dlen, tsum, n, voff,
