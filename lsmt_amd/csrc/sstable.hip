@@ -1236,6 +1236,9 @@ constexpr uint32_t kDecodeLds = 16384;  // staged output bytes per block
 #ifdef CB_EXPERIMENTS
 __constant__ int g_b64_x;
 #endif
+// (Two adjacent keys per thread, so all of a 1M-key batch's value loads are
+// in flight in one round, measured slower: read path 14.3 against 14.8-14.9 G
+// gets/s, wide fan-out 1.97-2.00 against 2.04-2.06; tools/gpu/r05_b64kpt.sh.)
 __global__ __launch_bounds__(kNT) void k_b64_decode(const uint64_t* __restrict__ vsrc,
                                                     const uint64_t* __restrict__ dlen,
                                                     const uint64_t* __restrict__ tsum, uint64_t n,
