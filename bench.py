@@ -276,9 +276,12 @@ def main():
     # probe. A step is still one full probe (+ exchange) of one batch; lanes
     # never share a buffer, so no cross-stream event is needed per step.
     P = args.probe_streams
-    lane_streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(P - 1)]
+    # every lane stream the line will use (the probe lanes first, then the
+    # build's extra ones), made together at its start (leg_lanes)
+    all_lanes = [stream] + [torch.cuda.Stream(device=dev) for _ in range(max(P, args.build_streams) - 1)]
+    lane_streams = all_lanes[:P]
     global _LANES
-    _LANES = lane_streams
+    _LANES = all_lanes
     lane_sh = [st.cuda_stream for st in lane_streams]
     # The exchange runs through the C ABI (cb_hits_allgather over the
     # library's own RCCL communicator, lsmt_amd/csrc/comm.cpp): the same call
@@ -444,6 +447,12 @@ def main():
                     kus[nm].append(v["avg_us"])
         del flush, rd
         torch.cuda.synchronize(dev)
+        # the 1.5 GiB of eviction buffers go back to the device: left in
+        # torch's cache, later legs' tensors are carved from them, and the
+        # one-lane C2 build measured 16.5-16.6 us after the C3 cold leg
+        # against 15.4 with them released (cold 22.7 -> 21.3 us;
+        # tools/gpu/r05_c2cold.sh)
+        torch.cuda.empty_cache()
         return (float(np.median(step_ms)),
                 {nm: round(float(np.median(v)), 2) for nm, v in kus.items() if v})
 
@@ -846,7 +855,7 @@ def main():
     # in flight, one HIP stream each; 4 measured 10.8 against 11.3 us per C2
     # step for 3)
     BP = args.build_streams
-    b_streams = lane_streams[:BP] + [torch.cuda.Stream(device=dev) for _ in range(BP - len(lane_streams))]
+    b_streams = _LANES[:BP] + [torch.cuda.Stream(device=dev) for _ in range(BP - len(_LANES))]
     b_sh = [st.cuda_stream for st in b_streams]
     bk = torch.from_numpy(workload.c2_build_keys(args.build_keys)).to(dev)
     bfs = [lsmt_amd.BloomFilter(args.build_m_bits, device=local) for _ in range(BP)]
