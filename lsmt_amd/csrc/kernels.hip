@@ -985,7 +985,7 @@ TilePlan plan_build(uint64_t m, uint64_t n, uint32_t nb) {
   // passes are bandwidth-bound there, and the entries are a third of the
   // bytes. Single builds keep 32-bit entries (their tile pass is bound by its
   // dependent loads, where the sub-tile arithmetic cost more than the bytes
-  // saved: DESIGN §9.6).
+  // saved: HISTORY.md, round 3 build notes).
   // Their tiles are 2^18 bits (4 sub-tiles) worked by 512-thread
   // workgroups, four per CU instead of two 1024-thread ones on 2^19-bit
   // tiles: C4 141 -> 128-131 us per step on one lane, 147-151 -> 139-141 on
