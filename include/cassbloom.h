@@ -122,7 +122,11 @@ int cb_may_contain(const cb_filter* f, const uint8_t* key, uint64_t len, int* ou
 /* Host mirror policy: 1 on, 0 off, -1 auto (the default: on when m <= 2^24,
  * i.e. up to 2 MiB of host words; past that a write records no event, and
  * the first refresh after the mirror is turned on synchronises the stream that
- * write was issued on, not the device). */
+ * write was issued on, not the device). A caller that destroys that stream
+ * before the filter's next refresh synchronises it first (a destroyed
+ * stream's handle makes the refresh synchronise the whole device instead,
+ * and a handle HIP has already reused for a new stream would not cover the
+ * write). */
 int cb_filter_host_mirror(cb_filter* f, int mode);
 /* *on = whether cb_may_contain uses the mirror; *current = whether the mirror
  * already holds the latest write (either may be NULL). Host only. */

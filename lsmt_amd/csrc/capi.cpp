@@ -1276,7 +1276,13 @@ int refresh_mirror(const cb_filter* cf) {
         // a write made while the mirror was off recorded no event: wait for
         // the stream it was issued on (every write to one filter is ordered
         // by its exclusive writer, so that stream's tail covers them all)
-        HIP_TRY(hipStreamSynchronize(f->unmarked_stream.load(std::memory_order_relaxed)));
+        // (a stream destroyed since is an invalid handle to HIP: then the
+        // whole device; the header asks writers to keep a write's stream
+        // until the filter's next read or to synchronize it first)
+        if (hipStreamSynchronize(f->unmarked_stream.load(std::memory_order_relaxed)) != hipSuccess) {
+          (void)hipGetLastError();
+          HIP_TRY(hipDeviceSynchronize());
+        }
       }
       // and the last recorded write (a write made after the mirror came on)
       const std::shared_ptr<WriteMark> m = std::atomic_load(&f->wmark);
