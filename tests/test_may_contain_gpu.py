@@ -195,6 +195,27 @@ def test_unrecorded_refresh_waits_for_its_stream_only(gpu):
     assert still_busy, "the mirror refresh waited for an unrelated stream"
 
 
+def test_unrecorded_write_on_a_destroyed_stream(gpu):
+    """A write made while the mirror was off, on a stream the caller then
+    destroys: the refresh's stream sync fails on the dead handle and falls
+    back to a device sync, so the mirror still holds the write."""
+    import ctypes
+    m = 1 << 26
+    keys = workload.key_range(71, 100_000)
+    probe = np.concatenate([keys[:500], workload.key_range(72, 500)])
+    o = oracle.OracleFilter(m)
+    o.insert_fixed(keys)
+    b = gpu.BloomFilter(m)
+    b.host_mirror(0)
+    hip = ctypes.CDLL("libamdhip64.so")
+    st = ctypes.c_void_p()
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(st), 1) == 0
+    b.insert_batch(keys, stream=st.value)  # unrecorded, on the raw stream
+    assert hip.hipStreamDestroy(st) == 0
+    b.host_mirror(1)
+    assert np.array_equal(np.array([b.may_contain(bytes(k)) for k in probe]), oracle_hits(o, probe))
+
+
 def test_latency_tool_mirror_under_1us(gpu):
     """The C-ABI per-key call (no Python in the loop) at the product's m =
     1024 and at the C3 filter size: the mirror agrees with the GPU probe on
