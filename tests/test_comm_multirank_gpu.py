@@ -82,6 +82,44 @@ def _filters(nf):
 CASES = [(2, 5), (3, 7), (8, 19), (2, 6)]
 
 
+@pytest.mark.parametrize("mode", ["dense", "sparse", "overflow_sync", "probe"])
+def test_rccl_single_rank(gpu, mode):
+    """The RCCL transport itself (cb_comm_unique_id's ncclGetUniqueId and its
+    socket bootstrap, ncclCommInitRank, ncclAllGather on the caller's stream,
+    ncclCommDestroy) at world 1 on this box's one GPU: the calls every
+    multi-GPU line makes, here with one rank (RCCL refuses two ranks on one
+    device, so world > 1 runs only on the driver's 8-GPU node)."""
+    import torch
+
+    import lsmt_amd
+    from lsmt_amd.shard import Comm
+    nf = 5
+    gf, expect, look = _filters(nf)
+    keys = torch.from_numpy(look).cuda()
+    words = (N + 63) // 64
+    s = lsmt_amd.FilterSet(M, 32)
+    s.assign_all(gf)
+    st = torch.cuda.Stream()
+    full = torch.full((nf, words), -1, dtype=torch.int64, device="cuda")
+    c = Comm(0, 1, 0, Comm.unique_id())
+    try:
+        if mode == "probe":
+            local = torch.zeros((nf, words), dtype=torch.int64, device="cuda")
+            c.probe_allgather(s, keys, nf, local, full, sparse=True,
+                              cap=sparse_cap(N, nf, 1), stream=st)
+        else:
+            local = torch.zeros((nf, words), dtype=torch.int64, device="cuda")
+            s.probe(lsmt_amd.DeviceKeys(keys), out=local)
+            torch.cuda.synchronize()
+            cap = 5 if mode == "overflow_sync" else sparse_cap(N, nf, 1)
+            used = c.allgather(local, nf, full, sparse=mode != "dense", cap=cap, stream=st)
+            assert used == (mode == "sparse")
+        st.synchronize()
+        assert np.array_equal(full.cpu().numpy().view(np.uint64), expect)
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("world,nf", CASES)
 @pytest.mark.parametrize("mode", ["dense", "sparse", "sparse_async", "overflow_sync", "overflow_async"])
 def test_loopback_hits_allgather(gpu, world, nf, mode):
