@@ -451,7 +451,7 @@ def main():
         # torch's cache, later legs' tensors are carved from them, and the
         # one-lane C2 build measured 16.5-16.6 us after the C3 cold leg
         # against 15.4 with them released (cold 22.7 -> 21.3 us;
-        # tools/gpu/r05_c2cold.sh)
+        # experiment r05_c2cold, HISTORY.md)
         torch.cuda.empty_cache()
         return (float(np.median(step_ms)),
                 {nm: round(float(np.median(v)), 2) for nm, v in kus.items() if v})
@@ -1272,7 +1272,7 @@ def warm_up(torch, dev, step, steps, seconds=WARM_S):
     whether the leg runs inside the default line (after seconds of other
     legs) or alone in a fresh process (tools/profile_round.sh). C4 alone after
     5 steps ran at 121.5-123.4 us per step against 112.5-113.3 after 3000
-    (tools/gpu/r05_warm.sh); the profiles' one-lane durations were taken that
+    (experiment r05_warm, HISTORY.md); the profiles' one-lane durations were taken that
     way, which round 4 and early round 5 read as box-to-box variation."""
     t0 = time.perf_counter()
     i = 0
@@ -1292,7 +1292,7 @@ def leg_lanes(torch, dev, P):
     queue run one after the other: the C5 leg on the current stream plus two
     more pool streams drawn after the C4 leg's took 206-208 us per step on
     three lanes, against 188-189 on the line's lanes, on fresh pool streams
-    or on hipStreamCreate streams (tools/gpu/r05_c5ctx3.sh)."""
+    or on hipStreamCreate streams (experiment r05_c5ctx3, HISTORY.md)."""
     if _LANES and len(_LANES) >= P:
         return list(_LANES[:P])
     return [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(device=dev) for _ in range(P - 1)]

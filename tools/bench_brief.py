@@ -2,14 +2,16 @@
 import json
 import sys
 
-d = json.load(open(sys.argv[1]))
-r = d["roofline"]
-print(f"probe C3 {d['value'] / 1e12:.3f} T/s {d['ms_per_step'] * 1e3:.1f} us/step  frac {r['frac']} "
-      f"one-lane {r.get('frac_one_lane')} ({r.get('kernel_avg_us_one_lane')} us)  "
-      f"rr {r['random_read_roofline']['frac']}")
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])  # the line (a leg run prints only its leg)
+r = d.get("roofline")
+if r:
+    print(f"probe C3 {d['value'] / 1e12:.3f} T/s {d['ms_per_step'] * 1e3:.1f} us/step  frac {r['frac']} "
+          f"one-lane {r.get('frac_one_lane')} ({r.get('kernel_avg_us_one_lane')} us)  "
+          f"rr {r['random_read_roofline']['frac']}")
 b = d.get("build")
 if b:
     print(f"build C2 {b['value'] / 1e9:.1f} G keys/s {b['ms_per_step'] * 1e3:.2f} us/step lanes {b['pipeline_lanes']} "
+          f"one-lane {b.get('one_lane', {}).get('us_per_build')} us cold {(b.get('cold') or {}).get('ms_per_step')} ms "
           f"{b['kernels']}")
 rp = d.get("read_path")
 if rp:

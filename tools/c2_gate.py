@@ -4,7 +4,7 @@ alternating: (spin) a ~11.7 ms one-wave spin kernel, as the bench does;
 (warm) W real builds queued first, the K timed builds issued while the device
 still works through them; (warm+spin) a 0.3 s warm-up, then the spin gate.
 Prints device us per build for each, and whether the K builds were all queued
-before the device reached them. Diagnostic only (tools/gpu/r05_c2gate.sh)."""
+before the device reached them. Diagnostic only: `timeout -k 10 300 python tools/c2_gate.py` on the box."""
 import os
 import sys
 import time

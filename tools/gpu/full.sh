@@ -1,8 +1,9 @@
 #!/bin/bash
-# Round 5: the whole -m gpu suite, smoke(), then the default bench line.
+# The round's validation: the whole -m gpu suite, smoke(), then the default
+# bench line (gpurun_out/full/bench_full.json).
 set -o pipefail
-mkdir -p gpurun_out/r05
-O=gpurun_out/r05
+O=${OUT:-gpurun_out/full}
+mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_all.log 2>&1 || { tail -30 $O/pytest_all.log; exit 1; }
 tail -1 $O/pytest_all.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }

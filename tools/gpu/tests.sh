@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU parity suite (+ optional bench) on one box. Outputs under gpurun_out/.
-# Usage: bash tools/gpu_tests.sh [pytest -k expr]
+# Usage: bash tools/gpu/tests.sh [pytest -k expr]
 set -o pipefail
 mkdir -p gpurun_out
 K=${1:+-k "$1"}
