@@ -122,7 +122,7 @@ int table_buckets(cb_table* t, hipStream_t s, cb::TableView* v) {
 // 300 tables of 1024 lines: 64 bins (a 2.6 MB screen) 1.91-1.92 G gets/s
 // against 1.84-1.87 for 32 and 1.76-1.77 for 16; then 256 bins (10.5 MB)
 // 1.92-1.99 against 1.89-1.92 for 64 and 1.90-1.96 for 128
-// (tools/gpu/r05_wide5.sh, r05_wide6.sh, alternating on one box).
+// (experiments r05_wide5 and r05_wide6, HISTORY.md; alternating on one box).
 constexpr uint32_t kScreenHbits = 8;
 constexpr uint64_t kScreenMaxBytes = 16ull << 20;
 int wide_screen(Workspace& ws, const cb_table* const* tables, const std::vector<cb::TableView>& views,

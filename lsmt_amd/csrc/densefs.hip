@@ -51,7 +51,7 @@ constexpr uint32_t kDenseNT = 1024;
 // fewer, larger blocks shorten the probe's per-region run table. One batch
 // of 7 keys per thread (C = 7168, 1396 blocks at C5) measured 209-211 us per
 // C5 step on three lanes; two of 5 (977 blocks) 194-196; three of 4 (814
-// blocks) 190-191 (tools/gpu/r05_c5nb.sh, same box, alternating).
+// blocks) 190-191 (experiment r05_c5nb, HISTORY.md, same box, alternating).
 #if defined(CB_EXPERIMENTS) && defined(CB_DENSE_KPT)
 constexpr uint32_t kDenseKPT = CB_DENSE_KPT;  // (experiment builds: keys per partition thread and batch)
 #else
@@ -76,7 +76,7 @@ constexpr uint32_t kProbeU = 4;              // entries per lane per round of th
 // 1954 partition blocks instead of 1396 cost the probe 9 us, and the C5 step
 // on three lanes went 209-211 -> 221-225 us (one lane 249 -> 242); at 4 keys
 // per thread (no spill) the batch needs two chunks and the set is streamed
-// twice: 265-268 us (tools/gpu/r05_c5part.sh).
+// twice: 265-268 us (experiment r05_c5part, HISTORY.md).
 #if defined(CB_EXPERIMENTS) && defined(CB_DENSE_PART_LB8)
 #define CB_DENSE_PART_WAVES 8
 #elif defined(CB_EXPERIMENTS) && defined(CB_DENSE_PART_W)

@@ -985,7 +985,7 @@ constexpr uint32_t kScreen = 8;
 // against 782-804 M gets/s.)
 // Four waves per SIMD, 109 VGPRs and no spill (round 5, with the screen):
 // 1.81-1.84 against 1.63 G gets/s for five waves at 96 VGPRs and 56 B of
-// spill per lane (tools/gpu/r05_wide4.sh, alternating on one box).
+// spill per lane (experiment r05_wide4, HISTORY.md, alternating on one box).
 template <int KEYK, int MODE>
 __global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __restrict__ set, uint32_t R, ModP mp,
                                                        WideZone z, const TableView* __restrict__ tv, uint32_t nt,
@@ -1238,7 +1238,7 @@ __constant__ int g_b64_x;
 #endif
 // (Two adjacent keys per thread, so all of a 1M-key batch's value loads are
 // in flight in one round, measured slower: read path 14.3 against 14.8-14.9 G
-// gets/s, wide fan-out 1.97-2.00 against 2.04-2.06; tools/gpu/r05_b64kpt.sh.)
+// gets/s, wide fan-out 1.97-2.00 against 2.04-2.06; experiment r05_b64kpt, HISTORY.md.)
 __global__ __launch_bounds__(kNT) void k_b64_decode(const uint64_t* __restrict__ vsrc,
                                                     const uint64_t* __restrict__ dlen,
                                                     const uint64_t* __restrict__ tsum, uint64_t n,

@@ -3,7 +3,8 @@
 // per-call host time of K enqueue-only creates, and beside it the host cost of
 // the HIP calls a create is made of (an empty kernel launch, a small
 // hipMemsetAsync, a D2H copy into pinned memory, hipEventRecord). Output: one
-// JSON object. Diagnostic only. Build: see tools/gpu_r04m.sh.
+// JSON object. Diagnostic only. Build: hipcc --offload-arch=gfx950 -O3 -Iinclude tools/create_host.hip -o build/create_host
+// -Llsmt_amd -lcassbloom -Wl,-rpath,'$ORIGIN/../lsmt_amd'.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
