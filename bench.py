@@ -1580,7 +1580,11 @@ def wide_fanout_leg(args, torch, dev, local, sh, LK, timed, kernel_ms, lsmt_amd,
                           wait=False)
 
     warm_up(torch, dev, step, 2)
-    k = max(3, LK // 20)
+    # 100 steps at the default K (12 ms): the host issues a step in ~30 us
+    # against ~122 us of device time (tools/wide_issue.py), so the queue runs
+    # ahead after the first step; 10 steps left that first step's issue and
+    # the box's host jitter in the figure (128-142 us per step against 122)
+    k = max(20, LK // 2)
     el = timed(step, k, lanes=[torch.cuda.current_stream(dev)])
     kus = kernel_ms(["k_wide_get_many", "k_tile_scan", "k_b64_decode"], step, k)
     torch.cuda.synchronize(dev)

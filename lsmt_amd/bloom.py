@@ -25,6 +25,7 @@ There is no CPU fallback: every operation goes through libcassbloom.so.
 from __future__ import annotations
 
 import ctypes
+import operator
 from dataclasses import dataclass, field
 from typing import Iterable, Sequence
 
@@ -815,6 +816,31 @@ def _to_var(b: KeyBatch) -> KeyBatch:
     return KeyBatch(n=b.n, data=data, offsets=offs)
 
 
+_TABLE_ARRAYS: dict = {}  # id(sequence) -> (the tables' handle objects, their C array)
+_HANDLE = operator.attrgetter("_h")
+
+
+def _table_array(tables: Sequence[Table]):
+    """The tables' handles as one C array, kept per sequence object while it
+    holds the same open tables in the same order. A store passes its table
+    list batch after batch (Database::get walks self.sstables, src/lib.rs:
+    129-134), and converting 300 handles into a fresh ctypes array took ~70 us
+    of host time per call, more than half the wide fan-out's device step.
+    The check is one identity test per table against the handle objects
+    stored here: Table.close() replaces a table's handle object, so a closed
+    or different table never reuses a stored array (and holding the handle
+    objects keeps no table alive)."""
+    hs = list(map(_HANDLE, tables))
+    hit = _TABLE_ARRAYS.get(id(tables))
+    if hit is not None and hit[0] == hs:  # (ctypes handles compare by identity)
+        return hit[1]
+    arr = (ctypes.c_void_p * max(len(hs), 1))(*[h.value for h in hs])
+    if len(_TABLE_ARRAYS) >= 8:
+        _TABLE_ARRAYS.pop(next(iter(_TABLE_ARRAYS)))
+    _TABLE_ARRAYS[id(tables)] = (hs, arr)
+    return arr
+
+
 def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=None, out=None, wait=True,
              filterset=None):
     """Database::get's newest-first walk for a key batch (tables[0] newest).
@@ -838,7 +864,7 @@ def get_many(tables: Sequence[Table], keys, hits=None, hit_rows=None, stream=Non
         raise ValueError("filterset= computes the gate itself: pass hits=None")
     b = as_batch(keys)
     nt = len(tables)
-    arr = (ctypes.c_void_p * max(nt, 1))(*[t.handle.value for t in tables])
+    arr = _table_array(tables)
     hp, hk = _ptr_of(hits) if hits is not None else (None, None)
     rows = None
     if hit_rows is not None:

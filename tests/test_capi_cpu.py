@@ -86,3 +86,30 @@ def test_meta_encode_rejects_non_utf8_like_rust_strings():
             ok = False
         rc, _ = _zone_encode(L, s, b"z")
         assert (rc == 0) == ok, s
+
+
+def test_table_handle_array_is_reused_only_for_the_same_open_tables():
+    # get_many's C array of table handles (lsmt_amd.bloom._table_array) is
+    # kept per sequence while it names the same handle objects; a closed table
+    # (Table.close() replaces its handle object), a replaced or reordered
+    # table, or another sequence gets a fresh array with the current handles
+    from lsmt_amd import bloom
+
+    class T:
+        def __init__(self, v):
+            self._h = ctypes.c_void_p(v)
+
+    ts = [T(0x1000 + 64 * i) for i in range(300)]
+    a = bloom._table_array(ts)
+    assert bloom._table_array(ts) is a
+    assert [a[i] for i in range(300)] == [0x1000 + 64 * i for i in range(300)]
+    ts[7]._h = ctypes.c_void_p()  # closed
+    b = bloom._table_array(ts)
+    assert b is not a and b[7] is None
+    ts[3], ts[4] = ts[4], ts[3]
+    c = bloom._table_array(ts)
+    assert c is not b and (c[3], c[4]) == (0x1000 + 64 * 4, 0x1000 + 64 * 3)
+    rev = ts[::-1]
+    d = bloom._table_array(rev)
+    assert d[0] == 0x1000 + 64 * 299 and bloom._table_array(ts) is c
+    assert len(bloom._table_array([])) == 1  # the C ABI never reads it (nt = 0)

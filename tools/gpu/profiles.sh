@@ -9,5 +9,7 @@ for shape in "$@"; do
   echo "== $shape"; tail -12 gpurun_out/prof/$shape.log
   # the summary holds what the traces and counter dumps gave; drop them so the
   # call's gpurun_out stays under the 64 MiB it may bring back
-  find gpurun_out/prof/$shape \( -name '*_kernel_trace.csv' -o -name '*_counter_collection.csv' \) -delete
+  # (and the call's file count: keep the summary, the kernel stats and the logs)
+  find gpurun_out/prof/$shape \( -name '*_kernel_trace.csv' -o -name '*_counter_collection.csv' \
+    -o -name '*_agent_info.csv' -o -name '*_domain_stats.csv' \) -delete
 done
