@@ -796,7 +796,9 @@ def main():
             k_fl = max(3, LK // 4)
             # warm-up: as many flushes as the timed region, then freed, so the
             # timed region's allocations come from the library's block pool
-            for _ in range(max(1, args.warmup, k_fl)):
+            # (not --warmup flushes: they are all held until the warm-up ends,
+            # ~60 MB of HBM each, and 3000 of them exhausted the device)
+            for _ in range(max(1, k_fl)):
                 step_flush()
             for t, _, _ in made:
                 t.wait()

@@ -1,7 +1,8 @@
 #!/bin/bash
 # rocprofv3 trace + PMC evidence for the given shapes, one after the
 # other (tools/profile_round.sh), each into gpurun_out/prof/<shape>
-# (copy the summaries to profiles/ under the round's name).
+# (copy the summaries to profiles/ under the round's name). Run c3 after
+# another shape (`c4 c5 c3 wide`), so the chip's clock has ramped up.
 set -o pipefail
 mkdir -p gpurun_out/prof
 for shape in "$@"; do

@@ -8,6 +8,10 @@
 #   SHAPE: c3 (the headline), c4 (64 batched builds), c5 (the C5 rank slice),
 #   wide (300 m=1024 tables in one wide set)
 # Output: $PROF_OUT (default gpurun_out/prof_SHAPE)/summary.json
+# (c3 warms up for 1000 steps per leg: its stats average every k_set_probe
+# launch of the run, and on a box that has just started the first launches run
+# at a low clock; round 5 measured 46.6 against 38.7 us with 5 warm-up steps
+# as the call's first shape)
 set -o pipefail
 export TMPDIR=/tmp
 SHAPE=$1
@@ -15,7 +19,7 @@ shift
 OUT=${PROF_OUT:-gpurun_out/prof_$SHAPE}
 mkdir -p $OUT
 case $SHAPE in
-  c3) BENCH="python bench.py --no-cpu --no-e2e --no-cold --no-c4 --no-c5 --no-wide --steps 50 --warmup 5"; META="shape=c3" ;;
+  c3) BENCH="python bench.py --no-cpu --no-e2e --no-cold --no-c4 --no-c5 --no-wide --steps 50 --warmup 1000"; META="shape=c3" ;;
   c4) BENCH="python bench.py --workload c4 --no-cpu --steps 50 --warmup 5"; META="shape=c4 filters_per_launch=64" ;;
   c5) BENCH="python bench.py --leg c5 --no-cpu --steps 20 --warmup 3"; META="shape=c5" ;;
   wide) BENCH="python bench.py --leg wide --no-cpu --steps 10 --warmup 2"; META="shape=wide" ;;
