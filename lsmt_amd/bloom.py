@@ -836,7 +836,7 @@ def _table_array(tables: Sequence[Table]):
         return hit[1]
     arr = (ctypes.c_void_p * max(len(hs), 1))(*[h.value for h in hs])
     if len(_TABLE_ARRAYS) >= 8:
-        _TABLE_ARRAYS.pop(next(iter(_TABLE_ARRAYS)))
+        _TABLE_ARRAYS.clear()  # (one call, so safe against another thread's insert)
     _TABLE_ARRAYS[id(tables)] = (hs, arr)
     return arr
 
