@@ -230,6 +230,41 @@ def test_get_many_batches_of_changing_size(gpu):
         assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals, nk
 
 
+def test_get_many_same_list_mutated_between_calls(gpu):
+    """One table list passed batch after batch while it changes in place
+    (get_many keeps its handle array per list object, lsmt_amd.bloom.
+    _table_array): a table replaced by a new one, the list reordered, a table
+    closed and its slot refilled, the list grown. Every call equals the
+    oracle over the list as it is at that call."""
+    per = [workload.key_range(1600 + t, 8_000) for t in range(4)]
+    files = [workload.sstable_bytes(k, workload.table_value(k, 500 + t)) for t, k in enumerate(per)]
+    pool = np.concatenate(per + [workload.key_range(4325, 8_000)])
+    look = np.ascontiguousarray(pool[np.random.default_rng(6).permutation(len(pool))][:20_000])
+    d = np.ascontiguousarray(look.reshape(-1))
+    offs = np.arange(0, 16 * (len(look) + 1), 16, dtype=np.uint64)
+    tables = [gpu.Table(f) for f in files[:3]]
+    idx = [0, 1, 2]
+
+    def check():
+        ow, ovoff, ovals = oracle.get_many([oracle.OracleTable(files[i].tobytes()) for i in idx], None, d, offs)
+        which, voff, vals = gpu.get_many(tables, look)
+        assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals, idx
+
+    check()
+    check()  # the kept array
+    tables[1], idx[1] = gpu.Table(files[3]), 3  # replaced
+    check()
+    tables.reverse()
+    idx.reverse()
+    check()
+    tables[0].close()  # closed, then its slot refilled
+    tables[0], idx[0] = gpu.Table(files[1]), 1
+    check()
+    tables.append(gpu.Table(files[0]))
+    idx.append(0)
+    check()
+
+
 def test_set_get_many_long_keys_and_exact_tables(gpu):
     """The fused form over ragged keys of 0..40 bytes (the long-key compares
     past the 16-byte index words), with one table indexed for the exact
