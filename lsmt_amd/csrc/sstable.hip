@@ -975,6 +975,8 @@ __global__ __launch_bounds__(kNT) void k_wide_screen(const TableView* __restrict
 // The wide walk's summary words loaded together: 4 / 8 / 16 at once measured
 // 671-679 / 792-809 / 816-820 M gets/s against 517-519 one at a time (300
 // tables of m = 1024); 16 doubles the scratch spill (36 -> 72 B per lane).
+// With the screen (round 5) the batch no longer matters: 8 / 4 / 2 at once
+// measured 2.145 / 2.140 / 2.139 G gets/s, the same VGPRs (experiment builds).
 #if defined(CB_EXPERIMENTS) && defined(CB_WIDE_SCREEN_BATCH)
 constexpr uint32_t kScreen = CB_WIDE_SCREEN_BATCH;
 #else
