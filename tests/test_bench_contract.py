@@ -66,3 +66,21 @@ def test_host_cpus_is_consistent():
     if c["cgroup_quota"]:
         assert c["usable"] <= c["cgroup_quota"]
     assert "nproc" in c["note"]
+
+
+def test_gpu_scripts_parse_and_name_existing_legs():
+    # tools/gpu/*.sh are what a round runs on the box (full validation,
+    # profiles, A/Bs): syntax-checked here, and the A/B driver's legs and the
+    # profile shapes must be ones bench.py / profile_round.sh accept
+    import glob
+    import subprocess
+    scripts = sorted(glob.glob(os.path.join(ROOT, "tools", "gpu", "*.sh")))
+    assert {os.path.basename(s) for s in scripts} >= {"ab.sh", "full.sh", "profiles.sh"}
+    for s in scripts + [os.path.join(ROOT, "tools", "profile_round.sh")]:
+        subprocess.run(["bash", "-n", s], check=True)
+    a = _parse(["--leg", "c5"])
+    assert a.leg == "c5" and _parse(["--leg", "wide"]).leg == "wide"
+    assert _parse(["--workload", "c4"]).workload == "c4"
+    text = open(os.path.join(ROOT, "tools", "profile_round.sh")).read()
+    for shape in ("c3)", "c4)", "c5)", "wide)"):
+        assert shape in text
