@@ -69,6 +69,15 @@ int cb_device_count(int* out);
 const char* cb_last_error(void);
 const char* cb_version(void);
 int cb_stream_synchronize(void* stream);
+/* The caller is done with `stream` (call before hipStreamDestroy, with no
+ * library call on it in flight): waits for the stream's queued work, frees
+ * the per-stream buffers the library keeps for it (keys staging, partition
+ * scratch, search outputs) and forgets it. Destroying handles never waits for
+ * the device: a filter, table or set's memory is retired behind an event on
+ * every stream the library has seen and reused once they have all passed
+ * them, so a stream destroyed without this call makes the next destroy fall
+ * back to a device-wide synchronise. Ends no work of the caller's. */
+int cb_stream_release(void* stream);
 /* Pinned (page-locked, device-mapped) host memory for key and hit buffers:
  * FilterSet probes whose keys AND hits live in it run zero-copy (see
  * cb_set_probe_fixed). For callers without the HIP runtime (the Rust shim,
@@ -120,13 +129,11 @@ int cb_probe_var(const cb_filter* const* filters, uint32_t nf, const uint8_t* by
  * Reentrant: concurrent callers may share a filter (`&self`). */
 int cb_may_contain(const cb_filter* f, const uint8_t* key, uint64_t len, int* out);
 /* Host mirror policy: 1 on, 0 off, -1 auto (the default: on when m <= 2^24,
- * i.e. up to 2 MiB of host words; past that a write records no event, and
- * the first refresh after the mirror is turned on synchronises the stream that
- * write was issued on, not the device). A caller that destroys that stream
- * before the filter's next refresh synchronises it first (a destroyed
- * stream's handle makes the refresh synchronise the whole device instead,
- * and a handle HIP has already reused for a new stream would not cover the
- * write). */
+ * i.e. up to 2 MiB of host words). Every write records an event on its
+ * stream (with the mirror off, one without the system-scope fence, which
+ * costs the stream nothing); the first refresh waits for the last write's
+ * event, never for a stream or the device, so the write's stream may be
+ * destroyed at any time. */
 int cb_filter_host_mirror(cb_filter* f, int mode);
 /* *on = whether cb_may_contain uses the mirror; *current = whether the mirror
  * already holds the latest write (either may be NULL). Host only. */

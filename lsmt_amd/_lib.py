@@ -82,6 +82,7 @@ def load():
         "cb_last_error": ([], ctypes.c_char_p),
         "cb_version": ([], ctypes.c_char_p),
         "cb_stream_synchronize": ([P], i32),
+        "cb_stream_release": ([P], i32),
         "cb_host_alloc": ([u64, ctypes.POINTER(P)], i32),
         "cb_host_free": ([P], i32),
         "cb_hits_compress": ([P, u64, u64, P, u64, P], i32),

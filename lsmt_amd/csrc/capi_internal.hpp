@@ -27,9 +27,13 @@
 
 // An event recorded after a device write to one or more filters (a batched
 // build shares one among all its filters: one hipEventRecord per call, not
-// per filter).
+// per filter). `fenced`: recorded with the system-scope release (the mirror
+// was on: its refresh copies right after the wait). A write made with the
+// mirror off records an unfenced one, which costs the stream nothing; the
+// rare refresh that meets it adds the release itself (capi.cpp wait_mark).
 struct WriteMark {
   hipEvent_t ev = nullptr;
+  bool fenced = true;
   ~WriteMark() {
     if (ev) (void)hipEventDestroy(ev);
   }
@@ -62,14 +66,12 @@ struct cb_filter {
   std::mutex host_mu;                 // one refresh at a time
   std::mutex zero_mu;                 // the lazy clear's issue vs. a refresh (capi.cpp ensure_zeroed)
   std::vector<uint32_t> host;         // ceil(m/32) words
-  std::shared_ptr<WriteMark> wmark;   // recorded after the last device write (atomic_load / atomic_store)
-  // a write went unrecorded (mirror off): the refresh synchronises the stream
-  // of the last such write (unmarked_stream; hipStreamSynchronize on it, not
-  // the whole device). Writes from several streams while unrecorded keep the
-  // last stream only when each write was ordered after the previous one (the
-  // reference's `&mut self` insert: exclusive, so ordered by the caller).
-  std::atomic<bool> unmarked{false};
-  std::atomic<hipStream_t> unmarked_stream{nullptr};
+  // recorded after the last device write (atomic_load / atomic_store), with
+  // the mirror on or off: the refresh waits for an event, never for a stream
+  // handle (which a destroyed stream's successor may reuse). Writes
+  // from several streams are ordered by their exclusive writer (the
+  // reference's `&mut self` insert), so the last mark covers them all.
+  std::shared_ptr<WriteMark> wmark;
   // -1 auto (m <= kMirrorAutoBits), 0 off, 1 on; read by concurrent `&self`
   // callers (cb_may_contain, probes) while cb_filter_host_mirror may write it
   std::atomic<int> mirror{-1};
@@ -91,6 +93,7 @@ struct cb_filterset {
   uint32_t width = 32;
   void* words = nullptr;  // device, m (rounded up to 32) words of width bits
   uint32_t* any = nullptr;  // device, ceil(m/32) words: bit p = (words[p] != 0)
+  size_t words_cap = 0, any_cap = 0;  // their pool blocks
   uint32_t used = 0;      // 1 + highest assigned slot
   std::vector<uint64_t> dirty;  // word j bit i: slot 64 j + i may hold set bits
   int mode = 0;
@@ -253,9 +256,11 @@ struct DevBuf {
   }
 };
 
-// Device block pool for table and filter storage (capi.cpp). *cap receives
-// the block's size (pass it back to pool_release); release synchronises the
-// device first, as hipFree would.
+// Device block pool for table, filter and set storage (capi.cpp). *cap
+// receives the block's size (pass it back to pool_release). Release is
+// stream-ordered: the block is retired behind an event on every stream the
+// library knows on that device and reused only once they have all completed;
+// the host never waits.
 hipError_t pool_alloc(int device, size_t bytes, void** p, size_t* cap);
 void pool_release(int device, void* p, size_t cap);
 
@@ -285,6 +290,13 @@ struct Workspace {
 constexpr size_t kHostScratch = 16 + sizeof(uint64_t) * cb::kDirPos * 4;  // Workspace::htot bytes
 
 Workspace& workspace(int device, hipStream_t s);
+// Registers s as a stream the library has enqueued on for `device` (its
+// workspace, created empty if need be): pool_release retires blocks behind
+// every registered stream. Every entry point that enqueues work touching a
+// pool block on the caller's stream goes through workspace() or this.
+void note_stream(int device, hipStream_t s);
+// Frees what a workspace holds (cb_stream_release, once its stream is idle).
+void workspace_free(Workspace& ws);
 
 // The stream's compress state, its counters allocated and zeroed on first
 // use (ws.mu held by the caller).
@@ -296,10 +308,6 @@ int compress_state(Workspace& ws, hipStream_t s, cb::CompressState** out);
 // claim words). Used by cb_set_probe_pack_fixed and the comm layer.
 int set_probe_device(const cb_filterset* set, const uint8_t* keys, uint32_t key_len, uint64_t n, bool gated,
                      uint64_t* hits, uint32_t* sink_pack, uint64_t cap, hipStream_t s);
-// Whether a probe of n keys with these settings takes the dense (region-
-// partitioned) FilterSet probe, which writes no exchange pack: the fused
-// probe + sparse exchange then compresses the rows in a separate pass.
-bool set_probe_dense(const cb_filterset* set, uint64_t n, bool gated);
 
 // A launch that reads set's device zone table was enqueued on s (capi.cpp).
 int note_zone_read(const cb_filterset* set, hipStream_t s);

@@ -531,9 +531,12 @@ int sstable_enqueue(const uint8_t* keys, const uint64_t* key_off, uint64_t kbyte
   // an error return past this point may leave work enqueued that reads the
   // staged block or writes the result slot: finish the stream before `pend`
   // hands them back (declared after pend, so it runs first)
+  // (armed only at the first enqueue: a refusal before it — bad offsets,
+  // bounds, a failed allocation — returns without blocking on the caller's
+  // stream)
   struct SyncOnError {
     hipStream_t s;
-    bool ok = false;
+    bool ok = true;
     ~SyncOnError() {
       if (!ok) (void)hipStreamSynchronize(s);
     }
@@ -568,6 +571,7 @@ int sstable_enqueue(const uint8_t* keys, const uint64_t* key_off, uint64_t kbyte
       p.staged = nullptr;
       return fail(CB_ENOMEM, "device allocation failed for a staged flush batch");
     }
+    on_error.ok = false;  // the staging copies are the first enqueued work
     uint8_t* at = (uint8_t*)p.staged;
     auto put = [&](const void* src, uint64_t bytes) -> uint8_t* {
       uint8_t* d = at;
@@ -607,6 +611,7 @@ int sstable_enqueue(const uint8_t* keys, const uint64_t* key_off, uint64_t kbyte
     return fail(CB_ENOMEM, "device allocation failed for an SSTable buffer");
   }
   if (!n) {  // an empty file: nothing to sort, index or bound
+    on_error.ok = false;
     HIP_TRY(hipMemsetAsync(t->data, 0, 16, s));
     if (bloom_out) {
       cb_filter* fp = nullptr;
@@ -629,6 +634,7 @@ int sstable_enqueue(const uint8_t* keys, const uint64_t* key_off, uint64_t kbyte
   if ((rc = result_slot(&slot))) return rc;
   p.hres = slot.h;
   p.ev = slot.ev;
+  on_error.ok = false;  // from here on every step enqueues
   Workspace& ws = workspace(device, s);
   std::unique_lock<std::mutex> lk(ws.mu);
   HIP_TRY(ws.f_flag.reserve(sizeof(cb::CreateResult), s));
@@ -788,6 +794,7 @@ int cb_table_create(const uint8_t* data, uint64_t len, int device, void* stream,
   if (rc) return rc;
   DeviceGuard dg(device);
   hipStream_t s = (hipStream_t)stream;
+  note_stream(device, s);
   std::unique_ptr<cb_table, int (*)(cb_table*)> t(new cb_table(), cb_table_destroy);
   t->device = device;
   t->len = len;

@@ -251,6 +251,23 @@ int new_comm(int rank, int world, int device, std::unique_ptr<cb_comm>* out) {
   return CB_OK;
 }
 
+// cb_set_probe_allgather_fixed's pack format: the fused probe's
+// per-probe-block pack, or the separate compress's. Every rank must choose
+// the same, since the two all-gather different byte counts in different
+// layouts (a choice read from the rank's own set, whose zone
+// state or width may differ, can split the ranks and hang the collective).
+// So the choice reads only what every rank of one call shares: max_rows
+// (from total_rows and world), n, the caller's gated flag and m (uniform over
+// a store's tables: every SSTable filter has the same m,
+// /root/reference/src/sstable.rs:44,59). A gated call always takes the fused
+// pack (the dense probe does not gate); an ungated dense-shaped batch takes
+// the separate compress, whichever kernel each rank's probe then runs (the
+// density test is priced at the width the shard would use).
+bool sparse_separate(uint64_t max_rows, uint64_t m, uint64_t n, bool gated) {
+  if (max_rows > 64) return true;
+  return !gated && cb::set_probe_dense_ok(max_rows <= 32 ? 32u : 64u, m, n);
+}
+
 int check_world(int rank, int world) {
   if (world < 1 || (uint32_t)world > cb::kMaxRanks || rank < 0 || rank >= world)
     return fail(CB_EINVAL, "need 0 <= rank < world <= 64");
@@ -444,12 +461,13 @@ int cb_set_probe_allgather_fixed(cb_comm* c, const cb_filterset* set, const uint
   }
   if (!cap) return fail(CB_EINVAL, "sparse exchange needs cap > 0");
   const uint64_t max_rows = (total_rows + (uint64_t)c->world - 1) / (uint64_t)c->world;
-  if (max_rows > 64 || set_probe_dense(set, n, gated != 0)) {
+  if (sparse_separate(max_rows, set->m, n, gated != 0)) {
     // shards past 64 tables (wide sets: the product's hundreds of m = 1024
     // tables over a few GPUs), and dense batches (C5: the region-partitioned
     // probe writes no pack): the probe writes the rows, then the separate
-    // compress and the same sparse all-gather (every rank takes this branch:
-    // max_rows, n and the sets' shape are the same everywhere)
+    // compress and the same sparse all-gather. The branch depends only on
+    // values every rank shares (sparse_separate); each rank's own probe
+    // still picks its kernel from its own set.
     int rc = set_probe_device(set, keys, key_len, n, gated != 0, local_hits, nullptr, 0, s);
     if (rc) return rc;
     return cb_hits_allgather(c, local_hits, rows, hwords, total_rows, full, CB_XCHG_SPARSE, cap, ok, sparse_used,

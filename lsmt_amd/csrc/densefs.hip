@@ -34,6 +34,7 @@
 // same bits, checked against the oracle (tests/test_dense_probe_gpu.py).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -84,6 +85,11 @@ constexpr uint32_t kProbeU = 4;              // entries per lane per round of th
 #else
 #define CB_DENSE_PART_WAVES 1
 #endif
+
+// Dynamic LDS of a partition block over R regions: the R + 1 counts (padded)
+// and a discard word, then the block's C staged entries.
+constexpr size_t dense_part_lds(uint32_t R) { return (size_t)(((R + 4) & ~3u) + 4) * 4 + (size_t)kDenseC * 8; }
+constexpr size_t dense_part_lds_max() { return dense_part_lds(kDenseMaxRegions); }
 
 // XCD-aware region order (workgroups are dealt round-robin over the 8 XCDs):
 // XCD x takes regions [x R/8, (x+1) R/8) in order.
@@ -252,13 +258,16 @@ __global__ __launch_bounds__(kDenseNT, 8) void k_dense_probe(const void* __restr
                                                              const uint16_t* __restrict__ seg, uint32_t segstride,
                                                              uint32_t nblk, const uint2* __restrict__ ent,
                                                              uint64_t k0, uint64_t* __restrict__ hits,
-                                                             uint64_t hwords, uint32_t xflags) {
+                                                             uint64_t hwords, uint32_t used, uint32_t xflags) {
   typedef typename std::conditional<W == 32, uint32_t, uint64_t>::type word_t;
   constexpr uint32_t NT = kDenseNT, C = kDenseC, P = kRegionBytes / sizeof(word_t);
   __shared__ __attribute__((aligned(16))) word_t stage[P];
   __shared__ uint32_t scan[kDenseMaxBlocks + 1];
   __shared__ uint16_t starts[kDenseMaxBlocks];
   const word_t* __restrict__ set = reinterpret_cast<const word_t*>(setp);
+  // rows exist for the used slots only (hits is used x hwords): slots past
+  // them are never written, whatever their set words hold
+  const word_t usedm = used >= W ? ~(word_t)0 : (((word_t)1 << used) - 1);
   const uint32_t tid = threadIdx.x;
   const uint32_t r = xcd_region(blockIdx.x, R);
   const uint64_t p0 = (uint64_t)r << rshift;
@@ -325,7 +334,7 @@ __global__ __launch_bounds__(kDenseNT, 8) void k_dense_probe(const void* __restr
       vb[u] = va[u] ? ((xflags & 1u) ? va[u] : set[e[u].x]) : (word_t)0;  // src/bloom.rs:50's &&
 #pragma unroll
     for (uint32_t u = 0; u < kProbeU; ++u) {
-      word_t mask = va[u] & vb[u];
+      word_t mask = va[u] & vb[u] & usedm;
       if (mask && !(xflags & 2u)) {
         const uint64_t key = k0 + (uint64_t)blk[u] * C + (e[u].y & 0xFFFFu);
         const unsigned long long bit = 1ull << (key & 63u);
@@ -344,6 +353,12 @@ template <int KK, int MM, int WW>
 void dense_part(uint32_t nblk, size_t lds, hipStream_t s, const KeySrc& ks, uint64_t k0, uint64_t kend,
                 const ModP& mp, uint32_t rshift, uint32_t R, uint16_t* seg, uint32_t stride, uint2* ent,
                 uint64_t* hits, uint64_t hwords, uint32_t used) {
+  // ~115 KiB of dynamic LDS at C5: past the 64 KiB a launch gets without
+  // asking, set once per instantiation
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_dense_part<KK, MM, WW>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)dense_part_lds_max());
+  (void)attr;
   hipLaunchKernelGGL((k_dense_part<KK, MM, WW>), dim3(nblk), dim3(kDenseNT), lds, s, ks, k0, kend, mp, rshift, R,
                      seg, stride, ent, hits, hwords, used);
 }
@@ -355,8 +370,30 @@ uint32_t dense_regions(uint32_t width, uint64_t m) {
   return (uint32_t)((m + P - 1) / P);
 }
 
+// The device's LDS per workgroup (queried once; the current device is the
+// set's, every caller holds a DeviceGuard): the partition block needs
+// dense_part_lds(R), the probe 64 KiB + its run tables.
+static size_t device_lds_limit() {
+  static thread_local int dev = -1;
+  static thread_local size_t lim = 0;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return 0;
+  if (d != dev) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, d) != hipSuccess) v = 0;
+    dev = d;
+    lim = (size_t)v;
+  }
+  return lim;
+}
+
 bool set_dense_shape_ok(uint32_t width, uint64_t m) {
-  return (width == 32 || width == 64) && m && m <= (1ull << 32) && dense_regions(width, m) <= kDenseMaxRegions;
+  if (!((width == 32 || width == 64) && m && m <= (1ull << 32) && dense_regions(width, m) <= kDenseMaxRegions))
+    return false;
+  // a device with less LDS than the passes need takes k_set_probe instead
+  const size_t probe_lds = kRegionBytes + (kDenseMaxBlocks + 1) * 4 + kDenseMaxBlocks * 2;
+  const size_t need = std::max(dense_part_lds(dense_regions(width, m)), probe_lds);
+  return device_lds_limit() >= need;
 }
 
 bool set_probe_dense_ok(uint32_t width, uint64_t m, uint64_t n) {
@@ -391,7 +428,7 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
   uint2* ent = reinterpret_cast<uint2*>(scratch);
   uint16_t* seg = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(scratch) + (uint64_t)nblk0 * kDenseC * 8);
   uint16_t* segT = seg + (uint64_t)nblk0 * stride;
-  const size_t lds1 = (size_t)(((R + 4) & ~3u) + 4) * 4 + (size_t)kDenseC * 8;
+  const size_t lds1 = dense_part_lds(R);
   uint32_t xflags = 0;
 #ifdef CB_EXPERIMENTS
   // timing-only A/B (the hits are wrong): CB_DENSE_X bit 0 skips the set[b]
@@ -422,10 +459,10 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
       ProfScope ps("k_dense_probe", s);
       if (width == 32)
         hipLaunchKernelGGL((k_dense_probe<32>), dim3(R), dim3(kDenseNT), 0, s, set, mp.m, rshift, R, segT, tstride,
-                           nblk, ent, k0, hits, hwords, xflags);
+                           nblk, ent, k0, hits, hwords, used, xflags);
       else
         hipLaunchKernelGGL((k_dense_probe<64>), dim3(R), dim3(kDenseNT), 0, s, set, mp.m, rshift, R, segT, tstride,
-                           nblk, ent, k0, hits, hwords, xflags);
+                           nblk, ent, k0, hits, hwords, used, xflags);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }

@@ -237,6 +237,75 @@ def test_loopback_probe_allgather(gpu, world, nf, mode):
             c.close()
 
 
+@pytest.mark.parametrize("world,nf", [(2, 5), (3, 7)])
+@pytest.mark.parametrize("gated", [0, 1])
+def test_loopback_probe_allgather_uneven_sets(gpu, world, nf, gated):
+    """The ranks' sets differ in what the caller cannot see: rank 0's slots
+    carry zone bounds and the others' do not, and the last rank's set is 64
+    wide instead of 32, on a batch dense enough for the region-partitioned
+    probe (N = 30001 against m = 2^17). Every rank must still take the same
+    pack format (comm.cpp sparse_separate reads only shared values; ADVICE
+    r5: a choice read from the rank's own zone state split the ranks into
+    different all-gather sizes and hung them). The map: rank 0's rows gated
+    by its zones, the others' plain."""
+    import torch
+
+    import lsmt_amd
+    from lsmt_amd.shard import Comm
+    from oracle import oracle
+    gf, plain, look = _filters(nf)
+    keys = torch.from_numpy(look).cuda()
+    words = (N + 63) // 64
+    expect = plain.copy()
+    lo0, hi0 = shard_range(nf, world, 0)
+    zones = []
+    for f in range(lo0, hi0):
+        srt = workload.sort_keys16(workload.key_range(500 + f, KPF))
+        zones.append((bytes(srt[KPF // 4]), bytes(srt[3 * KPF // 4])))
+    if gated:
+        of = []
+        for f in range(lo0, hi0):
+            o = oracle.OracleFilter(M)
+            o.insert_fixed(workload.key_range(500 + f, KPF))
+            of.append(o)
+        d = np.ascontiguousarray(look.reshape(-1))
+        offs = np.arange(0, 16 * (N + 1), 16, dtype=np.uint64)
+        expect[lo0:hi0] = oracle.probe_gated(of, [oracle.OracleZone(a, b) for a, b in zones], d, offs)
+    comms = Comm.loopback(world, 0)
+    sets = []
+    for r in range(world):
+        lo, hi = shard_range(nf, world, r)
+        s = lsmt_amd.FilterSet(M, 64 if r == world - 1 else 32)
+        s.assign_all(gf[lo:hi])
+        if r == 0:
+            for i, z in enumerate(zones):
+                s.set_zone(i, z)
+        sets.append(s)
+    torch.cuda.synchronize()
+    cap = sparse_cap(N, nf, world)
+    streams = [torch.cuda.Stream() for _ in range(world)]
+    fulls = [torch.full((nf, words), -1, dtype=torch.int64, device="cuda") for _ in range(world)]
+    locs = [torch.full((shard_range(nf, world, r)[1] - shard_range(nf, world, r)[0], words), -1,
+                       dtype=torch.int64, device="cuda") for r in range(world)]
+
+    def rank(r):
+        used = comms[r].probe_allgather(sets[r], keys, nf, locs[r], fulls[r], sparse=True, cap=cap,
+                                        gated=bool(gated), stream=streams[r])
+        streams[r].synchronize()
+        return used
+
+    try:
+        used = _run_ranks(world, rank)
+        assert all(used), used
+        for r in range(world):
+            lo, hi = shard_range(nf, world, r)
+            assert np.array_equal(locs[r].cpu().numpy().view(np.uint64), expect[lo:hi]), f"rank {r} rows"
+            assert np.array_equal(fulls[r].cpu().numpy().view(np.uint64), expect), f"rank {r} map"
+    finally:
+        for c in comms:
+            c.close()
+
+
 def test_loopback_pipelined_lanes(gpu):
     """Three lanes per rank (streams) sharing one communicator, several
     batches in flight: each lane keeps its own packs and the collectives run
