@@ -85,10 +85,19 @@ def parse():
     p.add_argument("--set-dense", choices=["auto", "on", "off"], default="auto",
                    help="FilterSet probes of dense batches (cb_set_dense): auto = the region-partitioned "
                         "probe when a batch holds >= 2 keys per 128-B set line (C5), on / off = always / never")
-    p.add_argument("--leg", choices=["c5", "wide"], default=None,
-                   help="run only that secondary leg (the C5 rank slice, or the wide fan-out) and print one "
+    p.add_argument("--leg", choices=["c2", "c5", "wide"], default=None,
+                   help="run only that secondary leg (the C2 build, the C5 rank slice, or the wide fan-out) and print one "
                         "line holding it: the rocprofv3 passes of tools/profile_round.sh, so the trace and the "
                         "counters hold that leg's kernels alone")
+    p.add_argument("--full-line", default=None, metavar="PATH",
+                   help="also write the full (uncompacted) JSON line, with every leg's prose fields, to PATH; stdout "
+                        "carries the compact line (compact_line: <= 8 KB, the legs the driver's tail must show last)")
+    p.add_argument("--phase-deadline", type=float, default=120.0,
+                   help="per-rank watchdog: seconds a guarded phase (rendezvous, RCCL init, each timed region and "
+                        "its warm-up, each check's collective) may take before the rank aborts its communicator, "
+                        "prints one JSON diagnostic line to stderr and exits 4")
+    p.add_argument("--job-deadline", type=float, default=1200.0,
+                   help="`--gpus N` parent: seconds the N ranks may take in all before it kills them and exits 5")
     p.add_argument("--dry-run", action="store_true",
                    help="launch / join the ranks over gloo and report them; no GPU work")
     p.add_argument("--rehearse-one-gpu", action="store_true",
@@ -107,8 +116,17 @@ def launch_ranks(args) -> int:
     running this same command line, relay rank 0's JSON line to stdout, and
     return the launcher's exit status (non-zero when any rank failed). The
     parent never imports torch or touches HIP: each rank initialises its own
-    GPU."""
+    GPU.
+
+    Failure bound: a rank whose guarded phase outlives
+    --phase-deadline aborts its communicator and exits 4 (Watchdog), and
+    torch.distributed.run then ends the other ranks and fails; as a backstop,
+    when the whole job outlives --job-deadline the parent kills the launcher's
+    process group (every rank) and exits 5, printing one JSON diagnostic line
+    to stderr."""
+    import signal
     import socket
+    import threading
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -118,14 +136,37 @@ def launch_ranks(args) -> int:
     env = dict(os.environ, CB_BENCH_LAUNCHER="bench.py")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL over dmabuf IPC on this host driver
     log(f"[launcher] {args.gpus} ranks: {' '.join(cmd)}")
-    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    t0 = time.monotonic()
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, start_new_session=True)
     out = []
-    for line in p.stdout:  # the ranks' stderr is inherited (progress stays visible)
-        if line.lstrip().startswith("{"):
-            out.append(line.strip())
-        elif line.strip():
-            log(line.rstrip())
-    rc = p.wait()
+
+    def relay():
+        for line in p.stdout:  # the ranks' stderr is inherited (progress stays visible)
+            if line.lstrip().startswith("{"):
+                out.append(line.strip())
+            elif line.strip():
+                log(line.rstrip())
+
+    reader = threading.Thread(target=relay, daemon=True)
+    reader.start()
+    try:
+        rc = p.wait(timeout=args.job_deadline)
+    except subprocess.TimeoutExpired:
+        log(json.dumps({"error": "job deadline", "seconds": round(time.monotonic() - t0, 1),
+                        "job_deadline": args.job_deadline, "n_ranks": args.gpus,
+                        "action": "killed the launcher's process group (every rank)"}))
+        for sig, wait in ((signal.SIGTERM, 10), (signal.SIGKILL, 10)):
+            try:
+                os.killpg(p.pid, sig)
+            except ProcessLookupError:
+                break
+            try:
+                p.wait(timeout=wait)
+                break
+            except subprocess.TimeoutExpired:
+                continue
+        return 5
+    reader.join(timeout=10)
     if rc == 0 and len(out) != 1:
         log(f"[launcher] error: expected one JSON line from rank 0, got {len(out)}")
         return 1
@@ -136,16 +177,96 @@ def launch_ranks(args) -> int:
     return rc
 
 
+class Watchdog:
+    """A rank's failure bound (Next 3): the first N > 1 RCCL run
+    must not spend the driver's whole timeout on a hang at init or in a
+    collective. Guarded phases (`with guard("name"):`) each get
+    --phase-deadline seconds; a daemon thread checks the clock, and when a
+    phase outlives it the rank aborts its library communicator
+    (cb_comm_abort = ncclCommAbort, which also ends a collective another
+    thread is blocked in), prints one JSON line {"error": "deadline", rank,
+    phase, seconds, rccl_world} to stderr and leaves with os._exit(4) (no
+    re-exec, no cleanup that could block on the device).
+    CB_BENCH_STALL="RANK:PHASE" makes that rank stall inside that phase (the
+    CPU test of the bound)."""
+
+    def __init__(self, rank: int, world: int, seconds: float):
+        import threading
+        self.rank, self.world, self.seconds = rank, world, seconds
+        self.comm = None
+        self._lock = threading.Lock()
+        self._phase, self._until, self._t0 = None, None, None
+        stall = os.environ.get("CB_BENCH_STALL", "")
+        self._stall = tuple(stall.split(":", 1)) if ":" in stall else None
+        threading.Thread(target=self._watch, daemon=True).start()
+
+    def guard(self, phase: str, seconds: float | None = None):
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            with self._lock:
+                outer = (self._phase, self._until, self._t0)
+                self._phase = phase
+                self._t0 = time.monotonic()
+                self._until = self._t0 + (seconds or self.seconds)
+            try:
+                if self._stall == (str(self.rank), phase):
+                    log(f"[rank {self.rank}] CB_BENCH_STALL: stalling in phase {phase}")
+                    while True:
+                        time.sleep(1)
+                yield
+            finally:
+                with self._lock:
+                    self._phase, self._until, self._t0 = outer
+        return cm()
+
+    def _watch(self):
+        while True:
+            time.sleep(0.25)
+            with self._lock:
+                late = self._until is not None and time.monotonic() > self._until
+                phase, t0 = self._phase, self._t0
+            if late:
+                self._fire(phase, time.monotonic() - t0)
+
+    def _fire(self, phase, took):
+        rc = None
+        cw = None
+        if self.comm is not None:
+            cw = getattr(self.comm, "world", None)
+            try:
+                rc = self.comm.abort()
+            except Exception as e:  # the diagnostic must still go out
+                rc = repr(e)
+        sys.stderr.write(json.dumps({"error": "deadline", "rank": self.rank, "world": self.world, "phase": phase,
+                                     "seconds": round(took, 1), "phase_deadline": self.seconds,
+                                     "rccl_world": cw, "comm_abort": rc}) + "\n")
+        sys.stderr.flush()
+        os._exit(4)
+
+
+_WD = None  # this rank's Watchdog
+
+
+def guard(phase: str, seconds: float | None = None):
+    """A guarded phase of this rank (Watchdog), or a no-op without one."""
+    import contextlib
+    return _WD.guard(phase, seconds) if _WD is not None else contextlib.nullcontext()
+
+
 def dry_run(args, world, rank, local, result) -> None:
     """Join the ranks over gloo and report each one's identity (no GPU)."""
     import torch.distributed as dist
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    with guard("rendezvous"):
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     me = {"rank": rank, "local_rank": local, "world_size": int(os.environ.get("WORLD_SIZE", "1")),
           "pid": os.getpid()}
     every = [None] * world
-    dist.all_gather_object(every, me)
+    with guard("dry_run"):
+        dist.all_gather_object(every, me)
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "gpus_arg": args.gpus,
                           "launcher": os.environ.get("CB_BENCH_LAUNCHER", "external"), "ranks": every}),
@@ -172,6 +293,9 @@ def main():
         log(f"error: --gpus {args.gpus} but WORLD_SIZE={world}: run `bench.py --gpus N` alone (it starts the N "
             "ranks) or under a launcher with --nproc-per-node N")
         sys.exit(2)
+    global _WD
+    if world > 1 or args.force_dist:
+        _WD = Watchdog(rank, world, args.phase_deadline)
     if args.dry_run:
         return dry_run(args, world, rank, local, result)
     import torch
@@ -196,7 +320,8 @@ def main():
         # group is gloo on every path (no second NCCL/RCCL communicator on the
         # device, no torch collective that could interleave with the library's
         # on a GPU stream). Every barrier follows a device synchronize.
-        dist.init_process_group("gloo")
+        with guard("rendezvous"):
+            dist.init_process_group("gloo")
     # host-side reductions (timing max, check flags) run on the CPU (gloo)
     red_dev = torch.device("cpu")
     log(f"[rank {rank}] local rank {local_rank} on cuda:{local} of world {world}")
@@ -298,11 +423,23 @@ def main():
             for r, part in enumerate(parts):
                 recv[r * nb:(r + 1) * nb] = part.numpy()
 
-        xcomm = Comm.host(rank, world, local, gloo_allgather)
+        with guard("comm_init"):
+            xcomm = Comm.host(rank, world, local, gloo_allgather)
     else:
-        xcomm = Comm.from_process_group(local) if use_dist else None
+        with guard("rccl_init"):
+            xcomm = Comm.from_process_group(local) if use_dist else None
+    if _WD is not None:
+        _WD.comm = xcomm
     if xcomm is not None and xcomm.world != world:
         raise RuntimeError(f"RCCL communicator has {xcomm.world} ranks, WORLD_SIZE is {world}")
+    # every rank's own view of its communicator's world (the line's
+    # rccl_world: one entry per rank, each the library's cb_comm_info)
+    rccl_world = None
+    if use_dist:
+        every = [None] * world
+        with guard("rccl_world"):
+            dist.all_gather_object(every, xcomm.world)
+        rccl_world = every
 
     def exchange(buf):
         """All-gather this step's hit rows from every rank (filter-major ->
@@ -344,6 +481,10 @@ def main():
     region = {}  # HIP events on the kernels' stream around the last timed region
 
     def timed(fn, k, lanes=None):
+        with guard("timed"):
+            return _timed(fn, k, lanes)
+
+    def _timed(fn, k, lanes=None):
         lanes = lane_streams if lanes is None else lanes
         torch.cuda.synchronize(dev)  # all streams: every exchange of the K steps is inside
         if use_dist:
@@ -378,8 +519,10 @@ def main():
     probes_per_step = n * nf_total
     legs = {}
     for name, fn in (("tiled", step_tiled), ("filterset", step_set)):
-        for _ in range(args.warmup):
-            fn()
+        with guard("warmup"):
+            for _ in range(args.warmup):
+                fn()
+            torch.cuda.synchronize(dev)
         el_leg = timed(fn, args.steps)
         legs[name] = {"el": el_leg, "value": probes_per_step / (el_leg / args.steps),
                       "ms_per_step": el_leg / args.steps * 1e3, "fn": fn,
@@ -408,81 +551,9 @@ def main():
         return out
 
     def cold_run(names, fn, reps=8, clean=False):
-        """SURVEY.md §8d timing protocol, cold leg: before every rep a 1 GiB
-        streaming device write evicts the L2s and the 256 MiB Infinity Cache,
-        then ONE step runs; medians over reps of the step (HIP events on the
-        kernels' stream) and of each kernel (cb_profile events). clean: a
-        512 MiB read follows the write, so the caches hold clean unrelated
-        lines and the step does not also pay the write-back of the flush's
-        dirty ones."""
-        flush = torch.empty(1 << 28, dtype=torch.int32, device=dev)
-        rd = torch.ones(1 << 27, dtype=torch.int32, device=dev) if clean else None
-        step_ms, kus = [], {nm: [] for nm in names}
-        for r in range(2 * reps):
-            torch.cuda.synchronize(dev)
-            if use_dist:
-                dist.barrier()
-            flush.fill_(r)
-            if clean:
-                rd.sum()
+        def reset():
             step_no[0] = 0  # the rep's step runs on lane 0 (= `stream`, where the events are)
-            if r >= reps:
-                torch.cuda.synchronize(dev)
-            if r < reps:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                # device-resident (SURVEY.md §8d): the cache-evicting write
-                # (~0.2 ms, on the same stream) is still running while the
-                # host issues the step, so the interval is the step's device
-                # time, not the host's issue latency. (Round 5 first gated
-                # with a 200 us spin kernel after a synchronize; the chip
-                # idles through a spin, and C2 one lane measured 0.5 us slower
-                # behind an 11.7 ms one: tools/c2_gate.py.)
-                e0.record(stream)
-                fn()
-                e1.record(stream)
-                torch.cuda.synchronize(dev)
-                step_ms.append(e0.elapsed_time(e1))
-            else:
-                for nm, v in kernel_ms(names, fn, 1).items():
-                    kus[nm].append(v["avg_us"])
-        del flush, rd
-        torch.cuda.synchronize(dev)
-        # the 1.5 GiB of eviction buffers go back to the device: left in
-        # torch's cache, later legs' tensors are carved from them, and the
-        # one-lane C2 build measured 16.5-16.6 us after the C3 cold leg
-        # against 15.4 with them released (cold 22.7 -> 21.3 us;
-        # experiment r05_c2cold, HISTORY.md)
-        torch.cuda.empty_cache()
-        return (float(np.median(step_ms)),
-                {nm: round(float(np.median(v)), 2) for nm, v in kus.items() if v})
-
-    def gated_steps(fn, k, st, w=600):
-        """K steps of fn queued behind W more steps of fn on st (the host
-        issues faster than the device runs them, so the device starts the K
-        timed steps only after the host has issued all of them): (device us
-        per step from HIP events around the K, host issue us per step, whether
-        the W steps outlasted the issue). The gate is real work rather than a
-        spin kernel: behind an ~11.7 ms one-wave spin the same C2 builds
-        measured 15.9-16.0 us, behind 600 builds 15.45-15.5 (the chip idles
-        through a spin; tools/c2_gate.py)."""
-        torch.cuda.synchronize(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        es = torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        es.record(st)
-        for _ in range(w):
-            fn()
-        e0.record(st)
-        t1 = time.perf_counter()
-        for _ in range(k):
-            fn()
-        t2 = time.perf_counter()
-        e1.record(st)
-        torch.cuda.synchronize(dev)
-        # the gate's steps must still have been running when the last timed
-        # step was issued
-        ok = (t2 - t0) * 1e3 < es.elapsed_time(e0)
-        return e0.elapsed_time(e1) * 1e3 / k, (t2 - t1) * 1e6 / k, bool(ok)
+        return _cold_steps(torch, dist, use_dist, dev, stream, L, names, fn, reset, reps, clean)
 
     probe_kernels = ["k_part_probe", "k_tile_probe", "k_masks_to_hits", "k_probe_direct",
                      "k_set_probe"]
@@ -850,73 +921,10 @@ def main():
             flush["oracle_file_bit_exact"] = bool(oracle.sstable_create(ents) == flush_file)
             del ents, flush_file
 
-    # ---- C2 build: 1M keys -> one fresh 16 MiB filter (zero-fill + batched insert)
-    # (a step builds one fresh filter; consecutive steps go to the pipeline
-    # lanes, each lane with its own filter, stream and workspace)
-    # (the build has its own lane count, --build-streams: independent flushes
-    # in flight, one HIP stream each; 4 measured 10.8 against 11.3 us per C2
-    # step for 3)
-    BP = args.build_streams
-    b_streams = _LANES[:BP] + [torch.cuda.Stream(device=dev) for _ in range(BP - len(_LANES))]
-    b_sh = [st.cuda_stream for st in b_streams]
-    bk = torch.from_numpy(workload.c2_build_keys(args.build_keys)).to(dev)
-    bfs = [lsmt_amd.BloomFilter(args.build_m_bits, device=local) for _ in range(BP)]
-    bkb = lsmt_amd.DeviceKeys(bk)
-
-    def build_step():
-        i = step_no[0] % BP  # (cold_run resets step_no: its reps run on lane 0 = `stream`)
-        step_no[0] += 1
-        bfs[i].clear(stream=b_sh[i])
-        bfs[i].insert_batch(bkb, stream=b_sh[i])
-
-    for _ in range(args.warmup):
-        build_step()
-    bel = timed(build_step, LK, lanes=b_streams)
-    b_region_us = region["ms"] * 1e3 / region["k"]
-    # the same build on ONE lane (one flush at a time, as a real flush runs):
-    # each step waits for the previous one on the stream
-    BP_saved, BP = BP, 1
-    timed(build_step, LK, lanes=b_streams[:1])
-    b_one_issued_us = region["ms"] * 1e3 / region["k"]
-    # ... and its device time: 64 steps queued behind 600 more, so the host's
-    # per-step issue (Python + the C call) is not in the interval
-    b_one_us, b_issue_us, b_gated_ok = gated_steps(build_step, 64, stream)
-    BP = BP_saved
-    bprof = kernel_ms(["k_build_part", "k_build_tile", "k_insert_direct"], build_step, LK)
-    bcold = None
-    if not args.no_cold:
-        bcold_ms, bcold_k = cold_run(["k_build_part", "k_build_tile", "k_insert_direct"], build_step)
-        bcold = {"value": round(args.build_keys * world / (bcold_ms * 1e-3), 1),
-                 "ms_per_step": round(bcold_ms, 4), "kernels_us": bcold_k}
-        bclean_ms, bclean_k = cold_run(["k_build_part", "k_build_tile", "k_insert_direct"], build_step, clean=True)
-        bcold["clean_caches"] = {"value": round(args.build_keys * world / (bclean_ms * 1e-3), 1),
-                                 "ms_per_step": round(bclean_ms, 4), "kernels_us": bclean_k}
-    if args.check:  # every lane's filter holds the C2 bits
-        from oracle import oracle
-        o = oracle.OracleFilter(args.build_m_bits)
-        o.insert_fixed(workload.c2_build_keys(args.build_keys))
-        assert all(np.array_equal(f.bools(), o.bools()) for f in bfs), "C2 build differs from the oracle"
-        del o
-    b_alg = 16 * args.build_keys + args.build_m_bits / 8
-    frac = lambda us: round(b_alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
-    build = {"metric": "build keys/s (C2: 1M 16-B keys -> one 16 MiB filter, m=2^27)",
-             "value": round(args.build_keys * world / (bel / LK), 1), "unit": "keys/s",
-             "ms_per_step": round(bel / LK * 1e3, 4), "steps": LK, "path": int(L.cb_last_path()),
-             "kernels": {k: round(v["avg_us"], 2) for k, v in bprof.items()},
-             "algorithmic_bytes": int(b_alg),
-             "step_effective_GBps": round(b_alg / (bel / LK) / 1e9, 1),
-             "pipeline_lanes": BP, "cold": bcold,
-             "region_us_per_step": round(b_region_us, 2), "frac": frac(b_region_us),
-             "one_lane": {"us_per_build": round(b_one_us, 2), "frac": frac(b_one_us),
-                          "note": "one build at a time on one stream, device time: HIP events around 64 builds "
-                                  "queued behind 600 more (the latency a flush's kernels take)",
-                          "queued_fully": b_gated_ok, "host_issue_us_per_build": round(b_issue_us, 2),
-                          "host_issued_us_per_build": round(b_one_issued_us, 2),
-                          "host_issued_note": "the same K builds issued live from Python: a build's device "
-                                              "time or the host's issue time, whichever is longer"}}
-    if bcold:
-        bcold["frac"] = frac(bcold["ms_per_step"] * 1e3)
-        bcold["clean_caches"]["frac"] = frac(bcold["clean_caches"]["ms_per_step"] * 1e3)
+    # ---- C2 build: 1M keys -> one fresh 16 MiB filter (zero-fill + batched
+    # insert): c2_leg, also run alone by `--leg c2` (tools/profile_round.sh c2)
+    build = c2_leg(args, torch, dist, dev, local, world, use_dist, red_dev, LK, args.warmup,
+                   _LANES[:args.build_streams], cold=not args.no_cold)
 
     # ---- PCIe-inclusive end-to-end probe (pinned host keys -> host hits)
     e2e = None
@@ -1019,7 +1027,8 @@ def main():
                 nlo, nhi = shard_range(nf_total, world, (rank + 1) % world)
                 good &= bool(np.array_equal(full[nlo:nhi], oracle_rows(nlo, nhi)))
             flag = torch.tensor([1 if good else 0], dtype=torch.int32, device=red_dev)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            with guard("check"):
+                dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             good = bool(flag.item())
         assert good, "bench hits differ from the oracle"
         if rank == 0:
@@ -1074,20 +1083,99 @@ def main():
             "zone_gate": zone, "read_path": read, "flush": flush, "may_contain": may_contain,
             "c4": c4, "c5": c5, "wide_fanout": wide,
         }
+        if rccl_world is not None:
+            line["rccl_world"] = rccl_world
         if x_fit is False:
             line["valid"] = False
         if rehearse:
             line["rehearsal"] = (f"{world} ranks on ONE GPU over the host transport (gloo): checks the N-rank "
                                  "flow, not a scaling measurement")
             line["valid"] = False
-        print(json.dumps(line), file=result, flush=True)
+        emit(line, result, args.full_line)
     if use_dist:
-        torch.cuda.synchronize(dev)
-        dist.barrier()
+        with guard("teardown"):
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+        if _WD is not None:
+            _WD.comm = None
         xcomm.close()
         dist.destroy_process_group()
     if x_fit is False:
         sys.exit(3)
+
+
+# ---- the result line -------------------------------------------------------
+# The driver keeps ~9 KB of a run's stdout, and round 5's 14.7 KB line lost
+# its first legs (build, e2e, cold) to it. Stdout therefore carries a compact
+# line: the prose fields (what each number means, its sources; DESIGN.md §6
+# "Bench line fields" keeps them) and per-kernel breakdowns of the secondary
+# legs go, floats are rounded, and the keys are ordered so that the legs the
+# driver's tail must show (build, e2e, cold, may_contain) come last. The full
+# line goes to --full-line PATH when asked.
+LINE_BUDGET = 8000
+PROSE = {"note", "kernels_us_source", "kernel_avg_source", "algorithmic_def", "traffic_note", "host_issued_note",
+         "protocol", "form", "oracle_sample", "launches_per_batch", "sink", "cpus", "slice", "source", "kernels",
+         "metric", "sample", "path", "tables", "all_cores", "forms", "cpu_model"}
+# per-leg keys dropped from the compact line (kept in the full line)
+DETAIL = {"flush": {"kernels_us", "file_bytes", "flushes", "pipeline_lanes"},
+          "read_path": {"files_bytes", "file_generation_s", "value_bytes", "pipeline_lanes"},
+          "may_contain": {"m_bits", "keys", "probe_keys", "hits", "mirror_calls", "gpu_calls", "sink"},
+          "zone_gate": {"gated_hits_last_step", "zone_build_keys_per_s", "bloom_pass_pairs", "gate_pass_pairs"},
+          "profile_check": {"traced_run_events_us", "plain_run_events_us", "ratio_to_traced_run_events"},
+          "c4": {"filters_total", "keys_per_filter", "m_bits", "warmup", "pipeline_lanes", "lanes_region_us_per_step"},
+          "c5": {"n_keys", "filters", "m_bits", "pipeline_lanes"},
+          "wide_fanout": {"set_width", "lookups", "table_build_s"},
+          "e2e": {"h2d_bytes", "d2h_bytes", "host_buffers"},
+          "random_read_roofline": {"reads_per_launch", "achieved_reads_per_s", "peak_reads_per_s"}}
+TAIL = ("build", "e2e", "cold", "may_contain")  # last in the line: what the driver's tail must hold
+CONTRACT = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline")
+
+
+def _compact(v, key=None, top=False, leg=None):
+    """v without its prose and detail fields (DETAIL applies at every depth
+    of its leg, and to dicts of its own name), floats rounded."""
+    if isinstance(v, dict):
+        out = {}
+        drop = DETAIL.get(key, set()) | DETAIL.get(leg, set())
+        for k, x in v.items():
+            if k in drop:
+                continue
+            if k in PROSE and isinstance(x, (str, list, dict)) and not top and not (
+                    key == "cpu_baseline" and k in ("sample", "cpu_model")):
+                continue
+            if k == "kernels_us" and isinstance(x, dict):  # {kernel: {avg_us, launches}} -> {kernel: avg_us}
+                x = {kk: (vv["avg_us"] if isinstance(vv, dict) else vv) for kk, vv in x.items()}
+            out[k] = _compact(x, k, leg=k if top else leg)
+        return out
+    if isinstance(v, list):
+        return [_compact(x, key, leg=leg) for x in v]
+    if isinstance(v, float):
+        return int(round(v)) if abs(v) >= 1000 else round(v, 4)
+    return v
+
+
+def compact_line(line: dict) -> dict:
+    """The stdout form of the result line (see LINE_BUDGET above)."""
+    c = _compact(line, top=True)
+    order = [k for k in CONTRACT if k in c] + [k for k in c if k not in CONTRACT and k not in TAIL] + \
+        [k for k in TAIL if k in c]
+    c = {k: c[k] for k in order}
+    # still over budget: the least-read secondary fields go first
+    for k in ("alt_kernels_us", "rotating_batches", "filterset", "alt_paths", "kernels_us"):
+        if len(json.dumps(c, separators=(",", ":"))) <= LINE_BUDGET:
+            break
+        c.pop(k, None)
+    return c
+
+
+def emit(line: dict, result, full_path=None) -> None:
+    """Print the compact line to the result stream; write the full one to
+    full_path when given."""
+    if full_path:
+        with open(full_path, "w") as fh:
+            fh.write(json.dumps(line) + "\n")
+    print(json.dumps(compact_line(line), separators=(",", ":")), file=result, flush=True)
 
 
 def _golden():
@@ -1104,6 +1192,11 @@ def _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes, fn, k):
     """K steps of fn between a barrier + device sync on both sides; HIP events
     on lanes[0] around them (every other lane joined into the end event).
     Returns (wall seconds, event ms), each the max over ranks."""
+    with guard("timed"):
+        return _timed_lanes_body(torch, dist, dev, use_dist, red_dev, lanes, fn, k)
+
+
+def _timed_lanes_body(torch, dist, dev, use_dist, red_dev, lanes, fn, k):
     torch.cuda.synchronize(dev)
     if use_dist:
         dist.barrier()
@@ -1131,7 +1224,8 @@ def _all_ranks_true(torch, dist, use_dist, red_dev, ok: bool) -> bool:
     if not use_dist:
         return ok
     flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=red_dev)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    with guard("check"):
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     return bool(flag.item())
 
 
@@ -1150,6 +1244,180 @@ def _kernel_us(L, torch, dev, names, fn, k):
         L.cb_profile_read(nm.encode(), ctypes.byref(tot), ctypes.byref(cnt))
         if cnt.value:
             out[nm] = {"avg_us": round(tot.value * 1e3 / cnt.value, 2), "launches": int(cnt.value)}
+    return out
+
+
+def _cold_steps(torch, dist, use_dist, dev, stream, L, names, fn, reset, reps=8, clean=False):
+    """SURVEY.md §8d timing protocol, cold leg: before every rep a 1 GiB
+    streaming device write evicts the L2s and the 256 MiB Infinity Cache,
+    then ONE step runs (reset() first, so it runs on `stream`, where the
+    events are); medians over reps of the step (HIP events on the kernels'
+    stream) and of each kernel (cb_profile events). clean: a 512 MiB read
+    follows the write, so the caches hold clean unrelated lines and the step
+    does not also pay the write-back of the flush's dirty ones."""
+    flush = torch.empty(1 << 28, dtype=torch.int32, device=dev)
+    rd = torch.ones(1 << 27, dtype=torch.int32, device=dev) if clean else None
+    step_ms, kus = [], {nm: [] for nm in names}
+    for r in range(2 * reps):
+        torch.cuda.synchronize(dev)
+        if use_dist:
+            with guard("cold"):
+                dist.barrier()
+        flush.fill_(r)
+        if clean:
+            rd.sum()
+        reset()
+        if r >= reps:
+            torch.cuda.synchronize(dev)
+        if r < reps:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            # device-resident (SURVEY.md §8d): the cache-evicting write (~0.2
+            # ms, on the same stream) is still running while the host issues
+            # the step, so the interval is the step's device time, not the
+            # host's issue latency. (Round 5 first gated with a 200 us spin
+            # kernel after a synchronize; the chip idles through a spin, and
+            # C2 one lane measured 0.5 us slower behind an 11.7 ms one:
+            # tools/c2_gate.py.)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            step_ms.append(e0.elapsed_time(e1))
+        else:
+            for nm, v in _kernel_us(L, torch, dev, names, fn, 1).items():
+                kus[nm].append(v["avg_us"])
+    del flush, rd
+    torch.cuda.synchronize(dev)
+    # the 1.5 GiB of eviction buffers go back to the device: left in torch's
+    # cache, later legs' tensors are carved from them, and the one-lane C2
+    # build measured 16.5-16.6 us after the C3 cold leg against 15.4 with them
+    # released (cold 22.7 -> 21.3 us; experiment r05_c2cold, HISTORY.md)
+    torch.cuda.empty_cache()
+    return (float(np.median(step_ms)),
+            {nm: round(float(np.median(v)), 2) for nm, v in kus.items() if v})
+
+
+def _gated_steps(torch, dev, fn, k, st, w=600):
+    """K steps of fn queued behind W more steps of fn on st (the host issues
+    faster than the device runs them, so the device starts the K timed steps
+    only after the host has issued all of them): (device us per step from HIP
+    events around the K, host issue us per step, whether the W steps outlasted
+    the issue). The gate is real work rather than a spin kernel: behind an
+    ~11.7 ms one-wave spin the same C2 builds measured 15.9-16.0 us, behind 600
+    builds 15.45-15.5 (the chip idles through a spin; tools/c2_gate.py)."""
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    es = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    es.record(st)
+    for _ in range(w):
+        fn()
+    e0.record(st)
+    t1 = time.perf_counter()
+    for _ in range(k):
+        fn()
+    t2 = time.perf_counter()
+    e1.record(st)
+    torch.cuda.synchronize(dev)
+    # the gate's steps must still have been running when the last timed step
+    # was issued
+    ok = (t2 - t0) * 1e3 < es.elapsed_time(e0)
+    return e0.elapsed_time(e1) * 1e3 / k, (t2 - t1) * 1e6 / k, bool(ok)
+
+
+def c2_leg(args, torch, dist, dev, local, world, use_dist, red_dev, steps, warmup, lanes, cold=True):
+    """BASELINE C2: one fresh 16 MiB filter (m = 2^27) built from 1M 16-B keys
+    per step (clear + cb_filter_insert_fixed: SsTable::create's insert loop,
+    /root/reference/src/sstable.rs:62-65, over BloomFilter::insert,
+    src/bloom.rs:40-44). Consecutive steps go round-robin to len(lanes) lanes,
+    each with its own filter, stream and workspace (independent flushes in
+    flight); then the same build on one lane, as device time (64 builds
+    queued behind 600 more) and as issued live; cold reps after a 1 GiB
+    eviction. The roofline's traffic and profile check come from the C2 PMC
+    summary (tools/profile_round.sh c2, one build per launch pair)."""
+    import lsmt_amd
+    from lsmt_amd import _lib, workload
+    L = _lib.load()
+    BP = len(lanes)
+    b_sh = [st.cuda_stream for st in lanes]
+    bk = torch.from_numpy(workload.c2_build_keys(args.build_keys)).to(dev)
+    bfs = [lsmt_amd.BloomFilter(args.build_m_bits, device=local) for _ in range(BP)]
+    bkb = lsmt_amd.DeviceKeys(bk)
+    nstep = [0]
+    nl = [BP]
+
+    def build_step():
+        i = nstep[0] % nl[0]  # (the cold reps reset nstep: they run on lane 0, where the events are)
+        nstep[0] += 1
+        bfs[i].clear(stream=b_sh[i])
+        bfs[i].insert_batch(bkb, stream=b_sh[i])
+
+    warm_up(torch, dev, build_step, warmup)
+    el, ev_ms = _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes, build_step, steps)
+    region_us = ev_ms * 1e3 / steps
+    # the same build on ONE lane (one flush at a time, as a real flush runs):
+    # each step waits for the previous one on the stream
+    nstep[0], nl[0] = 0, 1
+    _, ev1_ms = _timed_lanes(torch, dist, dev, use_dist, red_dev, lanes[:1], build_step, steps)
+    issued_us = ev1_ms * 1e3 / steps
+    # ... and its device time: 64 steps queued behind 600 more, so the host's
+    # per-step issue (Python + the C call) is not in the interval
+    one_us, issue_us, gated_ok = _gated_steps(torch, dev, build_step, 64, lanes[0])
+    kn = ["k_build_part", "k_build_tile", "k_insert_direct"]
+    bprof = _kernel_us(L, torch, dev, kn, build_step, steps)  # one lane (nl = 1)
+    if cold:
+        def reset():
+            nstep[0] = 0
+        bcold_ms, bcold_k = _cold_steps(torch, dist, use_dist, dev, lanes[0], L, kn, build_step, reset)
+        bclean_ms, bclean_k = _cold_steps(torch, dist, use_dist, dev, lanes[0], L, kn, build_step, reset, clean=True)
+    nl[0] = BP
+    path = int(L.cb_last_path())
+    if args.check:  # every lane's filter holds the C2 bits
+        from oracle import oracle
+        o = oracle.OracleFilter(args.build_m_bits)
+        o.insert_fixed(workload.c2_build_keys(args.build_keys))
+        assert all(np.array_equal(f.bools(), o.bools()) for f in bfs), "C2 build differs from the oracle"
+        del o
+    del bfs, bk, bkb
+    torch.cuda.synchronize(dev)
+    b_alg = 16 * args.build_keys + args.build_m_bits / 8
+    frac = lambda us: round(b_alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+    kus = {k: round(v["avg_us"], 2) for k, v in bprof.items()}
+    out = {"metric": "build keys/s (C2: 1M 16-B keys -> one 16 MiB filter, m=2^27)",
+           "value": round(args.build_keys * world / (el / steps), 1), "unit": "keys/s",
+           "ms_per_step": round(el / steps * 1e3, 4), "steps": steps, "path": path, "pipeline_lanes": BP,
+           "region_us_per_step": round(region_us, 2),
+           "one_lane": {"us_per_build": round(one_us, 2), "frac": frac(one_us),
+                        "note": "one build at a time on one stream, device time: HIP events around 64 builds "
+                                "queued behind 600 more (the latency a flush's kernels take)",
+                        "queued_fully": gated_ok, "host_issue_us_per_build": round(issue_us, 2),
+                        "host_issued_us_per_build": round(issued_us, 2),
+                        "host_issued_note": "the same K builds issued live from Python: a build's device "
+                                            "time or the host's issue time, whichever is longer"},
+           "kernels_us": kus, "kernels_us_source": "library HIP events around each launch, one lane"}
+    roof = {"bound": "hbm", "achieved": round(b_alg / (region_us * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": frac(region_us), "frac_one_lane": frac(one_us),
+            "kernel": "k_build_part+k_build_tile", "kernel_avg_us": round(region_us, 2),
+            "kernel_avg_source": f"HIP events around the timed region / K ({BP} lanes); frac_one_lane: one build "
+                                 "alone, device time",
+            "algorithmic_bytes": int(b_alg),
+            "algorithmic_def": "16 B x 2^20 keys + 2^27/8 B (the filter written once) (SURVEY.md §8d C2 row)"}
+    # PMC bytes of one build (the C2 summary holds one filter per launch pair)
+    part, tile = _pmc_traffic("k_build_part", "c2"), _pmc_traffic("k_build_tile", "c2")
+    c2_shape = args.build_keys == 1 << 20 and args.build_m_bits == 1 << 27
+    roof["traffic"] = int(part + tile) if (part and tile and c2_shape and world == 1) else None
+    if roof["traffic"]:
+        roof["traffic_over_algorithmic"] = round(roof["traffic"] / b_alg, 3)
+        roof["traffic_source"] = _pmc_source("c2")
+    if c2_shape and world == 1:
+        roof["profile_check"] = _profile_check("c2", ["k_build_part", "k_build_tile"], b_alg, roof["frac_one_lane"])
+    out["roofline"] = roof
+    if cold:
+        out["cold"] = {"value": round(args.build_keys * world / (bcold_ms * 1e-3), 1),
+                       "ms_per_step": round(bcold_ms, 4), "kernels_us": bcold_k, "frac": frac(bcold_ms * 1e3),
+                       "clean_caches": {"value": round(args.build_keys * world / (bclean_ms * 1e-3), 1),
+                                        "ms_per_step": round(bclean_ms, 4), "kernels_us": bclean_k,
+                                        "frac": frac(bclean_ms * 1e3)}}
     return out
 
 
@@ -1440,14 +1708,19 @@ def run_c4(args, torch, dist, world, rank, local, dev, use_dist, result, red_dev
 
 
 def run_leg(args, torch, dist, world, rank, local, dev, use_dist, result, red_dev):
-    """`--leg c5|wide`: one secondary leg alone, its dict as the line's
-    "c5" / "wide_fanout" field (the profiling passes' workload; the default
-    line runs the same functions)."""
+    """`--leg c2|c5|wide`: one secondary leg alone, its dict as the line's
+    "build" / "c5" / "wide_fanout" field (the profiling passes' workload; the
+    default line runs the same functions)."""
     import lsmt_amd
     from lsmt_amd import _lib, workload
     L = _lib.load()
     lanes = [torch.cuda.current_stream(dev)]
-    if args.leg == "c5":
+    if args.leg == "c2":  # --build-streams lanes (1: the one-lane profile pass)
+        lanes = leg_lanes(torch, dev, args.build_streams)
+        out = c2_leg(args, torch, dist, dev, local, world, use_dist, red_dev, max(args.steps, args.leg_steps),
+                     args.warmup, lanes, cold=not args.no_cold)
+        key = "build"
+    elif args.leg == "c5":
         out = c5_leg(args, torch, dev, local, world, rank, args.steps, args.warmup, args.probe_streams,
                      True, red_dev, dist, use_dist)  # golden + oracle row always; the CPU baseline unless --no-cpu
         key = "c5"
@@ -1660,8 +1933,12 @@ def may_contain_latency():
     the host mirror (steady state and the first call after the build) against
     a one-key GPU probe per call; the two agree on every probe key."""
     exe = os.path.join(ROOT, "build", "tests", "may_contain_latency")
-    if not os.path.exists(exe):
-        return {"error": "build/tests/may_contain_latency not built"}
+    if not os.path.exists(exe):  # (a tree without the prebuilt tools: gcc over the header and the .so)
+        try:
+            subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], check=True,
+                           capture_output=True, timeout=120)
+        except Exception as e:  # reported in the line, never fatal to the headline
+            return {"error": f"building tests/cpp/may_contain_latency failed: {e!r}"[:300]}
     out = {"metric": "single-key may_contain latency, one host thread, C ABI (SsTable::get's per-table "
                      "bloom.may_contain, src/sstable.rs:138)"}
     for label, m, nk in (("m1024", 1024, 100), ("m2^26", 1 << 26, 1 << 19)):

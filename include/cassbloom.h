@@ -480,6 +480,13 @@ int cb_comm_init_loopback(int world, int device, cb_comm** ranks);
 int cb_comm_init_host(int rank, int world, int device, cb_host_allgather_fn fn, void* user,
                       cb_comm** out);
 int cb_comm_destroy(cb_comm* c);
+/* Ends the communicator on this rank (ncclCommAbort for RCCL; a loopback
+ * group wakes every rank): callable from any thread, also while another
+ * thread is blocked inside a collective of c, which then returns an error.
+ * Every later exchange on c fails with CB_EINVAL; cb_comm_destroy still
+ * frees the handle. For a rank's watchdog: a peer that never joins a
+ * collective would otherwise hold this rank forever. */
+int cb_comm_abort(cb_comm* c);
 int cb_comm_info(const cb_comm* c, int* rank, int* world, int* device);
 int cb_comm_shard(uint64_t total_rows, int world, int rank, uint64_t* first_row, uint64_t* rows);
 int cb_hits_allgather(cb_comm* c, const uint64_t* local, uint64_t rows, uint64_t words,

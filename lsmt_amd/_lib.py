@@ -93,6 +93,7 @@ def load():
         "cb_comm_init_loopback": ([i32, i32, P], i32),
         "cb_comm_init_host": ([i32, i32, i32, HOST_ALLGATHER_FN, P, pp], i32),
         "cb_comm_destroy": ([P], i32),
+        "cb_comm_abort": ([P], i32),
         "cb_comm_info": ([P, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
         "cb_comm_shard": ([u64, i32, i32, pu64, pu64], i32),
         "cb_hits_allgather": ([P, P, u64, u64, u64, P, i32, u64, P, ctypes.POINTER(i32), P], i32),

@@ -40,21 +40,30 @@ struct LoopGroup {
   std::condition_variable cv;
   int arrived = 0;
   uint64_t gen = 0;
+  bool aborted = false;  // cb_comm_abort on any rank: every waiter returns, every later call fails
   std::vector<const void*> send;
   std::vector<size_t> bytes;
   std::vector<hipEvent_t> ready, done;  // per rank: its send data written / its copies issued
   std::vector<int> err;                 // per rank: a step failed (every rank then fails the call)
 
-  void barrier() {
+  // false: the group was aborted (the rendezvous will not complete)
+  bool barrier() {
     std::unique_lock<std::mutex> lk(mu);
+    if (aborted) return false;
     const uint64_t g = gen;
     if (++arrived == world) {
       arrived = 0;
       ++gen;
       cv.notify_all();
     } else {
-      cv.wait(lk, [&] { return gen != g; });
+      cv.wait(lk, [&] { return gen != g || aborted; });
     }
+    return !aborted;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(mu);
+    aborted = true;
+    cv.notify_all();
   }
   ~LoopGroup() {
     for (hipEvent_t e : ready)
@@ -83,6 +92,9 @@ struct cb_comm {
   hipStream_t order_stream = nullptr;
   bool order_set = false;
   std::vector<uint32_t> counts;  // host: the gathered pack counts (sync overflow check)
+  // cb_comm_abort (any thread, even while another is inside a collective):
+  // RCCL's communicator is aborted and freed, every later call fails
+  std::atomic<bool> aborted{false};
 };
 
 namespace {
@@ -128,10 +140,10 @@ int loop_allgather(cb_comm* c, const void* send, void* recv, size_t bytes, hipSt
     g.bytes[me] = bytes;
     g.err[me] = e != hipSuccess;
   }
-  g.barrier();
+  if (!g.barrier()) return fail(CB_EINVAL, "loopback all-gather: the communicator was aborted");
   bool bad = false;
   for (int r = 0; r < g.world; ++r) bad |= g.err[r] || g.bytes[r] != bytes;
-  g.barrier();  // every rank has read err / bytes before anyone writes them again
+  if (!g.barrier()) return fail(CB_EINVAL, "loopback all-gather: the communicator was aborted");
   if (!bad) {
     for (int r = 0; r < g.world && e == hipSuccess; ++r) {
       e = hipStreamWaitEvent(s, g.ready[r], 0);
@@ -144,12 +156,12 @@ int loop_allgather(cb_comm* c, const void* send, void* recv, size_t bytes, hipSt
     std::lock_guard<std::mutex> lk(g.mu);
     g.err[me] = e != hipSuccess;
   }
-  g.barrier();
+  if (!g.barrier()) return fail(CB_EINVAL, "loopback all-gather: the communicator was aborted");
   for (int r = 0; r < g.world; ++r) bad |= g.err[r] != 0;
   if (!bad)
     for (int r = 0; r < g.world && e == hipSuccess; ++r)
       if (r != me) e = hipStreamWaitEvent(s, g.done[r], 0);
-  g.barrier();  // the events may be recorded again after this
+  if (!g.barrier()) return fail(CB_EINVAL, "loopback all-gather: the communicator was aborted");  // events reusable after
   if (e != hipSuccess) return hip_fail(e, "loopback all-gather");
   if (bad) return fail(CB_EINVAL, "loopback all-gather: a rank failed or the ranks' sizes differ");
   return CB_OK;
@@ -171,6 +183,7 @@ int host_allgather(cb_comm* c, const void* send, void* recv, size_t bytes, hipSt
 // The all-gather of `bytes` per rank from send into recv (world * bytes), on
 // stream s, after the communicator's previous collective (any stream).
 int allgather_bytes(cb_comm* c, const void* send, void* recv, size_t bytes, hipStream_t s) {
+  if (c->aborted.load()) return fail(CB_EINVAL, "the communicator was aborted (cb_comm_abort)");
   if (c->order_set && c->order_stream != s) HIP_TRY(hipStreamWaitEvent(s, c->order, 0));
   int rc = CB_OK;
   switch (c->transport) {
@@ -353,12 +366,26 @@ int cb_comm_init_host(int rank, int world, int device, cb_host_allgather_fn fn, 
   return CB_OK;
 }
 
+int cb_comm_abort(cb_comm* c) {
+  if (!c) return fail(CB_EINVAL, "null comm");
+  if (c->aborted.exchange(true)) return CB_OK;  // once
+  if (c->loop) c->loop->abort();
+  if (c->transport == kRccl && c->comm) {
+    DeviceGuard dg(c->device);
+    // ncclCommAbort may run while another thread is blocked in a collective
+    // of this communicator (its documented use): the collective returns an
+    // error, the kernels it queued end, and the communicator is freed
+    NCCL_TRY(ncclCommAbort(c->comm));
+  }
+  return CB_OK;
+}
+
 int cb_comm_destroy(cb_comm* c) {
   if (!c) return CB_OK;
   {
     DeviceGuard dg(c->device);
     (void)hipDeviceSynchronize();  // queued exchanges may still use the buffers
-    if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->comm && !c->aborted.load()) (void)ncclCommDestroy(c->comm);  // (an aborted one is already freed)
     for (auto& kv : c->bufs)
       for (DevBuf* b : {&kv.second.pack, &kv.second.packs, &kv.second.pad})
         if (b->p) (void)hipFree(b->p);

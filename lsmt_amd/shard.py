@@ -158,6 +158,14 @@ class Comm:
         dist.broadcast_object_list(obj, src=0, group=group)
         return cls(rank, world, device, obj[0])
 
+    def abort(self) -> int:
+        """cb_comm_abort: end the communicator from any thread (a watchdog),
+        also while another thread is blocked in one of its collectives.
+        Returns the C status (0 on success)."""
+        if getattr(self, "_h", None) is None or not self._h.value:
+            return 0
+        return int(self._L.cb_comm_abort(self._h))
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             self._L.cb_comm_destroy(self._h)

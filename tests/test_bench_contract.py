@@ -84,3 +84,47 @@ def test_gpu_scripts_parse_and_name_existing_legs():
     text = open(os.path.join(ROOT, "tools", "profile_round.sh")).read()
     for shape in ("c3)", "c4)", "c5)", "wide)"):
         assert shape in text
+
+
+def test_compact_line_fits_the_driver_tail():
+    """The stdout line stays under 8 KB with every leg present, ends with the
+    legs the driver's ~9 KB tail must show (build, e2e, cold, may_contain),
+    and keeps the contract keys and each leg's numbers (the 14.7
+    KB round-5 line lost build, e2e and cold to the tail). Input: round 5's
+    full default line (profiles/bench_r05k.json) with a round-6-sized build
+    roofline added."""
+    import json
+    with open(os.path.join(ROOT, "profiles", "bench_r05k.json")) as fh:
+        line = json.load(fh)
+    line["build"]["roofline"] = {"bound": "hbm", "achieved": 2171.3, "peak": 8000.0, "unit": "GB/s",
+                                 "frac": 0.4903, "frac_one_lane": 0.2714, "kernel": "k_build_part+k_build_tile",
+                                 "kernel_avg_us": 8.55, "kernel_avg_source": "x" * 200,
+                                 "algorithmic_bytes": 33554432, "algorithmic_def": "y" * 120,
+                                 "traffic": 41234567, "traffic_over_algorithmic": 1.229,
+                                 "traffic_source": "profiles/pmc_c2_r06.json",
+                                 "profile_check": {"source": "z" * 80, "kernels": ["k_build_part", "k_build_tile"],
+                                                   "step_us": 15.4, "frac": 0.2721,
+                                                   "ratio_to_line_frac_one_lane": 1.0026}}
+    c = bench.compact_line(line)
+    text = json.dumps(c, separators=(",", ":"))
+    assert len(text) <= bench.LINE_BUDGET, len(text)
+    keys = list(c)
+    assert keys[-4:] == ["build", "e2e", "cold", "may_contain"]
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in c, k
+    assert c["roofline"]["frac"] == line["roofline"]["frac"] and c["roofline"]["traffic"]
+    assert c["cpu_baseline"]["sample"] and c["cpu_baseline"]["kind"] == "port"
+    b = c["build"]
+    assert b["value"] and b["one_lane"]["us_per_build"] and b["roofline"]["frac"] and b["roofline"]["traffic"]
+    assert "error" not in json.dumps(c["may_contain"])
+    assert c["c5"]["golden_slice_bit_exact"] is True and c["c4"]["roofline"]["traffic"]
+    # numbers survive: every leg's value is the full line's, rounded
+    for leg in ("c4", "c5", "wide_fanout", "read_path"):
+        assert abs(c[leg]["value"] - line[leg]["value"]) < 1
+
+
+def test_c2_leg_and_profile_shape_exist():
+    assert _parse(["--leg", "c2"]).leg == "c2"
+    text = open(os.path.join(ROOT, "tools", "profile_round.sh")).read()
+    assert "c2)" in text and "--leg c2" in text and "--build-streams 1" in text

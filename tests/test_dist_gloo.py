@@ -90,3 +90,49 @@ def test_bench_rank_refuses_wrong_world():
                        capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
     assert not p.stdout.strip()
+
+
+def _bench_env():
+    return {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT", "CB_BENCH_STALL")}
+
+
+def test_stalled_rank_ends_the_job_within_the_bound():
+    """A rank that stalls inside a guarded phase (CB_BENCH_STALL="1:dry_run":
+    rank 1 never joins the all-gather, as a rank hung at RCCL init or in a
+    collective would) passes its --phase-deadline; so does rank 0, blocked
+    in the same all-gather: the first to fire prints one JSON diagnostic line
+    and exits 4, torch.distributed.run ends the other, and the `--gpus 2`
+    parent exits non-zero
+    well inside the bound, with no result line (Next 3)."""
+    import time
+    env = dict(_bench_env(), CB_BENCH_STALL="1:dry_run")
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--phase-deadline", "8", "--job-deadline", "200"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    took = time.monotonic() - t0
+    assert p.returncode != 0, p.stderr[-3000:]
+    assert not p.stdout.strip()
+    diag = [json.loads(ln) for ln in p.stderr.splitlines() if ln.startswith('{"error": "deadline"')]
+    # the stalled rank, or its peer blocked in the same all-gather: whichever
+    # watchdog fires first ends the job
+    assert diag and diag[0]["phase"] == "dry_run" and diag[0]["seconds"] >= 8, p.stderr[-3000:]
+    assert took < 120, took
+
+
+def test_job_deadline_kills_every_rank():
+    """The parent's backstop: with the ranks' own bound out of reach
+    (--phase-deadline 1000) a stalled rank holds the job until the parent's
+    --job-deadline, which kills the launcher's process group and exits 5
+    with a JSON diagnostic line."""
+    import time
+    env = dict(_bench_env(), CB_BENCH_STALL="0:dry_run")
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--phase-deadline", "1000", "--job-deadline", "25"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    took = time.monotonic() - t0
+    assert p.returncode == 5, (p.returncode, p.stderr[-3000:])
+    assert any(ln.startswith('{"error": "job deadline"') for ln in p.stderr.splitlines()), p.stderr[-3000:]
+    assert took < 90, took

@@ -10,9 +10,11 @@ if r:
           f"rr {r['random_read_roofline']['frac']}")
 b = d.get("build")
 if b:
-    print(f"build C2 {b['value'] / 1e9:.1f} G keys/s {b['ms_per_step'] * 1e3:.2f} us/step lanes {b['pipeline_lanes']} "
+    br = b.get("roofline") or {}
+    print(f"build C2 {b['value'] / 1e9:.1f} G keys/s {b['ms_per_step'] * 1e3:.2f} us/step lanes {b.get('pipeline_lanes')} "
           f"one-lane {b.get('one_lane', {}).get('us_per_build')} us cold {(b.get('cold') or {}).get('ms_per_step')} ms "
-          f"{b['kernels']}")
+          f"frac {br.get('frac')} one-lane {br.get('frac_one_lane')} traffic {br.get('traffic')} "
+          f"{b.get('kernels_us', b.get('kernels'))}")
 rp = d.get("read_path")
 if rp:
     print(f"read path {rp['value'] / 1e9:.2f} G gets/s")
@@ -20,7 +22,7 @@ f = d.get("flush")
 if f:
     for k in ("sorted_input", "unsorted_input", "unsorted_shared_prefix_input"):
         if k in f:
-            print(f"flush {k}: {f[k]['ms_per_flush']} ms  {f[k]['kernels_us']}")
+            print(f"flush {k}: {f[k]['ms_per_flush']} ms  {f[k].get('kernels_us', '')}")
 for k in ("c4", "c5"):
     leg = d.get(k)
     if leg:

@@ -116,6 +116,8 @@ def main():
             us = d["c5"].get("one_lane_us_per_step")
         elif shape == "wide" and d.get("wide_fanout"):
             us = d["wide_fanout"].get("kernels_us", {}).get("k_wide_get_many")
+        elif shape == "c2" and d.get("build"):
+            us = d["build"].get("one_lane", {}).get("us_per_build")
         elif shape == "c3" and d.get("roofline"):
             us = d["roofline"].get("kernel_avg_us_one_lane")
         if us:
