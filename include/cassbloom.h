@@ -129,11 +129,14 @@ int cb_probe_var(const cb_filter* const* filters, uint32_t nf, const uint8_t* by
  * Reentrant: concurrent callers may share a filter (`&self`). */
 int cb_may_contain(const cb_filter* f, const uint8_t* key, uint64_t len, int* out);
 /* Host mirror policy: 1 on, 0 off, -1 auto (the default: on when m <= 2^24,
- * i.e. up to 2 MiB of host words). Every write records an event on its
- * stream (with the mirror off, one without the system-scope fence, which
- * costs the stream nothing); the first refresh waits for the last write's
- * event, never for a stream or the device, so the write's stream may be
- * destroyed at any time. */
+ * i.e. up to 2 MiB of host words). With the mirror on every write records an
+ * event and the first refresh waits for it. A write made with the mirror off
+ * records nothing (it costs the write's stream no event); the first refresh
+ * after the mirror is turned on then waits, by events, for the work queued
+ * on every stream the library has seen on the device: never for a stored
+ * stream handle and never for the whole device, unless such a stream was
+ * destroyed without cb_stream_release (then its handle is invalid and the
+ * refresh synchronises the device). */
 int cb_filter_host_mirror(cb_filter* f, int mode);
 /* *on = whether cb_may_contain uses the mirror; *current = whether the mirror
  * already holds the latest write (either may be NULL). Host only. */

@@ -193,6 +193,41 @@ void pool_release(int device, void* p, size_t cap) {
   (void)hipFree(p);
 }
 
+int wait_known_streams(int device) {
+  std::vector<hipStream_t> streams;
+  {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (auto& kv : g_ws)
+      if (kv.first.first == device) streams.push_back((hipStream_t)kv.first.second);
+  }
+  bool device_sync = false;
+  std::vector<hipEvent_t> evs;
+  for (hipStream_t s : streams) {
+    hipEvent_t ev = nullptr;
+    // fenced (system-scope release): the host copies right after the wait
+    if (s == hipStreamPerThread || hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      device_sync = true;
+      break;
+    }
+    evs.push_back(ev);
+    if (hipEventRecord(ev, s) != hipSuccess) {  // a stream destroyed without cb_stream_release
+      (void)hipGetLastError();
+      device_sync = true;
+      break;
+    }
+  }
+  hipError_t e = hipSuccess;
+  if (device_sync) {
+    e = hipDeviceSynchronize();
+  } else {
+    for (hipEvent_t ev : evs)
+      if (e == hipSuccess) e = hipEventSynchronize(ev);
+  }
+  for (hipEvent_t ev : evs) (void)hipEventDestroy(ev);
+  if (e != hipSuccess) return hip_fail(e, "waiting for the library's streams");
+  return CB_OK;
+}
+
 Workspace& workspace(int device, hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_ws_mu);
   auto& slot = g_ws[{device, (void*)s}];
@@ -281,27 +316,30 @@ hipError_t ensure_pad_zeroed(const cb_filter* cf, hipStream_t s) {
   return hipSuccess;
 }
 
-// A new write mark: fenced (system-scope release at the record) when a
-// mirror refresh will copy right after waiting on it.
-hipError_t make_mark(bool fenced, std::shared_ptr<WriteMark>* out) {
+// A new write mark (recorded with the system-scope release: the mirror's
+// refresh copies right after waiting on it).
+hipError_t make_mark(std::shared_ptr<WriteMark>* out) {
   auto m = std::make_shared<WriteMark>();
-  m->fenced = fenced;
-  const hipError_t e = hipEventCreateWithFlags(
-      &m->ev, fenced ? hipEventDisableTiming : (hipEventDisableTiming | hipEventDisableSystemFence));
+  const hipError_t e = hipEventCreateWithFlags(&m->ev, hipEventDisableTiming);
   if (e != hipSuccess) return e;
   *out = std::move(m);
   return hipSuccess;
 }
 
 // Record f's write mark on s: its own mark again when no one else holds it
-// (no batch shares it, no mirror refresh is waiting on it) and it has the
-// fence the mirror's state asks for, else a new one. Recorded whether the
-// mirror is on or not (round 5 kept only the stream handle while it was off).
+// (no batch shares it, no mirror refresh is waiting on it), else a new one.
+// With the mirror off nothing is recorded (an event per write cost the C2
+// one-lane build 1 us of device time, round 6): the write is only flagged,
+// and the refresh that meets the flag waits for every stream the library
+// knows (wait_known_streams), never for a stored stream handle.
 hipError_t record_own_mark(cb_filter* f, hipStream_t s) {
-  const bool fenced = mirror_on(f);
+  if (!mirror_on(f)) {
+    f->unmarked.store(true, std::memory_order_release);
+    return hipSuccess;
+  }
   std::shared_ptr<WriteMark> m = std::atomic_load(&f->wmark);
-  if (!m || m.use_count() > 2 || m->fenced != fenced) {  // (2: f's reference and this copy)
-    const hipError_t e = make_mark(fenced, &m);
+  if (!m || m.use_count() > 2) {  // (2: f's reference and this copy)
+    const hipError_t e = make_mark(&m);
     if (e != hipSuccess) return e;
   }
   const hipError_t e = hipEventRecord(m->ev, s);
@@ -476,15 +514,21 @@ int mark_written_many(Workspace& ws, cb_filter* const* fs, uint32_t nf, hipStrea
   if (!nf) return CB_OK;
   bool any_on = false;
   for (uint32_t i = 0; i < nf; ++i) any_on |= mirror_on(fs[i]);
-  // one mark for the batch; fenced only when a mirror will copy after it
+  if (!any_on) {  // no mirror to order: flagged only (see record_own_mark)
+    for (uint32_t i = 0; i < nf; ++i) {
+      fs[i]->unmarked.store(true, std::memory_order_release);
+      fs[i]->gen.fetch_add(1, std::memory_order_acq_rel);
+    }
+    return CB_OK;
+  }
   std::shared_ptr<WriteMark> m;
   for (auto& c : ws.marks)
-    if (c.use_count() == 1 && c->fenced == any_on) {  // only the pool holds it: no filter, no waiting refresh
+    if (c.use_count() == 1) {  // only the pool holds it: no filter, no waiting refresh
       m = c;
       break;
     }
   if (!m) {
-    HIP_TRY(make_mark(any_on, &m));
+    HIP_TRY(make_mark(&m));
     ws.marks.push_back(m);
   }
   HIP_TRY(hipEventRecord(m->ev, s));
@@ -1406,32 +1450,11 @@ namespace {
 // the last write's event (on its own stream: no device-wide sync), then copy
 // the words back once. Readers race only on the flag (acquire/release).
 //
-// wait_mark: the host waits for a write mark. A fenced mark was recorded with
-// the system-scope release, so the copy after it sees the words. An unfenced
-// one (the write was made with the mirror off) gets that release here: a
-// private stream waits on it and records a fenced event, and the host waits
-// for that one. No stream of the caller's and no device-wide sync.
-int wait_mark(int device, const WriteMark& m) {
-  if (m.fenced) {
-    HIP_TRY(hipEventSynchronize(m.ev));
-    return CB_OK;
-  }
-  struct Fence {
-    hipStream_t s = nullptr;
-    hipEvent_t ev = nullptr;
-  };
-  static std::mutex mu;
-  static std::map<int, Fence> fences;
-  std::lock_guard<std::mutex> lk(mu);
-  Fence& fc = fences[device];
-  if (!fc.s) HIP_TRY(hipStreamCreateWithFlags(&fc.s, hipStreamNonBlocking));
-  if (!fc.ev) HIP_TRY(hipEventCreateWithFlags(&fc.ev, hipEventDisableTiming));
-  HIP_TRY(hipStreamWaitEvent(fc.s, m.ev, 0));
-  HIP_TRY(hipEventRecord(fc.ev, fc.s));
-  HIP_TRY(hipEventSynchronize(fc.ev));
-  return CB_OK;
-}
-
+// A write made while the mirror was off recorded nothing (record_own_mark):
+// the refresh that meets it waits for every stream the library has enqueued
+// on for the device (wait_known_streams), by events, so a destroyed stream's
+// handle never matters and streams the library never saw (the
+// caller's other work) are not waited for.
 int refresh_mirror(const cb_filter* cf) {
   cb_filter* f = const_cast<cb_filter*>(cf);
   const uint64_t g = f->gen.load(std::memory_order_acquire);
@@ -1450,11 +1473,12 @@ int refresh_mirror(const cb_filter* cf) {
       // the last write's mark (every write to one filter is ordered by its
       // exclusive writer, so it covers them all): an event, not a stream, so
       // a stream destroyed since, or its handle reused, changes nothing
-      const std::shared_ptr<WriteMark> m = std::atomic_load(&f->wmark);
-      if (m) {
-        int rc = wait_mark(f->device, *m);
+      if (f->unmarked.exchange(false, std::memory_order_acq_rel)) {
+        int rc = wait_known_streams(f->device);
         if (rc) return rc;
       }
+      const std::shared_ptr<WriteMark> m = std::atomic_load(&f->wmark);
+      if (m) HIP_TRY(hipEventSynchronize(m->ev));
       HIP_TRY(hipMemcpy(f->host.data(), f->words, nw * 4, hipMemcpyDeviceToHost));
     }
   }

@@ -24,6 +24,52 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _forget_streams(torch):
+    """cb_stream_release on every stream earlier tests may have handed to the
+    library (torch's pool streams, which rotate, and the null stream), so a
+    refresh waits only on the streams the test itself uses. HIP multiplexes
+    streams onto GPU_MAX_HW_QUEUES (4) hardware queues in creation order: an
+    event on any stream sharing the busy stream's queue completes only after
+    the busy kernel, so the busy stream must share a queue with no stream the
+    library knows (the tests create the writer's stream right before it)."""
+    from lsmt_amd import _lib
+    L = _lib.load()
+    for _ in range(64):
+        assert L.cb_stream_release(torch.cuda.Stream().cuda_stream) == 0
+    assert L.cb_stream_release(torch.cuda.current_stream().cuda_stream) == 0
+    assert L.cb_stream_release(None) == 0
+
+
+def _raw_stream():
+    import ctypes
+    raw = ctypes.c_void_p()
+    assert ctypes.CDLL("libamdhip64.so").hipStreamCreateWithFlags(ctypes.byref(raw), 1) == 0
+    return raw
+
+
+def _busy_stream(torch):
+    """A fresh HIP stream the library has never seen, running ~1 s of spin;
+    (stream, event recorded after the spin, raw handle)."""
+    raw = _raw_stream()
+    st = torch.cuda.ExternalStream(raw.value)
+    with torch.cuda.stream(st):
+        torch.cuda._sleep(2_000_000_000)
+        done = torch.cuda.Event()
+        done.record(st)
+    return st, done, raw
+
+
+def _release(raw):
+    import ctypes
+    ctypes.CDLL("libamdhip64.so").hipStreamDestroy(raw)
+
+
+def _lib_release(raw):
+    from lsmt_amd import _lib
+    assert _lib.load().cb_stream_release(raw) == 0
+    _release(raw)
+
+
 def oracle_hits(o, keys):
     h = oracle.probe_fixed([o], keys)
     return np.unpackbits(h.view(np.uint8), bitorder="little")[:len(keys)].astype(bool)
@@ -168,12 +214,12 @@ def test_mirror_turned_on_after_unrecorded_writes(gpu):
 
 
 def test_unrecorded_refresh_waits_for_its_stream_only(gpu):
-    """A write made while the mirror was off records an unfenced event; the
-    first refresh after the mirror comes on waits for that event (plus a
-    fence on the library's private stream), not for any other stream or the
-    whole device: a long kernel on another stream (a ~1 s spin) is still
-    running when the refresh has returned the oracle's answers (VERDICT r3:
-    the refresh used to call hipDeviceSynchronize)."""
+    """A write made while the mirror was off records nothing; the first
+    refresh after the mirror comes on waits, by events, for the streams the
+    library has enqueued on, not for the whole device: a long kernel on a
+    stream the library never saw (a ~1 s spin) is still running when the
+    refresh has returned the oracle's answers (the refresh used to
+    call hipDeviceSynchronize)."""
     import torch
     m = 1 << 26
     keys = workload.key_range(61, 100_000)
@@ -182,28 +228,30 @@ def test_unrecorded_refresh_waits_for_its_stream_only(gpu):
     o.insert_fixed(keys)
     b = gpu.BloomFilter(m)
     b.host_mirror(0)
-    wr, busy = torch.cuda.Stream(), torch.cuda.Stream()
-    b.insert_batch(gpu.DeviceKeys(torch.from_numpy(keys).cuda()), stream=wr)  # unrecorded
-    with torch.cuda.stream(busy):
-        torch.cuda._sleep(2_000_000_000)  # ~1 s of spinning on the other stream
-        done = torch.cuda.Event()
-        done.record(busy)
+    _forget_streams(torch)
+    wr = _raw_stream()  # (created right before the busy stream: the next hardware queue)
+    dkeys = torch.from_numpy(keys).cuda()
+    torch.cuda.synchronize()
+    b.insert_batch(gpu.DeviceKeys(dkeys), stream=wr.value)  # unrecorded
+    busy, done, raw = _busy_stream(torch)
     b.host_mirror(1)
     got = np.array([b.may_contain(bytes(k)) for k in probe])
     still_busy = not done.query()
     busy.synchronize()
+    _release(raw)
+    _lib_release(wr)
     assert np.array_equal(got, oracle_hits(o, probe))
     assert still_busy, "the mirror refresh waited for an unrelated stream"
 
 
 def test_unrecorded_write_on_a_destroyed_stream(gpu):
     """A write made while the mirror was off, on a stream the caller then
-    releases (cb_stream_release) and destroys: the refresh waits for the
-    write's event, which outlives its stream, so the mirror holds the write
-    with no stream handle and no device-wide sync in the path (VERDICT r5:
-    the refresh used to synchronise a stored raw stream handle, falling back
-    to the whole device for a dead one): a ~1 s kernel on another stream is
-    still running when the answers are back."""
+    releases (cb_stream_release: it synchronises that stream and forgets it)
+    and destroys: the refresh keeps no stream handle (it used to
+    synchronise a stored raw handle, falling back to the whole device for a
+    dead one) and waits only on the streams the library still knows, so the
+    mirror holds the write with no device-wide sync in the path: a ~1 s
+    kernel on another stream is still running when the answers are back."""
     import ctypes
 
     import torch
@@ -216,20 +264,17 @@ def test_unrecorded_write_on_a_destroyed_stream(gpu):
     b = gpu.BloomFilter(m)
     b.host_mirror(0)
     hip = ctypes.CDLL("libamdhip64.so")
-    st = ctypes.c_void_p()
-    assert hip.hipStreamCreateWithFlags(ctypes.byref(st), 1) == 0
+    _forget_streams(torch)
+    st = _raw_stream()
     b.insert_batch(keys, stream=st.value)  # on the raw stream, mirror off
     assert _lib.load().cb_stream_release(st) == 0
     assert hip.hipStreamDestroy(st) == 0
-    busy = torch.cuda.Stream()
-    with torch.cuda.stream(busy):
-        torch.cuda._sleep(2_000_000_000)  # ~1 s of spinning on another stream
-        done = torch.cuda.Event()
-        done.record(busy)
+    busy, done, raw = _busy_stream(torch)
     b.host_mirror(1)
     got = np.array([b.may_contain(bytes(k)) for k in probe])
     still_busy = not done.query()
     busy.synchronize()
+    _release(raw)
     assert np.array_equal(got, oracle_hits(o, probe))
     assert still_busy, "the mirror refresh waited for an unrelated stream"
 
