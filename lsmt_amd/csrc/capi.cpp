@@ -241,7 +241,7 @@ void note_stream(int device, hipStream_t s) { (void)workspace(device, s); }
 void workspace_free(Workspace& ws) {
   for (DevBuf* b : {&ws.keys, &ws.offsets, &ws.hits, &ws.seg, &ws.ent, &ws.masks, &ws.bools, &ws.lkey, &ws.zone,
                     &ws.t_views, &ws.t_rows, &ws.t_which, &ws.t_line, &ws.t_dlen, &ws.t_voff, &ws.t_scan,
-                    &ws.t_vals, &ws.t_groups, &ws.w_scr, &ws.i_cnt, &ws.i_base, &ws.i_tmp, &ws.i_end, &ws.i_err,
+                    &ws.t_vals, &ws.t_groups, &ws.t_maps, &ws.w_scr, &ws.i_cnt, &ws.i_base, &ws.i_tmp, &ws.i_end, &ws.i_err,
                     &ws.i_start, &ws.f_vb, &ws.f_vo, &ws.f_sk, &ws.f_sk2, &ws.f_sort, &ws.f_tsum, &ws.f_flag,
                     &ws.f_vsp, &ws.x_ctl, &ws.dense}) {
     if (b->p) (void)hipFree(b->p);

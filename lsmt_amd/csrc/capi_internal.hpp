@@ -271,6 +271,8 @@ struct Workspace {
   std::vector<uint8_t> t_views_host;
   std::vector<uint32_t> t_rows_host;
   DevBuf t_groups;                          // a wide set's table groups (cb::WideGroup)
+  DevBuf t_maps;                            // the tables' DirMaps, contiguous (the wide walk stages them)
+  std::vector<uint64_t> t_maps_sig;         // what t_maps was gathered from (table uids and map pointers)
   DevBuf w_scr;                             // the wide walk's screen (sstable.hpp WideScreen)
   std::vector<uint64_t> w_scr_sig;          // what it was built from (table uids, slots, buckets)
   uint32_t w_scr_bits = 0, w_scr_hbits = 0;

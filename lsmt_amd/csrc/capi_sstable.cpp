@@ -300,10 +300,30 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
     const cb::WideZone wz = wide_zone_view(set);
     cb::WideScreen scr{nullptr, 0, 0, 0};
     if ((rc = wide_screen(ws, tables, views, rows, set->R, dviews, drows, s, &scr))) return rc;
+    // the tables' DirMaps in one contiguous array (gathered on the device
+    // when the table list changes: the walk stages a group's maps in the same
+    // pass as its views)
+    std::vector<uint64_t> msig;
+    msig.reserve(2 * (size_t)nt);
+    for (uint32_t i = 0; i < nt; ++i) {
+      msig.push_back(tables[i]->uid);
+      msig.push_back((uint64_t)(uintptr_t)views[i].dmap);
+    }
+    if (msig != ws.t_maps_sig) {
+      HIP_TRY(ws.t_maps.reserve((size_t)nt * sizeof(cb::DirMap), s));
+      HIP_TRY(cb::launch_gather_maps(dviews, nt, (cb::DirMap*)ws.t_maps.p, s));
+      ws.t_maps_sig.swap(msig);
+    }
+    const cb::DirMap* dmaps = (const cb::DirMap*)ws.t_maps.p;
+#ifdef CB_EXPERIMENTS
+    // the A/B: maps found through the views (the round-5 staging)
+    static const bool no_maps = getenv("CB_WIDE_MAPS") && getenv("CB_WIDE_MAPS")[0] == '0';
+    if (no_maps) dmaps = nullptr;
+#endif
     HIP_TRY(cb::launch_wide_get_many(sk.keyk, set->mode, set->R, (const uint64_t*)set->words, set->mp,
                                      set->zany ? &wz : nullptr, dviews, nt, (const cb::WideGroup*)ws.t_groups.p,
                                      need_slots ? drows : nullptr, sk.ks, n, dwhich, (uint64_t*)ws.t_line.p,
-                                     (uint64_t*)ws.t_dlen.p, tsum, s, scr.scr ? &scr : nullptr));
+                                     (uint64_t*)ws.t_dlen.p, tsum, s, scr.scr ? &scr : nullptr, dmaps));
     if (set->zany && (rc = note_zone_read(set, s))) return rc;
   } else if (set) {
     const cb::ZoneView zv = set_zone_view(set);

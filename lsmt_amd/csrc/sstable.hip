@@ -995,7 +995,7 @@ __global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __rest
                                                        const uint32_t* __restrict__ slots, KeySrc ks, uint64_t n,
                                                        int32_t* __restrict__ which, uint64_t* __restrict__ vsrc,
                                                        uint64_t* __restrict__ dlen, uint64_t* __restrict__ tsum,
-                                                       WideScreen ws) {
+                                                       WideScreen ws, const DirMap* __restrict__ maps) {
   const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
   const bool live = k < n;
   const Query q = make_query<KEYK>(ks, live ? k : 0);
@@ -1013,32 +1013,65 @@ __global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __rest
   // are staged in LDS once for the block (every search then reads its
   // table's view and map from LDS, not 56 + 320 B from global memory per
   // search), and the walk ends when no lane of the block is still looking.
+  // The maps come from the table list's contiguous copy (maps, round 6) in
+  // the same pass as the views, one barrier per group; without it each map
+  // is found through its view (a second pass after the views' barrier).
   __shared__ TableView stv[64];
   __shared__ DirMap sdm[64];
+  __shared__ WideGroup sg[kWideMax / 64];
+  const uint32_t ng = (nt + 63) / 64;
+  for (uint32_t i = threadIdx.x; i < ng; i += kNT) sg[i] = groups[i];
+  __syncthreads();
+  // A group's three row windows (rows a and b, the screen) are loaded
+  // together, and the next group's are in flight while this group's
+  // candidates are walked (round 6: they were three dependent round trips
+  // per group, row b read only after row a's window was seen non-zero). The
+  // reference's `&&` stays in the arithmetic: b's bits count only where a's
+  // window has bits (at m = 1024 a row window is non-zero for nearly every
+  // key, so the short-circuit saved no read there).
+  uint64_t wa = 0, wb = 0, wsc = ~0ull;
+  auto windows = [&](uint32_t g, uint64_t& a, uint64_t& b, uint64_t& c) {
+    const WideGroup gd = sg[g];
+    a = 0;
+    b = 0;
+    c = ~0ull;
+    if (gd.kind == 2) return;  // scattered slots: read bit by bit in the walk
+    a = wide_window(ra, R, gd.lo);
+    b = wide_window(rb, R, gd.lo);
+    if (rs) c = wide_window(rs, R, gd.lo);
+  };
+  if (live) windows(0, wa, wb, wsc);
   int32_t w = -1;
   uint64_t src = 0, d = 0;
   bool active = live;
-  const uint32_t ng = (nt + 63) / 64;
   for (uint32_t g = 0; g < ng; ++g) {
     if (!__syncthreads_or(active)) break;  // (also: the previous group's stage is consumed)
     const uint32_t t0 = 64 * g, gn = nt - t0 < 64 ? nt - t0 : 64;
-    {
+    if (maps) {
       const uint32_t* vs = reinterpret_cast<const uint32_t*>(tv + t0);
       uint32_t* vd = reinterpret_cast<uint32_t*>(stv);
       for (uint32_t i = threadIdx.x; i < gn * kViewDw; i += kNT) vd[i] = vs[i];
+      const uint4* ms = reinterpret_cast<const uint4*>(maps + t0);
+      uint4* md = reinterpret_cast<uint4*>(sdm);
+      for (uint32_t i = threadIdx.x; i < gn * kMapWords; i += kNT) md[i] = ms[i];
+      __syncthreads();
+    } else {
+      const uint32_t* vs = reinterpret_cast<const uint32_t*>(tv + t0);
+      uint32_t* vd = reinterpret_cast<uint32_t*>(stv);
+      for (uint32_t i = threadIdx.x; i < gn * kViewDw; i += kNT) vd[i] = vs[i];
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i < gn * kMapWords; i += kNT) {
+        const uint32_t t = i / kMapWords, j = i - t * kMapWords;
+        const DirMap* gm = stv[t].dmap;
+        if (gm) reinterpret_cast<uint4*>(sdm + t)[j] = reinterpret_cast<const uint4*>(gm)[j];
+      }
+      __syncthreads();
     }
-    __syncthreads();
-#if !(defined(CB_EXPERIMENTS) && defined(CB_WIDE_NO_SDM))
-    for (uint32_t i = threadIdx.x; i < gn * kMapWords; i += kNT) {
-      const uint32_t t = i / kMapWords, j = i - t * kMapWords;
-      const DirMap* gm = stv[t].dmap;
-      if (gm) reinterpret_cast<uint4*>(sdm + t)[j] = reinterpret_cast<const uint4*>(gm)[j];
-    }
-    __syncthreads();
-#endif
     if (!active) continue;
-    const WideGroup gd = groups[g];
+    const WideGroup gd = sg[g];
     const uint64_t gmask = gd.gn >= 64 ? ~0ull : ((1ull << gd.gn) - 1);
+    const uint64_t ca = wa, cb = wb, cs = wsc;
+    if (g + 1 < ng) windows(g + 1, wa, wb, wsc);  // in flight during this group's walk
     uint64_t cand = 0;
     if (gd.kind == 2) {  // scattered slots: one bit per table
       for (uint32_t i = 0; i < gd.gn; ++i) {
@@ -1046,9 +1079,9 @@ __global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __rest
         if ((ra[s >> 6] >> (s & 63)) & 1ull) cand |= ((rb[s >> 6] >> (s & 63)) & 1ull) << i;
       }
     } else {
-      const uint64_t wa = wide_window(ra, R, gd.lo) & gmask;
-      cand = wa ? (wa & wide_window(rb, R, gd.lo)) : 0ull;
-      if (cand && rs) cand &= wide_window(rs, R, gd.lo);  // the screen (slot order, like the rows)
+      const uint64_t a = ca & gmask;
+      cand = a ? (a & cb) : 0ull;  // src/bloom.rs:50's &&
+      cand &= cs;                  // the screen (slot order, like the rows; all ones without one)
       if (gd.kind == 1 && cand) cand = __builtin_bitreverse64(cand) >> (64 - gd.gn);  // bit gn-1-i -> i
     }
     if (gd.kind == 2 && cand && rs) {
@@ -1118,11 +1151,7 @@ __global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __rest
         }
         const TableView& v = stv[i];
         LineRec r;
-#if defined(CB_EXPERIMENTS) && defined(CB_WIDE_NO_SDM)
-        if (search(v, q, r, v.dmap) < 0) continue;  // Ok(None)
-#else
         if (search(v, q, r, &sdm[i]) < 0) continue;  // Ok(None)
-#endif
         if (r.vdl == kBadValue) continue;             // Err(..) is skipped by `if let Ok(Some(v))`
         w = (int32_t)(t0 + i);
         src = (uint64_t)(uintptr_t)(v.data + r.start + r.klen + 1);
@@ -1517,11 +1546,29 @@ hipError_t launch_wide_screen(const TableView* tv, const uint32_t* slots, uint32
   return hipGetLastError();
 }
 
+// The tables' DirMaps copied into one contiguous array (a table without a
+// directory: zeros), so the walk stages a group's maps with plain loads in
+// the same pass as its views (k_wide_get_many). One lane per 16 B.
+__global__ __launch_bounds__(kNT) void k_gather_maps(const TableView* __restrict__ tv, uint32_t nt,
+                                                     DirMap* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  if (i >= (uint64_t)nt * kMapWords) return;
+  const uint32_t t = (uint32_t)(i / kMapWords), j = (uint32_t)(i - (uint64_t)t * kMapWords);
+  const DirMap* g = tv[t].dmap;
+  reinterpret_cast<uint4*>(out + t)[j] = g ? reinterpret_cast<const uint4*>(g)[j] : make_uint4(0, 0, 0, 0);
+}
+
+hipError_t launch_gather_maps(const TableView* tv, uint32_t nt, DirMap* out, hipStream_t s) {
+  if (!nt) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_maps, dim3(blocks_for((uint64_t)nt * kMapWords, kNT)), dim3(kNT), 0, s, tv, nt, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_wide_get_many(int keyk, int mode, uint32_t R, const uint64_t* set, const ModP& mp,
                                 const WideZone* zones, const TableView* tv, uint32_t nt, const WideGroup* groups,
                                 const uint32_t* slots, const KeySrc& ks, uint64_t n, int32_t* which,
                                 uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum, hipStream_t s,
-                                const WideScreen* screen) {
+                                const WideScreen* screen, const DirMap* maps) {
   if (!n) return hipSuccess;
   if (!nt || nt > 64 * R || R > kWideMax / 64) return hipErrorInvalidValue;
   const WideZone z = zones ? *zones : WideZone{nullptr, nullptr, nullptr, nullptr, 0};
@@ -1530,7 +1577,7 @@ hipError_t launch_wide_get_many(int keyk, int mode, uint32_t R, const uint64_t* 
   ProfScope ps("k_wide_get_many", s);
 #define WG(KK, MM)                                                                                                 \
   hipLaunchKernelGGL((k_wide_get_many<KK, MM>), g, dim3(kNT), 0, s, set, R, mp, z, tv, nt, groups, slots, ks, n, \
-                     which, vsrc, dlen, tsum, sc)
+                     which, vsrc, dlen, tsum, sc, maps)
   switch (keyk * 3 + mode) {
     case 0: WG(KEY_FIXED16, MOD_POW2_32); break;
     case 1: WG(KEY_FIXED16, MOD_POW2_64); break;

@@ -454,7 +454,10 @@ hipError_t launch_wide_get_many(int keyk, int mode, uint32_t R, const uint64_t* 
                                 const WideZone* zones, const TableView* tv, uint32_t nt, const WideGroup* groups,
                                 const uint32_t* slots, const KeySrc& ks, uint64_t n, int32_t* which,
                                 uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum, hipStream_t s,
-                                const WideScreen* screen = nullptr);
+                                const WideScreen* screen = nullptr, const DirMap* maps = nullptr);
+// The tables' DirMaps (tv[i].dmap, zeros where none) into out[0..nt): the
+// contiguous copy the wide walk stages with its views (maps above).
+hipError_t launch_gather_maps(const TableView* tv, uint32_t nt, DirMap* out, hipStream_t s);
 hipError_t launch_get_many(int keyk, const TableView* tv, uint32_t nt, const uint64_t* hits,
                            const uint32_t* rows, uint64_t hwords, const KeySrc& ks, uint64_t n,
                            int32_t* which, uint64_t* vsrc, uint64_t* dlen, uint64_t* tsum,

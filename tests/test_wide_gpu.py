@@ -207,3 +207,25 @@ def test_wide_screen_mixed_buckets_and_rebuilt_tables(gpu):
     ow, ovoff, ovals = expect()
     assert np.array_equal(np.asarray(which), ow)
     assert np.array_equal(np.asarray(voff, dtype=np.uint64), ovoff) and vals == ovals
+
+
+@pytest.mark.parametrize("mapping", ["descending", "scattered"])
+def test_wide_get_many_348_tables(gpu, lsm300, mapping):
+    """Six groups of 64 with a partial last one: 348 tables (the 300 plus the
+    48 oldest listed again, behind them, so absent keys walk them twice) in a
+    384-slot set, checked against the oracle like the 300-table case."""
+    d = lsm300
+    ages = list(range(48)) + list(range(300))  # position = age order: the 48 re-listed ones are the oldest
+    nt = len(ages)
+    s = gpu.FilterSet(1024, width=384)
+    slot_of_pos = np.arange(nt) if mapping == "descending" else np.random.default_rng(9).permutation(384)[:nt]
+    for pos, age in enumerate(ages):
+        s.assign(int(slot_of_pos[pos]), d["blooms"][age])
+        s.set_zone(int(slot_of_pos[pos]), d["zones"][age])
+    newest_first = list(range(nt))[::-1]
+    tabs = [d["tables"][ages[p]] for p in newest_first]
+    slots = slot_of_pos[newest_first].astype(np.uint32)
+    which, voff, vals = gpu.get_many(tabs, d["look"], filterset=s, hit_rows=slots)
+    ow, ovoff, ovals = _oracle_expect(d, [ages[p] for p in newest_first])
+    assert np.array_equal(np.asarray(which), ow)
+    assert np.array_equal(np.asarray(voff, dtype=np.uint64), ovoff) and vals == ovals
