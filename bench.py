@@ -1115,7 +1115,7 @@ def main():
 LINE_BUDGET = 8000
 PROSE = {"note", "kernels_us_source", "kernel_avg_source", "algorithmic_def", "traffic_note", "host_issued_note",
          "protocol", "form", "oracle_sample", "launches_per_batch", "sink", "cpus", "slice", "source", "kernels",
-         "metric", "sample", "path", "tables", "all_cores", "forms", "cpu_model"}
+         "metric", "sample", "path", "tables", "forms", "cpu_model"}
 # per-leg keys dropped from the compact line (kept in the full line)
 DETAIL = {"flush": {"kernels_us", "file_bytes", "flushes", "pipeline_lanes"},
           "read_path": {"files_bytes", "file_generation_s", "value_bytes", "pipeline_lanes"},
