@@ -105,7 +105,7 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
                                                          uint32_t rshift, uint32_t R,
                                                          uint16_t* __restrict__ seg, uint32_t segstride,
                                                          uint2* __restrict__ ent, uint64_t* __restrict__ hits,
-                                                         uint64_t hwords, uint32_t used) {
+                                                         uint64_t hwords, uint32_t used, uint32_t direct) {
   constexpr uint32_t NT = kDenseNT, KPT = kDenseKPT, C = kDenseC;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t b = blockIdx.x;
@@ -189,14 +189,26 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
     for (uint32_t t = tid; t <= R; t += NT) row[t] = (uint16_t)hist[t];
   }
   __syncthreads();  // the run row is out: hist becomes the bins' cursors
+  uint2* out = ent + (uint64_t)b * C;
+  if (direct) {  // (experiment builds: each entry stored straight to its slot in the block's run list)
 #pragma unroll
-  for (uint32_t g = 0; g < NB; ++g)
+    for (uint32_t g = 0; g < NB; ++g)
 #pragma unroll
-    for (int j = 0; j < (int)KPT; ++j)
-      if (live[g][j]) {
-        const uint32_t at = atomicAdd(&hist[pa[g][j] >> rshift], 1u);
-        stage[at] = make_uint2(pb[g][j], ((pa[g][j] & pmask) << 16) | (g * CB + j * NT + tid));
-      }
+      for (int j = 0; j < (int)KPT; ++j)
+        if (live[g][j]) {
+          const uint32_t at = atomicAdd(&hist[pa[g][j] >> rshift], 1u);
+          out[at] = make_uint2(pb[g][j], ((pa[g][j] & pmask) << 16) | (g * CB + j * NT + tid));
+        }
+  } else {
+#pragma unroll
+    for (uint32_t g = 0; g < NB; ++g)
+#pragma unroll
+      for (int j = 0; j < (int)KPT; ++j)
+        if (live[g][j]) {
+          const uint32_t at = atomicAdd(&hist[pa[g][j] >> rshift], 1u);
+          stage[at] = make_uint2(pb[g][j], ((pa[g][j] & pmask) << 16) | (g * CB + j * NT + tid));
+        }
+  }
   // the block's hit words (keys kb .. kb + C, whole words) start at zero:
   // the probe only ORs the set bits in
   {
@@ -207,9 +219,9 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
       if (w0 + w < nw) hits[(uint64_t)f * hwords + w0 + w] = 0ull;
     }
   }
+  if (direct) return;
   __syncthreads();
   const uint32_t total = hist[R];
-  uint2* out = ent + (uint64_t)b * C;
   const uint32_t n2 = total / 2;
   for (uint32_t i = tid; i < n2; i += NT) reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(stage)[i];
   if (tid == 0 && (total & 1u)) out[total - 1] = stage[total - 1];
@@ -352,7 +364,7 @@ __global__ __launch_bounds__(kDenseNT, 8) void k_dense_probe(const void* __restr
 template <int KK, int MM, int WW>
 void dense_part(uint32_t nblk, size_t lds, hipStream_t s, const KeySrc& ks, uint64_t k0, uint64_t kend,
                 const ModP& mp, uint32_t rshift, uint32_t R, uint16_t* seg, uint32_t stride, uint2* ent,
-                uint64_t* hits, uint64_t hwords, uint32_t used) {
+                uint64_t* hits, uint64_t hwords, uint32_t used, uint32_t direct) {
   // ~115 KiB of dynamic LDS at C5: past the 64 KiB a launch gets without
   // asking, set once per instantiation
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_dense_part<KK, MM, WW>),
@@ -360,7 +372,7 @@ void dense_part(uint32_t nblk, size_t lds, hipStream_t s, const KeySrc& ks, uint
                                                      (int)dense_part_lds_max());
   (void)attr;
   hipLaunchKernelGGL((k_dense_part<KK, MM, WW>), dim3(nblk), dim3(kDenseNT), lds, s, ks, k0, kend, mp, rshift, R,
-                     seg, stride, ent, hits, hwords, used);
+                     seg, stride, ent, hits, hwords, used, direct);
 }
 
 }  // namespace
@@ -428,7 +440,13 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
   uint2* ent = reinterpret_cast<uint2*>(scratch);
   uint16_t* seg = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(scratch) + (uint64_t)nblk0 * kDenseC * 8);
   uint16_t* segT = seg + (uint64_t)nblk0 * stride;
-  const size_t lds1 = dense_part_lds(R);
+  uint32_t direct = 0;
+#ifdef CB_EXPERIMENTS
+  static const uint32_t env_direct = getenv("CB_DENSE_DIRECT_ENT") && getenv("CB_DENSE_DIRECT_ENT")[0] == '1';
+  direct = env_direct;
+#endif
+  // (direct: the partition's LDS is the histogram only)
+  const size_t lds1 = direct ? (size_t)(((R + 4) & ~3u) + 4) * 4 : dense_part_lds(R);
   uint32_t xflags = 0;
 #ifdef CB_EXPERIMENTS
   // timing-only A/B (the hits are wrong): CB_DENSE_X bit 0 skips the set[b]
@@ -444,7 +462,7 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
       // the keys of this chunk: k in [k0, k0 + nk), indices global
       CB_SET_DISPATCH(keyk, mode, width,
                       (dense_part<KK, MM, WW>(nblk, lds1, s, ks, k0, k0 + nk, mp, rshift, R, seg, stride, ent, hits,
-                                              hwords, used)));
+                                              hwords, used, direct)));
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
