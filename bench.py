@@ -260,7 +260,7 @@ def dry_run(args, world, rank, local, result) -> None:
     import torch.distributed as dist
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
-    with guard("rendezvous"):
+    with guard("rendezvous", 5 * args.phase_deadline):
         dist.init_process_group("gloo", rank=rank, world_size=world)
     me = {"rank": rank, "local_rank": local, "world_size": int(os.environ.get("WORLD_SIZE", "1")),
           "pid": os.getpid()}
@@ -320,7 +320,10 @@ def main():
         # group is gloo on every path (no second NCCL/RCCL communicator on the
         # device, no torch collective that could interleave with the library's
         # on a GPU stream). Every barrier follows a device synchronize.
-        with guard("rendezvous"):
+        # (the ranks reach the rendezvous at different times: the first
+        # `import torch` on a fresh box can take 1-2 minutes, so this phase
+        # gets five times the deadline)
+        with guard("rendezvous", 5 * args.phase_deadline):
             dist.init_process_group("gloo")
     # host-side reductions (timing max, check flags) run on the CPU (gloo)
     red_dev = torch.device("cpu")
@@ -426,7 +429,7 @@ def main():
         with guard("comm_init"):
             xcomm = Comm.host(rank, world, local, gloo_allgather)
     else:
-        with guard("rccl_init"):
+        with guard("rccl_init", 2 * args.phase_deadline):
             xcomm = Comm.from_process_group(local) if use_dist else None
     if _WD is not None:
         _WD.comm = xcomm
