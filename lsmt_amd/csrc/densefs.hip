@@ -251,6 +251,41 @@ __global__ __launch_bounds__(256) void k_dense_seg_t(const uint16_t* __restrict_
   }
 }
 
+// The same transpose in 64-block x 128-region tiles moved as u32 pairs (half
+// the load and store instructions of k_dense_seg_t's u16 ones): a wave loads
+// one block's 128 run starts (256 B) per instruction and stores two regions'
+// 64 blocks (2 x 128 B) per instruction. istride and ostride are even (rows
+// padded to 64 u16), so every pair is 4-B aligned; a pair past ostride is
+// never written (the next row's first entries).
+__global__ __launch_bounds__(256) void k_dense_seg_t2(const uint16_t* __restrict__ in, uint32_t istride,
+                                                       uint32_t nblk, uint32_t nrow, uint16_t* __restrict__ out,
+                                                       uint32_t ostride) {
+  __shared__ uint16_t tile[64][130];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t b0 = blockIdx.x * 64, r0 = blockIdx.y * 128;
+#pragma unroll
+  for (uint32_t i = 0; i < 16; ++i) {
+    const uint32_t bi = wv * 16 + i, b = b0 + bi, r = r0 + 2 * lane;
+    uint32_t v = 0;
+    if (b < nblk && r < nrow) {
+      v = *reinterpret_cast<const uint32_t*>(in + (uint64_t)b * istride + r);
+      if (r + 1 >= nrow) v &= 0xFFFFu;
+    }
+    tile[bi][2 * lane] = (uint16_t)v;
+    tile[bi][2 * lane + 1] = (uint16_t)(v >> 16);
+  }
+  __syncthreads();
+  const uint32_t half = lane >> 5, l = lane & 31u;
+#pragma unroll
+  for (uint32_t i = 0; i < 16; ++i) {
+    const uint32_t ri = wv * 32 + 2 * i + half, r = r0 + ri, b = b0 + 2 * l;
+    if (r < nrow && b < ostride && b < nblk + 1) {
+      const uint32_t v = (uint32_t)tile[2 * l][ri] | ((uint32_t)tile[2 * l + 1][ri] << 16);
+      *reinterpret_cast<uint32_t*>(out + (uint64_t)r * ostride + b) = v;
+    }
+  }
+}
+
 // Last b with P[b] <= j (P: exclusive prefix of the runs' lengths, P[0] = 0).
 __device__ __forceinline__ uint32_t run_of(const uint32_t* P, uint32_t nblk, uint32_t j) {
   uint32_t lo = 0, hi = nblk;
@@ -441,7 +476,10 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
   uint16_t* seg = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(scratch) + (uint64_t)nblk0 * kDenseC * 8);
   uint16_t* segT = seg + (uint64_t)nblk0 * stride;
   uint32_t direct = 0;
+  bool segt2 = false;
 #ifdef CB_EXPERIMENTS
+  static const bool env_segt2 = getenv("CB_DENSE_SEGT") && getenv("CB_DENSE_SEGT")[0] == '2';
+  segt2 = env_segt2;
   static const uint32_t env_direct = getenv("CB_DENSE_DIRECT_ENT") && getenv("CB_DENSE_DIRECT_ENT")[0] == '1';
   direct = env_direct;
 #endif
@@ -468,8 +506,12 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
     }
     {
       ProfScope ps("k_dense_seg_t", s);
-      hipLaunchKernelGGL(k_dense_seg_t, dim3((nblk + 63) / 64, (R + 1 + 63) / 64), dim3(256), 0, s, seg, stride, nblk,
-                         R + 1, segT, tstride);
+      if (segt2)
+        hipLaunchKernelGGL(k_dense_seg_t2, dim3((nblk + 63) / 64, (R + 1 + 127) / 128), dim3(256), 0, s, seg, stride,
+                           nblk, R + 1, segT, tstride);
+      else
+        hipLaunchKernelGGL(k_dense_seg_t, dim3((nblk + 63) / 64, (R + 1 + 63) / 64), dim3(256), 0, s, seg, stride, nblk,
+                           R + 1, segT, tstride);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
