@@ -105,7 +105,7 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
                                                          uint32_t rshift, uint32_t R,
                                                          uint16_t* __restrict__ seg, uint32_t segstride,
                                                          uint2* __restrict__ ent, uint64_t* __restrict__ hits,
-                                                         uint64_t hwords, uint32_t used, uint32_t direct) {
+                                                         uint64_t hwords, uint32_t used) {
   constexpr uint32_t NT = kDenseNT, KPT = kDenseKPT, C = kDenseC;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t b = blockIdx.x;
@@ -189,26 +189,14 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
     for (uint32_t t = tid; t <= R; t += NT) row[t] = (uint16_t)hist[t];
   }
   __syncthreads();  // the run row is out: hist becomes the bins' cursors
-  uint2* out = ent + (uint64_t)b * C;
-  if (direct) {  // (experiment builds: each entry stored straight to its slot in the block's run list)
 #pragma unroll
-    for (uint32_t g = 0; g < NB; ++g)
+  for (uint32_t g = 0; g < NB; ++g)
 #pragma unroll
-      for (int j = 0; j < (int)KPT; ++j)
-        if (live[g][j]) {
-          const uint32_t at = atomicAdd(&hist[pa[g][j] >> rshift], 1u);
-          out[at] = make_uint2(pb[g][j], ((pa[g][j] & pmask) << 16) | (g * CB + j * NT + tid));
-        }
-  } else {
-#pragma unroll
-    for (uint32_t g = 0; g < NB; ++g)
-#pragma unroll
-      for (int j = 0; j < (int)KPT; ++j)
-        if (live[g][j]) {
-          const uint32_t at = atomicAdd(&hist[pa[g][j] >> rshift], 1u);
-          stage[at] = make_uint2(pb[g][j], ((pa[g][j] & pmask) << 16) | (g * CB + j * NT + tid));
-        }
-  }
+    for (int j = 0; j < (int)KPT; ++j)
+      if (live[g][j]) {
+        const uint32_t at = atomicAdd(&hist[pa[g][j] >> rshift], 1u);
+        stage[at] = make_uint2(pb[g][j], ((pa[g][j] & pmask) << 16) | (g * CB + j * NT + tid));
+      }
   // the block's hit words (keys kb .. kb + C, whole words) start at zero:
   // the probe only ORs the set bits in
   {
@@ -219,9 +207,9 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
       if (w0 + w < nw) hits[(uint64_t)f * hwords + w0 + w] = 0ull;
     }
   }
-  if (direct) return;
   __syncthreads();
   const uint32_t total = hist[R];
+  uint2* out = ent + (uint64_t)b * C;
   const uint32_t n2 = total / 2;
   for (uint32_t i = tid; i < n2; i += NT) reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(stage)[i];
   if (tid == 0 && (total & 1u)) out[total - 1] = stage[total - 1];
@@ -248,41 +236,6 @@ __global__ __launch_bounds__(256) void k_dense_seg_t(const uint16_t* __restrict_
   for (uint32_t i = ty; i < 64; i += 4) {
     const uint32_t r = r0 + i, b = b0 + tx;
     if (r < nrow && b < nblk) out[(uint64_t)r * ostride + b] = tile[tx][i];
-  }
-}
-
-// The same transpose in 64-block x 128-region tiles moved as u32 pairs (half
-// the load and store instructions of k_dense_seg_t's u16 ones): a wave loads
-// one block's 128 run starts (256 B) per instruction and stores two regions'
-// 64 blocks (2 x 128 B) per instruction. istride and ostride are even (rows
-// padded to 64 u16), so every pair is 4-B aligned; a pair past ostride is
-// never written (the next row's first entries).
-__global__ __launch_bounds__(256) void k_dense_seg_t2(const uint16_t* __restrict__ in, uint32_t istride,
-                                                       uint32_t nblk, uint32_t nrow, uint16_t* __restrict__ out,
-                                                       uint32_t ostride) {
-  __shared__ uint16_t tile[64][130];
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t b0 = blockIdx.x * 64, r0 = blockIdx.y * 128;
-#pragma unroll
-  for (uint32_t i = 0; i < 16; ++i) {
-    const uint32_t bi = wv * 16 + i, b = b0 + bi, r = r0 + 2 * lane;
-    uint32_t v = 0;
-    if (b < nblk && r < nrow) {
-      v = *reinterpret_cast<const uint32_t*>(in + (uint64_t)b * istride + r);
-      if (r + 1 >= nrow) v &= 0xFFFFu;
-    }
-    tile[bi][2 * lane] = (uint16_t)v;
-    tile[bi][2 * lane + 1] = (uint16_t)(v >> 16);
-  }
-  __syncthreads();
-  const uint32_t half = lane >> 5, l = lane & 31u;
-#pragma unroll
-  for (uint32_t i = 0; i < 16; ++i) {
-    const uint32_t ri = wv * 32 + 2 * i + half, r = r0 + ri, b = b0 + 2 * l;
-    if (r < nrow && b < ostride && b < nblk + 1) {
-      const uint32_t v = (uint32_t)tile[2 * l][ri] | ((uint32_t)tile[2 * l + 1][ri] << 16);
-      *reinterpret_cast<uint32_t*>(out + (uint64_t)r * ostride + b) = v;
-    }
   }
 }
 
@@ -399,7 +352,7 @@ __global__ __launch_bounds__(kDenseNT, 8) void k_dense_probe(const void* __restr
 template <int KK, int MM, int WW>
 void dense_part(uint32_t nblk, size_t lds, hipStream_t s, const KeySrc& ks, uint64_t k0, uint64_t kend,
                 const ModP& mp, uint32_t rshift, uint32_t R, uint16_t* seg, uint32_t stride, uint2* ent,
-                uint64_t* hits, uint64_t hwords, uint32_t used, uint32_t direct) {
+                uint64_t* hits, uint64_t hwords, uint32_t used) {
   // ~115 KiB of dynamic LDS at C5: past the 64 KiB a launch gets without
   // asking, set once per instantiation
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_dense_part<KK, MM, WW>),
@@ -407,7 +360,7 @@ void dense_part(uint32_t nblk, size_t lds, hipStream_t s, const KeySrc& ks, uint
                                                      (int)dense_part_lds_max());
   (void)attr;
   hipLaunchKernelGGL((k_dense_part<KK, MM, WW>), dim3(nblk), dim3(kDenseNT), lds, s, ks, k0, kend, mp, rshift, R,
-                     seg, stride, ent, hits, hwords, used, direct);
+                     seg, stride, ent, hits, hwords, used);
 }
 
 }  // namespace
@@ -475,16 +428,7 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
   uint2* ent = reinterpret_cast<uint2*>(scratch);
   uint16_t* seg = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(scratch) + (uint64_t)nblk0 * kDenseC * 8);
   uint16_t* segT = seg + (uint64_t)nblk0 * stride;
-  uint32_t direct = 0;
-  bool segt2 = false;
-#ifdef CB_EXPERIMENTS
-  static const bool env_segt2 = getenv("CB_DENSE_SEGT") && getenv("CB_DENSE_SEGT")[0] == '2';
-  segt2 = env_segt2;
-  static const uint32_t env_direct = getenv("CB_DENSE_DIRECT_ENT") && getenv("CB_DENSE_DIRECT_ENT")[0] == '1';
-  direct = env_direct;
-#endif
-  // (direct: the partition's LDS is the histogram only)
-  const size_t lds1 = direct ? (size_t)(((R + 4) & ~3u) + 4) * 4 : dense_part_lds(R);
+  const size_t lds1 = dense_part_lds(R);
   uint32_t xflags = 0;
 #ifdef CB_EXPERIMENTS
   // timing-only A/B (the hits are wrong): CB_DENSE_X bit 0 skips the set[b]
@@ -500,18 +444,14 @@ hipError_t launch_set_probe_dense(int keyk, int mode, uint32_t width, const void
       // the keys of this chunk: k in [k0, k0 + nk), indices global
       CB_SET_DISPATCH(keyk, mode, width,
                       (dense_part<KK, MM, WW>(nblk, lds1, s, ks, k0, k0 + nk, mp, rshift, R, seg, stride, ent, hits,
-                                              hwords, used, direct)));
+                                              hwords, used)));
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
     {
       ProfScope ps("k_dense_seg_t", s);
-      if (segt2)
-        hipLaunchKernelGGL(k_dense_seg_t2, dim3((nblk + 63) / 64, (R + 1 + 127) / 128), dim3(256), 0, s, seg, stride,
-                           nblk, R + 1, segT, tstride);
-      else
-        hipLaunchKernelGGL(k_dense_seg_t, dim3((nblk + 63) / 64, (R + 1 + 63) / 64), dim3(256), 0, s, seg, stride, nblk,
-                           R + 1, segT, tstride);
+      hipLaunchKernelGGL(k_dense_seg_t, dim3((nblk + 63) / 64, (R + 1 + 63) / 64), dim3(256), 0, s, seg, stride, nblk,
+                         R + 1, segT, tstride);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
