@@ -26,8 +26,8 @@ int hip_fail(hipError_t e, const char* where) {
 // Device block pool for table, filter and set storage. hipMalloc of tens of
 // MB costs ~0.1 ms, which dominates a 1M-entry flush; released blocks are
 // kept per device (up to kPoolCap bytes) and handed to the next request they
-// fit (blocks are rounded to 2 MiB; a block is reused for requests of at
-// least half its size).
+// fit (large blocks are rounded to 2 MiB; a block is reused for requests of
+// at least half its size).
 //
 // Release is stream-ordered (round 6; VERDICT r5: a Drop used to run
 // hipDeviceSynchronize, stalling every stream of a concurrent server, e.g.
@@ -38,8 +38,22 @@ int hip_fail(hipError_t e, const char* where) {
 // hands it out again only once all those events have completed, as seen by
 // the host (hipEventQuery), so no queued kernel can still be using it. The
 // host never waits, and no stream waits on another.
+//
+// Small blocks (round 6) come from slabs. A table of the reference's own
+// shape (1024 lines, src/lib.rs:72,105) needs ~44 KB of file, ~60 KB of index
+// and 128 KB of key buckets, and its m = 1024 filter 8 KB; rounded to 2 MiB
+// blocks, 300 such tables spread over ~1.8 GB of address space, and the wide
+// read walk missed the per-CU translation cache (UTCL1) on 8 % of its
+// requests, its value decode on 58 % (rocprofv3 TCP_UTCL1_TRANSLATION_MISS,
+// tools/gpu/tlb_pmc.sh). Requests of at most kSmallMax are rounded to a power
+// of two (at least 4 KiB) and carved, aligned to their size, from 64 MiB
+// slabs, so those tables sit in a few tens of MB; released small blocks go
+// to a free list per size (behind the same stream-ordered retirement), and
+// slabs are kept for the process's life.
 constexpr size_t kPoolGrain = 2u << 20;
 constexpr size_t kPoolCap = size_t(16) << 30;
+constexpr size_t kSmallMax = 1u << 20, kSmallMin = 4096;
+constexpr size_t kSlabBytes = 64u << 20;
 
 struct Retired {
   void* p = nullptr;
@@ -47,14 +61,47 @@ struct Retired {
   std::vector<hipEvent_t> evs;  // one per stream known at the release
 };
 
+struct Slab {
+  uint8_t* base = nullptr;
+  size_t used = 0;
+};
+
 struct BlockPool {
   std::mutex mu;
   std::map<int, std::multimap<size_t, void*>> free;
-  std::map<int, size_t> cached;               // bytes in free + retired
+  std::map<int, size_t> cached;               // bytes in free + retired (large blocks)
   std::map<int, std::vector<Retired>> retired;  // released, their streams' events still pending
   std::vector<hipEvent_t> spare;              // completed retire events, for reuse
+  std::map<std::pair<int, size_t>, std::vector<void*>> small_free;  // (device, block size)
+  std::map<int, Slab> slab;                   // the slab small blocks are carved from
 };
 BlockPool g_pool;
+
+// Experiment builds: CB_POOL_SLAB=0 gives small requests their own 2 MiB
+// blocks again (the A/B); CB_POOL_CONTIG=1 allocates slabs and large blocks
+// physically contiguous (hipDeviceMallocContiguous).
+bool small_blocks_on() {
+#ifdef CB_EXPERIMENTS
+  static const bool off = getenv("CB_POOL_SLAB") && getenv("CB_POOL_SLAB")[0] == '0';
+  return !off;
+#else
+  return true;
+#endif
+}
+
+hipError_t device_malloc(void** p, size_t bytes) {
+#ifdef CB_EXPERIMENTS
+  static const bool contig = getenv("CB_POOL_CONTIG") && getenv("CB_POOL_CONTIG")[0] == '1';
+  if (contig) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous);
+#endif
+  return hipMalloc(p, bytes);
+}
+
+size_t small_size(size_t bytes) {
+  size_t z = kSmallMin;
+  while (z < bytes) z <<= 1;
+  return z;
+}
 
 std::mutex g_ws_mu;
 std::map<std::pair<int, void*>, std::unique_ptr<Workspace>> g_ws;
@@ -84,7 +131,10 @@ void reap(int device, bool wait) {
       continue;
     }
     for (hipEvent_t e : r.evs) g_pool.spare.push_back(e);
-    fl.emplace(r.cap, r.p);
+    if (r.cap <= kSmallMax)
+      g_pool.small_free[{device, r.cap}].push_back(r.p);
+    else
+      fl.emplace(r.cap, r.p);
     rl[i] = std::move(rl.back());
     rl.pop_back();
   }
@@ -94,6 +144,34 @@ void reap(int device, bool wait) {
 
 // *cap receives the block's size (pass it back to pool_release).
 hipError_t pool_alloc(int device, size_t bytes, void** p, size_t* cap) {
+  if (bytes <= kSmallMax && small_blocks_on()) {
+    const size_t z = small_size(bytes);
+    std::lock_guard<std::mutex> lk(g_pool.mu);
+    if (!g_pool.retired[device].empty()) reap(device, false);
+    auto& fl = g_pool.small_free[{device, z}];
+    if (!fl.empty()) {
+      *p = fl.back();
+      fl.pop_back();
+      *cap = z;
+      return hipSuccess;
+    }
+    Slab& sb = g_pool.slab[device];
+    size_t off = (sb.used + z - 1) & ~(z - 1);
+    if (!sb.base || off + z > kSlabBytes) {  // a new slab (the old one's tail stays unused)
+      void* base = nullptr;
+      hipError_t e = device_malloc(&base, kSlabBytes);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return e;
+      }
+      sb.base = (uint8_t*)base;
+      off = 0;
+    }
+    *p = sb.base + off;
+    sb.used = off + z;
+    *cap = z;
+    return hipSuccess;
+  }
   const size_t want = pool_round(bytes);
   {
     std::lock_guard<std::mutex> lk(g_pool.mu);
@@ -108,7 +186,7 @@ hipError_t pool_alloc(int device, size_t bytes, void** p, size_t* cap) {
       return hipSuccess;
     }
   }
-  hipError_t e = hipMalloc(p, want);
+  hipError_t e = device_malloc(p, want);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     // out of memory: let the retired blocks' work finish, release every
@@ -121,7 +199,7 @@ hipError_t pool_alloc(int device, size_t bytes, void** p, size_t* cap) {
       g_pool.cached[device] = 0;
     }
     for (auto& b : drop) (void)hipFree(b.second);
-    e = hipMalloc(p, want);
+    e = device_malloc(p, want);
     if (e != hipSuccess) return e;
   }
   *cap = want;
@@ -141,10 +219,11 @@ void pool_release(int device, void* p, size_t cap) {
   Retired r;
   r.p = p;
   r.cap = cap;
+  const bool small = cap <= kSmallMax;  // a slab block (large blocks are whole multiples of 2 MiB)
   bool sync = false;
   {
     std::lock_guard<std::mutex> lk(g_pool.mu);
-    if (g_pool.cached[device] + cap > kPoolCap) {
+    if (!small && g_pool.cached[device] + cap > kPoolCap) {
       sync = true;  // the pool is full: hipFree below, which waits as it always has
     } else {
       for (hipStream_t s : streams) {
@@ -173,7 +252,7 @@ void pool_release(int device, void* p, size_t cap) {
         }
       }
       if (!sync) {
-        g_pool.cached[device] += cap;
+        if (!small) g_pool.cached[device] += cap;
         g_pool.retired[device].push_back(std::move(r));
         return;
       }
@@ -184,6 +263,10 @@ void pool_release(int device, void* p, size_t cap) {
   (void)hipDeviceSynchronize();  // what hipFree implies
   {
     std::lock_guard<std::mutex> lk(g_pool.mu);
+    if (small) {  // slab memory is never freed: back to its size's list
+      g_pool.small_free[{device, cap}].push_back(p);
+      return;
+    }
     if (g_pool.cached[device] + cap <= kPoolCap) {
       g_pool.free[device].emplace(cap, p);
       g_pool.cached[device] += cap;
