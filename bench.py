@@ -820,7 +820,7 @@ def main():
     # one wide FilterSet, Database::get over all of them in one launch
     wide = None
     if not args.no_wide and rank == 0 and world == 1:
-        wide = wide_fanout_leg(args, torch, dev, local, sh, LK, timed, kernel_ms, lsmt_amd, workload)
+        wide = wide_fanout_leg(args, torch, dev, local, lane_streams, LK, timed, kernel_ms, lsmt_amd, workload)
         log(f"[wide] {wide['value'] / 1e6:.1f} M gets/s over {wide['tables']} tables, "
             f"oracle {wide.get('oracle_sample_bit_exact')}")
 
@@ -1733,8 +1733,8 @@ def run_leg(args, torch, dist, world, rank, local, dev, use_dist, result, red_de
 
         def kernel_ms(names, fn, k):
             return _kernel_us(L, torch, dev, names, fn, k)
-        out = wide_fanout_leg(args, torch, dev, local, lanes[0].cuda_stream, args.steps * 20, timed, kernel_ms,
-                              lsmt_amd, workload)
+        out = wide_fanout_leg(args, torch, dev, local, leg_lanes(torch, dev, args.probe_streams), args.steps * 20,
+                              timed, kernel_ms, lsmt_amd, workload)
         key = "wide_fanout"
     if rank == 0:
         print(json.dumps({"leg": args.leg, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -1810,7 +1810,7 @@ def zone_partitioned_leg(args, torch, dev, local, sh, F, m, kpf, n, timed, kerne
     return out
 
 
-def wide_fanout_leg(args, torch, dev, local, sh, LK, timed, kernel_ms, lsmt_amd, workload):
+def wide_fanout_leg(args, torch, dev, local, lanes, LK, timed, kernel_ms, lsmt_amd, workload):
     """Database::get at the reference's own shape (SURVEY.md §8a a11): 300
     tables as 300 auto-flushes of 1024 entries leave them (keys from a
     shared pool, so later flushes rewrite keys; each table's filter m = 1024
@@ -1819,8 +1819,14 @@ def wide_fanout_leg(args, torch, dev, local, sh, LK, timed, kernel_ms, lsmt_amd,
     first in ONE launch (cb_set_get_many_fixed over a 320-slot set). At
     m = 1024 with 1024 keys a filter is 86 % ones, so ~75 % of the tables pass
     the Bloom gate for any key and a lookup searches ~100-225 tables: the
-    reference's own cost model. Oracle: the first 4096 lookups through the
-    CPU restatement of the same gate and walk."""
+    reference's own cost model. Batches alternate over the line's P lanes
+    (as the probe and read legs: each lane its own outputs and workspace), so
+    one batch's value scan and base64 decode overlap the next batch's walk;
+    the one-lane figure is reported beside it. Oracle: the first 4096 lookups
+    through the CPU restatement of the same gate and walk, and every lane's
+    answers equal."""
+    sh = lanes[0].cuda_stream
+    P = len(lanes)
     nt, per, n = 300, 1024, 1 << 18
     rng = np.random.default_rng(300)
     pool = workload.key_range(4242, 120_000)
@@ -1849,26 +1855,42 @@ def wide_fanout_leg(args, torch, dev, local, sh, LK, timed, kernel_ms, lsmt_amd,
     keys = lsmt_amd.DeviceKeys(torch.from_numpy(look_np).to(dev))
     newest_first = tables[::-1]
     slots = np.arange(nt, dtype=np.uint32)[::-1].copy()
-    which = torch.empty(n, dtype=torch.int32, device=dev)
-    voff = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    vals = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    which_l = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(P)]
+    voff_l = [torch.empty(n + 1, dtype=torch.int64, device=dev) for _ in range(P)]
+    vals_l = [torch.empty(n * 16, dtype=torch.uint8, device=dev) for _ in range(P)]
+    nxt = [0]
 
-    def step():
-        lsmt_amd.get_many(newest_first, keys, filterset=fset, hit_rows=slots, out=(which, voff, vals), stream=sh,
-                          wait=False)
+    def lane_step(b):
+        lsmt_amd.get_many(newest_first, keys, filterset=fset, hit_rows=slots, out=(which_l[b], voff_l[b], vals_l[b]),
+                          stream=lanes[b].cuda_stream, wait=False)
 
-    warm_up(torch, dev, step, 2)
+    def step():  # batches round-robin over the lanes
+        b = nxt[0] % P
+        nxt[0] += 1
+        lane_step(b)
+
+    def step1():
+        lane_step(0)
+
+    for b in range(P):  # each lane's workspace builds its screen once
+        warm_up(torch, dev, lambda: lane_step(b), 2)
     # 100 steps at the default K (12 ms): the host issues a step in ~30 us
-    # against ~122 us of device time (tools/wide_issue.py), so the queue runs
+    # against ~110 us of device time (tools/wide_issue.py), so the queue runs
     # ahead after the first step; 10 steps left that first step's issue and
-    # the box's host jitter in the figure (128-142 us per step against 122)
+    # the box's host jitter in the figure
     k = max(20, LK // 2)
-    el = timed(step, k, lanes=[torch.cuda.current_stream(dev)])
-    kus = kernel_ms(["k_wide_get_many", "k_tile_scan", "k_b64_decode"], step, k)
+    el1 = timed(step1, k, lanes=lanes[:1])
+    el = timed(step, k, lanes=lanes) if P > 1 else el1
+    kus = kernel_ms(["k_wide_get_many", "k_tile_scan", "k_b64_decode"], step1, k)
     torch.cuda.synchronize(dev)
-    found = int((which >= 0).sum().item())
+    found = int((which_l[0] >= 0).sum().item())
+    lanes_equal = all(torch.equal(which_l[0], w) and torch.equal(voff_l[0], v) and
+                      torch.equal(vals_l[0], x) for w, v, x in zip(which_l, voff_l, vals_l))
+    which, voff, vals = which_l[0], voff_l[0], vals_l[0]
     out = {"metric": f"gets/s: Database::get over {nt} tables of m=1024 (1024 entries each) in one wide set",
            "value": round(n / (el / k), 1), "unit": "keys/s", "ms_per_step": round(el / k * 1e3, 4), "steps": k,
+           "pipeline_lanes": P, "lanes_equal": bool(lanes_equal),
+           "one_lane": {"value": round(n / (el1 / k), 1), "ms_per_step": round(el1 / k * 1e3, 4)},
            "tables": nt, "set_width": 320, "lookups": n, "found": found,
            "kernels_us": {kk: round(v["avg_us"], 2) for kk, v in kus.items()},
            "launches_per_batch": {"search": 1, "tile_scan": 1, "b64_decode": 1},
@@ -1925,7 +1947,7 @@ def wide_fanout_leg(args, torch, dev, local, sh, LK, timed, kernel_ms, lsmt_amd,
         out["cpu_baseline"] = {"value": round(smp / tc, 1), "unit": "keys/s", "cores": 1, "kind": "port",
                                "sample": f"oracle gate + newest-first walk over {nt} tables for the first {smp} "
                                          f"lookups, {tc:.2f}s"}
-    del tables, blooms, fset, keys, which, voff, vals
+    del tables, blooms, fset, keys, which, voff, vals, which_l, voff_l, vals_l
     torch.cuda.synchronize(dev)
     return out
 

@@ -83,4 +83,44 @@ __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t* total) {
   return pre + (uint64_t)x - v;
 }
 
+// block_scan of v plus the block sums of a and b, in one LDS round and two
+// barriers (three block_scan calls take six): the decode's own scan of the
+// lengths with its sums of the tile sums before it and of all of them.
+template <int NT>
+__device__ __forceinline__ uint64_t block_scan_sum2(uint64_t v, uint64_t a, uint64_t b, uint64_t* total,
+                                                    uint64_t* sa, uint64_t* sb) {
+  static_assert(NT % 64 == 0 && NT <= 4096, "block size");
+  constexpr int NW = NT / 64;
+  __shared__ uint64_t ws[3][NW];
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long x = v, p = a, q = b;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long y = __shfl_up(x, d, 64);
+    if ((int)lane >= d) x += y;
+    p += __shfl_xor(p, d, 64);
+    q += __shfl_xor(q, d, 64);
+  }
+  if (lane == 63) ws[0][wid] = x;
+  if (lane == 0) {
+    ws[1][wid] = p;
+    ws[2][wid] = q;
+  }
+  __syncthreads();
+  uint64_t pre = 0, t = 0, s1 = 0, s2 = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < (uint32_t)NW; ++w) {
+    const uint64_t c = ws[0][w];
+    pre += w < wid ? c : 0;
+    t += c;
+    s1 += ws[1][w];
+    s2 += ws[2][w];
+  }
+  *total = t;
+  *sa = s1;
+  *sb = s2;
+  __syncthreads();  // ws is reused by the next call
+  return pre + (uint64_t)x - v;
+}
+
 }  // namespace cb

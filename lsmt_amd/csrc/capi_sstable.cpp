@@ -335,26 +335,33 @@ int get_many_impl(const cb_table* const* tables, uint32_t nt, const uint64_t* hi
     HIP_TRY(cb::launch_get_many(sk.keyk, dviews, nt, dhits, drows, hwords, sk.ks, n, dwhich,
                                 (uint64_t*)ws.t_line.p, (uint64_t*)ws.t_dlen.p, tsum, s));
   }
-  HIP_TRY(cb::launch_tile_scan(tsum, cb::get_tiles(n), dvoff + n, s));
+  // batches of up to 256K keys: the decode scans the tile sums itself (one
+  // launch fewer per batch); larger ones: the one-block scan between
+  bool raw = n && n <= cb::decode_raw_max();  // (n = 0: the scan kernel writes voff[0] = 0)
+#ifdef CB_EXPERIMENTS
+  static const bool no_raw = getenv("CB_DECODE_RAW") && getenv("CB_DECODE_RAW")[0] == '0';
+  if (no_raw) raw = false;
+#endif
+  if (!raw) HIP_TRY(cb::launch_tile_scan(tsum, cb::get_tiles(n), dvoff + n, s));
   if (!ws.htot) HIP_TRY(hipHostMalloc((void**)&ws.htot, kHostScratch, hipHostMallocDefault));
   if (async) {
-    HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, vals, vals ? cap : 0, s));
+    HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, vals, vals ? cap : 0, s, raw));
     return CB_OK;
   }
   if (vals && is_device_ptr(vals)) {
     // device values: offsets and values in one pass (the kernel skips the
     // value writes when the total exceeds cap): one host round trip
-    HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, vals, cap, s));
+    HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, vals, cap, s, raw));
     HIP_TRY(hipMemcpyAsync(ws.htot, dvoff + n, 8, hipMemcpyDeviceToHost, s));
   } else {
-    HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, nullptr, 0, s));  // offsets only
+    HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, nullptr, 0, s, raw));  // offsets only
     HIP_TRY(hipMemcpyAsync(ws.htot, dvoff + n, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     const uint64_t tot = *ws.htot;
     if (vals && cap >= tot && tot) {
       uint8_t* dvals;
       if ((rc = out_buf(ws.t_vals, vals, tot, s, &dvals))) return rc;
-      HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, dvals, tot, s));
+      HIP_TRY(cb::launch_b64_decode(vsrc, dlen, tsum, n, dvoff, dvals, tot, s, raw));
       HIP_TRY(hipMemcpyAsync(vals, dvals, tot, hipMemcpyDeviceToHost, s));
     }
   }

@@ -1270,6 +1270,14 @@ __constant__ int g_b64_x;
 // (Two adjacent keys per thread, so all of a 1M-key batch's value loads are
 // in flight in one round, measured slower: read path 14.3 against 14.8-14.9 G
 // gets/s, wide fan-out 1.97-2.00 against 2.04-2.06; experiment r05_b64kpt, HISTORY.md.)
+// RAW (grids of at most kRawTiles blocks): tsum holds the producer's
+// unscanned tile sums, and every block sums the ones before it (and all of
+// them, for the total; block 0 stores it as voff[n]) from one round of loads
+// issued with its other loads, in place of a k_tile_scan launch between the
+// two kernels.
+constexpr uint32_t kRawPer = 4, kRawTiles = kNT * kRawPer;
+static_assert(kNT == kDecodeTile && (uint64_t)kRawTiles * kNT == 262144, "decode_raw_max()");
+template <bool RAW>
 __global__ __launch_bounds__(kNT) void k_b64_decode(const uint64_t* __restrict__ vsrc,
                                                     const uint64_t* __restrict__ dlen,
                                                     const uint64_t* __restrict__ tsum, uint64_t n,
@@ -1283,20 +1291,43 @@ __global__ __launch_bounds__(kNT) void k_b64_decode(const uint64_t* __restrict__
   // and the block scan runs while the chars arrive.
   const uint64_t dl = k < n ? dlen[k] : 0;
   const uint8_t* src = (const uint8_t*)(uintptr_t)(k < n ? vsrc[k] : 0);
-  const uint64_t base = tsum[blockIdx.x];  // k_tile_scan: the tiles before
-  const uint64_t vn = voff[n];             // k_tile_scan's total
-  const bool write = out && vn <= cap;     // uniform
+  uint64_t base = 0, vn = 0, ts[kRawPer];
+  if constexpr (RAW) {
+#pragma unroll
+    for (uint32_t j = 0; j < kRawPer; ++j) {
+      const uint32_t i = threadIdx.x * kRawPer + j;
+      ts[j] = i < gridDim.x ? tsum[i] : 0;
+    }
+  } else {
+    base = tsum[blockIdx.x];  // k_tile_scan: the tiles before
+    vn = voff[n];             // k_tile_scan's total
+  }
   SmallB64 sv;
   const bool small = dl && dl <= kSmallB64Bytes;
+  // (RAW: the total is not known yet, so the chars load whenever there is an
+  // output; a total above cap then leaves them unused)
+  const bool want = out && (RAW || vn <= cap);
 #ifdef CB_EXPERIMENTS
   // (timing-only A/B, wrong bytes: CB_B64_X bit 0 skips the value loads)
-  if (write && small && !(g_b64_x & 1)) b64_small_load(src, dl, sv);
+  if (want && small && !(g_b64_x & 1)) b64_small_load(src, dl, sv);
   if (g_b64_x & 1) sv = SmallB64{{0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u, 0x41414141u}, 0};
 #else
-  if (write && small) b64_small_load(src, dl, sv);
+  if (want && small) b64_small_load(src, dl, sv);
 #endif
-  uint64_t total;
-  const uint64_t pre = block_scan<kNT>(dl, &total);
+  uint64_t total, pre;
+  if constexpr (RAW) {
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kRawPer; ++j) {
+      all += ts[j];
+      before += threadIdx.x * kRawPer + j < blockIdx.x ? ts[j] : 0;
+    }
+    pre = block_scan_sum2<kNT>(dl, before, all, &total, &base, &vn);
+    if (blockIdx.x == 0 && threadIdx.x == 0) voff[n] = vn;
+  } else {
+    pre = block_scan<kNT>(dl, &total);
+  }
+  const bool write = out && vn <= cap;  // uniform
   const uint64_t o = base + pre;
   if (k < n) voff[k] = o;
   if (!write) return;
@@ -1601,7 +1632,7 @@ hipError_t launch_tile_scan(uint64_t* tsum, uint64_t nt, uint64_t* total_out, hi
 }
 
 hipError_t launch_b64_decode(const uint64_t* vsrc, const uint64_t* dlen, const uint64_t* tsum,
-                             uint64_t n, uint64_t* voff, uint8_t* out, uint64_t cap, hipStream_t s) {
+                             uint64_t n, uint64_t* voff, uint8_t* out, uint64_t cap, hipStream_t s, bool raw) {
 #ifdef CB_EXPERIMENTS
   static const int env_x = [] {
     const int x = getenv("CB_B64_X") ? atoi(getenv("CB_B64_X")) : 0;
@@ -1611,9 +1642,13 @@ hipError_t launch_b64_decode(const uint64_t* vsrc, const uint64_t* dlen, const u
   (void)env_x;
 #endif
   if (!n) return hipSuccess;
+  const uint32_t nb = blocks_for(n, kNT);
+  if (raw && nb > kRawTiles) return hipErrorInvalidValue;
   ProfScope ps("k_b64_decode", s);
-  hipLaunchKernelGGL(k_b64_decode, dim3(blocks_for(n, kNT)), dim3(kNT), 0, s, vsrc, dlen, tsum, n, voff,
-                     out, cap);
+  if (raw)
+    hipLaunchKernelGGL(k_b64_decode<true>, dim3(nb), dim3(kNT), 0, s, vsrc, dlen, tsum, n, voff, out, cap);
+  else
+    hipLaunchKernelGGL(k_b64_decode<false>, dim3(nb), dim3(kNT), 0, s, vsrc, dlen, tsum, n, voff, out, cap);
   return hipGetLastError();
 }
 

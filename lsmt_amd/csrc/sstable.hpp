@@ -469,7 +469,12 @@ hipError_t launch_tile_scan(uint64_t* tsum, uint64_t nt, uint64_t* total_out, hi
 // voff[0..n) = exclusive scan of dlen from the scanned tsum (voff[n] is the
 // total launch_tile_scan wrote), and the decoded values into out + voff[k];
 // values are written only when out != nullptr and the total fits in cap.
+// raw: tsum is the producer's unscanned tile sums (left as they are) and the
+// kernel scans them itself, voff[n] included: no launch_tile_scan first.
+// Batches of at most decode_raw_max() keys.
 hipError_t launch_b64_decode(const uint64_t* vsrc, const uint64_t* dlen, const uint64_t* tsum,
-                             uint64_t n, uint64_t* voff, uint8_t* out, uint64_t cap, hipStream_t s);
+                             uint64_t n, uint64_t* voff, uint8_t* out, uint64_t cap, hipStream_t s,
+                             bool raw = false);
+inline uint64_t decode_raw_max() { return (uint64_t)kDecodeTile * 1024; }
 
 }  // namespace cb
