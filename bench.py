@@ -1884,8 +1884,9 @@ def wide_fanout_leg(args, torch, dev, local, lanes, LK, timed, kernel_ms, lsmt_a
     kus = kernel_ms(["k_wide_get_many", "k_tile_scan", "k_b64_decode"], step1, k)
     torch.cuda.synchronize(dev)
     found = int((which_l[0] >= 0).sum().item())
+    tot = int(voff_l[0][n].item())  # value bytes written (the buffers' tails are never written)
     lanes_equal = all(torch.equal(which_l[0], w) and torch.equal(voff_l[0], v) and
-                      torch.equal(vals_l[0], x) for w, v, x in zip(which_l, voff_l, vals_l))
+                      torch.equal(vals_l[0][:tot], x[:tot]) for w, v, x in zip(which_l, voff_l, vals_l))
     which, voff, vals = which_l[0], voff_l[0], vals_l[0]
     out = {"metric": f"gets/s: Database::get over {nt} tables of m=1024 (1024 entries each) in one wide set",
            "value": round(n / (el / k), 1), "unit": "keys/s", "ms_per_step": round(el / k * 1e3, 4), "steps": k,
