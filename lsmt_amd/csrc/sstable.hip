@@ -1022,25 +1022,6 @@ __global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __rest
   const uint32_t ng = (nt + 63) / 64;
   for (uint32_t i = threadIdx.x; i < ng; i += kNT) sg[i] = groups[i];
   __syncthreads();
-  // A group's three row windows (rows a and b, the screen) are loaded
-  // together, and the next group's are in flight while this group's
-  // candidates are walked (round 6: they were three dependent round trips
-  // per group, row b read only after row a's window was seen non-zero). The
-  // reference's `&&` stays in the arithmetic: b's bits count only where a's
-  // window has bits (at m = 1024 a row window is non-zero for nearly every
-  // key, so the short-circuit saved no read there).
-  uint64_t wa = 0, wb = 0, wsc = ~0ull;
-  auto windows = [&](uint32_t g, uint64_t& a, uint64_t& b, uint64_t& c) {
-    const WideGroup gd = sg[g];
-    a = 0;
-    b = 0;
-    c = ~0ull;
-    if (gd.kind == 2) return;  // scattered slots: read bit by bit in the walk
-    a = wide_window(ra, R, gd.lo);
-    b = wide_window(rb, R, gd.lo);
-    if (rs) c = wide_window(rs, R, gd.lo);
-  };
-  if (live) windows(0, wa, wb, wsc);
   int32_t w = -1;
   uint64_t src = 0, d = 0;
   bool active = live;
@@ -1070,8 +1051,19 @@ __global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __rest
     if (!active) continue;
     const WideGroup gd = sg[g];
     const uint64_t gmask = gd.gn >= 64 ? ~0ull : ((1ull << gd.gn) - 1);
-    const uint64_t ca = wa, cb = wb, cs = wsc;
-    if (g + 1 < ng) windows(g + 1, wa, wb, wsc);  // in flight during this group's walk
+    // The group's row windows one after another, each only when it can
+    // matter: row b where row a's window has bits (src/bloom.rs:50's &&),
+    // the screen where both do. Loading the three together, with the next
+    // group's in flight during this group's walk, measured slower (round 6:
+    // 93.9-94.2 against 92.1-92.3 us one lane, 3.07 against 3.29 G gets/s
+    // on three lanes) and cost ~2 more L2 requests per lookup: a lane found
+    // in this group had already loaded the next group's three windows.
+    uint64_t ca = 0, cb = 0, cs = ~0ull;
+    if (gd.kind != 2) {
+      ca = wide_window(ra, R, gd.lo) & gmask;
+      cb = ca ? wide_window(rb, R, gd.lo) : 0ull;
+      cs = (ca & cb) && rs ? wide_window(rs, R, gd.lo) : ~0ull;
+    }
     uint64_t cand = 0;
     if (gd.kind == 2) {  // scattered slots: one bit per table
       for (uint32_t i = 0; i < gd.gn; ++i) {
