@@ -162,7 +162,24 @@ hipError_t pool_alloc(int device, size_t bytes, void** p, size_t* cap) {
       hipError_t e = device_malloc(&base, kSlabBytes);
       if (e != hipSuccess) {
         (void)hipGetLastError();
-        return e;
+        // out of memory: as for large blocks, let the retired blocks' work
+        // finish, release every cached large block and retry once (on this
+        // rare path the pool's lock is held across the frees)
+        reap(device, true);
+        for (auto& b : g_pool.free[device]) (void)hipFree(b.second);
+        g_pool.free[device].clear();
+        g_pool.cached[device] = 0;
+        if (!fl.empty()) {  // a block of this size came back from the retired list
+          *p = fl.back();
+          fl.pop_back();
+          *cap = z;
+          return hipSuccess;
+        }
+        e = device_malloc(&base, kSlabBytes);
+        if (e != hipSuccess) {
+          (void)hipGetLastError();
+          return e;
+        }
       }
       sb.base = (uint8_t*)base;
       off = 0;

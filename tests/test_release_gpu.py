@@ -186,3 +186,62 @@ def test_set_destroy_is_stream_ordered(gpu):
     assert np.array_equal(hits.cpu().numpy().view(np.uint64), oracle.probe_fixed(ofs, look))
     h2 = s2.probe(look)
     assert np.array_equal(h2, oracle.probe_fixed(ofs[::-1], look))
+
+
+def test_small_block_not_reused_under_a_queued_reader(gpu):
+    """The same as above for a filter small enough to come from a slab
+    (m = 2^16: 8 KiB, capi.cpp pool_alloc's small blocks): the queued probe
+    reads A's bits, B's build gets another block or A's after the probe."""
+    import torch
+    m = 1 << 16
+    ka, kb = workload.key_range(34, 3000), workload.key_range(35, 3000)
+    look = np.concatenate([ka[:2000], kb[:2000], workload.key_range(36, 2000)])
+    a = gpu.BloomFilter(m)
+    a.insert_batch(ka)
+    torch.cuda.synchronize()
+    s, t = torch.cuda.Stream(), torch.cuda.Stream()
+    dkeys = torch.from_numpy(look).cuda()
+    hits = torch.zeros((1, (len(look) + 63) // 64), dtype=torch.int64, device="cuda")
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(400_000_000)  # ~0.2 s
+    gpu.probe([a], gpu.DeviceKeys(dkeys), out=hits, stream=s.cuda_stream)
+    a.close()
+    b = gpu.BloomFilter(m)
+    b.insert_batch(gpu.DeviceKeys(torch.from_numpy(kb).cuda()), stream=t.cuda_stream)
+    t.synchronize()
+    s.synchronize()
+    oa, ob = oracle.OracleFilter(m), oracle.OracleFilter(m)
+    oa.insert_fixed(ka)
+    ob.insert_fixed(kb)
+    assert np.array_equal(hits.cpu().numpy().view(np.uint64), oracle.probe_fixed([oa], look))
+    assert np.array_equal(b.bools(), ob.bools())
+
+
+def test_small_blocks_are_reused(gpu):
+    """Tables of the reference's auto-flush shape (1024 entries, m = 1024)
+    made and dropped in rounds: once a round's blocks are retired and their
+    events done, the next round's tables take them again (no new slabs: the
+    device's free memory does not fall round over round), and every table
+    answers its own keys."""
+    import torch
+
+    def round_(seed):
+        ts = []
+        for i in range(60):
+            ks = workload.sort_keys16(workload.key_range(seed + i, 1024))
+            t, bloom, _ = gpu.sstable_create([(bytes(k), bytes(k)) for k in ks], m=1024)
+            ts.append((t, bloom, ks))
+        torch.cuda.synchronize()
+        for t, bloom, ks in ts[::17]:
+            assert bloom.may_contain_batch(ks[:64]).all()
+        for t, bloom, _ in ts:
+            t.close()
+            bloom.close()
+        torch.cuda.synchronize()
+
+    round_(5000)
+    free1 = torch.cuda.mem_get_info()[0]
+    for r in range(3):
+        round_(6000 + 100 * r)
+    free2 = torch.cuda.mem_get_info()[0]
+    assert free2 >= free1 - (8 << 20), f"device free memory fell by {(free1 - free2) >> 20} MiB over 3 rounds"
