@@ -128,3 +128,22 @@ def test_c2_leg_and_profile_shape_exist():
     assert _parse(["--leg", "c2"]).leg == "c2"
     text = open(os.path.join(ROOT, "tools", "profile_round.sh")).read()
     assert "c2)" in text and "--leg c2" in text and "--build-streams 1" in text
+
+
+def test_compact_line_of_this_round_fits_at_eight_ranks():
+    """This round's full default line (profiles/bench_r06o_full.json), with
+    what a line at N = 8 adds (the exchange's mode and counters, one
+    rccl_world entry per rank), still compacts under the budget, the tail
+    legs last; the N = 1-only legs (read path, wide fan-out) only shrink it."""
+    import json
+    with open(os.path.join(ROOT, "profiles", "bench_r06o_full.json")) as fh:
+        line = json.load(fh)
+    line["n_gpus"] = 8
+    line["exchange"] = {"sparse_steps": 20, "mode": "sparse", "cap": 1234567, "all_fit": True}
+    line["rccl_world"] = [8] * 8
+    c = bench.compact_line(line)
+    text = json.dumps(c, separators=(",", ":"))
+    assert len(text) <= bench.LINE_BUDGET, len(text)
+    assert list(c)[-4:] == ["build", "e2e", "cold", "may_contain"]
+    assert c["rccl_world"] == [8] * 8 and c["exchange"]["mode"] == "sparse"
+    assert c["wide_fanout"]["one_lane"]["value"] and c["wide_fanout"]["lanes_equal"] is True
