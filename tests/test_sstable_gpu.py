@@ -230,6 +230,38 @@ def test_get_many_batches_of_changing_size(gpu):
         assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals, nk
 
 
+def test_get_many_decode_scan_boundary(gpu):
+    """Batches at the edge of the decode's own tile-sum scan (sstable.hip
+    k_b64_decode<RAW>: up to 256K keys, 1024 tiles; one key more takes the
+    k_tile_scan launch), on device and host outputs, each equal to the
+    oracle, and a value buffer one byte short left untouched with the total
+    still reported."""
+    import torch
+    per = [workload.key_range(1700 + t, 150_000) for t in range(2)]
+    files = [workload.sstable_bytes(k, workload.table_value(k, 700 + t)) for t, k in enumerate(per)]
+    tables = [gpu.Table(f) for f in files]
+    otables = [oracle.OracleTable(f.tobytes()) for f in files]
+    pool = np.concatenate([per[0], per[1], workload.key_range(4325, 40_000)])
+    pool = pool[np.random.default_rng(9).permutation(len(pool))]
+    for nk in (262_144, 262_145, 262_143, 255 * 256 + 1):
+        look = np.ascontiguousarray(pool[:nk])
+        d = np.ascontiguousarray(look.reshape(-1))
+        offs = np.arange(0, 16 * (nk + 1), 16, dtype=np.uint64)
+        ow, ovoff, ovals = oracle.get_many(otables, None, d, offs)
+        which, voff, vals = gpu.get_many(tables, look)
+        assert np.array_equal(which, ow) and np.array_equal(voff, ovoff) and vals == ovals, nk
+        dw = torch.empty(nk, dtype=torch.int32, device="cuda")
+        dv = torch.empty(nk + 1, dtype=torch.int64, device="cuda")
+        short = torch.full((len(ovals) - 1,), 7, dtype=torch.uint8, device="cuda")
+        dk = gpu.DeviceKeys(torch.from_numpy(look).cuda())
+        _, _, total = gpu.get_many(tables, dk, out=(dw, dv, short))
+        assert total == len(ovals) and bool((short == 7).all()), nk
+        assert np.array_equal(dv.cpu().numpy().astype(np.uint64), ovoff), nk
+        full = torch.empty(len(ovals), dtype=torch.uint8, device="cuda")
+        _, _, total = gpu.get_many(tables, dk, out=(dw, dv, full))
+        assert bytes(full.cpu().numpy()) == ovals and np.array_equal(dw.cpu().numpy(), ow), nk
+
+
 def test_get_many_same_list_mutated_between_calls(gpu):
     """One table list passed batch after batch while it changes in place
     (get_many keeps its handle array per list object, lsmt_amd.bloom.
