@@ -988,15 +988,24 @@ constexpr uint32_t kScreen = 8;
 // Four waves per SIMD, 109 VGPRs and no spill (round 5, with the screen):
 // 1.81-1.84 against 1.63 G gets/s for five waves at 96 VGPRs and 56 B of
 // spill per lane (experiment r05_wide4, HISTORY.md, alternating on one box).
+// The walk's workgroup: kWideNT keys (two 256-key tiles of the value scan);
+// a group's views and maps are staged once per workgroup, so 512 keys per
+// workgroup halve the staging's L2 requests per lookup against 256.
+#if defined(CB_EXPERIMENTS) && defined(CB_WIDE_THREADS)
+constexpr uint32_t kWideNT = CB_WIDE_THREADS;
+#else
+constexpr uint32_t kWideNT = 512;
+#endif
+static_assert(kWideNT % kNT == 0 && kWideNT / kNT <= 4, "up to four value tiles per workgroup");
 template <int KEYK, int MODE>
-__global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __restrict__ set, uint32_t R, ModP mp,
+__global__ __launch_bounds__(kWideNT, 4) void k_wide_get_many(const uint64_t* __restrict__ set, uint32_t R, ModP mp,
                                                        WideZone z, const TableView* __restrict__ tv, uint32_t nt,
                                                        const WideGroup* __restrict__ groups,
                                                        const uint32_t* __restrict__ slots, KeySrc ks, uint64_t n,
                                                        int32_t* __restrict__ which, uint64_t* __restrict__ vsrc,
                                                        uint64_t* __restrict__ dlen, uint64_t* __restrict__ tsum,
                                                        WideScreen ws, const DirMap* __restrict__ maps) {
-  const uint64_t k = (uint64_t)blockIdx.x * kNT + threadIdx.x;
+  const uint64_t k = (uint64_t)blockIdx.x * kWideNT + threadIdx.x;
   const bool live = k < n;
   const Query q = make_query<KEYK>(ks, live ? k : 0);
   uint64_t pa = 0, pb = 0;
@@ -1020,7 +1029,7 @@ __global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __rest
   __shared__ DirMap sdm[64];
   __shared__ WideGroup sg[kWideMax / 64];
   const uint32_t ng = (nt + 63) / 64;
-  for (uint32_t i = threadIdx.x; i < ng; i += kNT) sg[i] = groups[i];
+  for (uint32_t i = threadIdx.x; i < ng; i += kWideNT) sg[i] = groups[i];
   __syncthreads();
   int32_t w = -1;
   uint64_t src = 0, d = 0;
@@ -1031,17 +1040,17 @@ __global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __rest
     if (maps) {
       const uint32_t* vs = reinterpret_cast<const uint32_t*>(tv + t0);
       uint32_t* vd = reinterpret_cast<uint32_t*>(stv);
-      for (uint32_t i = threadIdx.x; i < gn * kViewDw; i += kNT) vd[i] = vs[i];
+      for (uint32_t i = threadIdx.x; i < gn * kViewDw; i += kWideNT) vd[i] = vs[i];
       const uint4* ms = reinterpret_cast<const uint4*>(maps + t0);
       uint4* md = reinterpret_cast<uint4*>(sdm);
-      for (uint32_t i = threadIdx.x; i < gn * kMapWords; i += kNT) md[i] = ms[i];
+      for (uint32_t i = threadIdx.x; i < gn * kMapWords; i += kWideNT) md[i] = ms[i];
       __syncthreads();
     } else {
       const uint32_t* vs = reinterpret_cast<const uint32_t*>(tv + t0);
       uint32_t* vd = reinterpret_cast<uint32_t*>(stv);
-      for (uint32_t i = threadIdx.x; i < gn * kViewDw; i += kNT) vd[i] = vs[i];
+      for (uint32_t i = threadIdx.x; i < gn * kViewDw; i += kWideNT) vd[i] = vs[i];
       __syncthreads();
-      for (uint32_t i = threadIdx.x; i < gn * kMapWords; i += kNT) {
+      for (uint32_t i = threadIdx.x; i < gn * kMapWords; i += kWideNT) {
         const uint32_t t = i / kMapWords, j = i - t * kMapWords;
         const DirMap* gm = stv[t].dmap;
         if (gm) reinterpret_cast<uint4*>(sdm + t)[j] = reinterpret_cast<const uint4*>(gm)[j];
@@ -1162,9 +1171,21 @@ __global__ __launch_bounds__(kNT, 4) void k_wide_get_many(const uint64_t* __rest
     vsrc[k] = src;
     dlen[k] = d;
   }
+  // one value-byte sum per 256-key tile (get_tiles): the workgroup's tiles
+  // from the prefixes at their bounds
   uint64_t total;
-  (void)block_scan<kNT>(d, &total);
-  if (threadIdx.x == 0) tsum[blockIdx.x] = total;
+  const uint64_t pre = block_scan<kWideNT>(d, &total);
+  if constexpr (kWideNT == kNT) {
+    if (threadIdx.x == 0) tsum[blockIdx.x] = total;
+  } else {
+    constexpr uint32_t T = kWideNT / kNT;
+    __shared__ uint64_t bnd[T + 1];
+    if (threadIdx.x % kNT == 0) bnd[threadIdx.x / kNT] = pre;
+    if (threadIdx.x == 0) bnd[T] = total;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)T * blockIdx.x;
+    if (threadIdx.x < T && (t0 + threadIdx.x) * kNT < n) tsum[t0 + threadIdx.x] = bnd[threadIdx.x + 1] - bnd[threadIdx.x];
+  }
 }
 
 // ---- base64 decode of the found values ----
@@ -1596,10 +1617,10 @@ hipError_t launch_wide_get_many(int keyk, int mode, uint32_t R, const uint64_t* 
   if (!nt || nt > 64 * R || R > kWideMax / 64) return hipErrorInvalidValue;
   const WideZone z = zones ? *zones : WideZone{nullptr, nullptr, nullptr, nullptr, 0};
   const WideScreen sc = screen ? *screen : WideScreen{nullptr, 0, 0, 0};
-  const dim3 g(blocks_for(n, kNT));
+  const dim3 g(blocks_for(n, kWideNT));
   ProfScope ps("k_wide_get_many", s);
 #define WG(KK, MM)                                                                                                 \
-  hipLaunchKernelGGL((k_wide_get_many<KK, MM>), g, dim3(kNT), 0, s, set, R, mp, z, tv, nt, groups, slots, ks, n, \
+  hipLaunchKernelGGL((k_wide_get_many<KK, MM>), g, dim3(kWideNT), 0, s, set, R, mp, z, tv, nt, groups, slots, ks, n, \
                      which, vsrc, dlen, tsum, sc, maps)
   switch (keyk * 3 + mode) {
     case 0: WG(KEY_FIXED16, MOD_POW2_32); break;
