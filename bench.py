@@ -1894,7 +1894,7 @@ def wide_fanout_leg(args, torch, dev, local, lanes, LK, timed, kernel_ms, lsmt_a
            "one_lane": {"value": round(n / (el1 / k), 1), "ms_per_step": round(el1 / k * 1e3, 4)},
            "tables": nt, "set_width": 320, "lookups": n, "found": found,
            "kernels_us": {kk: round(v["avg_us"], 2) for kk, v in kus.items()},
-           "launches_per_batch": {"search": 1, "tile_scan": 1, "b64_decode": 1},
+           "launches_per_batch": {kk.replace("k_", "", 1): round(v["launches"] / k, 2) for kk, v in kus.items()},
            "table_build_s": round(flush_s, 2)}
     # roofline of the search launch: its compulsory HBM bytes are the keys
     # (16 B) and its three per-lookup outputs (which 4 B, value source 8 B,
