@@ -64,12 +64,18 @@ hipError_t launch_wide_probe(int keyk, int mode, uint32_t R, const uint64_t* set
 // ---- device helpers shared with the fused read path (sstable.hip) ----
 
 // Bits [lo, lo + 64) of a row (R words), zero past the row.
+// A window across two words takes them in one 16-byte load (rows are 8-byte
+// aligned; gfx950 loads them unaligned): two loads of one line issued back to
+// back are two L2 requests, the L1 does not merge them (round 6).
 __device__ __forceinline__ uint64_t wide_window(const uint64_t* __restrict__ row, uint32_t R, uint32_t lo) {
   const uint32_t j = lo >> 6, sh = lo & 63u;
-  const uint64_t a = j < R ? row[j] : 0ull;
-  if (!sh) return a;
-  const uint64_t b = j + 1 < R ? row[j + 1] : 0ull;
-  return (a >> sh) | (b << (64 - sh));
+  if (!sh) return j < R ? row[j] : 0ull;
+  if (j + 1 < R) {
+    typedef uint64_t u64x2a __attribute__((ext_vector_type(2), aligned(8)));
+    const u64x2a v = *(const __attribute__((address_space(1))) u64x2a*)(row + j);
+    return (v.x >> sh) | (v.y << (64 - sh));
+  }
+  return j < R ? row[j] >> sh : 0ull;
 }
 
 // ZoneMap::contains for slot s of a wide set (src/zonemap.rs:37-42): true
