@@ -264,6 +264,19 @@ def test_codec_matches_oracle(gpu):
             gpu.BloomFilter.from_bytes(bad)
 
 
+def test_codec_pinned_to_the_protobuf_wire_format(gpu):
+    """BloomFilter.to_bytes / from_bytes on the device against wire bytes
+    written from the protobuf encoding spec (tests/test_oracle.py _wire)."""
+    from tests.test_oracle import _wire
+    for m in (1, 10, 127, 128, 130, 300, 16384):
+        rng = np.random.default_rng(m)
+        bits = [int(x) for x in rng.integers(0, 2, m)]
+        wire = _wire(bits)
+        f = gpu.BloomFilter.from_bytes(wire)
+        assert f.m == m and list(f.bools()) == bits
+        assert f.to_bytes() == wire
+
+
 def test_packed_import_masks_tail(gpu):
     f = gpu.BloomFilter(40)
     f.load_packed(np.array([0xFFFFFFFF, 0xFFFFFFFF], np.uint32))
