@@ -79,6 +79,21 @@ def test_meta_roundtrip_vs_oracle(gpu, m):
     assert gpu.TableMeta(None, gpu.ZoneMap(lo, None)).encode() == oracle.meta_encode(None, oracle.OracleZone(lo, None))
 
 
+def test_meta_pinned_to_the_protobuf_wire_format(gpu):
+    """The device codec's TableMeta bytes against bytes written from the
+    protobuf encoding spec (tests/test_oracle.py _meta_wire), and decoded
+    back field by field."""
+    from tests.test_oracle import _meta_wire, _wire
+    for m, lo, hi in [(10, b"apple", b"pear"), (200, b"a" * 130, b"z"), (1, None, None), (64, b"k", None)]:
+        rng = np.random.default_rng(m)
+        bits = [int(x) for x in rng.integers(0, 2, m)]
+        want = _meta_wire(bits, lo, hi)
+        b = gpu.BloomFilter.from_bytes(_wire(bits))
+        assert gpu.TableMeta(b, gpu.ZoneMap(lo, hi)).encode() == want, m
+        t = gpu.TableMeta.decode(want)
+        assert list(t.bloom.bools()) == bits and (t.zone_map.min, t.zone_map.max) == (lo, hi), m
+
+
 def test_meta_encode_into_device_buffer(gpu):
     import ctypes
 
