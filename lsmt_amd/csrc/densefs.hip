@@ -91,6 +91,16 @@ constexpr uint32_t kProbeU = 4;              // entries per lane per round of th
 constexpr size_t dense_part_lds(uint32_t R) { return (size_t)(((R + 4) & ~3u) + 4) * 4 + (size_t)kDenseC * 8; }
 constexpr size_t dense_part_lds_max() { return dense_part_lds(kDenseMaxRegions); }
 
+// The partition pass's entry stores (experiment builds: CB_DENSE_ST 1 =
+// write-through (sc1) 16-B buffer stores, 2 = non-temporal; product: plain).
+#if defined(CB_EXPERIMENTS) && defined(CB_DENSE_ST)
+constexpr int kDenseSt = CB_DENSE_ST;
+#else
+constexpr int kDenseSt = 0;
+#endif
+typedef uint32_t dense_u32x4 __attribute__((ext_vector_type(4)));
+typedef int dense_i32x4 __attribute__((ext_vector_type(4)));
+
 // XCD-aware region order (workgroups are dealt round-robin over the 8 XCDs):
 // XCD x takes regions [x R/8, (x+1) R/8) in order.
 __device__ __forceinline__ uint32_t xcd_region(uint32_t bid, uint32_t R) {
@@ -211,7 +221,22 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
   const uint32_t total = hist[R];
   uint2* out = ent + (uint64_t)b * C;
   const uint32_t n2 = total / 2;
-  for (uint32_t i = tid; i < n2; i += NT) reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(stage)[i];
+  if constexpr (kDenseSt == 1) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, 0, total * 8, 0x00020000);
+    for (uint32_t i = tid; i < n2; i += NT) {
+      const uint4 v = reinterpret_cast<const uint4*>(stage)[i];
+      const dense_i32x4 w = {(int)v.x, (int)v.y, (int)v.z, (int)v.w};
+      __builtin_amdgcn_raw_buffer_store_b128(w, rs, i * 16, 0, 16);
+    }
+  } else if constexpr (kDenseSt == 2) {
+    for (uint32_t i = tid; i < n2; i += NT) {
+      const uint4 v = reinterpret_cast<const uint4*>(stage)[i];
+      const dense_u32x4 w = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(w, reinterpret_cast<dense_u32x4*>(out) + i);
+    }
+  } else {
+    for (uint32_t i = tid; i < n2; i += NT) reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(stage)[i];
+  }
   if (tid == 0 && (total & 1u)) out[total - 1] = stage[total - 1];
 }
 
