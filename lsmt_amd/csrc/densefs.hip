@@ -91,12 +91,23 @@ constexpr uint32_t kProbeU = 4;              // entries per lane per round of th
 constexpr size_t dense_part_lds(uint32_t R) { return (size_t)(((R + 4) & ~3u) + 4) * 4 + (size_t)kDenseC * 8; }
 constexpr size_t dense_part_lds_max() { return dense_part_lds(kDenseMaxRegions); }
 
-// The partition pass's entry stores (experiment builds: CB_DENSE_ST 1 =
-// write-through (sc1) 16-B buffer stores, 2 = non-temporal; product: plain).
+// The partition pass's stores of the entries and of the zeroed hit words:
+// non-temporal (written once, read by the probe launch on every XCD; the hit
+// words then ORed there): k_dense_probe 150.3-150.7 -> 141.8-142.1 us, C5
+// one lane 227.5-228.3 -> 219.9-220.3 us, three lanes 188.9-189.8 -> 177.6-
+// 178.1 us, against plain stores; write-through (sc1) buffer stores measured
+// as plain, and the entries alone non-temporal 143.4 us (round 6, HISTORY.md).
+// Experiment builds: CB_DENSE_ST 0 plain, 1 write-through, 2 non-temporal;
+// CB_DENSE_HST 0 the hit words plain.
 #if defined(CB_EXPERIMENTS) && defined(CB_DENSE_ST)
 constexpr int kDenseSt = CB_DENSE_ST;
 #else
-constexpr int kDenseSt = 0;
+constexpr int kDenseSt = 2;
+#endif
+#if defined(CB_EXPERIMENTS) && defined(CB_DENSE_HST)
+constexpr bool kDenseHitsNt = CB_DENSE_HST;
+#else
+constexpr bool kDenseHitsNt = true;
 #endif
 typedef uint32_t dense_u32x4 __attribute__((ext_vector_type(4)));
 typedef int dense_i32x4 __attribute__((ext_vector_type(4)));
@@ -214,7 +225,12 @@ __global__ __launch_bounds__(kDenseNT, CB_DENSE_PART_WAVES) void k_dense_part(Ke
     constexpr uint32_t WPB = C / 64;
     for (uint32_t i = tid; i < used * WPB; i += NT) {
       const uint32_t f = i / WPB, w = i % WPB;
-      if (w0 + w < nw) hits[(uint64_t)f * hwords + w0 + w] = 0ull;
+      if (w0 + w < nw) {
+        if constexpr (kDenseHitsNt)
+          __builtin_nontemporal_store(0ull, reinterpret_cast<unsigned long long*>(hits) + (uint64_t)f * hwords + w0 + w);
+        else
+          hits[(uint64_t)f * hwords + w0 + w] = 0ull;
+      }
     }
   }
   __syncthreads();
