@@ -314,7 +314,9 @@ __device__ __forceinline__ void part_phases(const uint32_t (&q)[2 * KPT], uint32
   // kernel's end has no dirty L2 lines to write back, and the tile pass (on
   // other XCDs) still finds them there; C2 on four lanes 101 -> 105-107 G
   // keys/s (non-temporal stores instead made the tile pass's reads slower)
-  if (pol & 1u) {
+  if (pol & 4u) {  // (bit 2: non-temporal entries)
+    for (uint32_t i = tid; i < n4; i += NT) store16_nt(reinterpret_cast<uint4*>(out) + i, reinterpret_cast<const uint4*>(stage)[i]);
+  } else if (pol & 1u) {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, 2 * C * sizeof(E), 0x00020000);
     for (uint32_t i = tid; i < n4; i += NT) store16_wt(r, i * 16, reinterpret_cast<const uint4*>(stage)[i]);
   } else {
